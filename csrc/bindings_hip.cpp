@@ -1,0 +1,249 @@
+// Python bindings of the MI355X runtime (`llama_fastapi_k8s_gpu_amd.runtime._hip`).
+//
+// Two surfaces:
+//   * Engine      - the serving engine (load, generate, test hooks); the GIL is
+//                   released for the whole generation loop and re-acquired only
+//                   for the optional per-token callback / cancel poll.
+//   * kernel hooks - thin wrappers taking raw device pointers (torch
+//                   `data_ptr()`) and a stream handle, used by the numerics tests
+//                   that compare each kernel with a PyTorch fp32 reference.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <rccl/rccl.h>
+
+#include "kernels/kernels.h"
+#include "runtime/engine.h"
+#include "runtime/repack.h"
+
+namespace py = pybind11;
+using namespace lfk;
+
+template <class T>
+static T* P(uintptr_t p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void hip_ok(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "MI355X (gfx950) runtime: GGUF engine + HIP kernels";
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
+                       int tp_size, py::bytes nccl_id) {
+             EngineOptions o;
+             o.n_ctx = n_ctx;
+             o.n_batch = n_batch;
+             o.device = device;
+             o.use_graph = use_graph;
+             o.tp_rank = tp_rank;
+             o.tp_size = tp_size;
+             o.nccl_id = std::string(nccl_id);
+             py::gil_scoped_release nogil;
+             return std::make_unique<Engine>(path, o);
+           }),
+           py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
+           py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
+           py::arg("nccl_id") = py::bytes(""))
+      .def(
+          "generate",
+          [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
+             const std::vector<int>& stop_ids, py::object poll, py::object on_token) {
+            SamplingOpts o;
+            o.top_k = sp.contains("top_k") ? sp["top_k"].cast<int>() : 40;
+            o.top_p = sp.contains("top_p") ? sp["top_p"].cast<float>() : 0.95f;
+            o.min_p = sp.contains("min_p") ? sp["min_p"].cast<float>() : 0.05f;
+            o.temp = sp.contains("temperature") ? sp["temperature"].cast<float>() : 0.8f;
+            o.repeat_penalty = sp.contains("repeat_penalty") ? sp["repeat_penalty"].cast<float>() : 1.1f;
+            o.freq_penalty = sp.contains("frequency_penalty") ? sp["frequency_penalty"].cast<float>() : 0.f;
+            o.presence_penalty = sp.contains("presence_penalty") ? sp["presence_penalty"].cast<float>() : 0.f;
+            o.last_n = sp.contains("last_n") ? sp["last_n"].cast<int>() : 64;
+            o.seed = sp.contains("seed") ? sp["seed"].cast<unsigned long long>() : 0ull;
+            std::function<bool()> pf;
+            std::function<void(int)> tf;
+            if (!poll.is_none()) pf = [poll]() { py::gil_scoped_acquire g; return poll().cast<bool>(); };
+            if (!on_token.is_none()) tf = [on_token](int t) { py::gil_scoped_acquire g; on_token(t); };
+            GenOut r;
+            {
+              py::gil_scoped_release nogil;
+              r = e.generate(prompt, n_keep, max_new, o, stop_ids, pf, tf);
+            }
+            py::dict d;
+            d["tokens"] = r.tokens;
+            d["finish"] = r.finish;
+            d["n_evaluated"] = r.n_evaluated;
+            d["n_prefilled"] = r.n_prefilled;
+            d["prefill_s"] = r.prefill_s;
+            d["decode_s"] = r.decode_s;
+            return d;
+          },
+          py::arg("prompt"), py::arg("n_keep"), py::arg("max_new"), py::arg("sampling"), py::arg("stop_ids"),
+          py::arg("poll") = py::none(), py::arg("on_token") = py::none())
+      .def("eval_logits",
+           [](Engine& e, const std::vector<int>& tokens, int pos0) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.eval_logits(tokens, pos0);
+             }
+             return py::array_t<float>(v.size(), v.data());
+           })
+      .def("decode_logits",
+           [](Engine& e, int token, int pos) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.decode_logits(token, pos);
+             }
+             return py::array_t<float>(v.size(), v.data());
+           })
+      .def("bench_decode",
+           [](Engine& e, int n, int pos0) {
+             double ms = 0;
+             py::gil_scoped_release nogil;
+             e.bench_decode(n, pos0, &ms);
+             return ms;
+           })
+      .def_property_readonly("device_bytes", &Engine::device_bytes)
+      .def_property_readonly("healthy", &Engine::healthy)
+      .def_property_readonly("last_error", &Engine::last_error)
+      .def_property_readonly("n_ctx", &Engine::n_ctx)
+      .def_property_readonly("tp_rank", &Engine::tp_rank)
+      .def_property_readonly("tp_size", &Engine::tp_size)
+      .def_property_readonly("hparams", [](const Engine& e) {
+        const HParams& h = e.hparams();
+        py::dict d;
+        d["n_vocab"] = h.n_vocab; d["n_embd"] = h.n_embd; d["n_layer"] = h.n_layer; d["n_head"] = h.n_head;
+        d["n_head_kv"] = h.n_head_kv; d["head_dim"] = h.head_dim; d["n_ff"] = h.n_ff;
+        d["n_expert"] = h.n_expert; d["n_expert_used"] = h.n_expert_used;
+        d["rope_base"] = h.rope_base; d["rms_eps"] = h.rms_eps;
+        return d;
+      });
+
+  m.def("nccl_unique_id", []() {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+    return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  });
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    return n;
+  });
+
+  // ------------------------------------------------------------------ kernel hooks (tests)
+  m.def("repack", [](int type, py::array_t<uint8_t, py::array::c_style> src, size_t K_src, size_t r0, size_t R,
+                     size_t c0, size_t K, size_t R_dst, int G, int off) {
+    py::array_t<uint8_t> dst(qbytes(type, R_dst, K));
+    std::memset(dst.mutable_data(), 0, dst.size());
+    repack_planar(type, src.data(), K_src, r0, R, c0, K, dst.mutable_data(), R_dst, G, off);
+    return dst;
+  });
+  m.def("qbytes", [](int type, size_t R, size_t K) { return qbytes(type, R, K); });
+
+  m.def("gemv", [](uintptr_t w, int type, int rows, int K, uintptr_t x, uintptr_t norm, float eps, uintptr_t out,
+                   int n_out, int epi, uintptr_t stream, int n_slots, uintptr_t ids, size_t expert_stride,
+                   int slot_stride, uintptr_t resid) {
+    GemvArgs a;
+    a.w = make_qmat(P<void>(w), type, rows, K, expert_stride);
+    a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.out = P<float>(out); a.n_out = n_out;
+    a.n_slots = n_slots; a.expert_ids = P<int>(ids); a.out_slot_stride = slot_stride; a.resid = P<float>(resid);
+    gemv(a, epi, S(stream));
+    hip_ok("gemv");
+  }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("norm"), py::arg("eps"),
+     py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
+     py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0);
+
+  m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,
+                       uintptr_t x, uintptr_t norm, float eps, uintptr_t q_out, uintptr_t kc, uintptr_t vc, int n_ctx,
+                       int hd, uintptr_t pos, uintptr_t rope, uintptr_t stream) {
+    QkvArgs a;
+    a.wq = make_qmat(P<void>(wq), tq, nq, K);
+    a.wk = make_qmat(P<void>(wk), tk, nkv, K);
+    a.wv = make_qmat(P<void>(wv), tv, nkv, K);
+    a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.q_out = P<float>(q_out);
+    a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.n_ctx = n_ctx; a.head_dim = hd;
+    a.pos = P<int>(pos); a.rope = P<float2>(rope);
+    gemv_qkv(a, S(stream));
+    hip_ok("gemv_qkv");
+  });
+
+  m.def("moe_down", [](uintptr_t w, int type, int rows, int K, size_t expert_stride, uintptr_t h, uintptr_t ids,
+                       uintptr_t ew, int n_slots, uintptr_t out, uintptr_t stream) {
+    MoeDownArgs a;
+    a.w = make_qmat(P<void>(w), type, rows, K, expert_stride);
+    a.h = P<float>(h); a.expert_ids = P<int>(ids); a.expert_w = P<float>(ew); a.n_slots = n_slots;
+    a.out = P<float>(out);
+    gemv_moe_down(a, S(stream));
+    hip_ok("moe_down");
+  });
+  m.def("moe_route", [](uintptr_t logits, int E, int k, uintptr_t ids, uintptr_t w, uintptr_t stream) {
+    moe_route(P<float>(logits), E, k, P<int>(ids), P<float>(w), S(stream));
+    hip_ok("moe_route");
+  });
+
+  m.def("gemm", [](uintptr_t w, int type, int rows, int K, uintptr_t x, int T, uintptr_t out, uintptr_t out_bf16,
+                   int ldo, int epi, uintptr_t stream, uintptr_t resid) {
+    GemmArgs a;
+    a.w = make_qmat(P<void>(w), type, rows, K);
+    a.x = P<__hip_bfloat16>(x); a.T = T; a.out = P<float>(out); a.out_bf16 = P<__hip_bfloat16>(out_bf16);
+    a.ldo = ldo; a.resid = P<float>(resid);
+    gemm_dq(a, epi, S(stream));
+    hip_ok("gemm");
+  }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
+     py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
+
+  m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
+                          int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream) {
+    AttnDecodeArgs a;
+    a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.pos = P<int>(pos);
+    a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
+    a.part = P<float>(part); a.out = P<float>(out);
+    attn_decode(a, S(stream));
+    hip_ok("attn_decode");
+  });
+  m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
+  m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
+                           int hd, float scale, uintptr_t out, uintptr_t stream) {
+    AttnPrefillArgs a;
+    a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.T = T; a.pos0 = pos0;
+    a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
+    a.out = P<float>(out); a.out_stride = n_head * hd;
+    attn_prefill(a, S(stream));
+    hip_ok("attn_prefill");
+  });
+  m.def("embed", [](uintptr_t w, int type, int V, int d, uintptr_t tokens, int T, uintptr_t x, uintptr_t stream) {
+    embed_rows(make_qmat(P<void>(w), type, V, d), P<int>(tokens), T, P<float>(x), S(stream));
+    hip_ok("embed");
+  });
+  m.def("rmsnorm_bf16", [](uintptr_t x, uintptr_t w, float eps, int T, int d, uintptr_t y, uintptr_t stream) {
+    rmsnorm_bf16(P<float>(x), P<float>(w), eps, T, d, P<__hip_bfloat16>(y), S(stream));
+    hip_ok("rmsnorm_bf16");
+  });
+  m.def("sampler_blocks", &sampler_blocks);
+  m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cv,
+                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream) {
+    SamplerArgs a;
+    a.logits = P<float>(logits); a.V = V; a.p = P<SamplerParamsDev>(params); a.ring = P<int>(ring);
+    a.state = P<int>(state); a.cand_val = P<float>(cv); a.cand_idx = P<int>(ci); a.out_tokens = P<int>(out_tokens);
+    a.out_cap = out_cap; a.advance_pos = advance;
+    sample(a, S(stream));
+    hip_ok("sample");
+  });
+  m.def("sampler_params_bytes", [](int top_k, float top_p, float min_p, float temp, float rp, float fp, float pp,
+                                   int last_n, unsigned long long seed, int greedy) {
+    SamplerParamsDev p;
+    p.top_k = top_k; p.top_p = top_p; p.min_p = min_p; p.temp = temp; p.repeat_penalty = rp;
+    p.freq_penalty = fp; p.presence_penalty = pp; p.last_n = last_n; p.seed = seed; p.greedy = greedy;
+    return py::bytes(reinterpret_cast<const char*>(&p), sizeof(p));
+  });
+  m.def("fill_random", [](uintptr_t base, int type, size_t rows, size_t K, float std, unsigned long long seed,
+                          uintptr_t stream) {
+    fill_random_planar(P<uint8_t>(base), type, rows, K, std, seed, S(stream));
+    hip_ok("fill_random");
+  });
+}

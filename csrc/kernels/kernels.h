@@ -1,0 +1,174 @@
+// Host-side launch interface of the gfx950 kernels. Every launcher is
+// asynchronous on the given stream, does no allocation and no host sync, and
+// reads run-time scalars (position, KV length, sampled token) from device
+// memory - so a whole decode step can be captured into one hipGraph and
+// replayed unchanged.
+#pragma once
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../common.h"
+
+namespace lfk {
+
+// ---------------------------------------------------------------- weights
+struct QMat {
+  const uint8_t* base = nullptr;
+  int type = 0;
+  int rows = 0;  // rows of ONE matrix (one expert)
+  int K = 0;
+  Planes P{};
+  size_t expert_stride = 0;  // bytes between experts (0 = not an expert tensor)
+};
+
+QMat make_qmat(const void* base, int type, int rows, int K, size_t expert_stride = 0);
+
+// ---------------------------------------------------------------- GEMV (decode, T = 1)
+enum GemvEpi : int {
+  EPI_STORE = 0,   // out[row] = acc
+  EPI_ADD = 1,     // out[row] += acc            (residual, in place)
+  EPI_SWIGLU = 2,  // out[f] = silu(acc_gate)*acc_up ; W = gate/up interleaved in 32-row groups
+};
+
+struct GemvArgs {
+  QMat w;
+  const float* x = nullptr;       // [K] f32 activation
+  const float* norm_w = nullptr;  // optional RMSNorm weight (fused into the prologue)
+  float eps = 1e-5f;
+  float* out = nullptr;
+  int n_out = 0;                   // outputs per slot (rows, or features for SWIGLU)
+  int n_slots = 1;                 // MoE: experts used per token
+  const int* expert_ids = nullptr; // [n_slots] expert index per slot (device)
+  int out_slot_stride = 0;
+  const float* resid = nullptr;    // EPI_STORE: out = acc + resid (TP rank 0 residual)
+};
+void gemv(const GemvArgs& a, int epi, hipStream_t s);
+
+// Fused QKV projection + RoPE (adjacent pairs) + KV-cache append.
+struct QkvArgs {
+  QMat wq, wk, wv;
+  const float* x = nullptr;
+  const float* norm_w = nullptr;
+  float eps = 1e-5f;
+  float* q_out = nullptr;          // [n_q] f32 (roped)
+  __half* k_cache = nullptr;       // layer base, [n_kv_heads][n_ctx][head_dim]
+  __half* v_cache = nullptr;
+  int n_ctx = 0;
+  int head_dim = 0;
+  const int* pos = nullptr;        // device scalar: position of this token
+  const float2* rope = nullptr;    // [n_ctx][head_dim/2] (cos, sin)
+};
+void gemv_qkv(const QkvArgs& a, hipStream_t s);
+
+// MoE down projection: out[r] += sum_s w[s] * dot(W_{ids[s]}[r], h_s)
+struct MoeDownArgs {
+  QMat w;
+  const float* h = nullptr;        // [n_slots][K]
+  const int* expert_ids = nullptr;
+  const float* expert_w = nullptr; // [n_slots]
+  int n_slots = 2;
+  float* out = nullptr;            // [rows]
+};
+void gemv_moe_down(const MoeDownArgs& a, hipStream_t s);
+
+// Router: softmax over n_expert logits, top-k, renormalise -> ids / weights (device).
+void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s);
+// Prefill router over T rows -> dense [T][E] weights (0 for unselected experts).
+void moe_route_dense(const float* logits, int T, int n_expert, int k, float* w_dense, hipStream_t s);
+// acc[t][:] += w_dense[t][e] * y[t][:]
+void axpy_rows(float* acc, const float* y, const float* w_dense, int e, int E, int T, int d, hipStream_t s);
+
+// ---------------------------------------------------------------- attention
+// Decode: split-L flash decoding over chunks of 64 keys, GQA-packed.
+struct AttnDecodeArgs {
+  const float* q = nullptr;       // [n_head][hd]
+  const __half* k_cache = nullptr;
+  const __half* v_cache = nullptr;
+  const int* pos = nullptr;       // KV length = *pos + 1
+  int n_ctx = 0, n_head = 0, n_kv_head = 0, head_dim = 0;
+  float scale = 1.f;
+  float* part = nullptr;          // workspace [n_split][n_head][hd + 2]
+  float* out = nullptr;           // [n_head][hd]
+};
+void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
+size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim);
+
+// Prefill: causal attention of T queries at positions pos0.. over the cache.
+struct AttnPrefillArgs {
+  const float* q = nullptr;       // [T][n_head][hd] (roped)
+  const __half* k_cache = nullptr;
+  const __half* v_cache = nullptr;
+  int T = 0, pos0 = 0, n_ctx = 0, n_head = 0, n_kv_head = 0, head_dim = 0;
+  float scale = 1.f;
+  float* out = nullptr;           // [T][n_head][hd]
+  int out_stride = 0;
+};
+void attn_prefill(const AttnPrefillArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- prefill GEMM (MFMA)
+enum GemmEpi : int { GEMM_STORE = 0, GEMM_ADD = 1, GEMM_SWIGLU = 2 };
+struct GemmArgs {
+  QMat w;                          // [N][K] planar
+  const __hip_bfloat16* x = nullptr;  // [T][K] bf16 (row stride K)
+  int T = 0;
+  float* out = nullptr;            // f32 [T][ldo] (STORE/ADD)
+  __hip_bfloat16* out_bf16 = nullptr; // SWIGLU -> bf16 [T][N/2]
+  int ldo = 0;
+  const float* resid = nullptr;    // STORE: out = acc + resid[t][n] (TP rank 0)
+};
+void gemm_dq(const GemmArgs& a, int epi, hipStream_t s);
+
+// ---------------------------------------------------------------- elementwise / misc
+// x[t][:] = dequant(token_embd[tokens[t]][:])
+void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s);
+// y_bf16[t] = rmsnorm(x[t]) * w
+void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s);
+// f32 activation [T][d] -> bf16 (for the next GEMM)
+void to_bf16(const float* x, int n, __hip_bfloat16* y, hipStream_t s);
+// prefill: rope q/k of QKV rows, write q (f32) and k/v to the caches at pos0+t
+void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int head_dim, int n_ctx,
+                     const float2* rope, float* q_out, __half* k_cache, __half* v_cache, hipStream_t s);
+// out[i] = x[i] (+) ... small helpers
+void add_inplace(float* x, const float* y, int n, hipStream_t s);
+void set_i32(int* p, int v, hipStream_t s);
+
+// ---------------------------------------------------------------- sampling
+// Sampling parameters live in DEVICE memory so a captured decode graph serves
+// every request unchanged (they are written once per request, before replay).
+struct SamplerParamsDev {
+  int top_k = 40;
+  int last_n = 64;
+  int greedy = 0;
+  int pad = 0;
+  float top_p = 0.95f, min_p = 0.05f, temp = 0.8f;
+  float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
+  unsigned long long seed = 0;
+};
+// Device state block (ints) shared by the decode kernels.
+enum StateIdx : int { S_TOKEN = 0, S_POS = 1, S_STEP = 2, S_RING_LEN = 3, S_RING_HEAD = 4, S_NOUT = 5, S_NSTATE = 8 };
+
+struct SamplerArgs {
+  const float* logits = nullptr;   // [V]; penalties are applied on a copy in LDS
+  int V = 0;
+  const SamplerParamsDev* p = nullptr;
+  int* ring = nullptr;             // [64] penalty window ring (prompt + generated tokens)
+  int* state = nullptr;            // [S_NSTATE]
+  float* cand_val = nullptr;       // workspace [sampler_blocks(V) * 64]
+  int* cand_idx = nullptr;
+  int* out_tokens = nullptr;       // optional device ring of sampled tokens [out_cap]
+  int out_cap = 0;
+  int advance_pos = 1;             // also bump state.pos (decode) after sampling
+};
+int sampler_blocks(int V);
+void sample(const SamplerArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------- synthetic fill
+// Random valid quant blocks generated on device (for synthetic models without a file).
+void fill_random_planar(uint8_t* base, int type, size_t rows, size_t K, float std, unsigned long long seed,
+                        hipStream_t s);
+
+}  // namespace lfk

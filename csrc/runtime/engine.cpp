@@ -1,0 +1,579 @@
+#include "engine.h"
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+#include "repack.h"
+
+namespace lfk {
+
+#define HIPCHK(x) check((x), #x)
+
+static double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+HParams read_hparams(const GGUFFile& f) {
+  HParams h;
+  std::string arch = f.get_str("general.architecture", "llama");
+  if (arch != "llama" && arch != "mistral" && arch != "mixtral")
+    throw std::runtime_error("unsupported architecture " + arch);
+  auto gi = [&](const char* k, int64_t d) { return (int)f.get_int(arch + "." + k, d); };
+  h.n_embd = gi("embedding_length", 0);
+  h.n_layer = gi("block_count", 0);
+  h.n_head = gi("attention.head_count", 0);
+  h.n_head_kv = gi("attention.head_count_kv", h.n_head);
+  h.head_dim = gi("rope.dimension_count", h.n_head ? h.n_embd / h.n_head : 0);
+  h.n_ff = gi("feed_forward_length", 0);
+  h.n_expert = gi("expert_count", 0);
+  h.n_expert_used = gi("expert_used_count", 0);
+  h.n_ctx_train = gi("context_length", 2048);
+  h.rope_base = (float)f.get_float(arch + ".rope.freq_base", 10000.0);
+  h.rms_eps = (float)f.get_float(arch + ".attention.layer_norm_rms_epsilon", 1e-5);
+  const GGUFTensor* emb = f.find("token_embd.weight");
+  if (!emb) throw std::runtime_error("missing token_embd.weight");
+  h.n_vocab = (int)emb->ne[1];
+  return h;
+}
+
+void Engine::check(hipError_t e, const char* what) {
+  if (e != hipSuccess) {
+    healthy_ = false;
+    last_error_ = std::string(what) + ": " + hipGetErrorString(e);
+    throw std::runtime_error(last_error_);
+  }
+}
+
+static void ncclchk(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+void* Engine::dalloc(size_t bytes) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, bytes < 16 ? 16 : bytes));
+  allocs_.push_back(p);
+  dev_bytes_ += bytes;
+  return p;
+}
+
+Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) {
+  HIPCHK(hipSetDevice(opt_.device));
+  HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  for (auto& e : step_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  GGUFFile f(path);
+  hp_ = read_hparams(f);
+  const int tp = opt_.tp_size, r = opt_.tp_rank;
+  if (hp_.n_head % tp || hp_.n_head_kv % tp) throw std::runtime_error("tensor parallel degree must divide head counts");
+  nh_l_ = hp_.n_head / tp;
+  nkv_l_ = hp_.n_head_kv / tp;
+  nq_ = nh_l_ * hp_.head_dim;
+  nkvd_ = nkv_l_ * hp_.head_dim;
+  if (hp_.n_ff % tp) throw std::runtime_error("tensor parallel degree must divide n_ff");
+  F_l_ = hp_.n_ff / tp;
+  V_l_ = (hp_.n_vocab + tp - 1) / tp;
+  V_pad_ = V_l_ * tp;
+  if (opt_.n_ctx <= 0) opt_.n_ctx = hp_.n_ctx_train;
+  if (tp > 1) {
+    if (opt_.nccl_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad nccl id");
+    ncclUniqueId id;
+    std::memcpy(&id, opt_.nccl_id.data(), sizeof(id));
+    ncclComm_t c;
+    ncclchk(ncclCommInitRank(&c, tp, id, r), "ncclCommInitRank");
+    comm_ = c;
+  }
+  load(f);
+  alloc_buffers();
+  build_rope();
+  HIPCHK(hipStreamSynchronize(stream_));
+}
+
+Engine::~Engine() {
+  if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  if (graph_) hipGraphDestroy(graph_);
+  if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
+  for (void* p : allocs_) hipFree(p);
+  if (h_ring_) hipHostFree(h_ring_);
+  if (h_tokens_) hipHostFree(h_tokens_);
+  for (auto& e : step_ev_) if (e) hipEventDestroy(e);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+// ------------------------------------------------------------------------ loading
+QMat Engine::upload_matrix(const GGUFFile& f, const std::string& name, size_t r0, size_t R, size_t c0, size_t K,
+                           int n_expert) {
+  const GGUFTensor* t = f.find(name);
+  if (!t) throw std::runtime_error("missing tensor " + name);
+  const size_t K_src = (size_t)t->ne[0];
+  const size_t R_src = (size_t)t->ne[1];
+  const int E = n_expert > 0 ? n_expert : 1;
+  const size_t one = qbytes(t->type, R, K);
+  std::vector<uint8_t> host(one * E);
+  const TypeInfo ti = type_info(t->type);
+  const size_t src_expert = R_src * (K_src / ti.block) * ti.bytes;
+  f.prefetch(*t);
+  for (int e = 0; e < E; ++e) {
+    const size_t rows_avail = r0 < R_src ? std::min(R, R_src - r0) : 0;
+    if (rows_avail < R) std::memset(host.data() + one * e, 0, one);
+    repack_planar(t->type, f.data(*t) + src_expert * e, K_src, r0, rows_avail, c0, K, host.data() + one * e, R, 0, 0);
+  }
+  void* d = dalloc(host.size());
+  HIPCHK(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
+  return make_qmat(d, t->type, (int)R, (int)K, n_expert > 0 ? one : 0);
+}
+
+QMat Engine::upload_gate_up(const GGUFFile& f, const std::string& gate, const std::string& up, size_t f0, size_t F,
+                            int n_expert) {
+  const GGUFTensor* tg = f.find(gate);
+  const GGUFTensor* tu = f.find(up);
+  if (!tg || !tu) throw std::runtime_error("missing " + gate + " / " + up);
+  if (tg->type != tu->type) throw std::runtime_error("gate/up projections must share a quant type");
+  if (F % 32) throw std::runtime_error("n_ff per rank must be a multiple of 32");
+  const size_t K = (size_t)tg->ne[0];
+  const int E = n_expert > 0 ? n_expert : 1;
+  const size_t one = qbytes(tg->type, 2 * F, K);
+  std::vector<uint8_t> host(one * E);
+  const TypeInfo ti = type_info(tg->type);
+  const size_t src_expert = (size_t)tg->ne[1] * (K / ti.block) * ti.bytes;
+  f.prefetch(*tg);
+  f.prefetch(*tu);
+  for (int e = 0; e < E; ++e) {
+    repack_planar(tg->type, f.data(*tg) + src_expert * e, K, f0, F, 0, K, host.data() + one * e, 2 * F, 32, 0);
+    repack_planar(tu->type, f.data(*tu) + src_expert * e, K, f0, F, 0, K, host.data() + one * e, 2 * F, 32, 32);
+  }
+  void* d = dalloc(host.size());
+  HIPCHK(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
+  return make_qmat(d, tg->type, (int)(2 * F), (int)K, n_expert > 0 ? one : 0);
+}
+
+float* Engine::upload_f32(const GGUFFile& f, const std::string& name) {
+  const GGUFTensor* t = f.find(name);
+  if (!t) throw std::runtime_error("missing tensor " + name);
+  if (t->type != T_F32) throw std::runtime_error(name + ": expected F32");
+  float* d = static_cast<float*>(dalloc(t->nbytes));
+  HIPCHK(hipMemcpy(d, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+  return d;
+}
+
+void Engine::load(const GGUFFile& f) {
+  const int r = opt_.tp_rank;
+  const int d = hp_.n_embd, hd = hp_.head_dim;
+  tok_embd_ = upload_matrix(f, "token_embd.weight", 0, hp_.n_vocab, 0, d);
+  out_norm_ = upload_f32(f, "output_norm.weight");
+  const std::string out_name = f.find("output.weight") ? "output.weight" : "token_embd.weight";
+  output_ = upload_matrix(f, out_name, (size_t)r * V_l_, V_l_, 0, d);
+  layers_.resize(hp_.n_layer);
+  for (int l = 0; l < hp_.n_layer; ++l) {
+    const std::string p = "blk." + std::to_string(l) + ".";
+    Layer& L = layers_[l];
+    L.attn_norm = upload_f32(f, p + "attn_norm.weight");
+    L.ffn_norm = upload_f32(f, p + "ffn_norm.weight");
+    L.wq = upload_matrix(f, p + "attn_q.weight", (size_t)r * nq_, nq_, 0, d);
+    L.wk = upload_matrix(f, p + "attn_k.weight", (size_t)r * nkvd_, nkvd_, 0, d);
+    L.wv = upload_matrix(f, p + "attn_v.weight", (size_t)r * nkvd_, nkvd_, 0, d);
+    L.wo = upload_matrix(f, p + "attn_output.weight", 0, d, (size_t)r * nq_, nq_);
+    if (hp_.n_expert > 0) {
+      L.router = upload_matrix(f, p + "ffn_gate_inp.weight", 0, hp_.n_expert, 0, d);
+      L.gu_exps = upload_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", (size_t)r * F_l_, F_l_,
+                                 hp_.n_expert);
+      L.down_exps = upload_matrix(f, p + "ffn_down_exps.weight", 0, d, (size_t)r * F_l_, F_l_, hp_.n_expert);
+    } else {
+      L.w_gu = upload_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight", (size_t)r * F_l_, F_l_);
+      L.w_down = upload_matrix(f, p + "ffn_down.weight", 0, d, (size_t)r * F_l_, F_l_);
+    }
+    (void)hd;
+  }
+}
+
+void Engine::alloc_buffers() {
+  const int B = opt_.n_batch, d = hp_.n_embd, hd = hp_.head_dim;
+  const int E = std::max(hp_.n_expert, 1), KU = std::max(hp_.n_expert_used, 1);
+  x_ = (float*)dalloc(sizeof(float) * B * d);
+  tmp_ = (float*)dalloc(sizeof(float) * B * d);
+  xb_ = (__hip_bfloat16*)dalloc(2ull * B * d);
+  qkv_ = (float*)dalloc(sizeof(float) * B * (nq_ + 2 * nkvd_));
+  q_ = (float*)dalloc(sizeof(float) * B * nq_);
+  attn_ = (float*)dalloc(sizeof(float) * B * nq_);
+  attnb_ = (__hip_bfloat16*)dalloc(2ull * B * nq_);
+  h_ = (__hip_bfloat16*)dalloc(2ull * B * F_l_);
+  hf_ = (float*)dalloc(sizeof(float) * KU * F_l_);
+  logits_ = (float*)dalloc(sizeof(float) * V_pad_);
+  logits_l_ = (float*)dalloc(sizeof(float) * V_l_);
+  HIPCHK(hipMemset(logits_l_, 0, sizeof(float) * V_l_));
+  const size_t kv = (size_t)hp_.n_layer * nkv_l_ * opt_.n_ctx * hd;
+  kc_ = (__half*)dalloc(kv * 2);
+  vc_ = (__half*)dalloc(kv * 2);
+  HIPCHK(hipMemset(kc_, 0, kv * 2));
+  HIPCHK(hipMemset(vc_, 0, kv * 2));
+  rope_ = (float2*)dalloc(sizeof(float2) * opt_.n_ctx * (hd / 2));
+  attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
+  const int nb = sampler_blocks(hp_.n_vocab);
+  cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
+  cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
+  state_ = (int*)dalloc(sizeof(int) * S_NSTATE);
+  ring_ = (int*)dalloc(sizeof(int) * 64);
+  out_tokens_ = (int*)dalloc(sizeof(int) * 64);
+  tokens_ = (int*)dalloc(sizeof(int) * B);
+  sparams_ = (SamplerParamsDev*)dalloc(sizeof(SamplerParamsDev));
+  router_logits_ = (float*)dalloc(sizeof(float) * B * E);
+  route_w_ = (float*)dalloc(sizeof(float) * B * E);
+  moe_ids_ = (int*)dalloc(sizeof(int) * KU);
+  moe_w_ = (float*)dalloc(sizeof(float) * KU);
+  if (hp_.n_expert > 0) moe_y_ = (float*)dalloc(sizeof(float) * B * d);
+  HIPCHK(hipMemset(state_, 0, sizeof(int) * S_NSTATE));
+  HIPCHK(hipMemset(ring_, 0, sizeof(int) * 64));
+  HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
+  HIPCHK(hipHostMalloc((void**)&h_ring_, sizeof(int) * 64, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&h_tokens_, sizeof(int) * B, hipHostMallocDefault));
+}
+
+void Engine::build_rope() {
+  const int hd = hp_.head_dim, n = opt_.n_ctx;
+  std::vector<float2> t((size_t)n * (hd / 2));
+  for (int p = 0; p < n; ++p)
+    for (int i = 0; i < hd / 2; ++i) {
+      const double inv = std::pow((double)hp_.rope_base, -2.0 * i / hd);
+      const double a = p * inv;
+      t[(size_t)p * (hd / 2) + i] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+  HIPCHK(hipMemcpy(rope_, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
+}
+
+// ------------------------------------------------------------------------ schedule
+void Engine::allreduce_into(const float* send, float* recv, size_t n, hipStream_t s) {
+  ncclchk(ncclAllReduce(send, recv, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s), "ncclAllReduce");
+}
+
+void Engine::enqueue_layer_decode(int l, hipStream_t s) {
+  const Layer& L = layers_[l];
+  const int d = hp_.n_embd, hd = hp_.head_dim;
+  const bool tp = opt_.tp_size > 1;
+  const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
+  QkvArgs qa;
+  qa.wq = L.wq; qa.wk = L.wk; qa.wv = L.wv;
+  qa.x = x_; qa.norm_w = L.attn_norm; qa.eps = hp_.rms_eps;
+  qa.q_out = q_;
+  qa.k_cache = kc_ + kv_layer * l;
+  qa.v_cache = vc_ + kv_layer * l;
+  qa.n_ctx = opt_.n_ctx; qa.head_dim = hd;
+  qa.pos = state_ + S_POS;
+  qa.rope = rope_;
+  gemv_qkv(qa, s);
+
+  AttnDecodeArgs aa;
+  aa.q = q_; aa.k_cache = qa.k_cache; aa.v_cache = qa.v_cache; aa.pos = state_ + S_POS;
+  aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
+  aa.scale = 1.f / std::sqrt((float)hd);
+  aa.part = attn_part_; aa.out = attn_;
+  attn_decode(aa, s);
+
+  GemvArgs o;
+  o.w = L.wo; o.x = attn_; o.n_out = d;
+  if (!tp) {
+    o.out = x_;
+    gemv(o, EPI_ADD, s);
+  } else {
+    o.out = tmp_;
+    o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+    gemv(o, EPI_STORE, s);
+    allreduce_into(tmp_, x_, d, s);
+  }
+
+  if (hp_.n_expert > 0) {
+    GemvArgs ra;
+    ra.w = L.router; ra.x = x_; ra.norm_w = L.ffn_norm; ra.eps = hp_.rms_eps;
+    ra.out = router_logits_; ra.n_out = hp_.n_expert;
+    gemv(ra, EPI_STORE, s);
+    moe_route(router_logits_, hp_.n_expert, hp_.n_expert_used, moe_ids_, moe_w_, s);
+    GemvArgs g;
+    g.w = L.gu_exps; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
+    g.out = hf_; g.n_out = F_l_; g.n_slots = hp_.n_expert_used; g.expert_ids = moe_ids_; g.out_slot_stride = F_l_;
+    gemv(g, EPI_SWIGLU, s);
+    MoeDownArgs md;
+    md.w = L.down_exps; md.h = hf_; md.expert_ids = moe_ids_; md.expert_w = moe_w_; md.n_slots = hp_.n_expert_used;
+    if (!tp) {
+      md.out = x_;
+      gemv_moe_down(md, s);
+    } else {
+      if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * d, hipMemcpyDeviceToDevice, s));
+      else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * d, s));
+      md.out = tmp_;
+      gemv_moe_down(md, s);
+      allreduce_into(tmp_, x_, d, s);
+    }
+  } else {
+    GemvArgs g;
+    g.w = L.w_gu; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
+    g.out = hf_; g.n_out = F_l_;
+    gemv(g, EPI_SWIGLU, s);
+    GemvArgs dn;
+    dn.w = L.w_down; dn.x = hf_; dn.n_out = d;
+    if (!tp) {
+      dn.out = x_;
+      gemv(dn, EPI_ADD, s);
+    } else {
+      dn.out = tmp_;
+      dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+      gemv(dn, EPI_STORE, s);
+      allreduce_into(tmp_, x_, d, s);
+    }
+  }
+}
+
+void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
+  GemvArgs h;
+  h.w = output_; h.x = xrow; h.norm_w = out_norm_; h.eps = hp_.rms_eps;
+  const int rows_real = std::max(0, std::min(V_l_, hp_.n_vocab - opt_.tp_rank * V_l_));
+  h.n_out = rows_real;
+  h.out = opt_.tp_size > 1 ? logits_l_ : logits_;
+  if (h.n_out > 0) gemv(h, EPI_STORE, s);
+  if (opt_.tp_size > 1)
+    ncclchk(ncclAllGather(logits_l_, logits_, V_l_, ncclFloat32, static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
+  SamplerArgs sa;
+  sa.logits = logits_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
+  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.out_tokens = out_tokens_; sa.out_cap = 64;
+  sa.advance_pos = advance_pos;
+  sample(sa, s);
+  HIPCHK(hipMemcpyAsync(h_ring_, out_tokens_, sizeof(int) * 64, hipMemcpyDeviceToHost, s));
+}
+
+void Engine::enqueue_decode(hipStream_t s) {
+  embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
+  for (int l = 0; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
+  enqueue_head(x_, 1, s);
+}
+
+void Engine::enqueue_prefill(int T, int pos0, hipStream_t s) {
+  const int d = hp_.n_embd, hd = hp_.head_dim;
+  const bool tp = opt_.tp_size > 1;
+  const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
+  const int ncol = nq_ + 2 * nkvd_;
+  embed_rows(tok_embd_, tokens_, T, x_, s);
+  for (int l = 0; l < hp_.n_layer; ++l) {
+    const Layer& L = layers_[l];
+    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s);
+    GemmArgs g;
+    g.x = xb_; g.T = T; g.ldo = ncol;
+    g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
+    g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
+    g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
+    __half* kcl = kc_ + kv_layer * l;
+    __half* vcl = vc_ + kv_layer * l;
+    rope_kv_prefill(qkv_, T, pos0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s);
+    AttnPrefillArgs pa;
+    pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
+    pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
+    pa.out = attn_; pa.out_stride = nq_;
+    attn_prefill(pa, s);
+    to_bf16(attn_, T * nq_, attnb_, s);
+    GemmArgs o;
+    o.w = L.wo; o.x = attnb_; o.T = T; o.ldo = d;
+    if (!tp) {
+      o.out = x_;
+      gemm_dq(o, GEMM_ADD, s);
+    } else {
+      o.out = tmp_;
+      o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+      gemm_dq(o, GEMM_STORE, s);
+      allreduce_into(tmp_, x_, (size_t)T * d, s);
+    }
+    rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s);
+    if (hp_.n_expert > 0) {
+      const int E = hp_.n_expert;
+      GemmArgs ra;
+      ra.w = L.router; ra.x = xb_; ra.T = T; ra.out = router_logits_; ra.ldo = E;
+      gemm_dq(ra, GEMM_STORE, s);
+      moe_route_dense(router_logits_, T, E, hp_.n_expert_used, route_w_, s);
+      if (tp) {
+        if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * T * d, hipMemcpyDeviceToDevice, s));
+        else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * T * d, s));
+      }
+      float* acc = tp ? tmp_ : x_;
+      for (int e = 0; e < E; ++e) {
+        GemmArgs gu;
+        gu.w = L.gu_exps; gu.w.base += L.gu_exps.expert_stride * e;
+        gu.x = xb_; gu.T = T; gu.out_bf16 = h_;
+        gemm_dq(gu, GEMM_SWIGLU, s);
+        GemmArgs dn;
+        dn.w = L.down_exps; dn.w.base += L.down_exps.expert_stride * e;
+        dn.x = h_; dn.T = T; dn.ldo = d; dn.out = moe_y_;
+        gemm_dq(dn, GEMM_STORE, s);
+        axpy_rows(acc, moe_y_, route_w_, e, E, T, d, s);
+      }
+      if (tp) allreduce_into(tmp_, x_, (size_t)T * d, s);
+    } else {
+      GemmArgs gu;
+      gu.w = L.w_gu; gu.x = xb_; gu.T = T; gu.out_bf16 = h_;
+      gemm_dq(gu, GEMM_SWIGLU, s);
+      GemmArgs dn;
+      dn.w = L.w_down; dn.x = h_; dn.T = T; dn.ldo = d;
+      if (!tp) {
+        dn.out = x_;
+        gemm_dq(dn, GEMM_ADD, s);
+      } else {
+        dn.out = tmp_;
+        dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+        gemm_dq(dn, GEMM_STORE, s);
+        allreduce_into(tmp_, x_, (size_t)T * d, s);
+      }
+    }
+  }
+}
+
+void Engine::launch_step() {
+  if (opt_.use_graph) {
+    if (!graph_exec_) {
+      HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      enqueue_decode(stream_);
+      HIPCHK(hipStreamEndCapture(stream_, &graph_));
+      HIPCHK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+    }
+    HIPCHK(hipGraphLaunch(graph_exec_, stream_));
+  } else {
+    enqueue_decode(stream_);
+  }
+}
+
+// ------------------------------------------------------------------------ generation
+GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
+                        const std::vector<int>& stop_ids, const std::function<bool()>& poll,
+                        const std::function<void(int)>& on_token) {
+  GenOut out;
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  if (sp.top_k < 0 || sp.top_k > 64) throw std::runtime_error("GPU sampler: top_k must be in [0, 64]");
+  const double t0 = now_s();
+
+  // per-request device state: sampling params, penalty ring (prompt tail), counters
+  SamplerParamsDev p;
+  p.greedy = sp.temp <= 0.f ? 1 : 0;
+  p.top_k = p.greedy ? 1 : (sp.top_k == 0 ? 64 : sp.top_k);
+  p.top_p = sp.top_p; p.min_p = sp.min_p; p.temp = sp.temp;
+  p.repeat_penalty = sp.repeat_penalty; p.freq_penalty = sp.freq_penalty; p.presence_penalty = sp.presence_penalty;
+  p.last_n = std::min(sp.last_n, 64);
+  p.seed = sp.seed;
+  int hstate[S_NSTATE] = {0};
+  int hring[64] = {0};
+  const int rl = std::min(n_prompt, 64);
+  for (int i = 0; i < rl; ++i) hring[i] = prompt[n_prompt - rl + i];
+  hstate[S_TOKEN] = prompt.back();
+  hstate[S_POS] = n_prompt;  // position the first generated token will occupy
+  hstate[S_RING_LEN] = rl;
+  hstate[S_RING_HEAD] = rl & 63;
+  HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(ring_, hring, sizeof(hring), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+
+  // prefill in n_batch chunks
+  int pos = n_keep;
+  while (pos < n_prompt) {
+    const int T = std::min(opt_.n_batch, n_prompt - pos);
+    std::memcpy(h_tokens_, prompt.data() + pos, sizeof(int) * T);
+    HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    enqueue_prefill(T, pos, stream_);
+    pos += T;
+    if (pos == n_prompt) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
+    HIPCHK(hipStreamSynchronize(stream_));  // h_tokens_ is reused by the next chunk
+  }
+  HIPCHK(hipGetLastError());
+  const double t1 = now_s();
+  out.prefill_s = t1 - t0;
+  out.n_prefilled = n_prompt - n_keep;
+
+  auto is_stop = [&](int t) {
+    for (int s : stop_ids) if (s == t) return true;
+    return false;
+  };
+  int tok = h_ring_[0];
+  out.tokens.push_back(tok);
+  if (on_token) on_token(tok);
+  out.finish = "length";
+  const int max_steps = std::min(max_new - 1, opt_.n_ctx - n_prompt);
+  if (is_stop(tok)) {
+    out.finish = "stop";
+  } else if (max_steps > 0) {
+    int launched = 0;
+    while (launched < std::min(kDepth, max_steps)) {
+      launch_step();
+      HIPCHK(hipEventRecord(step_ev_[launched % kDepth], stream_));
+      ++launched;
+    }
+    for (int i = 1; i <= max_steps; ++i) {
+      HIPCHK(hipEventSynchronize(step_ev_[(i - 1) % kDepth]));
+      tok = h_ring_[i & 63];
+      out.tokens.push_back(tok);
+      if (on_token) on_token(tok);
+      if (is_stop(tok)) { out.finish = "stop"; break; }
+      if (poll && (i & 3) == 0 && poll()) { out.finish = "cancelled"; break; }
+      if (launched < max_steps) {
+        launch_step();
+        HIPCHK(hipEventRecord(step_ev_[launched % kDepth], stream_));
+        ++launched;
+      }
+    }
+    HIPCHK(hipStreamSynchronize(stream_));
+  }
+  HIPCHK(hipGetLastError());
+  out.decode_s = now_s() - t1;
+  out.n_evaluated = n_prompt + (int)out.tokens.size() - 1;
+  return out;
+}
+
+std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0) {
+  const int T = (int)tokens.size();
+  if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_logits: bad size");
+  SamplerParamsDev p;
+  p.greedy = 1; p.top_k = 1; p.repeat_penalty = 1.f;
+  int hstate[S_NSTATE] = {0};
+  hstate[S_POS] = pos0 + T;
+  HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+  std::memcpy(h_tokens_, tokens.data(), sizeof(int) * T);
+  HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+  enqueue_prefill(T, pos0, stream_);
+  enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
+  std::vector<float> out(hp_.n_vocab);
+  HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+std::vector<float> Engine::decode_logits(int token, int pos) {
+  if (pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
+  SamplerParamsDev p;
+  p.greedy = 1; p.top_k = 1; p.repeat_penalty = 1.f;
+  int hstate[S_NSTATE] = {0};
+  hstate[S_TOKEN] = token;
+  hstate[S_POS] = pos;
+  HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+  launch_step();
+  std::vector<float> out(hp_.n_vocab);
+  HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+void Engine::bench_decode(int n_steps, int pos0, double* ms_per_step) {
+  if (n_steps < 1 || pos0 + n_steps + 1 > opt_.n_ctx) throw std::runtime_error("bench_decode: exceeds n_ctx");
+  SamplerParamsDev p;
+  p.greedy = 1; p.top_k = 1;
+  int hstate[S_NSTATE] = {0};
+  hstate[S_TOKEN] = 1;
+  hstate[S_POS] = pos0;
+  HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+  launch_step();  // warm (captures the graph on first use)
+  HIPCHK(hipStreamSynchronize(stream_));
+  const double t0 = now_s();
+  for (int i = 0; i < n_steps; ++i) launch_step();
+  HIPCHK(hipStreamSynchronize(stream_));
+  *ms_per_step = (now_s() - t0) * 1e3 / n_steps;
+}
+
+}  // namespace lfk

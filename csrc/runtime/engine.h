@@ -1,0 +1,163 @@
+// MI355X inference engine: owns the device weights, KV cache,
+// workspaces and RCCL communicator of ONE rank, and runs prefill / decode /
+// sampling as a fixed kernel schedule (no graph IR, no allocator at run time).
+//
+// One process drives one GPU. Tensor parallelism (split_mode=row, the
+// `tensor_split` path of the reference) shards heads and FFN
+// features across ranks; each rank runs the same schedule with two RCCL
+// all-reduces per layer and one all-gather of vocabulary-sharded logits.
+// The decode step (embedding -> layers -> lm_head -> sampler -> token D2H) is
+// captured once into a hipGraph and replayed per token.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.h"
+#include "gguf.h"
+
+namespace lfk {
+
+struct HParams {
+  int n_vocab = 0, n_embd = 0, n_layer = 0, n_head = 0, n_head_kv = 0, head_dim = 0, n_ff = 0;
+  int n_expert = 0, n_expert_used = 0, n_ctx_train = 0;
+  float rope_base = 10000.f, rms_eps = 1e-5f;
+};
+HParams read_hparams(const GGUFFile& f);
+
+struct EngineOptions {
+  int n_ctx = 1024;
+  int n_batch = 512;
+  int device = 0;
+  bool use_graph = true;
+  int tp_rank = 0;
+  int tp_size = 1;
+  std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1)
+  bool verbose = false;
+};
+
+struct SamplingOpts {
+  int top_k = 40;
+  float top_p = 0.95f, min_p = 0.05f, temp = 0.8f;
+  float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
+  int last_n = 64;
+  unsigned long long seed = 0;
+};
+
+struct GenOut {
+  std::vector<int> tokens;
+  std::string finish;
+  int n_evaluated = 0;
+  int n_prefilled = 0;
+  double prefill_s = 0, decode_s = 0;
+};
+
+struct Layer {
+  float* attn_norm = nullptr;
+  float* ffn_norm = nullptr;
+  QMat wq, wk, wv, wo;
+  QMat w_gu, w_down;                 // dense FFN (gate/up interleaved in 32-row groups)
+  QMat router, gu_exps, down_exps;   // MoE
+};
+
+class Engine {
+ public:
+  Engine(const std::string& path, const EngineOptions& opts);
+  ~Engine();
+  Engine(const Engine&) = delete;
+  Engine& operator=(const Engine&) = delete;
+
+  GenOut generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
+                  const std::vector<int>& stop_ids, const std::function<bool()>& poll,
+                  const std::function<void(int)>& on_token);
+  // test hooks (numerics vs the reference model)
+  std::vector<float> eval_logits(const std::vector<int>& tokens, int pos0);  // prefill path
+  std::vector<float> decode_logits(int token, int pos);                      // decode path (eager)
+  void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing
+
+  const HParams& hparams() const { return hp_; }
+  size_t device_bytes() const { return dev_bytes_; }
+  int tp_rank() const { return opt_.tp_rank; }
+  int tp_size() const { return opt_.tp_size; }
+  bool healthy() const { return healthy_; }
+  std::string last_error() const { return last_error_; }
+  int n_ctx() const { return opt_.n_ctx; }
+
+ private:
+  void* dalloc(size_t bytes);
+  QMat upload_matrix(const GGUFFile& f, const std::string& name, size_t r0, size_t R, size_t c0, size_t K,
+                     int n_expert = 0);
+  QMat upload_gate_up(const GGUFFile& f, const std::string& gate, const std::string& up, size_t f0, size_t F,
+                      int n_expert = 0);
+  float* upload_f32(const GGUFFile& f, const std::string& name);
+  void load(const GGUFFile& f);
+  void alloc_buffers();
+  void build_rope();
+
+  void allreduce_into(const float* send, float* recv, size_t n, hipStream_t s);
+  void enqueue_layer_decode(int l, hipStream_t s);
+  void enqueue_decode(hipStream_t s);
+  void enqueue_prefill(int T, int pos0, hipStream_t s);
+  void enqueue_head(const float* xrow, int advance_pos, hipStream_t s);
+  void launch_step();
+  void check(hipError_t e, const char* what);
+
+  HParams hp_;
+  EngineOptions opt_;
+  hipStream_t stream_ = nullptr;
+  void* comm_ = nullptr;  // ncclComm_t
+  std::vector<void*> allocs_;
+  size_t dev_bytes_ = 0;
+  bool healthy_ = true;
+  std::string last_error_;
+
+  // local (per-rank) sizes
+  int nh_l_ = 0, nkv_l_ = 0, nq_ = 0, nkvd_ = 0, F_l_ = 0, V_l_ = 0, V_pad_ = 0;
+
+  // weights
+  QMat tok_embd_, output_;
+  float* out_norm_ = nullptr;
+  std::vector<Layer> layers_;
+
+  // buffers
+  float* x_ = nullptr;        // [n_batch][d]
+  float* tmp_ = nullptr;      // [n_batch][d]  (TP partial / MoE expert output)
+  __hip_bfloat16* xb_ = nullptr;    // [n_batch][d]
+  float* qkv_ = nullptr;      // [n_batch][nq + 2 nkvd]
+  float* q_ = nullptr;        // [n_batch][nq]
+  float* attn_ = nullptr;     // [n_batch][nq]
+  __hip_bfloat16* attnb_ = nullptr; // [n_batch][nq]
+  __hip_bfloat16* h_ = nullptr;     // [n_batch][F_l]
+  float* hf_ = nullptr;       // [n_expert_used or 1][F_l]
+  float* logits_ = nullptr;   // [V_pad]
+  float* logits_l_ = nullptr; // [V_l]
+  __half* kc_ = nullptr;      // [n_layer][nkv_l][n_ctx][hd]
+  __half* vc_ = nullptr;
+  float2* rope_ = nullptr;
+  float* attn_part_ = nullptr;
+  float* cand_val_ = nullptr;
+  int* cand_idx_ = nullptr;
+  int* state_ = nullptr;
+  int* ring_ = nullptr;
+  int* out_tokens_ = nullptr;
+  int* tokens_ = nullptr;     // [n_batch]
+  SamplerParamsDev* sparams_ = nullptr;
+  float* router_logits_ = nullptr;  // [n_batch][E]
+  float* route_w_ = nullptr;        // [n_batch][E] dense routing weights (prefill)
+  float* moe_y_ = nullptr;          // [n_batch][d] one expert's output (prefill)
+  int* moe_ids_ = nullptr;
+  float* moe_w_ = nullptr;
+  int* h_ring_ = nullptr;     // pinned [64]
+  int* h_tokens_ = nullptr;   // pinned [n_batch]
+
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr;
+  static constexpr int kDepth = 2;
+  hipEvent_t step_ev_[kDepth] = {};
+};
+
+}  // namespace lfk

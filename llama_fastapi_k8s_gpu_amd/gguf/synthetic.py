@@ -112,8 +112,10 @@ def tensor_types(spec: ModelSpec, layer: int) -> Dict[str, GGMLType]:
         return {k: t for k in ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down")}
     if q == "mixed-test":  # every quant format in one model, to test all kernels end to end
         cyc = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0]
-        names = ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down")
-        return {k: cyc[(layer + j) % 4] for j, k in enumerate(names)}
+        names = ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_down")
+        out = {k: cyc[(layer + j) % 4] for j, k in enumerate(names)}
+        out["ffn_up"] = out["ffn_gate"]  # gate/up are one interleaved matrix on the GPU
+        return out
     assert q == "q4_k_m"
     n = spec.n_layer
     bump = use_more_bits(layer, n)

@@ -1,1 +1,39 @@
+"""Native runtime bindings.
 
+``load_hip()`` / ``load_cpu()`` import the in-tree extensions built by
+``runtime/build.py``. They fail loudly when the extension is missing instead of
+silently falling back to Python (a GPU test that passes on a fallback would be
+measuring the wrong code).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+
+_MODS = {}
+
+
+def _load(name: str, builder: str):
+    if name in _MODS:
+        return _MODS[name]
+    try:
+        mod = importlib.import_module(f"{__name__}.{name}")
+    except ImportError as e:
+        if os.environ.get("LFK_AUTOBUILD", "1") != "0":
+            from . import build
+            getattr(build, builder)(verbose=False)
+            importlib.invalidate_caches()
+            mod = importlib.import_module(f"{__name__}.{name}")
+        else:
+            raise ImportError(f"native extension {name} is not built: run "
+                              f"`python -m llama_fastapi_k8s_gpu_amd.runtime.build` ({e})") from e
+    _MODS[name] = mod
+    return mod
+
+
+def load_hip():
+    return _load("_hip", "build_hip")
+
+
+def load_cpu():
+    return _load("_cpu", "build_cpu")

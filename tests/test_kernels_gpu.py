@@ -1,0 +1,334 @@
+"""T3 - every gfx950 kernel against a plain PyTorch/NumPy fp32 reference of the
+same op (shape sweeps include non-multiple-of-tile edges)."""
+import numpy as np
+import pytest
+
+from llama_fastapi_k8s_gpu_amd.gguf.constants import GGMLType
+from gpu_helpers import dev_bytes, hip, make_matrix, q8_emulate, rel_err, rmsnorm, stream, to_planar
+
+pytestmark = pytest.mark.gpu
+
+QTYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.F16, GGMLType.F32]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("t", QTYPES)
+@pytest.mark.parametrize("R,K", [(64, 256), (130, 4096), (33, 1024), (96, 14336)])
+def test_gemv_types(torch, t, R, K):
+    rng = np.random.default_rng(R * K + int(t))
+    raw, W = make_matrix(t, R, K, rng)
+    x = rng.standard_normal(K).astype(np.float32)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    dx = torch.from_numpy(x).cuda()
+    out = torch.zeros(R, device="cuda")
+    hip().gemv(dw.data_ptr(), int(t), R, K, dx.data_ptr(), 0, 1e-5, out.data_ptr(), R, 0, stream())
+    torch.cuda.synchronize()
+    ref_q8 = W.astype(np.float64) @ q8_emulate(x).astype(np.float64)
+    assert rel_err(out.cpu().numpy(), ref_q8) < 2e-4
+    ref = W.astype(np.float64) @ x.astype(np.float64)
+    assert rel_err(out.cpu().numpy(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_gemv_norm_add_and_resid(torch, t):
+    rng = np.random.default_rng(7)
+    R, K = 256, 4096
+    raw, W = make_matrix(t, R, K, rng)
+    x = rng.standard_normal(K).astype(np.float32) * 3
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(np.float32)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    dx, dn = torch.from_numpy(x).cuda(), torch.from_numpy(nw).cuda()
+    y0 = rng.standard_normal(R).astype(np.float32)
+    out = torch.from_numpy(y0.copy()).cuda()
+    hip().gemv(dw.data_ptr(), int(t), R, K, dx.data_ptr(), dn.data_ptr(), 1e-5, out.data_ptr(), R, 1, stream())
+    torch.cuda.synchronize()
+    ref = y0 + W @ q8_emulate(rmsnorm(x, nw))
+    assert rel_err(out.cpu().numpy() - y0, ref - y0) < 1e-3
+    # EPI_STORE with a residual vector
+    res = torch.from_numpy(y0.copy()).cuda()
+    out2 = torch.zeros(R, device="cuda")
+    hip().gemv(dw.data_ptr(), int(t), R, K, dx.data_ptr(), dn.data_ptr(), 1e-5, out2.data_ptr(), R, 0, stream(),
+               resid=res.data_ptr())
+    torch.cuda.synchronize()
+    assert rel_err(out2.cpu().numpy() - y0, ref - y0) < 1e-3
+
+
+def test_gemv_swiglu_interleaved(torch):
+    rng = np.random.default_rng(8)
+    F, K = 96, 512
+    t = GGMLType.Q4_K
+    rg, Wg = make_matrix(t, F, K, rng)
+    ru, Wu = make_matrix(t, F, K, rng)
+    pg = to_planar(t, rg, F, K, R_dst=2 * F, G=32, off=0)
+    pu = to_planar(t, ru, F, K, R_dst=2 * F, G=32, off=32)
+    planar = pg | pu  # disjoint rows; the rest is zero in each
+    dw = dev_bytes(planar)
+    x = rng.standard_normal(K).astype(np.float32)
+    dx = torch.from_numpy(x).cuda()
+    out = torch.zeros(F, device="cuda")
+    hip().gemv(dw.data_ptr(), int(t), 2 * F, K, dx.data_ptr(), 0, 1e-5, out.data_ptr(), F, 2, stream())
+    torch.cuda.synchronize()
+    xq = q8_emulate(x)
+    g, u = Wg @ xq, Wu @ xq
+    ref = g / (1 + np.exp(-g)) * u
+    assert rel_err(out.cpu().numpy(), ref) < 1e-3
+
+
+def test_gemv_moe_slots_and_down(torch):
+    rng = np.random.default_rng(9)
+    E, F, K, d = 4, 256, 256, 128
+    t = GGMLType.Q4_K
+    mats = [(make_matrix(t, F, K, rng), make_matrix(t, F, K, rng)) for _ in range(E)]
+    planar = []
+    for (rg, Wg), (ru, Wu) in mats:
+        planar.append(to_planar(t, rg, F, K, R_dst=2 * F, G=32, off=0) | to_planar(t, ru, F, K, R_dst=2 * F, G=32, off=32))
+    stride = planar[0].size
+    dw = dev_bytes(np.concatenate(planar))
+    x = rng.standard_normal(K).astype(np.float32)
+    dx = torch.from_numpy(x).cuda()
+    ids = torch.tensor([3, 1], dtype=torch.int32, device="cuda")
+    out = torch.zeros(2, F, device="cuda")
+    hip().gemv(dw.data_ptr(), int(t), 2 * F, K, dx.data_ptr(), 0, 1e-5, out.data_ptr(), F, 2, stream(),
+               n_slots=2, ids=ids.data_ptr(), expert_stride=stride, slot_stride=F)
+    torch.cuda.synchronize()
+    xq = q8_emulate(x)
+    for s, e in enumerate([3, 1]):
+        g, u = mats[e][0][1] @ xq, mats[e][1][1] @ xq
+        assert rel_err(out[s].cpu().numpy(), g / (1 + np.exp(-g)) * u) < 1e-3
+    # down projection, weighted over the two slots
+    downs = [make_matrix(t, d, F, rng) for _ in range(E)]
+    dd = dev_bytes(np.concatenate([to_planar(t, r, d, F) for r, _ in downs]))
+    h = rng.standard_normal((2, F)).astype(np.float32)
+    dh = torch.from_numpy(h).cuda()
+    wts = torch.tensor([0.7, 0.3], device="cuda")
+    y = torch.ones(d, device="cuda")
+    hip().moe_down(dd.data_ptr(), int(t), d, F, to_planar(t, downs[0][0], d, F).size, dh.data_ptr(), ids.data_ptr(),
+                   wts.data_ptr(), 2, y.data_ptr(), stream())
+    torch.cuda.synchronize()
+    ref = 1 + 0.7 * downs[3][1] @ q8_emulate(h[0]) + 0.3 * downs[1][1] @ q8_emulate(h[1])
+    assert rel_err(y.cpu().numpy() - 1, ref - 1) < 1e-3
+
+
+def test_moe_route(torch):
+    logits = torch.tensor([0.1, 2.0, -1.0, 1.5, 0.3, 0.0, -2.0, 1.9], device="cuda")
+    ids = torch.zeros(2, dtype=torch.int32, device="cuda")
+    w = torch.zeros(2, device="cuda")
+    hip().moe_route(logits.data_ptr(), 8, 2, ids.data_ptr(), w.data_ptr(), stream())
+    torch.cuda.synchronize()
+    assert ids.tolist() == [1, 7]
+    p = torch.softmax(logits.cpu(), 0)
+    np.testing.assert_allclose(w.cpu().numpy(), (p[[1, 7]] / p[[1, 7]].sum()).numpy(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("tq,tk,tv", [(GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q6_K),
+                                      (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0)])
+def test_gemv_qkv_rope_kvstore(torch, tq, tk, tv):
+    rng = np.random.default_rng(10)
+    K, hd, nh, nkv, n_ctx, pos = 512, 64, 8, 2, 32, 5
+    (rq, Wq), (rk, Wk), (rv, Wv) = make_matrix(tq, nh * hd, K, rng), make_matrix(tk, nkv * hd, K, rng), \
+        make_matrix(tv, nkv * hd, K, rng)
+    dq, dk, dv = (dev_bytes(to_planar(t, r, R, K)) for t, r, R in ((tq, rq, nh * hd), (tk, rk, nkv * hd), (tv, rv, nkv * hd)))
+    x = rng.standard_normal(K).astype(np.float32)
+    nw = np.ones(K, np.float32)
+    dx, dn = torch.from_numpy(x).cuda(), torch.from_numpy(nw).cuda()
+    qo = torch.zeros(nh * hd, device="cuda")
+    kc = torch.zeros(nkv, n_ctx, hd, dtype=torch.float16, device="cuda")
+    vc = torch.zeros_like(kc)
+    dpos = torch.tensor([pos], dtype=torch.int32, device="cuda")
+    inv = 10000.0 ** (-2 * np.arange(hd // 2) / hd)
+    ang = np.arange(n_ctx)[:, None] * inv[None]
+    rope = torch.from_numpy(np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)).cuda()
+    hip().gemv_qkv(dq.data_ptr(), int(tq), dk.data_ptr(), int(tk), dv.data_ptr(), int(tv), nh * hd, nkv * hd, K,
+                   dx.data_ptr(), dn.data_ptr(), 1e-5, qo.data_ptr(), kc.data_ptr(), vc.data_ptr(), n_ctx, hd,
+                   dpos.data_ptr(), rope.data_ptr(), stream())
+    torch.cuda.synchronize()
+    xq = q8_emulate(rmsnorm(x, nw))
+
+    def rot(v):
+        v = v.reshape(-1, hd)
+        c, s = np.cos(ang[pos]), np.sin(ang[pos])
+        o = v.copy()
+        o[:, 0::2] = v[:, 0::2] * c - v[:, 1::2] * s
+        o[:, 1::2] = v[:, 0::2] * s + v[:, 1::2] * c
+        return o
+    assert rel_err(qo.cpu().numpy().reshape(nh, hd), rot(Wq @ xq)) < 1e-3
+    assert rel_err(kc[:, pos].float().cpu().numpy(), rot(Wk @ xq)) < 2e-3
+    assert rel_err(vc[:, pos].float().cpu().numpy(), (Wv @ xq).reshape(nkv, hd)) < 2e-3
+    assert float(kc[:, pos + 1].abs().sum()) == 0.0
+
+
+def _attn_ref(q, K, V, L, scale):
+    # q [H, D], K/V [Hkv, L, D]
+    H, D = q.shape
+    G = H // K.shape[0]
+    out = np.zeros((H, D))
+    for h in range(H):
+        k = K[h // G, :L].astype(np.float64)
+        s = k @ q[h].astype(np.float64) * scale
+        p = np.exp(s - s.max())
+        p /= p.sum()
+        out[h] = p @ V[h // G, :L].astype(np.float64)
+    return out
+
+
+@pytest.mark.parametrize("hd,H,Hkv", [(128, 32, 8), (64, 32, 4)])
+@pytest.mark.parametrize("L", [1, 31, 64, 65, 1000])
+def test_attn_decode(torch, hd, H, Hkv, L):
+    rng = np.random.default_rng(L + hd)
+    n_ctx = 1024
+    q = rng.standard_normal((H, hd)).astype(np.float32)
+    K = rng.standard_normal((Hkv, n_ctx, hd)).astype(np.float16)
+    V = rng.standard_normal((Hkv, n_ctx, hd)).astype(np.float16)
+    dq = torch.from_numpy(q).cuda()
+    dK, dV = torch.from_numpy(K).cuda(), torch.from_numpy(V).cuda()
+    pos = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
+    ws = torch.zeros(hip().attn_decode_workspace_floats(n_ctx, H, hd), device="cuda")
+    out = torch.zeros(H, hd, device="cuda")
+    scale = 1 / np.sqrt(hd)
+    hip().attn_decode(dq.data_ptr(), dK.data_ptr(), dV.data_ptr(), pos.data_ptr(), n_ctx, H, Hkv, hd, scale,
+                      ws.data_ptr(), out.data_ptr(), stream())
+    torch.cuda.synchronize()
+    assert rel_err(out.cpu().numpy(), _attn_ref(q, K, V, L, scale)) < 1e-4
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+@pytest.mark.parametrize("T,pos0", [(1, 0), (17, 0), (40, 23)])
+def test_attn_prefill(torch, hd, T, pos0):
+    rng = np.random.default_rng(T + pos0)
+    H, Hkv, n_ctx = 8, 2, 128
+    q = rng.standard_normal((T, H, hd)).astype(np.float32)
+    K = rng.standard_normal((Hkv, n_ctx, hd)).astype(np.float16)
+    V = rng.standard_normal((Hkv, n_ctx, hd)).astype(np.float16)
+    out = torch.zeros(T, H, hd, device="cuda")
+    scale = 1 / np.sqrt(hd)
+    dq, dK, dV = (torch.from_numpy(a).cuda() for a in (q, K, V))  # keep the device copies alive
+    hip().attn_prefill(dq.data_ptr(), dK.data_ptr(), dV.data_ptr(), T, pos0, n_ctx, H, Hkv, hd, scale,
+                       out.data_ptr(), stream())
+    torch.cuda.synchronize()
+    ref = np.stack([_attn_ref(q[t], K, V, pos0 + t + 1, scale) for t in range(T)])
+    assert rel_err(out.cpu().numpy(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("t", QTYPES)
+@pytest.mark.parametrize("T,N,K", [(1, 128, 256), (33, 256, 512), (130, 384, 1024)])
+def test_gemm_mfma(torch, t, T, N, K):
+    rng = np.random.default_rng(T * N + int(t))
+    raw, W = make_matrix(t, N, K, rng)
+    dw = dev_bytes(to_planar(t, raw, N, K))
+    x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
+    out = torch.zeros(T, N, device="cuda")
+    hip().gemm(dw.data_ptr(), int(t), N, K, x.data_ptr(), T, out.data_ptr(), 0, N, 0, stream())
+    torch.cuda.synchronize()
+    Wb = torch.from_numpy(W).to(torch.bfloat16).float()  # the kernel stages weights as bf16
+    ref = x.float().cpu() @ Wb.T
+    assert rel_err(out.cpu().numpy(), ref.numpy()) < 5e-3
+    # residual-add epilogue
+    base = torch.randn(T, N, device="cuda")
+    acc = base.clone()
+    hip().gemm(dw.data_ptr(), int(t), N, K, x.data_ptr(), T, acc.data_ptr(), 0, N, 1, stream())
+    torch.cuda.synchronize()
+    assert rel_err((acc - base).cpu().numpy(), ref.numpy()) < 5e-3
+
+
+def test_gemm_swiglu(torch):
+    rng = np.random.default_rng(11)
+    F, K, T = 128, 512, 70
+    t = GGMLType.Q4_K
+    rg, Wg = make_matrix(t, F, K, rng)
+    ru, Wu = make_matrix(t, F, K, rng)
+    planar = to_planar(t, rg, F, K, R_dst=2 * F, G=32, off=0) | to_planar(t, ru, F, K, R_dst=2 * F, G=32, off=32)
+    dw = dev_bytes(planar)
+    x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
+    h = torch.zeros(T, F, dtype=torch.bfloat16, device="cuda")
+    hip().gemm(dw.data_ptr(), int(t), 2 * F, K, x.data_ptr(), T, 0, h.data_ptr(), 0, 2, stream())
+    torch.cuda.synchronize()
+    xf = x.float().cpu().numpy()
+    g = xf @ torch.from_numpy(Wg).to(torch.bfloat16).float().numpy().T
+    u = xf @ torch.from_numpy(Wu).to(torch.bfloat16).float().numpy().T
+    ref = g / (1 + np.exp(-g)) * u
+    assert rel_err(h.float().cpu().numpy(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("t", QTYPES)
+def test_embed(torch, t):
+    rng = np.random.default_rng(12)
+    V, d = 300, 256
+    raw, W = make_matrix(t, V, d, rng)
+    dw = dev_bytes(to_planar(t, raw, V, d))
+    toks = torch.tensor([0, 5, 299, 17], dtype=torch.int32, device="cuda")
+    x = torch.zeros(4, d, device="cuda")
+    hip().embed(dw.data_ptr(), int(t), V, d, toks.data_ptr(), 4, x.data_ptr(), stream())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(x.cpu().numpy(), W[[0, 5, 299, 17]], rtol=1e-5, atol=1e-6)
+
+
+def test_rmsnorm_bf16(torch):
+    x = torch.randn(5, 4096, device="cuda")
+    w = torch.rand(4096, device="cuda") + 0.5
+    y = torch.zeros(5, 4096, dtype=torch.bfloat16, device="cuda")
+    hip().rmsnorm_bf16(x.data_ptr(), w.data_ptr(), 1e-5, 5, 4096, y.data_ptr(), stream())
+    torch.cuda.synchronize()
+    ref = x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-5) * w
+    assert rel_err(y.float().cpu().numpy(), ref.cpu().numpy()) < 5e-3
+
+
+def _run_sampler(torch, logits, ring_tokens, params, seed, step=0):
+    h = hip()
+    V = logits.shape[0]
+    dl = torch.from_numpy(logits).cuda()
+    pb = np.frombuffer(h.sampler_params_bytes(params.top_k, params.top_p, params.min_p, params.temperature,
+                                              params.repeat_penalty, params.frequency_penalty,
+                                              params.presence_penalty, params.last_n, seed,
+                                              int(params.temperature <= 0)), np.uint8)
+    dp = torch.from_numpy(pb.copy()).cuda()
+    ring = np.zeros(64, np.int32)
+    rl = min(len(ring_tokens), 64)
+    ring[:rl] = ring_tokens[-rl:] if rl else []
+    state = np.zeros(8, np.int32)
+    state[2] = step
+    state[3] = rl
+    state[4] = rl & 63
+    dr, ds = torch.from_numpy(ring).cuda(), torch.from_numpy(state).cuda()
+    nb = h.sampler_blocks(V)
+    cv = torch.zeros(nb * 64, device="cuda")
+    ci = torch.zeros(nb * 64, dtype=torch.int32, device="cuda")
+    h.sample(dl.data_ptr(), V, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), cv.data_ptr(), ci.data_ptr(), 0, 0, 1,
+             stream())
+    torch.cuda.synchronize()
+    return int(ds[0].item()), ds.cpu().numpy()
+
+
+def test_sampler_greedy_with_penalties(torch):
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams, apply_penalties
+    rng = np.random.default_rng(13)
+    logits = rng.standard_normal(128256).astype(np.float32) * 4
+    top = int(np.argmax(logits))
+    p = SamplingParams(temperature=0.0, top_k=1, repeat_penalty=1.5, frequency_penalty=2.0, presence_penalty=1.0)
+    tok, st = _run_sampler(torch, logits, [top, top, 7], p, 0)
+    assert tok == int(np.argmax(apply_penalties(logits, [top, top, 7], p)))
+    assert st[1] == 1 and st[2] == 1  # pos and step advanced
+
+
+def test_sampler_matches_host_chain(torch):
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams, filtered_candidates, sample_token
+    rng = np.random.default_rng(14)
+    agree = 0
+    n = 40
+    for i in range(n):
+        V = [32000, 128256, 1000][i % 3]
+        logits = (rng.standard_normal(V) * 3).astype(np.float32)
+        hist = list(rng.integers(0, V, 80))
+        p = SamplingParams(temperature=1.2, top_k=40, top_p=0.9, min_p=0.05, repeat_penalty=1.1,
+                           frequency_penalty=0.7, presence_penalty=0.8, seed=1000 + i)
+        tok, _ = _run_sampler(torch, logits, hist, p, p.seed, step=i)
+        ids, _ = filtered_candidates(logits, hist[-64:], p)
+        assert tok in set(ids.tolist())
+        agree += tok == sample_token(logits, hist[-64:], p, i)
+    assert agree >= n - 2

@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: kernel numerics, engine tests, smoke, raw decode timing.
+# Test failures (exit 1) do not stop the session; a crash/abort/timeout does.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name" >&2
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" >&2
+  tail -5 "gpurun_out/$name.log" >&2
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc" >&2; exit $rc; fi
+  return 0
+}
+for s in "$@"; do
+  case $s in
+    kern) step kern 900 python -m pytest tests/test_kernels_gpu.py -q -p no:cacheprovider ;;
+    eng) step eng 900 python -m pytest tests/test_engine_gpu.py -q -p no:cacheprovider ;;
+    gputests) step gputests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) step smoke 300 python __graft_entry__.py smoke ;;
+    decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
+    bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
+    prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o decode \
+            --output-format csv -- python3 tools/decode_bench.py --steps 64 --no-graph ;;
+  esac
+done
