@@ -198,8 +198,9 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
-                          int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream) {
+                          int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters) {
     AttnDecodeArgs a;
+    a.counters = P<int>(counters);
     a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.pos = P<int>(pos);
     a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
     a.part = P<float>(part); a.out = P<float>(out);
@@ -226,8 +227,9 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("sampler_blocks", &sampler_blocks);
   m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cv,
-                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream) {
+                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream, uintptr_t ct) {
     SamplerArgs a;
+    a.cand_tau = P<unsigned>(ct);
     a.logits = P<float>(logits); a.V = V; a.p = P<SamplerParamsDev>(params); a.ring = P<int>(ring);
     a.state = P<int>(state); a.cand_val = P<float>(cv); a.cand_idx = P<int>(ci); a.out_tokens = P<int>(out_tokens);
     a.out_cap = out_cap; a.advance_pos = advance;

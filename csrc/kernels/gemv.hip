@@ -59,76 +59,129 @@ __device__ __forceinline__ void quantize_x(const float* __restrict__ x, const fl
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+// NR rows of one matrix against the LDS-resident q8 x, K-slice `ks` of `wk`
+// (chunks ks*64 + lane + 64*wk*j). Loads for two passes of all NR rows are
+// issued before any math (2*NR independent 16-B loads per lane in flight);
+// out-of-range chunks are clamped (loaded, then ignored).
 template <int QT, int NR>
-__device__ __forceinline__ void dot_rows(const uint8_t* base, const Planes& P, const size_t (&rows)[NR], int nchunks,
-                                         const int8_t* xq, const float* xd, float (&acc)[NR], int lane) {
-#pragma unroll 2
-  for (int c = lane; c < nchunks; c += 64) {
-    XChunk X;
-    load_x<QT>(X, xq, xd, c);
+__device__ __forceinline__ void load_pair(WRaw<QT> (&w)[2][NR], const RowPtr (&R)[NR], int c0, int step, int nchunks,
+                                          int lane) {
 #pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] += chunk_dot<QT>(base, P, rows[r], c, X);
+  for (int u = 0; u < 2; ++u) {
+    const int c = min(c0 + step * u + lane, nchunks - 1);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wload<QT>(w[u][r], R[r], c);
+  }
+}
+
+template <int QT, int NR>
+__device__ __forceinline__ void dot_pair(const WRaw<QT> (&w)[2][NR], int c0, int step, int nchunks, const int8_t* xq,
+                                         const float* xd, float (&acc)[NR], int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = c0 + step * u + lane;
+    if (c < nchunks) {
+      XChunk X;
+      load_x<QT>(X, xq, xd, c);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[r] += wdot<QT>(w[u][r], X, c);
+    }
+  }
+}
+
+template <int QT, int NR>
+__device__ __forceinline__ void dot_rows(const RowPtr (&R)[NR], int nchunks, const int8_t* xq, const float* xd,
+                                         float (&acc)[NR], int lane) {
+  for (int c0 = 0; c0 < nchunks; c0 += 128) {
+    WRaw<QT> w[2][NR];
+    load_pair<QT, NR>(w, R, c0, 64, nchunks, lane);
+    dot_pair<QT, NR>(w, c0, 64, nchunks, xq, xd, acc, lane);
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r) acc[r] = wave_sum(acc[r]);
 }
 
-template <int QT, int EPI, int NR>
-__device__ void gemv_body(const GemvArgs& a, const int8_t* xq, const float* xd) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nchunks = a.w.K >> 5;
-  const int groups = (a.n_out + NR - 1) / NR;
-  const int total = groups * a.n_slots;
-  constexpr int NROW = (EPI == EPI_SWIGLU) ? 2 * NR : NR;
-  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
-    const int slot = item / groups;
-    const int g = item - slot * groups;
-    const uint8_t* base = a.w.base;
-    if (a.expert_ids) base += (size_t)a.expert_ids[slot] * a.w.expert_stride;
-    size_t rows[NROW];
-    const int f0 = g * NR;
+// rows per wave-item: enough independent loads in flight without dropping below
+// 2 waves/SIMD (Q6_K carries 4 loads per chunk, F16/F32 8)
+template <int QT>
+constexpr int rows_per_item() { return (QT == T_Q4_K || QT == T_Q8_0 || QT == T_Q5_K) ? 4 : 2; }
+
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+// pick acc[lane] for lanes < NR (every lane holds every reduced row)
+template <int NR>
+__device__ __forceinline__ float pick(const float (&acc)[NR], int lane) {
+  float v = acc[0];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if constexpr (EPI == EPI_SWIGLU) {
-        const int f = f0 + r;
-        rows[r] = (size_t)((f >> 5) * 64 + (f & 31));
-        rows[NR + r] = rows[r] + 32;
-      } else {
-        rows[r] = (size_t)min(f0 + r, a.n_out - 1);
-      }
-    }
-    float acc[NROW];
+  for (int r = 1; r < NR; ++r) v = lane == r ? acc[r] : v;
+  return v;
+}
+
+// K split over `wk` waves of the block (wk = 1, 2 or 4, chosen on the host so
+// every wave has >= one full 64-chunk pass): a block holds 4/wk row groups;
+// the wk partial sums of a group meet in LDS.
+template <int EPI, int NR>
+__device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups, RowPtr (&R)[NR], int& slot, int& f0) {
+  constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
+  slot = it / groups;
+  f0 = (it - slot * groups) * NF;
+  const uint8_t* base = a.w.base;
+  if (a.expert_ids) base += (size_t)a.expert_ids[slot] * a.w.expert_stride;
 #pragma unroll
-    for (int r = 0; r < NROW; ++r) acc[r] = 0.f;
-    dot_rows<QT, NROW>(base, a.w.P, rows, nchunks, xq, xd, acc, lane);
-    if (lane < NR && f0 + lane < a.n_out) {
-      float v = acc[0];
-#pragma unroll
-      for (int r = 1; r < NR; ++r) if (lane == r) v = acc[r];
-      float* o = a.out + (size_t)slot * a.out_slot_stride + f0 + lane;
-      if constexpr (EPI == EPI_STORE) {
-        *o = a.resid ? v + a.resid[f0 + lane] : v;
-      } else if constexpr (EPI == EPI_ADD) {
-        *o += v;
-      } else {
-        float u = acc[NR];
-#pragma unroll
-        for (int r = 1; r < NR; ++r) if (lane == r) u = acc[NR + r];
-        *o = silu(v) * u;
-      }
+  for (int r = 0; r < NF; ++r) {
+    if constexpr (EPI == EPI_SWIGLU) {
+      const int f = f0 + r;
+      const unsigned gr = (unsigned)((f >> 5) * 64 + (f & 31));
+      R[r] = row_ptr(base, a.w.P, gr);
+      R[NF + r] = row_ptr(base, a.w.P, gr + 32);
+    } else {
+      R[r] = row_ptr(base, a.w.P, (unsigned)min(f0 + r, a.n_out - 1));
     }
   }
 }
 
-template <int EPI, int NR, bool NORM>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
+// One wave = one row group of NR rows (NF outputs); 4 waves per block; grid
+// capped at 4 blocks/CU and strided over row groups. Measured on MI355X this
+// simple form (115 VGPRs for Q4_K, 4 waves/SIMD) beat variants that prefetch
+// across the prologue or split K across waves (170-200 VGPRs): occupancy wins.
+template <int QT, int EPI, int NR, bool NORM>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a, int /*unused*/) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int K = a.w.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + K);
   float* red = xd + (K >> 5);
   quantize_x<NORM>(a.x, a.norm_w, a.eps, K, xq, xd, red);
-  LFK_DISPATCH_TYPE(a.w.type, gemv_body<QT, EPI, NR>(a, xq, xd));
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  const int nchunks = K >> 5;
+  constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
+  const int groups = (a.n_out + NF - 1) / NF;
+  const int total = groups * a.n_slots;
+  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
+    RowPtr R[NR];
+    int slot, f0;
+    item_rows<EPI, NR>(a, item, groups, R, slot, f0);
+    float acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = 0.f;
+    dot_rows<QT, NR>(R, nchunks, xq, xd, acc, lane);
+    if (lane < NF && f0 + lane < a.n_out) {
+      float* o = a.out + (size_t)slot * a.out_slot_stride + f0 + lane;
+      if constexpr (EPI == EPI_SWIGLU) {
+        float g = acc[0], u = acc[NF];
+#pragma unroll
+        for (int r = 1; r < NF; ++r) {
+          g = lane == r ? acc[r] : g;
+          u = lane == r ? acc[NF + r] : u;
+        }
+        *o = silu(g) * u;
+      } else {
+        const float v = pick<NR>(acc, lane);
+        if constexpr (EPI == EPI_STORE) *o = a.resid ? v + a.resid[f0 + lane] : v;
+        else *o += v;
+      }
+    }
+  }
 }
 
 QMat make_qmat(const void* base, int type, int rows, int K, size_t expert_stride) {
@@ -142,82 +195,118 @@ QMat make_qmat(const void* base, int type, int rows, int K, size_t expert_stride
   return m;
 }
 
-static inline int grid_for(int items) {
-  int b = (items + 3) / 4;
+static inline int grid_for(int items, int per_block = 4) {
+  int b = (items + per_block - 1) / per_block;
   return b < 1 ? 1 : (b > kMaxBlocks ? kMaxBlocks : b);
 }
 
+
+template <int QT, int EPI>
+static void launch_gemv(const GemvArgs& a, hipStream_t s) {
+  constexpr int NR = rows_per_item<QT>();
+  constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
+  const size_t lds = a.w.K + (a.w.K / 32) * 4 + 32 + 4 * NR * 4 + 64;
+  const int items = (a.n_out + NF - 1) / NF * a.n_slots;
+  dim3 grid(grid_for(items)), block(256);
+  const int wk = 1;
+  if (a.norm_w) hipLaunchKernelGGL((gemv_kernel<QT, EPI, NR, true>), grid, block, lds, s, a, wk);
+  else hipLaunchKernelGGL((gemv_kernel<QT, EPI, NR, false>), grid, block, lds, s, a, wk);
+}
+
+template <int QT>
+static void gemv_t(const GemvArgs& a, int epi, hipStream_t s) {
+  switch (epi) {
+    case EPI_STORE: launch_gemv<QT, EPI_STORE>(a, s); break;
+    case EPI_ADD: launch_gemv<QT, EPI_ADD>(a, s); break;
+    case EPI_SWIGLU: launch_gemv<QT, EPI_SWIGLU>(a, s); break;
+    default: throw std::runtime_error("gemv: bad epilogue");
+  }
+}
+
 void gemv(const GemvArgs& a, int epi, hipStream_t s) {
-  constexpr int NR = 2;
   if (epi == EPI_SWIGLU && (a.n_out % 32)) throw std::runtime_error("gemv: swiglu features must be a multiple of 32");
   if (a.w.K % 32) throw std::runtime_error("gemv: K must be a multiple of 32");
   if (a.n_out <= 0) return;
-  const size_t lds = a.w.K + (a.w.K / 32) * 4 + 64;
-  const int items = (a.n_out + NR - 1) / NR * a.n_slots;
-  dim3 grid(grid_for(items)), block(256);
-  const bool norm = a.norm_w != nullptr;
-#define LAUNCH(E, N)                                                                         \
-  if (norm) hipLaunchKernelGGL((gemv_kernel<E, NR, true>), grid, block, lds, s, a);          \
-  else hipLaunchKernelGGL((gemv_kernel<E, NR, false>), grid, block, lds, s, a);
-  switch (epi) {
-    case EPI_STORE: LAUNCH(EPI_STORE, NR); break;
-    case EPI_ADD: LAUNCH(EPI_ADD, NR); break;
-    case EPI_SWIGLU: LAUNCH(EPI_SWIGLU, NR); break;
-    default: throw std::runtime_error("gemv: bad epilogue");
+  switch (a.w.type) {
+    case T_Q4_K: gemv_t<T_Q4_K>(a, epi, s); break;
+    case T_Q5_K: gemv_t<T_Q5_K>(a, epi, s); break;
+    case T_Q6_K: gemv_t<T_Q6_K>(a, epi, s); break;
+    case T_Q8_0: gemv_t<T_Q8_0>(a, epi, s); break;
+    case T_F16: gemv_t<T_F16>(a, epi, s); break;
+    case T_F32: gemv_t<T_F32>(a, epi, s); break;
+    default: throw std::runtime_error("gemv: unsupported weight type");
   }
-#undef LAUNCH
 }
 
 // ------------------------------------------------------------------ QKV + RoPE + KV append
-template <int QT>
-__device__ __forceinline__ void qkv_pair(const QMat& w, size_t row, int nchunks, const int8_t* xq, const float* xd,
-                                         float& a0, float& a1, int lane) {
-  size_t rows[2] = {row, row + 1};
-  float acc[2] = {0.f, 0.f};
-  dot_rows<QT, 2>(w.base, w.P, rows, nchunks, xq, xd, acc, lane);
-  a0 = acc[0];
-  a1 = acc[1];
-}
+// One launch covers a run of Q/K/V segments that share a quant type (Q4_K_M:
+// usually Q+K together, V separately when it is Q6_K). Items are 4 rows = two
+// RoPE pairs, so the rotation happens between lanes (2j, 2j+1) after the reduce.
+struct QkvSeg {
+  const uint8_t* base;
+  Planes P;
+  int rows;
+  int kind;  // 0 = Q, 1 = K, 2 = V
+};
+struct QkvLaunch {
+  QkvSeg seg[3];
+  int nseg;
+  int K;
+  const float* x;
+  const float* norm_w;
+  float eps;
+  float* q_out;
+  __half* k_cache;
+  __half* v_cache;
+  int n_ctx, head_dim;
+  const int* pos;
+  const float2* rope;
+};
 
-__global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvArgs a) {
+// One launch per run of Q/K/V segments sharing a quant type (measured: mixing
+// two types in one kernel raised VGPRs past 200 and ran slower than 2 launches).
+template <int QT>
+__global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int K = a.wq.K;
+  constexpr int NR = rows_per_item<QT>();
+  const int K = a.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + K);
   float* red = xd + (K >> 5);
   if (a.norm_w) quantize_x<true>(a.x, a.norm_w, a.eps, K, xq, xd, red);
   else quantize_x<false>(a.x, nullptr, a.eps, K, xq, xd, red);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nq = a.wq.rows, nkv = a.wk.rows;
-  const int total = (nq + 2 * nkv) >> 1;
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  int total = 0;
+  for (int i = 0; i < a.nseg; ++i) total += a.seg[i].rows / NR;
   const int nchunks = K >> 5;
   const int hd = a.head_dim;
   const int pos = *a.pos;
   for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
-    int r = item * 2;
-    int seg;
-    const QMat* w;
-    if (r < nq) { seg = 0; w = &a.wq; }
-    else if (r < nq + nkv) { seg = 1; r -= nq; w = &a.wk; }
-    else { seg = 2; r -= nq + nkv; w = &a.wv; }
-    float a0 = 0.f, a1 = 0.f;
-    LFK_DISPATCH_TYPE(w->type, qkv_pair<QT>(*w, (size_t)r, nchunks, xq, xd, a0, a1, lane));
-    if (lane == 0) {
+    int it = item, si = 0;
+    while (si < a.nseg - 1 && it >= a.seg[si].rows / NR) { it -= a.seg[si].rows / NR; ++si; }
+    const QkvSeg& sg = a.seg[si];
+    const int r0 = it * NR;
+    RowPtr R[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[r] = row_ptr(sg.base, sg.P, (unsigned)(r0 + r));
+    float acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = 0.f;
+    dot_rows<QT, NR>(R, nchunks, xq, xd, acc, lane);
+    float v = pick<NR>(acc, lane);
+    const float partner = __shfl_xor(v, 1);
+    if (lane < NR) {
+      const int r = r0 + lane;
       const int dd = r % hd;
-      float y0 = a0, y1 = a1;
-      if (seg < 2) {
+      if (sg.kind < 2) {
         const float2 cs = a.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
-        y0 = a0 * cs.x - a1 * cs.y;
-        y1 = a0 * cs.y + a1 * cs.x;
+        v = (lane & 1) ? partner * cs.y + v * cs.x : v * cs.x - partner * cs.y;
       }
-      if (seg == 0) {
-        a.q_out[r] = y0;
-        a.q_out[r + 1] = y1;
+      if (sg.kind == 0) {
+        a.q_out[r] = v;
       } else {
-        const int kvh = r / hd;
-        __half* c = (seg == 1 ? a.k_cache : a.v_cache) + ((size_t)kvh * a.n_ctx + pos) * hd + dd;
-        c[0] = __float2half(y0);
-        c[1] = __float2half(y1);
+        __half* c = (sg.kind == 1 ? a.k_cache : a.v_cache) + ((size_t)(r / hd) * a.n_ctx + pos) * hd + dd;
+        *c = __float2half(v);
       }
     }
   }
@@ -226,50 +315,83 @@ __global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvArgs a) {
 void gemv_qkv(const QkvArgs& a, hipStream_t s) {
   const int K = a.wq.K;
   if (K % 32 || a.wk.K != K || a.wv.K != K) throw std::runtime_error("gemv_qkv: K mismatch");
+  if (a.wq.rows % 4 || a.wk.rows % 4) throw std::runtime_error("gemv_qkv: rows must be multiples of 4");
+  const QMat* m[3] = {&a.wq, &a.wk, &a.wv};
   const size_t lds = K + (K / 32) * 4 + 64;
-  const int items = (a.wq.rows + 2 * a.wk.rows) / 2;
-  hipLaunchKernelGGL(gemv_qkv_kernel, dim3(grid_for(items)), dim3(256), lds, s, a);
-}
-
-// ------------------------------------------------------------------ MoE down projection
-template <int QT>
-__device__ void moe_down_body(const MoeDownArgs& a, const int8_t* xq, const float* xd) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int K = a.w.K, nchunks = K >> 5;
-  const int total = a.w.rows >> 1;
-  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
-    size_t rows[2] = {(size_t)item * 2, (size_t)item * 2 + 1};
-    float tot0 = 0.f, tot1 = 0.f;
-    for (int s = 0; s < a.n_slots; ++s) {
-      const uint8_t* base = a.w.base + (size_t)a.expert_ids[s] * a.w.expert_stride;
-      float acc[2] = {0.f, 0.f};
-      dot_rows<QT, 2>(base, a.w.P, rows, nchunks, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), acc, lane);
-      const float ws = a.expert_w[s];
-      tot0 += ws * acc[0];
-      tot1 += ws * acc[1];
+  for (int i = 0; i < 3;) {
+    QkvLaunch L{};
+    L.K = K; L.x = a.x; L.norm_w = a.norm_w; L.eps = a.eps; L.q_out = a.q_out; L.k_cache = a.k_cache;
+    L.v_cache = a.v_cache; L.n_ctx = a.n_ctx; L.head_dim = a.head_dim; L.pos = a.pos; L.rope = a.rope;
+    const int t = m[i]->type;
+    int items = 0;
+    while (i < 3 && m[i]->type == t) {
+      L.seg[L.nseg] = QkvSeg{m[i]->base, m[i]->P, m[i]->rows, i};
+      items += m[i]->rows / (t == T_Q4_K || t == T_Q5_K || t == T_Q8_0 ? 4 : 2);
+      ++L.nseg;
+      ++i;
     }
-    if (lane == 0) {
-      a.out[rows[0]] += tot0;
-      a.out[rows[1]] += tot1;
+    dim3 grid(grid_for(items)), block(256);
+    switch (t) {
+      case T_Q4_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q4_K>, grid, block, lds, s, L); break;
+      case T_Q5_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q5_K>, grid, block, lds, s, L); break;
+      case T_Q6_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q6_K>, grid, block, lds, s, L); break;
+      case T_Q8_0: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q8_0>, grid, block, lds, s, L); break;
+      case T_F16: hipLaunchKernelGGL(gemv_qkv_kernel<T_F16>, grid, block, lds, s, L); break;
+      case T_F32: hipLaunchKernelGGL(gemv_qkv_kernel<T_F32>, grid, block, lds, s, L); break;
+      default: throw std::runtime_error("gemv_qkv: unsupported type");
     }
   }
 }
 
+// ------------------------------------------------------------------ MoE down projection
+template <int QT>
 __global__ __launch_bounds__(256) void gemv_moe_down_kernel(MoeDownArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NR = 2;
   const int K = a.w.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + (size_t)a.n_slots * K);
   float* red = xd + (size_t)a.n_slots * (K >> 5);
   for (int s = 0; s < a.n_slots; ++s)
     quantize_x<false>(a.h + (size_t)s * K, nullptr, 0.f, K, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), red);
-  LFK_DISPATCH_TYPE(a.w.type, moe_down_body<QT>(a, xq, xd));
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  const int nchunks = K >> 5;
+  const int total = (a.w.rows + NR - 1) / NR;
+  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
+    const int r0 = item * NR;
+    float tot[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) tot[r] = 0.f;
+    for (int s = 0; s < a.n_slots; ++s) {
+      const uint8_t* base = a.w.base + (size_t)a.expert_ids[s] * a.w.expert_stride;
+      RowPtr R[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) R[r] = row_ptr(base, a.w.P, (unsigned)min(r0 + r, a.w.rows - 1));
+      float acc[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[r] = 0.f;
+      dot_rows<QT, NR>(R, nchunks, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), acc, lane);
+      const float ws = a.expert_w[s];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) tot[r] += ws * acc[r];
+    }
+    if (lane < NR && r0 + lane < a.w.rows) a.out[r0 + lane] += pick<NR>(tot, lane);
+  }
 }
 
 void gemv_moe_down(const MoeDownArgs& a, hipStream_t s) {
   const int K = a.w.K;
   const size_t lds = (size_t)a.n_slots * (K + (K / 32) * 4) + 64;
-  hipLaunchKernelGGL(gemv_moe_down_kernel, dim3(grid_for(a.w.rows / 2)), dim3(256), lds, s, a);
+  dim3 grid(grid_for((a.w.rows + 1) / 2)), block(256);
+  switch (a.w.type) {
+    case T_Q4_K: hipLaunchKernelGGL(gemv_moe_down_kernel<T_Q4_K>, grid, block, lds, s, a); break;
+    case T_Q5_K: hipLaunchKernelGGL(gemv_moe_down_kernel<T_Q5_K>, grid, block, lds, s, a); break;
+    case T_Q6_K: hipLaunchKernelGGL(gemv_moe_down_kernel<T_Q6_K>, grid, block, lds, s, a); break;
+    case T_Q8_0: hipLaunchKernelGGL(gemv_moe_down_kernel<T_Q8_0>, grid, block, lds, s, a); break;
+    case T_F16: hipLaunchKernelGGL(gemv_moe_down_kernel<T_F16>, grid, block, lds, s, a); break;
+    case T_F32: hipLaunchKernelGGL(gemv_moe_down_kernel<T_F32>, grid, block, lds, s, a); break;
+    default: throw std::runtime_error("moe_down: unsupported type");
+  }
 }
 
 // ------------------------------------------------------------------ MoE router (one wave)

@@ -92,6 +92,7 @@ struct AttnDecodeArgs {
   int n_ctx = 0, n_head = 0, n_kv_head = 0, head_dim = 0;
   float scale = 1.f;
   float* part = nullptr;          // workspace [n_split][n_head][hd + 2]
+  int* counters = nullptr;        // [n_kv_head] zero-initialised; each launch leaves them at 0
   float* out = nullptr;           // [n_head][hd]
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
@@ -152,13 +153,15 @@ struct SamplerParamsDev {
 enum StateIdx : int { S_TOKEN = 0, S_POS = 1, S_STEP = 2, S_RING_LEN = 3, S_RING_HEAD = 4, S_NOUT = 5, S_NSTATE = 8 };
 
 struct SamplerArgs {
-  const float* logits = nullptr;   // [V]; penalties are applied on a copy in LDS
+  float* logits = nullptr;         // [V]; the penalty kernel patches it in place
   int V = 0;
   const SamplerParamsDev* p = nullptr;
   int* ring = nullptr;             // [64] penalty window ring (prompt + generated tokens)
   int* state = nullptr;            // [S_NSTATE]
+  float* logits_rw = nullptr;      // unused (penalties patch `logits` in place)
   float* cand_val = nullptr;       // workspace [sampler_blocks(V) * 64]
   int* cand_idx = nullptr;
+  unsigned* cand_tau = nullptr;    // workspace [sampler_blocks(V)]
   int* out_tokens = nullptr;       // optional device ring of sampled tokens [out_cap]
   int out_cap = 0;
   int advance_pos = 1;             // also bump state.pos (decode) after sampling

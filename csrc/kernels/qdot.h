@@ -204,6 +204,136 @@ __device__ __forceinline__ float chunk_dot(const uint8_t* __restrict__ base, con
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split load / compute form of chunk_dot: the GEMV issues the loads of ALL its
+// rows x passes first (WRaw), then does the integer math, so every lane keeps
+// NR x 2 independent 16-B loads in flight instead of one at a time.
+template <int T> struct WRaw;
+template <> struct WRaw<T_Q4_K> { int4 q, m; };
+template <> struct WRaw<T_Q5_K> { int4 q, h, m; };
+template <> struct WRaw<T_Q6_K> { int4 l, h; int slo, shi; unsigned d; };
+template <> struct WRaw<T_Q8_0> { int4 a, b; unsigned d; };
+template <> struct WRaw<T_F16> { uint4 w[4]; };
+template <> struct WRaw<T_F32> { float4 w[8]; };
+
+// per-row plane pointers (wave-uniform -> SGPRs)
+struct RowPtr {
+  const uint8_t* p0;
+  const uint8_t* p1;
+  const uint8_t* p2;
+  const uint8_t* p3;
+};
+
+__device__ __forceinline__ RowPtr row_ptr(const uint8_t* base, const Planes& P, unsigned row) {
+  RowPtr r;
+  r.p0 = base + P.p0 + (size_t)row * P.s0;
+  r.p1 = base + P.p1 + (size_t)row * P.s1;
+  r.p2 = base + P.p2 + (size_t)row * P.s2;
+  r.p3 = base + P.p3 + (size_t)row * P.s3;
+  return r;
+}
+
+template <int T>
+__device__ __forceinline__ void wload(WRaw<T>& w, const RowPtr& R, int c) {
+  const int sb = c >> 3, j = c & 7;
+  if constexpr (T == T_Q4_K) {
+    w.q = ld_nt16(R.p0 + 16 * c);
+    w.m = *reinterpret_cast<const int4*>(R.p1 + 16 * sb);
+  } else if constexpr (T == T_Q5_K) {
+    w.q = ld_nt16(R.p0 + 16 * c);
+    w.h = *reinterpret_cast<const int4*>(R.p1 + 32 * sb + 16 * (j & 1));
+    w.m = *reinterpret_cast<const int4*>(R.p2 + 16 * sb);
+  } else if constexpr (T == T_Q6_K) {
+    const int n = j >> 2, o = 16 * (j & 3);
+    w.l = ld_nt16(R.p0 + 16 * c);
+    w.h = *reinterpret_cast<const int4*>(R.p1 + 64 * sb + 32 * n + (o & 31));
+    const int si = 8 * n + (o >> 4);
+    w.slo = *reinterpret_cast<const signed char*>(R.p2 + 16 * sb + si);
+    w.shi = *reinterpret_cast<const signed char*>(R.p2 + 16 * sb + si + 4);
+    w.d = *reinterpret_cast<const unsigned short*>(R.p3 + 2 * sb);
+  } else if constexpr (T == T_Q8_0) {
+    w.a = ld_nt16(R.p0 + 32 * c);
+    w.b = ld_nt16(R.p0 + 32 * c + 16);
+    w.d = *reinterpret_cast<const unsigned short*>(R.p1 + 2 * c);
+  } else if constexpr (T == T_F16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w.w[i] = reinterpret_cast<const uint4*>(R.p0 + 64 * c)[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w.w[i] = reinterpret_cast<const float4*>(R.p0 + 128 * c)[i];
+  }
+}
+
+template <int T>
+__device__ __forceinline__ float wdot(const WRaw<T>& w, const XChunk& X, int c) {
+  const int j = c & 7;
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+    const int g = j >> 1;
+    const unsigned dd = (unsigned)w.m.x;
+    const float d = h2f(dd & 0xFFFF), dmin = h2f(dd >> 16);
+    float sc_lo, m_lo, sc_hi, m_hi;
+    scale_min_pair(g, (unsigned)w.m.y, (unsigned)w.m.z, (unsigned)w.m.w, sc_lo, m_lo, sc_hi, m_hi);
+    const int qv[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
+    int dl = 0, dh = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int lo = qv[i] & 0x0F0F0F0F;
+      int hi = (qv[i] >> 4) & 0x0F0F0F0F;
+      if constexpr (T == T_Q5_K) {
+        const int hv = (i == 0 ? w.h.x : i == 1 ? w.h.y : i == 2 ? w.h.z : w.h.w);
+        lo |= ((hv >> (2 * g)) & 0x01010101) << 4;
+        hi |= ((hv >> (2 * g + 1)) & 0x01010101) << 4;
+      }
+      dl = dot4(lo, X.lo[i], dl);
+      dh = dot4(hi, X.hi[i], dh);
+    }
+    return d * (sc_lo * X.dlo * (float)dl + sc_hi * X.dhi * (float)dh) - dmin * (m_lo * X.slo + m_hi * X.shi);
+  } else if constexpr (T == T_Q6_K) {
+    const int o = 16 * (j & 3);
+    const int sc_lo = w.slo, sc_hi = w.shi;
+    const int s = (o >= 32) ? 2 : 0;
+    const int lv[4] = {w.l.x, w.l.y, w.l.z, w.l.w};
+    const int hv[4] = {w.h.x, w.h.y, w.h.z, w.h.w};
+    int dl = 0, dh = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int lo = (lv[i] & 0x0F0F0F0F) | (((hv[i] >> s) & 0x03030303) << 4);
+      const int hi = ((lv[i] >> 4) & 0x0F0F0F0F) | (((hv[i] >> (s + 4)) & 0x03030303) << 4);
+      dl = dot4(lo, X.lo[i], dl);
+      dh = dot4(hi, X.hi[i], dh);
+    }
+    const float d = h2f(w.d & 0xFFFF);
+    return d * ((float)sc_lo * (X.dlo * (float)dl - 32.f * X.slo) + (float)sc_hi * (X.dhi * (float)dh - 32.f * X.shi));
+  } else if constexpr (T == T_Q8_0) {
+    int acc = dot4(w.a.x, X.lo[0], 0);
+    acc = dot4(w.a.y, X.lo[1], acc);
+    acc = dot4(w.a.z, X.lo[2], acc);
+    acc = dot4(w.a.w, X.lo[3], acc);
+    acc = dot4(w.b.x, X.hi[0], acc);
+    acc = dot4(w.b.y, X.hi[1], acc);
+    acc = dot4(w.b.z, X.hi[2], acc);
+    acc = dot4(w.b.w, X.hi[3], acc);
+    return h2f(w.d & 0xFFFF) * X.dlo * (float)acc;
+  } else {
+    const int xv[8] = {X.lo[0], X.lo[1], X.lo[2], X.lo[3], X.hi[0], X.hi[1], X.hi[2], X.hi[3]};
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = xv[i];
+      const float x0 = (float)(signed char)(v & 0xFF), x1 = (float)(signed char)((v >> 8) & 0xFF);
+      const float x2 = (float)(signed char)((v >> 16) & 0xFF), x3 = (float)(signed char)((v >> 24) & 0xFF);
+      if constexpr (T == T_F32) {
+        const float4 ww = w.w[i];
+        s += ww.x * x0 + ww.y * x1 + ww.z * x2 + ww.w * x3;
+      } else {
+        const uint2 ww = (i & 1) ? make_uint2(w.w[i >> 1].z, w.w[i >> 1].w) : make_uint2(w.w[i >> 1].x, w.w[i >> 1].y);
+        s += h2f(ww.x & 0xFFFF) * x0 + h2f(ww.x >> 16) * x1 + h2f(ww.y & 0xFFFF) * x2 + h2f(ww.y >> 16) * x3;
+      }
+    }
+    return s * X.dlo;
+  }
+}
+
 // Dequantise 32 CONTIGUOUS weights [32*q, 32*q+32) of `row` into out[32] (used by
 // the embedding gather and the prefill GEMM's LDS staging).
 template <int T>

@@ -210,9 +210,12 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(vc_, 0, kv * 2));
   rope_ = (float2*)dalloc(sizeof(float2) * opt_.n_ctx * (hd / 2));
   attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
+  attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
+  HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   const int nb = sampler_blocks(hp_.n_vocab);
   cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
   cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
+  cand_tau_ = (unsigned*)dalloc(sizeof(unsigned) * nb);
   state_ = (int*)dalloc(sizeof(int) * S_NSTATE);
   ring_ = (int*)dalloc(sizeof(int) * 64);
   out_tokens_ = (int*)dalloc(sizeof(int) * 64);
@@ -267,7 +270,7 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.q = q_; aa.k_cache = qa.k_cache; aa.v_cache = qa.v_cache; aa.pos = state_ + S_POS;
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
-  aa.part = attn_part_; aa.out = attn_;
+  aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
   attn_decode(aa, s);
 
   GemvArgs o;
@@ -334,7 +337,7 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
     ncclchk(ncclAllGather(logits_l_, logits_, V_l_, ncclFloat32, static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
   SamplerArgs sa;
   sa.logits = logits_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
-  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.out_tokens = out_tokens_; sa.out_cap = 64;
+  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.cand_tau = cand_tau_; sa.out_tokens = out_tokens_; sa.out_cap = 64;
   sa.advance_pos = advance_pos;
   sample(sa, s);
   HIPCHK(hipMemcpyAsync(h_ring_, out_tokens_, sizeof(int) * 64, hipMemcpyDeviceToHost, s));

@@ -139,8 +139,10 @@ class Engine {
   __half* vc_ = nullptr;
   float2* rope_ = nullptr;
   float* attn_part_ = nullptr;
+  int* attn_cnt_ = nullptr;   // per-kv-head split counters (last-arriver combine)
   float* cand_val_ = nullptr;
   int* cand_idx_ = nullptr;
+  unsigned* cand_tau_ = nullptr;
   int* state_ = nullptr;
   int* ring_ = nullptr;
   int* out_tokens_ = nullptr;

@@ -20,6 +20,7 @@ for s in "$@"; do
     gputests) step gputests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
+    micro) step micro 300 python tools/launch_microbench.py ;;
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
     prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o decode \
             --output-format csv -- python3 tools/decode_bench.py --steps 64 --no-graph ;;
