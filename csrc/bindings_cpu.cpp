@@ -1,0 +1,78 @@
+// Python bindings of the C++ CPU backend (`llama_fastapi_k8s_gpu_amd.runtime._cpu`).
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "cpu/cpu_backend.h"
+#include "runtime/repack.h"
+
+namespace py = pybind11;
+using namespace lfk;
+
+static CpuSampling parse_sampling(py::dict sp) {
+  CpuSampling o;
+  if (sp.contains("top_k")) o.top_k = sp["top_k"].cast<int>();
+  if (sp.contains("top_p")) o.top_p = sp["top_p"].cast<float>();
+  if (sp.contains("min_p")) o.min_p = sp["min_p"].cast<float>();
+  if (sp.contains("temperature")) o.temp = sp["temperature"].cast<float>();
+  if (sp.contains("repeat_penalty")) o.repeat_penalty = sp["repeat_penalty"].cast<float>();
+  if (sp.contains("frequency_penalty")) o.freq_penalty = sp["frequency_penalty"].cast<float>();
+  if (sp.contains("presence_penalty")) o.presence_penalty = sp["presence_penalty"].cast<float>();
+  if (sp.contains("last_n")) o.last_n = sp["last_n"].cast<int>();
+  if (sp.contains("seed")) o.seed = sp["seed"].cast<unsigned long long>();
+  return o;
+}
+
+PYBIND11_MODULE(_cpu, m) {
+  m.doc() = "C++ CPU backend (OpenMP): GGUF engine for n_gpu_layers = 0";
+  py::class_<CpuEngine>(m, "CpuEngine")
+      .def(py::init([](const std::string& path, int n_ctx, int n_threads, int n_batch) {
+             py::gil_scoped_release nogil;
+             return std::make_unique<CpuEngine>(path, n_ctx, n_threads, n_batch);
+           }),
+           py::arg("path"), py::arg("n_ctx") = 512, py::arg("n_threads") = 0, py::arg("n_batch") = 64)
+      .def("generate",
+           [](CpuEngine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
+              const std::vector<int>& stop, py::object poll, py::object on_token) {
+             CpuSampling o = parse_sampling(sp);
+             std::function<bool()> pf;
+             std::function<void(int)> tf;
+             if (!poll.is_none()) pf = [poll]() { py::gil_scoped_acquire g; return poll().cast<bool>(); };
+             if (!on_token.is_none()) tf = [on_token](int t) { py::gil_scoped_acquire g; on_token(t); };
+             CpuGenOut r;
+             {
+               py::gil_scoped_release nogil;
+               r = e.generate(prompt, n_keep, max_new, o, stop, pf, tf);
+             }
+             py::dict d;
+             d["tokens"] = r.tokens;
+             d["finish"] = r.finish;
+             d["n_evaluated"] = r.n_evaluated;
+             d["n_prefilled"] = r.n_prefilled;
+             d["prefill_s"] = r.prefill_s;
+             d["decode_s"] = r.decode_s;
+             return d;
+           },
+           py::arg("prompt"), py::arg("n_keep"), py::arg("max_new"), py::arg("sampling"), py::arg("stop_ids"),
+           py::arg("poll") = py::none(), py::arg("on_token") = py::none())
+      .def("eval_logits",
+           [](CpuEngine& e, const std::vector<int>& tokens, int pos0) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.eval_logits(tokens, pos0);
+             }
+             return py::array_t<float>(v.size(), v.data());
+           })
+      .def_property_readonly("n_vocab", &CpuEngine::n_vocab)
+      .def_property_readonly("n_layer", &CpuEngine::n_layer)
+      .def_property_readonly("n_ctx", &CpuEngine::n_ctx);
+
+  m.def("sample", [](py::array_t<float, py::array::c_style> logits, const std::vector<int>& window, py::dict sp,
+                     int step) {
+    std::vector<float> l(logits.data(), logits.data() + logits.size());
+    return cpu_sample(l, window, parse_sampling(sp), step);
+  });
+  m.def("uniform", &splitmix_uniform);
+}

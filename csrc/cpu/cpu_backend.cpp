@@ -1,0 +1,557 @@
+#include "cpu_backend.h"
+
+#include <immintrin.h>
+#include <omp.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+
+#include "../runtime/gguf.h"
+#include "../runtime/repack.h"
+
+namespace lfk {
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline float h2f(uint16_t h) { return _cvtsh_ss(h); }
+inline uint16_t f2h(float f) { return _cvtss_sh(f, 0); }
+
+CpuMat load_mat(const GGUFFile& f, const std::string& name, int n_expert = 0) {
+  const GGUFTensor* t = f.find(name);
+  if (!t) throw std::runtime_error("missing tensor " + name);
+  CpuMat m;
+  m.type = t->type;
+  m.K = (int)t->ne[0];
+  m.rows = (int)t->ne[1];
+  const int E = n_expert > 0 ? n_expert : 1;
+  const size_t one = qbytes(m.type, m.rows, m.K);
+  m.data.resize(one * E);
+  for (int e = 0; e < E; ++e)
+    repack_planar(m.type, f.data(*t) + one * e, m.K, 0, m.rows, 0, m.K, m.data.data() + one * e, m.rows, 0, 0);
+  m.P = planes_of(m.type, m.rows, m.K);
+  m.expert_stride = n_expert > 0 ? one : 0;
+  return m;
+}
+
+CpuMat load_gate_up(const GGUFFile& f, const std::string& g, const std::string& u, int n_expert = 0) {
+  const GGUFTensor* tg = f.find(g);
+  const GGUFTensor* tu = f.find(u);
+  if (!tg || !tu) throw std::runtime_error("missing " + g);
+  if (tg->type != tu->type) throw std::runtime_error("gate/up projections must share a quant type");
+  CpuMat m;
+  m.type = tg->type;
+  m.K = (int)tg->ne[0];
+  const int F = (int)tg->ne[1];
+  m.rows = 2 * F;
+  const int E = n_expert > 0 ? n_expert : 1;
+  const size_t one = qbytes(m.type, m.rows, m.K);
+  const size_t src_one = qbytes(m.type, F, m.K);
+  m.data.resize(one * E);
+  for (int e = 0; e < E; ++e) {
+    repack_planar(m.type, f.data(*tg) + src_one * e, m.K, 0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 0);
+    repack_planar(m.type, f.data(*tu) + src_one * e, m.K, 0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 32);
+  }
+  m.P = planes_of(m.type, m.rows, m.K);
+  m.expert_stride = n_expert > 0 ? one : 0;
+  return m;
+}
+
+std::vector<float> load_f32(const GGUFFile& f, const std::string& name) {
+  const GGUFTensor* t = f.find(name);
+  if (!t || t->type != T_F32) throw std::runtime_error("missing F32 tensor " + name);
+  std::vector<float> v(t->n_elements());
+  std::memcpy(v.data(), f.data(*t), v.size() * 4);
+  return v;
+}
+
+// ---- q8 activations: identical rounding to the GPU prologue (round half to even)
+struct Q8 {
+  std::vector<int8_t> q;   // [T][K]
+  std::vector<float> d;    // [T][K/32]
+  std::vector<int> s16;    // [T][K/16] sums of q over 16
+  int K = 0;
+};
+
+void quantize_rows(const float* x, int T, int ldx, int K, const std::vector<float>* norm, float eps, Q8& o) {
+  o.K = K;
+  o.q.resize((size_t)T * K);
+  o.d.resize((size_t)T * K / 32);
+  o.s16.resize((size_t)T * K / 16);
+  for (int t = 0; t < T; ++t) {
+    const float* xr = x + (size_t)t * ldx;
+    float scale = 1.f;
+    if (norm) {
+      double ss = 0;
+      for (int i = 0; i < K; ++i) ss += (double)xr[i] * xr[i];
+      scale = 1.f / std::sqrt((float)(ss / K) + eps);
+    }
+    for (int b = 0; b < K / 32; ++b) {
+      float v[32], amax = 0.f;
+      for (int i = 0; i < 32; ++i) {
+        v[i] = norm ? xr[32 * b + i] * scale * (*norm)[32 * b + i] : xr[32 * b + i];
+        amax = std::max(amax, std::fabs(v[i]));
+      }
+      const float d = amax * (1.f / 127.f);
+      const float id = d > 0.f ? 1.f / d : 0.f;
+      int8_t* q = o.q.data() + (size_t)t * K + 32 * b;
+      for (int i = 0; i < 32; ++i) q[i] = (int8_t)std::nearbyint(v[i] * id);
+      o.d[(size_t)t * (K / 32) + b] = d;
+      int s0 = 0, s1 = 0;
+      for (int i = 0; i < 16; ++i) { s0 += q[i]; s1 += q[16 + i]; }
+      o.s16[(size_t)t * (K / 16) + 2 * b] = s0;
+      o.s16[(size_t)t * (K / 16) + 2 * b + 1] = s1;
+    }
+  }
+}
+
+// One 32-weight chunk decoded to int8 + per-half affine scales (the GPU chunk map).
+struct Chunk {
+  int8_t w[32];              // [0,16) lo half, [16,32) hi half
+  int off_lo, off_hi;        // x offsets of the halves
+  float s_lo, m_lo, s_hi, m_hi;  // sum = s*dot(w,x) - m*sum(x)   (x in q8 units, times xd)
+  bool is_float = false;
+  float wf[32];
+};
+
+inline void scale_min_k4(int j, const uint8_t* q, int& sc, int& m) {
+  if (j < 4) { sc = q[j] & 63; m = q[j + 4] & 63; }
+  else { sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4); m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4); }
+}
+
+inline float hf(const uint8_t* p) { uint16_t h; std::memcpy(&h, p, 2); return h2f(h); }
+
+void decode_chunk(const CpuMat& W, const uint8_t* base, size_t row, int c, Chunk& ch) {
+  const Planes& P = W.P;
+  const int sb = c >> 3, j = c & 7;
+  switch (W.type) {
+    case T_Q4_K:
+    case T_Q5_K: {
+      const int g = j >> 1, h = j & 1;
+      const uint8_t* qs = base + P.p0 + row * P.s0 + 16 * c;
+      const uint8_t* meta = base + (W.type == T_Q4_K ? P.p1 + row * P.s1 : P.p2 + row * P.s2) + 16 * sb;
+      const uint8_t* qh = W.type == T_Q5_K ? base + P.p1 + row * P.s1 + 32 * sb + 16 * h : nullptr;
+      const float d = hf(meta), dmin = hf(meta + 2);
+      int sc0, m0, sc1, m1;
+      scale_min_k4(2 * g, meta + 4, sc0, m0);
+      scale_min_k4(2 * g + 1, meta + 4, sc1, m1);
+      for (int i = 0; i < 16; ++i) {
+        int lo = qs[i] & 0xF, hi = qs[i] >> 4;
+        if (qh) { lo |= ((qh[i] >> (2 * g)) & 1) << 4; hi |= ((qh[i] >> (2 * g + 1)) & 1) << 4; }
+        ch.w[i] = (int8_t)lo;
+        ch.w[16 + i] = (int8_t)hi;
+      }
+      ch.off_lo = sb * 256 + 64 * g + 16 * h;
+      ch.off_hi = ch.off_lo + 32;
+      ch.s_lo = d * sc0; ch.m_lo = dmin * m0;
+      ch.s_hi = d * sc1; ch.m_hi = dmin * m1;
+      break;
+    }
+    case T_Q6_K: {
+      const int n = j >> 2, o = 16 * (j & 3);
+      const uint8_t* ql = base + P.p0 + row * P.s0 + 16 * c;
+      const uint8_t* qh = base + P.p1 + row * P.s1 + 64 * sb + 32 * n + (o & 31);
+      const int8_t* sc = reinterpret_cast<const int8_t*>(base + P.p2 + row * P.s2 + 16 * sb);
+      const float d = hf(base + P.p3 + row * P.s3 + 2 * sb);
+      const int s = o >= 32 ? 2 : 0;
+      for (int i = 0; i < 16; ++i) {
+        ch.w[i] = (int8_t)((ql[i] & 0xF) | (((qh[i] >> s) & 3) << 4));
+        ch.w[16 + i] = (int8_t)((ql[i] >> 4) | (((qh[i] >> (s + 4)) & 3) << 4));
+      }
+      const int si = 8 * n + (o >> 4);
+      ch.off_lo = sb * 256 + 128 * n + o;
+      ch.off_hi = ch.off_lo + 64;
+      ch.s_lo = d * sc[si]; ch.m_lo = 32.f * ch.s_lo;
+      ch.s_hi = d * sc[si + 4]; ch.m_hi = 32.f * ch.s_hi;
+      break;
+    }
+    case T_Q8_0: {
+      const int8_t* q = reinterpret_cast<const int8_t*>(base + P.p0 + row * P.s0 + 32 * c);
+      std::memcpy(ch.w, q, 32);
+      const float d = hf(base + P.p1 + row * P.s1 + 2 * c);
+      ch.off_lo = 32 * c;
+      ch.off_hi = 32 * c + 16;
+      ch.s_lo = ch.s_hi = d;
+      ch.m_lo = ch.m_hi = 0.f;
+      break;
+    }
+    case T_F32:
+    case T_F16: {
+      ch.is_float = true;
+      for (int i = 0; i < 32; ++i)
+        ch.wf[i] = W.type == T_F32 ? reinterpret_cast<const float*>(base + row * P.s0)[32 * c + i]
+                                   : h2f(reinterpret_cast<const uint16_t*>(base + row * P.s0)[32 * c + i]);
+      ch.off_lo = 32 * c;
+      ch.off_hi = 32 * c + 16;
+      break;
+    }
+    default:
+      throw std::runtime_error("cpu: unsupported weight type");
+  }
+}
+
+// y[t][r] (+)= W[r] . x_t for rows r of a (possibly expert-offset) matrix
+void gemm_rows(const CpuMat& W, const uint8_t* base, const Q8& xq, int T, float* y, int ldy, bool add) {
+  const int K = W.K, nchunks = K / 32, nb = K / 32, n16 = K / 16;
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < W.rows; ++r) {
+    float acc[128];
+    for (int t = 0; t < T; ++t) acc[t] = 0.f;
+    Chunk ch;
+    for (int c = 0; c < nchunks; ++c) {
+      decode_chunk(W, base, (size_t)r, c, ch);
+      const int blo = ch.off_lo >> 5, bhi = ch.off_hi >> 5;
+      for (int t = 0; t < T; ++t) {
+        const int8_t* x = xq.q.data() + (size_t)t * K;
+        const float* xd = xq.d.data() + (size_t)t * nb;
+        if (ch.is_float) {
+          float s = 0.f;
+          for (int i = 0; i < 16; ++i) s += ch.wf[i] * x[ch.off_lo + i] * xd[blo];
+          for (int i = 0; i < 16; ++i) s += ch.wf[16 + i] * x[ch.off_hi + i] * xd[bhi];
+          acc[t] += s;
+          continue;
+        }
+        int dl = 0, dh = 0;
+        for (int i = 0; i < 16; ++i) dl += (int)ch.w[i] * x[ch.off_lo + i];
+        for (int i = 0; i < 16; ++i) dh += (int)ch.w[16 + i] * x[ch.off_hi + i];
+        const int* s16 = xq.s16.data() + (size_t)t * n16;
+        acc[t] += xd[blo] * (ch.s_lo * (float)dl - ch.m_lo * (float)s16[ch.off_lo >> 4]) +
+                  xd[bhi] * (ch.s_hi * (float)dh - ch.m_hi * (float)s16[ch.off_hi >> 4]);
+      }
+    }
+    for (int t = 0; t < T; ++t) {
+      float* o = y + (size_t)t * ldy + r;
+      *o = add ? *o + acc[t] : acc[t];
+    }
+  }
+}
+
+inline float silu(float g) { return g / (1.f + std::exp(-g)); }
+
+}  // namespace
+
+float splitmix_uniform(uint64_t seed, uint64_t step) {
+  uint64_t x = seed ^ (step * 0xD1B54A32D192ED03ull);
+  x += 0x9E3779B97F4A7C15ull;
+  uint64_t z = x;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.f / 16777216.f);
+}
+
+int cpu_sample(std::vector<float> l, const std::vector<int>& window, const CpuSampling& sp, int step) {
+  const int V = (int)l.size();
+  // penalties (first occurrence applies, count = occurrences in the window)
+  if (sp.last_n > 0 && !window.empty()) {
+    const int n = (int)window.size(), w0 = std::max(0, n - sp.last_n);
+    for (int i = w0; i < n; ++i) {
+      const int t = window[i];
+      if (t < 0 || t >= V) continue;
+      bool first = true;
+      int cnt = 0;
+      for (int j = w0; j < n; ++j) {
+        if (window[j] == t) { ++cnt; if (j < i) first = false; }
+      }
+      if (!first) continue;
+      float v = l[t];
+      v = v <= 0.f ? v * sp.repeat_penalty : v / sp.repeat_penalty;
+      v -= (float)cnt * sp.freq_penalty + sp.presence_penalty;
+      l[t] = v;
+    }
+  }
+  if (sp.temp <= 0.f) return (int)(std::max_element(l.begin(), l.end()) - l.begin());
+  const int k = (sp.top_k > 0 && sp.top_k < V) ? sp.top_k : V;
+  std::vector<int> ids(V);
+  std::iota(ids.begin(), ids.end(), 0);
+  auto better = [&](int a, int b) { return l[a] > l[b] || (l[a] == l[b] && a < b); };
+  std::partial_sort(ids.begin(), ids.begin() + k, ids.end(), better);
+  ids.resize(k);
+  int n = k;
+  const double v0 = l[ids[0]];
+  if (sp.top_p < 1.f) {
+    double tot = 0;
+    for (int i = 0; i < n; ++i) tot += std::exp((double)l[ids[i]] - v0);
+    double cum = 0;
+    for (int i = 0; i < n; ++i) {
+      cum += std::exp((double)l[ids[i]] - v0) / tot;
+      if (cum >= sp.top_p) { n = i + 1; break; }
+    }
+  }
+  if (sp.min_p > 0.f) {
+    const double thr = v0 + std::log((double)sp.min_p);
+    int keep = 0;
+    for (int i = 0; i < n; ++i) keep += (double)l[ids[i]] >= thr;
+    n = std::max(1, keep);
+  }
+  std::vector<double> cw(n);
+  double acc = 0;
+  for (int i = 0; i < n; ++i) {
+    acc += std::exp(((double)l[ids[i]] - v0) / sp.temp);
+    cw[i] = acc;
+  }
+  const double u = splitmix_uniform(sp.seed, (uint64_t)step) * acc;
+  for (int i = 0; i < n; ++i)
+    if (cw[i] > u) return ids[i];
+  return ids[n - 1];
+}
+
+CpuEngine::CpuEngine(const std::string& path, int n_ctx, int n_threads, int n_batch)
+    : n_ctx_(n_ctx), n_threads_(n_threads > 0 ? n_threads : omp_get_max_threads()), n_batch_(std::min(n_batch, 128)) {
+  omp_set_num_threads(n_threads_);
+  GGUFFile f(path);
+  std::string arch = f.get_str("general.architecture", "llama");
+  auto gi = [&](const char* k, int64_t d) { return (int)f.get_int(arch + "." + k, d); };
+  n_embd_ = gi("embedding_length", 0);
+  n_layer_ = gi("block_count", 0);
+  n_head_ = gi("attention.head_count", 0);
+  n_head_kv_ = gi("attention.head_count_kv", n_head_);
+  head_dim_ = gi("rope.dimension_count", n_embd_ / n_head_);
+  n_ff_ = gi("feed_forward_length", 0);
+  n_expert_ = gi("expert_count", 0);
+  n_expert_used_ = gi("expert_used_count", 0);
+  eps_ = (float)f.get_float(arch + ".attention.layer_norm_rms_epsilon", 1e-5);
+  rope_base_ = (float)f.get_float(arch + ".rope.freq_base", 10000.0);
+  if (n_ctx_ <= 0) n_ctx_ = gi("context_length", 2048);
+  tok_embd_ = load_mat(f, "token_embd.weight");
+  n_vocab_ = tok_embd_.rows;
+  out_norm_ = load_f32(f, "output_norm.weight");
+  output_ = f.find("output.weight") ? load_mat(f, "output.weight") : tok_embd_;
+  layers_.resize(n_layer_);
+  for (int l = 0; l < n_layer_; ++l) {
+    const std::string p = "blk." + std::to_string(l) + ".";
+    CpuLayer& L = layers_[l];
+    L.attn_norm = load_f32(f, p + "attn_norm.weight");
+    L.ffn_norm = load_f32(f, p + "ffn_norm.weight");
+    L.wq = load_mat(f, p + "attn_q.weight");
+    L.wk = load_mat(f, p + "attn_k.weight");
+    L.wv = load_mat(f, p + "attn_v.weight");
+    L.wo = load_mat(f, p + "attn_output.weight");
+    if (n_expert_ > 0) {
+      L.router = load_mat(f, p + "ffn_gate_inp.weight");
+      L.gu_exps = load_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", n_expert_);
+      L.down_exps = load_mat(f, p + "ffn_down_exps.weight", n_expert_);
+    } else {
+      L.w_gu = load_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight");
+      L.w_down = load_mat(f, p + "ffn_down.weight");
+    }
+  }
+  const size_t kv = (size_t)n_layer_ * n_head_kv_ * n_ctx_ * head_dim_;
+  kc_.assign(kv, 0);
+  vc_.assign(kv, 0);
+  rope_cos_.resize((size_t)n_ctx_ * head_dim_ / 2);
+  rope_sin_.resize(rope_cos_.size());
+  for (int p = 0; p < n_ctx_; ++p)
+    for (int i = 0; i < head_dim_ / 2; ++i) {
+      const double a = p * std::pow((double)rope_base_, -2.0 * i / head_dim_);
+      rope_cos_[(size_t)p * head_dim_ / 2 + i] = (float)std::cos(a);
+      rope_sin_[(size_t)p * head_dim_ / 2 + i] = (float)std::sin(a);
+    }
+}
+
+void CpuEngine::matmul(const CpuMat& W, const float* x, int T, int ldx, float* y, int ldy,
+                       const std::vector<float>* norm, bool add) const {
+  Q8 q;
+  quantize_rows(x, T, ldx, W.K, norm, eps_, q);
+  gemm_rows(W, W.data.data(), q, T, y, ldy, add);
+}
+
+void CpuEngine::embed(const int* tokens, int T, float* x) const {
+  const int d = n_embd_;
+  for (int t = 0; t < T; ++t) {
+    Chunk ch;
+    for (int c = 0; c < d / 32; ++c) {
+      decode_chunk(tok_embd_, tok_embd_.data.data(), (size_t)tokens[t], c, ch);
+      float* xr = x + (size_t)t * d;
+      for (int i = 0; i < 16; ++i) {
+        xr[ch.off_lo + i] = ch.is_float ? ch.wf[i] : ch.s_lo * ch.w[i] - ch.m_lo;
+        xr[ch.off_hi + i] = ch.is_float ? ch.wf[16 + i] : ch.s_hi * ch.w[16 + i] - ch.m_hi;
+      }
+    }
+  }
+}
+
+void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) const {
+  const int hd = head_dim_, G = n_head_ / n_head_kv_;
+  const float scale = 1.f / std::sqrt((float)hd);
+  const uint16_t* kc = kc_.data() + (size_t)l * n_head_kv_ * n_ctx_ * hd;
+  const uint16_t* vc = vc_.data() + (size_t)l * n_head_kv_ * n_ctx_ * hd;
+#pragma omp parallel for collapse(2) schedule(static)
+  for (int t = 0; t < T; ++t)
+    for (int h = 0; h < n_head_; ++h) {
+      const int L = pos0 + t + 1, kvh = h / G;
+      const float* qh = q + ((size_t)t * n_head_ + h) * hd;
+      std::vector<float> s(L);
+      float m = -INFINITY;
+      for (int j = 0; j < L; ++j) {
+        const uint16_t* kr = kc + ((size_t)kvh * n_ctx_ + j) * hd;
+        float a = 0.f;
+        for (int i = 0; i < hd; ++i) a += qh[i] * h2f(kr[i]);
+        s[j] = a * scale;
+        m = std::max(m, s[j]);
+      }
+      float den = 0.f;
+      for (int j = 0; j < L; ++j) { s[j] = std::exp(s[j] - m); den += s[j]; }
+      float* o = out + ((size_t)t * n_head_ + h) * hd;
+      for (int i = 0; i < hd; ++i) o[i] = 0.f;
+      for (int j = 0; j < L; ++j) {
+        const uint16_t* vr = vc + ((size_t)kvh * n_ctx_ + j) * hd;
+        const float p = s[j] / den;
+        for (int i = 0; i < hd; ++i) o[i] += p * h2f(vr[i]);
+      }
+    }
+}
+
+void CpuEngine::ffn(const CpuLayer& L, float* x, int T) {
+  const int d = n_embd_, F = n_ff_;
+  if (n_expert_ == 0) {
+    std::vector<float> gu((size_t)T * 2 * F), h((size_t)T * F);
+    matmul(L.w_gu, x, T, d, gu.data(), 2 * F, &L.ffn_norm, false);
+    for (int t = 0; t < T; ++t)
+      for (int f = 0; f < F; ++f) {
+        const int r = (f >> 5) * 64 + (f & 31);
+        h[(size_t)t * F + f] = silu(gu[(size_t)t * 2 * F + r]) * gu[(size_t)t * 2 * F + r + 32];
+      }
+    matmul(L.w_down, h.data(), T, F, x, d, nullptr, true);
+    return;
+  }
+  const int E = n_expert_;
+  std::vector<float> rl((size_t)T * E);
+  matmul(L.router, x, T, d, rl.data(), E, &L.ffn_norm, false);
+  Q8 xq;
+  quantize_rows(x, T, d, d, &L.ffn_norm, eps_, xq);
+  std::vector<float> add((size_t)T * d, 0.f);
+  for (int t = 0; t < T; ++t) {
+    std::vector<double> p(E);
+    double mx = -1e300, sum = 0;
+    for (int e = 0; e < E; ++e) mx = std::max(mx, (double)rl[(size_t)t * E + e]);
+    for (int e = 0; e < E; ++e) { p[e] = std::exp(rl[(size_t)t * E + e] - mx); sum += p[e]; }
+    std::vector<int> ids(E);
+    std::iota(ids.begin(), ids.end(), 0);
+    std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return p[a] > p[b]; });
+    double wsum = 0;
+    for (int j = 0; j < n_expert_used_; ++j) wsum += p[ids[j]] / sum;
+    Q8 one;
+    one.K = d;
+    one.q.assign(xq.q.begin() + (size_t)t * d, xq.q.begin() + (size_t)(t + 1) * d);
+    one.d.assign(xq.d.begin() + (size_t)t * d / 32, xq.d.begin() + (size_t)(t + 1) * d / 32);
+    one.s16.assign(xq.s16.begin() + (size_t)t * d / 16, xq.s16.begin() + (size_t)(t + 1) * d / 16);
+    for (int j = 0; j < n_expert_used_; ++j) {
+      const int e = ids[j];
+      const float w = (float)(p[e] / sum / wsum);
+      std::vector<float> gu(2 * F), h(F), y(d);
+      CpuMat gm = L.gu_exps;  // shallow view: same planes, expert offset via base pointer
+      gemm_rows(L.gu_exps, L.gu_exps.data.data() + L.gu_exps.expert_stride * e, one, 1, gu.data(), 2 * F, false);
+      for (int f = 0; f < F; ++f) {
+        const int r = (f >> 5) * 64 + (f & 31);
+        h[f] = silu(gu[r]) * gu[r + 32];
+      }
+      Q8 hq;
+      quantize_rows(h.data(), 1, F, F, nullptr, eps_, hq);
+      gemm_rows(L.down_exps, L.down_exps.data.data() + L.down_exps.expert_stride * e, hq, 1, y.data(), d, false);
+      for (int i = 0; i < d; ++i) add[(size_t)t * d + i] += w * y[i];
+      (void)gm;
+    }
+  }
+  for (size_t i = 0; i < add.size(); ++i) x[i] += add[i];
+}
+
+void CpuEngine::run_layers(float* x, int T, int pos0, int l0, int l1) {
+  const int d = n_embd_, hd = head_dim_;
+  const int nq = n_head_ * hd, nkv = n_head_kv_ * hd;
+  std::vector<float> q((size_t)T * nq), k((size_t)T * nkv), v((size_t)T * nkv), att((size_t)T * nq);
+  for (int l = l0; l < l1; ++l) {
+    const CpuLayer& L = layers_[l];
+    Q8 xq;
+    quantize_rows(x, T, d, d, &L.attn_norm, eps_, xq);
+    gemm_rows(L.wq, L.wq.data.data(), xq, T, q.data(), nq, false);
+    gemm_rows(L.wk, L.wk.data.data(), xq, T, k.data(), nkv, false);
+    gemm_rows(L.wv, L.wv.data.data(), xq, T, v.data(), nkv, false);
+    for (int t = 0; t < T; ++t) {
+      const int pos = pos0 + t;
+      auto rope = [&](float* r, int n) {
+        for (int i = 0; i < n; i += 2) {
+          const int dd = i % hd;
+          const float c = rope_cos_[(size_t)pos * hd / 2 + dd / 2], s = rope_sin_[(size_t)pos * hd / 2 + dd / 2];
+          const float a0 = r[i], a1 = r[i + 1];
+          r[i] = a0 * c - a1 * s;
+          r[i + 1] = a0 * s + a1 * c;
+        }
+      };
+      rope(q.data() + (size_t)t * nq, nq);
+      rope(k.data() + (size_t)t * nkv, nkv);
+      for (int i = 0; i < nkv; ++i) {
+        const size_t ci = (((size_t)l * n_head_kv_ + i / hd) * n_ctx_ + pos) * hd + i % hd;
+        kc_[ci] = f2h(k[(size_t)t * nkv + i]);
+        vc_[ci] = f2h(v[(size_t)t * nkv + i]);
+      }
+    }
+    attention(l, q.data(), T, pos0, att.data());
+    matmul(L.wo, att.data(), T, nq, x, d, nullptr, true);
+    ffn(L, x, T);
+  }
+}
+
+void CpuEngine::head(const float* xrow, float* logits) const {
+  matmul(output_, xrow, 1, n_embd_, logits, n_vocab_, &out_norm_, false);
+}
+
+std::vector<float> CpuEngine::eval_logits(const std::vector<int>& tokens, int pos0) {
+  const int T = (int)tokens.size();
+  if (T <= 0 || pos0 + T > n_ctx_) throw std::runtime_error("eval_logits: bad range");
+  std::vector<float> x;
+  for (int p = 0; p < T; p += n_batch_) {
+    const int n = std::min(n_batch_, T - p);
+    x.assign((size_t)n * n_embd_, 0.f);
+    embed(tokens.data() + p, n, x.data());
+    run_layers(x.data(), n, pos0 + p, 0, n_layer_);
+  }
+  std::vector<float> logits(n_vocab_);
+  const int last = (T - 1) % n_batch_;
+  head(x.data() + (size_t)last * n_embd_, logits.data());
+  return logits;
+}
+
+CpuGenOut CpuEngine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const CpuSampling& sp,
+                              const std::vector<int>& stop, const std::function<bool()>& poll,
+                              const std::function<void(int)>& on_token) {
+  CpuGenOut out;
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt >= n_ctx_) throw std::runtime_error("prompt exceeds context window");
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  const double t0 = now_s();
+  std::vector<int> suffix(prompt.begin() + n_keep, prompt.end());
+  std::vector<float> logits = eval_logits(suffix, n_keep);
+  const double t1 = now_s();
+  out.prefill_s = t1 - t0;
+  out.n_prefilled = n_prompt - n_keep;
+  std::vector<int> hist(prompt);
+  out.finish = "length";
+  std::vector<float> x(n_embd_);
+  for (int step = 0; step < max_new; ++step) {
+    if (poll && poll()) { out.finish = "cancelled"; break; }
+    const int w0 = std::max(0, (int)hist.size() - std::max(sp.last_n, 0));
+    std::vector<int> window(hist.begin() + w0, hist.end());
+    const int tok = cpu_sample(logits, window, sp, step);
+    out.tokens.push_back(tok);
+    hist.push_back(tok);
+    if (on_token) on_token(tok);
+    if (std::find(stop.begin(), stop.end(), tok) != stop.end()) { out.finish = "stop"; break; }
+    const int pos = (int)hist.size() - 1;
+    if (step + 1 == max_new || pos >= n_ctx_) break;
+    embed(&tok, 1, x.data());
+    run_layers(x.data(), 1, pos, 0, n_layer_);
+    head(x.data(), logits.data());
+  }
+  out.decode_s = now_s() - t1;
+  out.n_evaluated = n_prompt + std::max(0, (int)out.tokens.size() - 1);
+  return out;
+}
+
+}  // namespace lfk

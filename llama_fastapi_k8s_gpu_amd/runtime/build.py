@@ -108,7 +108,7 @@ def build_hip(jobs: int = 8, verbose: bool = True) -> str:
 
 
 def build_cpu(jobs: int = 8, verbose: bool = True) -> str:
-    flags = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-mavx2", "-mfma", "-DLFK_NO_HIP"] + _includes()
+    flags = ["-O3", "-fPIC", "-std=c++17", "-fopenmp", "-mavx2", "-mfma", "-mf16c", "-DLFK_NO_HIP"] + _includes()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(["g++"], s, flags), CPU_SOURCES))
     out = cpu_so_path()

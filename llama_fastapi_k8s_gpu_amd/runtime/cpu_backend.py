@@ -1,0 +1,77 @@
+"""CpuBackend: the C++ CPU engine (``csrc/cpu/cpu_backend.cpp``) behind the
+``Llama`` facade for ``n_gpu_layers=0`` (BASELINE config #1: TinyLlama Q8_0 on
+the CPU, reference api.py:24-28 with ``N_GPU_LAYERS=0``).
+
+The CPU engine uses the same planar weight layout and the same q8-activation
+integer dot products as the gfx950 GEMV, the same f16 KV cache and the same
+SplitMix64 draw, so CPU and GPU runs of one seed agree up to float rounding.
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable, Optional, Sequence
+
+from ..engine.backends import GenerationResult
+from ..engine.sampling import SamplingParams, sample_token
+from . import load_cpu
+
+
+def sampling_dict(p: SamplingParams) -> dict:
+    return {"top_k": p.top_k, "top_p": p.top_p, "min_p": p.min_p, "temperature": p.temperature,
+            "repeat_penalty": p.repeat_penalty, "frequency_penalty": p.frequency_penalty,
+            "presence_penalty": p.presence_penalty, "last_n": p.last_n, "seed": p.seed & 0xFFFFFFFFFFFFFFFF}
+
+
+class CpuBackend:
+    name = "cpu"
+
+    def __init__(self, model_path: str, n_ctx: int = 512, n_threads: Optional[int] = None, n_batch: int = 64, **_):
+        cpu = load_cpu()
+        threads = int(n_threads or os.environ.get("N_THREADS", 0) or 0)
+        self.engine = cpu.CpuEngine(model_path, n_ctx=n_ctx, n_threads=threads, n_batch=min(n_batch, 128))
+        self.n_ctx = n_ctx
+
+    def health(self):
+        return {"ok": True, "backend": self.name}
+
+    def device_memory(self):
+        return {}
+
+    def eval_logits(self, tokens: Sequence[int], pos0: int = 0):
+        return self.engine.eval_logits(list(tokens), int(pos0))
+
+    def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
+                 stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
+                 on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:
+        if params.tfs_z != 1.0 or params.typical_p != 1.0:
+            return self._generate_host_sampler(prompt, n_keep, max_new, params, stop_ids, poll, on_token)
+        r = self.engine.generate(list(prompt), int(n_keep), int(max_new), sampling_dict(params), list(stop_ids),
+                                 poll, on_token)
+        return GenerationResult(list(r["tokens"]), r["finish"], int(r["n_evaluated"]), r["prefill_s"],
+                                r["decode_s"], int(r["n_prefilled"]))
+
+    def _generate_host_sampler(self, prompt, n_keep, max_new, params, stop_ids, poll, on_token):
+        import time
+        t0 = time.perf_counter()
+        hist = list(prompt)
+        logits = self.engine.eval_logits(hist[n_keep:], n_keep)
+        t1 = time.perf_counter()
+        out, reason = [], "length"
+        stops = set(stop_ids)
+        for step in range(max_new):
+            if poll is not None and poll():
+                reason = "cancelled"
+                break
+            tok = sample_token(logits, hist[-params.last_n:] if params.last_n else [], params, step)
+            out.append(tok)
+            hist.append(tok)
+            if on_token:
+                on_token(tok)
+            if tok in stops:
+                reason = "stop"
+                break
+            if step + 1 == max_new or len(hist) > self.n_ctx - 1:
+                break
+            logits = self.engine.eval_logits([tok], len(hist) - 1)
+        return GenerationResult(out, reason, len(prompt) + max(0, len(out) - 1), t1 - t0,
+                                time.perf_counter() - t1, len(prompt) - n_keep)
