@@ -7,6 +7,8 @@
 #include "cpu/cpu_backend.h"
 #include "runtime/repack.h"
 
+#include <cstring>
+
 namespace py = pybind11;
 using namespace lfk;
 
@@ -27,11 +29,53 @@ static CpuSampling parse_sampling(py::dict sp) {
 PYBIND11_MODULE(_cpu, m) {
   m.doc() = "C++ CPU backend (OpenMP): GGUF engine for n_gpu_layers = 0";
   py::class_<CpuEngine>(m, "CpuEngine")
-      .def(py::init([](const std::string& path, int n_ctx, int n_threads, int n_batch) {
+      .def(py::init([](const std::string& path, int n_ctx, int n_threads, int n_batch, int tp_rank, int tp_size,
+                       int layer_end, bool load_head) {
+             CpuOptions o;
+             o.n_ctx = n_ctx;
+             o.n_threads = n_threads;
+             o.n_batch = n_batch;
+             o.tp_rank = tp_rank;
+             o.tp_size = tp_size;
+             o.layer_end = layer_end;
+             o.load_head = load_head;
              py::gil_scoped_release nogil;
-             return std::make_unique<CpuEngine>(path, n_ctx, n_threads, n_batch);
+             return std::make_unique<CpuEngine>(path, o);
            }),
-           py::arg("path"), py::arg("n_ctx") = 512, py::arg("n_threads") = 0, py::arg("n_batch") = 64)
+           py::arg("path"), py::arg("n_ctx") = 512, py::arg("n_threads") = 0, py::arg("n_batch") = 64,
+           py::arg("tp_rank") = 0, py::arg("tp_size") = 1, py::arg("layer_end") = -1, py::arg("load_head") = true)
+      .def("set_comm",
+           [](CpuEngine& e, py::object allreduce, py::object allgather) {
+             // callbacks get numpy views of the engine's buffers (no copy); they run with the GIL held
+             auto ar = [allreduce](float* buf, size_t n) {
+               py::gil_scoped_acquire g;
+               py::array_t<float> a({(py::ssize_t)n}, {(py::ssize_t)sizeof(float)}, buf, py::none());
+               allreduce(a);
+             };
+             auto ag = [allgather](const float* loc, float* all, size_t n) {
+               py::gil_scoped_acquire g;
+               py::array_t<float> a({(py::ssize_t)n}, {(py::ssize_t)sizeof(float)}, const_cast<float*>(loc),
+                                    py::none());
+               py::array_t<float> out = allgather(a).cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+               std::memcpy(all, out.data(), sizeof(float) * out.size());
+             };
+             e.set_comm(ar, ag);
+           })
+      .def("eval_hidden",
+           [](CpuEngine& e, const std::vector<int>& tokens, int pos0) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.eval_hidden(tokens, pos0);
+             }
+             py::array_t<float> a({(py::ssize_t)tokens.size(), (py::ssize_t)(v.size() / tokens.size())});
+             std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+             return a;
+           })
+      .def_property_readonly("layer_end", &CpuEngine::layer_end)
+      .def_property_readonly("n_embd", &CpuEngine::n_embd)
+      .def_property_readonly("tp_rank", &CpuEngine::tp_rank)
+      .def_property_readonly("tp_size", &CpuEngine::tp_size)
       .def("generate",
            [](CpuEngine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
               const std::vector<int>& stop, py::object poll, py::object on_token) {

@@ -34,8 +34,9 @@ PYBIND11_MODULE(_hip, m) {
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
-                       int tp_size, py::bytes nccl_id) {
+                       int tp_size, py::bytes nccl_id, int layer_begin) {
              EngineOptions o;
+             o.layer_begin = layer_begin;
              o.n_ctx = n_ctx;
              o.n_batch = n_batch;
              o.device = device;
@@ -48,7 +49,7 @@ PYBIND11_MODULE(_hip, m) {
            }),
            py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
-           py::arg("nccl_id") = py::bytes(""))
+           py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0)
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
@@ -92,6 +93,20 @@ PYBIND11_MODULE(_hip, m) {
              }
              return py::array_t<float>(v.size(), v.data());
            })
+      .def("eval_hidden",
+           [](Engine& e, py::array_t<float, py::array::c_style | py::array::forcecast> x, int pos0) {
+             if (x.ndim() != 2 || x.shape(1) != e.hparams().n_embd)
+               throw std::runtime_error("eval_hidden: x must be [T, n_embd]");
+             std::vector<float> v;
+             const int T = (int)x.shape(0);
+             const float* ptr = x.data();
+             {
+               py::gil_scoped_release nogil;
+               v = e.eval_hidden(ptr, T, pos0);
+             }
+             return py::array_t<float>(v.size(), v.data());
+           })
+      .def_property_readonly("layer_begin", &Engine::layer_begin)
       .def("decode_logits",
            [](Engine& e, int token, int pos) {
              std::vector<float> v;

@@ -12,6 +12,7 @@
 
 #include "../runtime/gguf.h"
 #include "../runtime/repack.h"
+#include "../runtime/shard.h"
 
 namespace lfk {
 
@@ -23,24 +24,33 @@ double now_s() {
 inline float h2f(uint16_t h) { return _cvtsh_ss(h); }
 inline uint16_t f2h(float f) { return _cvtss_sh(f, 0); }
 
-CpuMat load_mat(const GGUFFile& f, const std::string& name, int n_expert = 0) {
+// rows [r0, r0+R) x columns [c0, c0+K) of a (per-expert) ggml matrix -> planar; rows past the
+// source are zero (vocab padding of the last TP shard). R < 0 / K < 0 = everything.
+CpuMat load_mat(const GGUFFile& f, const std::string& name, int n_expert = 0, size_t r0 = 0, long R = -1,
+                size_t c0 = 0, long K = -1) {
   const GGUFTensor* t = f.find(name);
   if (!t) throw std::runtime_error("missing tensor " + name);
+  const size_t K_src = (size_t)t->ne[0], R_src = (size_t)t->ne[1];
   CpuMat m;
   m.type = t->type;
-  m.K = (int)t->ne[0];
-  m.rows = (int)t->ne[1];
+  m.K = K < 0 ? (int)K_src : (int)K;
+  m.rows = R < 0 ? (int)R_src : (int)R;
   const int E = n_expert > 0 ? n_expert : 1;
   const size_t one = qbytes(m.type, m.rows, m.K);
-  m.data.resize(one * E);
+  const size_t src_one = qbytes(m.type, R_src, K_src);
+  const size_t avail = r0 < R_src ? std::min((size_t)m.rows, R_src - r0) : 0;
+  m.data.assign(one * E, 0);
   for (int e = 0; e < E; ++e)
-    repack_planar(m.type, f.data(*t) + one * e, m.K, 0, m.rows, 0, m.K, m.data.data() + one * e, m.rows, 0, 0);
+    repack_planar(m.type, f.data(*t) + src_one * e, K_src, r0, avail, c0, m.K, m.data.data() + one * e, m.rows, 0,
+                  0);
   m.P = planes_of(m.type, m.rows, m.K);
   m.expert_stride = n_expert > 0 ? one : 0;
   return m;
 }
 
-CpuMat load_gate_up(const GGUFFile& f, const std::string& g, const std::string& u, int n_expert = 0) {
+// gate/up features [f0, f0+F) interleaved in 32-row groups (the GPU layout)
+CpuMat load_gate_up(const GGUFFile& f, const std::string& g, const std::string& u, int n_expert, size_t f0,
+                    long F) {
   const GGUFTensor* tg = f.find(g);
   const GGUFTensor* tu = f.find(u);
   if (!tg || !tu) throw std::runtime_error("missing " + g);
@@ -48,15 +58,16 @@ CpuMat load_gate_up(const GGUFFile& f, const std::string& g, const std::string& 
   CpuMat m;
   m.type = tg->type;
   m.K = (int)tg->ne[0];
-  const int F = (int)tg->ne[1];
-  m.rows = 2 * F;
+  const size_t F_src = (size_t)tg->ne[1];
+  if (F < 0) F = (long)F_src;
+  m.rows = 2 * (int)F;
   const int E = n_expert > 0 ? n_expert : 1;
   const size_t one = qbytes(m.type, m.rows, m.K);
-  const size_t src_one = qbytes(m.type, F, m.K);
+  const size_t src_one = qbytes(m.type, F_src, m.K);
   m.data.resize(one * E);
   for (int e = 0; e < E; ++e) {
-    repack_planar(m.type, f.data(*tg) + src_one * e, m.K, 0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 0);
-    repack_planar(m.type, f.data(*tu) + src_one * e, m.K, 0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 32);
+    repack_planar(m.type, f.data(*tg) + src_one * e, m.K, f0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 0);
+    repack_planar(m.type, f.data(*tu) + src_one * e, m.K, f0, F, 0, m.K, m.data.data() + one * e, m.rows, 32, 32);
   }
   m.P = planes_of(m.type, m.rows, m.K);
   m.expert_stride = n_expert > 0 ? one : 0;
@@ -302,8 +313,9 @@ int cpu_sample(std::vector<float> l, const std::vector<int>& window, const CpuSa
   return ids[n - 1];
 }
 
-CpuEngine::CpuEngine(const std::string& path, int n_ctx, int n_threads, int n_batch)
-    : n_ctx_(n_ctx), n_threads_(n_threads > 0 ? n_threads : omp_get_max_threads()), n_batch_(std::min(n_batch, 128)) {
+CpuEngine::CpuEngine(const std::string& path, const CpuOptions& o)
+    : opt_(o), n_ctx_(o.n_ctx), n_threads_(o.n_threads > 0 ? o.n_threads : omp_get_max_threads()),
+      n_batch_(std::max(1, std::min(o.n_batch, 128))) {
   omp_set_num_threads(n_threads_);
   GGUFFile f(path);
   std::string arch = f.get_str("general.architecture", "llama");
@@ -319,30 +331,37 @@ CpuEngine::CpuEngine(const std::string& path, int n_ctx, int n_threads, int n_ba
   eps_ = (float)f.get_float(arch + ".attention.layer_norm_rms_epsilon", 1e-5);
   rope_base_ = (float)f.get_float(arch + ".rope.freq_base", 10000.0);
   if (n_ctx_ <= 0) n_ctx_ = gi("context_length", 2048);
+  const GGUFTensor* emb = f.find("token_embd.weight");
+  if (!emb) throw std::runtime_error("missing token_embd.weight");
+  n_vocab_ = (int)emb->ne[1];
+  sp_ = make_shard_plan(n_head_, n_head_kv_, head_dim_, n_ff_, n_vocab_, o.tp_size, o.tp_rank);
+  layer_end_ = o.layer_end < 0 ? n_layer_ : std::min(o.layer_end, n_layer_);
   tok_embd_ = load_mat(f, "token_embd.weight");
-  n_vocab_ = tok_embd_.rows;
-  out_norm_ = load_f32(f, "output_norm.weight");
-  output_ = f.find("output.weight") ? load_mat(f, "output.weight") : tok_embd_;
+  if (o.load_head) {
+    out_norm_ = load_f32(f, "output_norm.weight");
+    const std::string on = f.find("output.weight") ? "output.weight" : "token_embd.weight";
+    output_ = load_mat(f, on, 0, sp_.v_row0(), sp_.V_l);
+  }
   layers_.resize(n_layer_);
-  for (int l = 0; l < n_layer_; ++l) {
+  for (int l = 0; l < layer_end_; ++l) {
     const std::string p = "blk." + std::to_string(l) + ".";
     CpuLayer& L = layers_[l];
     L.attn_norm = load_f32(f, p + "attn_norm.weight");
     L.ffn_norm = load_f32(f, p + "ffn_norm.weight");
-    L.wq = load_mat(f, p + "attn_q.weight");
-    L.wk = load_mat(f, p + "attn_k.weight");
-    L.wv = load_mat(f, p + "attn_v.weight");
-    L.wo = load_mat(f, p + "attn_output.weight");
+    L.wq = load_mat(f, p + "attn_q.weight", 0, sp_.q_row0(), sp_.nq);
+    L.wk = load_mat(f, p + "attn_k.weight", 0, sp_.kv_row0(), sp_.nkvd);
+    L.wv = load_mat(f, p + "attn_v.weight", 0, sp_.kv_row0(), sp_.nkvd);
+    L.wo = load_mat(f, p + "attn_output.weight", 0, 0, -1, sp_.q_row0(), sp_.nq);
     if (n_expert_ > 0) {
       L.router = load_mat(f, p + "ffn_gate_inp.weight");
-      L.gu_exps = load_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", n_expert_);
-      L.down_exps = load_mat(f, p + "ffn_down_exps.weight", n_expert_);
+      L.gu_exps = load_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", n_expert_, sp_.f0(), sp_.F_l);
+      L.down_exps = load_mat(f, p + "ffn_down_exps.weight", n_expert_, 0, -1, sp_.f0(), sp_.F_l);
     } else {
-      L.w_gu = load_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight");
-      L.w_down = load_mat(f, p + "ffn_down.weight");
+      L.w_gu = load_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight", 0, sp_.f0(), sp_.F_l);
+      L.w_down = load_mat(f, p + "ffn_down.weight", 0, 0, -1, sp_.f0(), sp_.F_l);
     }
   }
-  const size_t kv = (size_t)n_layer_ * n_head_kv_ * n_ctx_ * head_dim_;
+  const size_t kv = (size_t)layer_end_ * sp_.nkv_l * n_ctx_ * head_dim_;
   kc_.assign(kv, 0);
   vc_.assign(kv, 0);
   rope_cos_.resize((size_t)n_ctx_ * head_dim_ / 2);
@@ -355,6 +374,18 @@ CpuEngine::CpuEngine(const std::string& path, int n_ctx, int n_threads, int n_ba
     }
 }
 
+void CpuEngine::set_comm(std::function<void(float*, size_t)> allreduce,
+                         std::function<void(const float*, float*, size_t)> allgather) {
+  allreduce_ = std::move(allreduce);
+  allgather_ = std::move(allgather);
+}
+
+void CpuEngine::reduce(float* y, size_t n) {
+  if (sp_.tp == 1) return;
+  if (!allreduce_) throw std::runtime_error("tensor parallel CPU engine: set_comm() was not called");
+  allreduce_(y, n);
+}
+
 void CpuEngine::matmul(const CpuMat& W, const float* x, int T, int ldx, float* y, int ldy,
                        const std::vector<float>* norm, bool add) const {
   Q8 q;
@@ -365,6 +396,7 @@ void CpuEngine::matmul(const CpuMat& W, const float* x, int T, int ldx, float* y
 void CpuEngine::embed(const int* tokens, int T, float* x) const {
   const int d = n_embd_;
   for (int t = 0; t < T; ++t) {
+    if (tokens[t] < 0 || tokens[t] >= n_vocab_) throw std::runtime_error("token id out of range");
     Chunk ch;
     for (int c = 0; c < d / 32; ++c) {
       decode_chunk(tok_embd_, tok_embd_.data.data(), (size_t)tokens[t], c, ch);
@@ -378,15 +410,15 @@ void CpuEngine::embed(const int* tokens, int T, float* x) const {
 }
 
 void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) const {
-  const int hd = head_dim_, G = n_head_ / n_head_kv_;
+  const int hd = head_dim_, nh = sp_.nh_l, nkv = sp_.nkv_l, G = nh / nkv;
   const float scale = 1.f / std::sqrt((float)hd);
-  const uint16_t* kc = kc_.data() + (size_t)l * n_head_kv_ * n_ctx_ * hd;
-  const uint16_t* vc = vc_.data() + (size_t)l * n_head_kv_ * n_ctx_ * hd;
+  const uint16_t* kc = kc_.data() + (size_t)l * nkv * n_ctx_ * hd;
+  const uint16_t* vc = vc_.data() + (size_t)l * nkv * n_ctx_ * hd;
 #pragma omp parallel for collapse(2) schedule(static)
   for (int t = 0; t < T; ++t)
-    for (int h = 0; h < n_head_; ++h) {
+    for (int h = 0; h < nh; ++h) {
       const int L = pos0 + t + 1, kvh = h / G;
-      const float* qh = q + ((size_t)t * n_head_ + h) * hd;
+      const float* qh = q + ((size_t)t * nh + h) * hd;
       std::vector<float> s(L);
       float m = -INFINITY;
       for (int j = 0; j < L; ++j) {
@@ -398,7 +430,7 @@ void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) co
       }
       float den = 0.f;
       for (int j = 0; j < L; ++j) { s[j] = std::exp(s[j] - m); den += s[j]; }
-      float* o = out + ((size_t)t * n_head_ + h) * hd;
+      float* o = out + ((size_t)t * nh + h) * hd;
       for (int i = 0; i < hd; ++i) o[i] = 0.f;
       for (int j = 0; j < L; ++j) {
         const uint16_t* vr = vc + ((size_t)kvh * n_ctx_ + j) * hd;
@@ -409,7 +441,8 @@ void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) co
 }
 
 void CpuEngine::ffn(const CpuLayer& L, float* x, int T) {
-  const int d = n_embd_, F = n_ff_;
+  const int d = n_embd_, F = sp_.F_l;
+  std::vector<float> part((size_t)T * d, 0.f);
   if (n_expert_ == 0) {
     std::vector<float> gu((size_t)T * 2 * F), h((size_t)T * F);
     matmul(L.w_gu, x, T, d, gu.data(), 2 * F, &L.ffn_norm, false);
@@ -418,54 +451,55 @@ void CpuEngine::ffn(const CpuLayer& L, float* x, int T) {
         const int r = (f >> 5) * 64 + (f & 31);
         h[(size_t)t * F + f] = silu(gu[(size_t)t * 2 * F + r]) * gu[(size_t)t * 2 * F + r + 32];
       }
-    matmul(L.w_down, h.data(), T, F, x, d, nullptr, true);
-    return;
-  }
-  const int E = n_expert_;
-  std::vector<float> rl((size_t)T * E);
-  matmul(L.router, x, T, d, rl.data(), E, &L.ffn_norm, false);
-  Q8 xq;
-  quantize_rows(x, T, d, d, &L.ffn_norm, eps_, xq);
-  std::vector<float> add((size_t)T * d, 0.f);
-  for (int t = 0; t < T; ++t) {
-    std::vector<double> p(E);
-    double mx = -1e300, sum = 0;
-    for (int e = 0; e < E; ++e) mx = std::max(mx, (double)rl[(size_t)t * E + e]);
-    for (int e = 0; e < E; ++e) { p[e] = std::exp(rl[(size_t)t * E + e] - mx); sum += p[e]; }
-    std::vector<int> ids(E);
-    std::iota(ids.begin(), ids.end(), 0);
-    std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return p[a] > p[b]; });
-    double wsum = 0;
-    for (int j = 0; j < n_expert_used_; ++j) wsum += p[ids[j]] / sum;
-    Q8 one;
-    one.K = d;
-    one.q.assign(xq.q.begin() + (size_t)t * d, xq.q.begin() + (size_t)(t + 1) * d);
-    one.d.assign(xq.d.begin() + (size_t)t * d / 32, xq.d.begin() + (size_t)(t + 1) * d / 32);
-    one.s16.assign(xq.s16.begin() + (size_t)t * d / 16, xq.s16.begin() + (size_t)(t + 1) * d / 16);
-    for (int j = 0; j < n_expert_used_; ++j) {
-      const int e = ids[j];
-      const float w = (float)(p[e] / sum / wsum);
-      std::vector<float> gu(2 * F), h(F), y(d);
-      CpuMat gm = L.gu_exps;  // shallow view: same planes, expert offset via base pointer
-      gemm_rows(L.gu_exps, L.gu_exps.data.data() + L.gu_exps.expert_stride * e, one, 1, gu.data(), 2 * F, false);
-      for (int f = 0; f < F; ++f) {
-        const int r = (f >> 5) * 64 + (f & 31);
-        h[f] = silu(gu[r]) * gu[r + 32];
+    matmul(L.w_down, h.data(), T, F, part.data(), d, nullptr, false);
+  } else {
+    const int E = n_expert_;
+    std::vector<float> rl((size_t)T * E);
+    matmul(L.router, x, T, d, rl.data(), E, &L.ffn_norm, false);
+    Q8 xq;
+    quantize_rows(x, T, d, d, &L.ffn_norm, eps_, xq);
+    for (int t = 0; t < T; ++t) {
+      std::vector<double> p(E);
+      double mx = -1e300, sum = 0;
+      for (int e = 0; e < E; ++e) mx = std::max(mx, (double)rl[(size_t)t * E + e]);
+      for (int e = 0; e < E; ++e) { p[e] = std::exp(rl[(size_t)t * E + e] - mx); sum += p[e]; }
+      std::vector<int> ids(E);
+      std::iota(ids.begin(), ids.end(), 0);
+      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) { return p[a] > p[b]; });
+      double wsum = 0;
+      for (int j = 0; j < n_expert_used_; ++j) wsum += p[ids[j]] / sum;
+      Q8 one;
+      one.K = d;
+      one.q.assign(xq.q.begin() + (size_t)t * d, xq.q.begin() + (size_t)(t + 1) * d);
+      one.d.assign(xq.d.begin() + (size_t)t * d / 32, xq.d.begin() + (size_t)(t + 1) * d / 32);
+      one.s16.assign(xq.s16.begin() + (size_t)t * d / 16, xq.s16.begin() + (size_t)(t + 1) * d / 16);
+      for (int j = 0; j < n_expert_used_; ++j) {
+        const int e = ids[j];
+        const float w = (float)(p[e] / sum / wsum);
+        std::vector<float> gu(2 * F), h(F), y(d);
+        gemm_rows(L.gu_exps, L.gu_exps.data.data() + L.gu_exps.expert_stride * e, one, 1, gu.data(), 2 * F, false);
+        for (int f = 0; f < F; ++f) {
+          const int r = (f >> 5) * 64 + (f & 31);
+          h[f] = silu(gu[r]) * gu[r + 32];
+        }
+        Q8 hq;
+        quantize_rows(h.data(), 1, F, F, nullptr, eps_, hq);
+        gemm_rows(L.down_exps, L.down_exps.data.data() + L.down_exps.expert_stride * e, hq, 1, y.data(), d, false);
+        for (int i = 0; i < d; ++i) part[(size_t)t * d + i] += w * y[i];
       }
-      Q8 hq;
-      quantize_rows(h.data(), 1, F, F, nullptr, eps_, hq);
-      gemm_rows(L.down_exps, L.down_exps.data.data() + L.down_exps.expert_stride * e, hq, 1, y.data(), d, false);
-      for (int i = 0; i < d; ++i) add[(size_t)t * d + i] += w * y[i];
-      (void)gm;
     }
   }
-  for (size_t i = 0; i < add.size(); ++i) x[i] += add[i];
+  reduce(part.data(), part.size());
+  for (size_t i = 0; i < part.size(); ++i) x[i] += part[i];
 }
 
 void CpuEngine::run_layers(float* x, int T, int pos0, int l0, int l1) {
+  if (l1 > layer_end_) throw std::runtime_error("run_layers: layer range not resident on the CPU");
+  if (pos0 + T > n_ctx_) throw std::runtime_error("run_layers: exceeds n_ctx");
   const int d = n_embd_, hd = head_dim_;
-  const int nq = n_head_ * hd, nkv = n_head_kv_ * hd;
+  const int nq = sp_.nq, nkv = sp_.nkvd, nkvh = sp_.nkv_l;
   std::vector<float> q((size_t)T * nq), k((size_t)T * nkv), v((size_t)T * nkv), att((size_t)T * nq);
+  std::vector<float> part((size_t)T * d);
   for (int l = l0; l < l1; ++l) {
     const CpuLayer& L = layers_[l];
     Q8 xq;
@@ -478,28 +512,39 @@ void CpuEngine::run_layers(float* x, int T, int pos0, int l0, int l1) {
       auto rope = [&](float* r, int n) {
         for (int i = 0; i < n; i += 2) {
           const int dd = i % hd;
-          const float c = rope_cos_[(size_t)pos * hd / 2 + dd / 2], s = rope_sin_[(size_t)pos * hd / 2 + dd / 2];
+          const float c = rope_cos_[(size_t)pos * hd / 2 + dd / 2], sn = rope_sin_[(size_t)pos * hd / 2 + dd / 2];
           const float a0 = r[i], a1 = r[i + 1];
-          r[i] = a0 * c - a1 * s;
-          r[i + 1] = a0 * s + a1 * c;
+          r[i] = a0 * c - a1 * sn;
+          r[i + 1] = a0 * sn + a1 * c;
         }
       };
       rope(q.data() + (size_t)t * nq, nq);
       rope(k.data() + (size_t)t * nkv, nkv);
       for (int i = 0; i < nkv; ++i) {
-        const size_t ci = (((size_t)l * n_head_kv_ + i / hd) * n_ctx_ + pos) * hd + i % hd;
+        const size_t ci = (((size_t)l * nkvh + i / hd) * n_ctx_ + pos) * hd + i % hd;
         kc_[ci] = f2h(k[(size_t)t * nkv + i]);
         vc_[ci] = f2h(v[(size_t)t * nkv + i]);
       }
     }
     attention(l, q.data(), T, pos0, att.data());
-    matmul(L.wo, att.data(), T, nq, x, d, nullptr, true);
+    matmul(L.wo, att.data(), T, nq, part.data(), d, nullptr, false);
+    reduce(part.data(), part.size());
+    for (size_t i = 0; i < part.size(); ++i) x[i] += part[i];
     ffn(L, x, T);
   }
 }
 
-void CpuEngine::head(const float* xrow, float* logits) const {
-  matmul(output_, xrow, 1, n_embd_, logits, n_vocab_, &out_norm_, false);
+void CpuEngine::head(const float* xrow, float* logits) {
+  if (!opt_.load_head) throw std::runtime_error("head: output layer not resident on the CPU");
+  if (sp_.tp == 1) {
+    matmul(output_, xrow, 1, n_embd_, logits, n_vocab_, &out_norm_, false);
+    return;
+  }
+  std::vector<float> loc(sp_.V_l), all(sp_.V_pad);
+  matmul(output_, xrow, 1, n_embd_, loc.data(), sp_.V_l, &out_norm_, false);
+  if (!allgather_) throw std::runtime_error("tensor parallel CPU engine: set_comm() was not called");
+  allgather_(loc.data(), all.data(), (size_t)sp_.V_l);
+  std::memcpy(logits, all.data(), sizeof(float) * n_vocab_);
 }
 
 std::vector<float> CpuEngine::eval_logits(const std::vector<int>& tokens, int pos0) {
@@ -516,6 +561,19 @@ std::vector<float> CpuEngine::eval_logits(const std::vector<int>& tokens, int po
   const int last = (T - 1) % n_batch_;
   head(x.data() + (size_t)last * n_embd_, logits.data());
   return logits;
+}
+
+std::vector<float> CpuEngine::eval_hidden(const std::vector<int>& tokens, int pos0) {
+  const int T = (int)tokens.size();
+  if (T <= 0 || pos0 + T > n_ctx_) throw std::runtime_error("eval_hidden: bad range");
+  std::vector<float> out((size_t)T * n_embd_);
+  for (int p = 0; p < T; p += n_batch_) {
+    const int n = std::min(n_batch_, T - p);
+    float* x = out.data() + (size_t)p * n_embd_;
+    embed(tokens.data() + p, n, x);
+    run_layers(x, n, pos0 + p, 0, layer_end_);
+  }
+  return out;
 }
 
 CpuGenOut CpuEngine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const CpuSampling& sp,

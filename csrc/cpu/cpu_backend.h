@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../common.h"
+#include "../runtime/shard.h"
 
 namespace lfk {
 
@@ -44,9 +45,20 @@ struct CpuGenOut {
   double prefill_s = 0, decode_s = 0;
 };
 
+struct CpuOptions {
+  int n_ctx = 512, n_threads = 0, n_batch = 64;
+  int tp_rank = 0, tp_size = 1;   // tensor parallel (same shard plan as the GPU engine)
+  int layer_end = -1;             // hybrid placement: only layers [0, layer_end) are resident
+  bool load_head = true;          // output norm + lm_head resident
+};
+
 class CpuEngine {
  public:
-  CpuEngine(const std::string& path, int n_ctx, int n_threads, int n_batch);
+  CpuEngine(const std::string& path, const CpuOptions& opts);
+  // collectives for tp_size > 1 (e.g. torch.distributed gloo from Python):
+  // allreduce(buf, n) sums in place; allgather(local, all, n_local) concatenates rank shards
+  void set_comm(std::function<void(float*, size_t)> allreduce,
+                std::function<void(const float*, float*, size_t)> allgather);
   CpuGenOut generate(const std::vector<int>& prompt, int n_keep, int max_new, const CpuSampling& sp,
                      const std::vector<int>& stop, const std::function<bool()>& poll,
                      const std::function<void(int)>& on_token);
@@ -56,18 +68,30 @@ class CpuEngine {
   // hybrid placement hooks: embed, run a layer range on hidden states, head
   void embed(const int* tokens, int T, float* x) const;
   void run_layers(float* x, int T, int pos0, int l0, int l1);
-  void head(const float* xrow, float* logits) const;
+  void head(const float* xrow, float* logits);
+  // hybrid: hidden states after layers [0, layer_end) for tokens at pos0.. ([T][n_embd])
+  std::vector<float> eval_hidden(const std::vector<int>& tokens, int pos0);
 
   int n_vocab() const { return n_vocab_; }
   int n_embd() const { return n_embd_; }
   int n_layer() const { return n_layer_; }
   int n_ctx() const { return n_ctx_; }
+  int layer_end() const { return layer_end_; }
+  int tp_rank() const { return sp_.rank; }
+  int tp_size() const { return sp_.tp; }
 
  private:
   void matmul(const CpuMat& W, const float* x, int T, int ldx, float* y, int ldy, const std::vector<float>* norm,
               bool add) const;
   void attention(int l, const float* q, int T, int pos0, float* out) const;
   void ffn(const CpuLayer& L, float* x, int T);
+  void reduce(float* y, size_t n);
+
+  CpuOptions opt_;
+  ShardPlan sp_;
+  int layer_end_ = 0;
+  std::function<void(float*, size_t)> allreduce_;
+  std::function<void(const float*, float*, size_t)> allgather_;
 
   int n_vocab_ = 0, n_embd_ = 0, n_layer_ = 0, n_head_ = 0, n_head_kv_ = 0, head_dim_ = 0, n_ff_ = 0;
   int n_expert_ = 0, n_expert_used_ = 0, n_ctx_ = 0, n_threads_ = 1, n_batch_ = 64;
@@ -75,7 +99,7 @@ class CpuEngine {
   CpuMat tok_embd_, output_;
   std::vector<float> out_norm_;
   std::vector<CpuLayer> layers_;
-  std::vector<uint16_t> kc_, vc_;      // [layer][kv_head][n_ctx][hd] f16
+  std::vector<uint16_t> kc_, vc_;      // [layer][local kv_head][n_ctx][hd] f16
   std::vector<float> rope_cos_, rope_sin_;
 };
 

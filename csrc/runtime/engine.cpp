@@ -8,6 +8,7 @@
 #include <stdexcept>
 
 #include "repack.h"
+#include "shard.h"
 
 namespace lfk {
 
@@ -67,15 +68,16 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   GGUFFile f(path);
   hp_ = read_hparams(f);
   const int tp = opt_.tp_size, r = opt_.tp_rank;
-  if (hp_.n_head % tp || hp_.n_head_kv % tp) throw std::runtime_error("tensor parallel degree must divide head counts");
-  nh_l_ = hp_.n_head / tp;
-  nkv_l_ = hp_.n_head_kv / tp;
-  nq_ = nh_l_ * hp_.head_dim;
-  nkvd_ = nkv_l_ * hp_.head_dim;
-  if (hp_.n_ff % tp) throw std::runtime_error("tensor parallel degree must divide n_ff");
-  F_l_ = hp_.n_ff / tp;
-  V_l_ = (hp_.n_vocab + tp - 1) / tp;
-  V_pad_ = V_l_ * tp;
+  const ShardPlan sp = make_shard_plan(hp_.n_head, hp_.n_head_kv, hp_.head_dim, hp_.n_ff, hp_.n_vocab, tp, r);
+  nh_l_ = sp.nh_l;
+  nkv_l_ = sp.nkv_l;
+  nq_ = sp.nq;
+  nkvd_ = sp.nkvd;
+  F_l_ = sp.F_l;
+  V_l_ = sp.V_l;
+  V_pad_ = sp.V_pad;
+  if (opt_.layer_begin < 0 || opt_.layer_begin > hp_.n_layer) throw std::runtime_error("bad layer_begin");
+  if (opt_.layer_begin > 0 && tp > 1) throw std::runtime_error("partial offload cannot be combined with split_mode=row");
   if (opt_.n_ctx <= 0) opt_.n_ctx = hp_.n_ctx_train;
   if (tp > 1) {
     if (opt_.nccl_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad nccl id");
@@ -166,7 +168,7 @@ void Engine::load(const GGUFFile& f) {
   const std::string out_name = f.find("output.weight") ? "output.weight" : "token_embd.weight";
   output_ = upload_matrix(f, out_name, (size_t)r * V_l_, V_l_, 0, d);
   layers_.resize(hp_.n_layer);
-  for (int l = 0; l < hp_.n_layer; ++l) {
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
     const std::string p = "blk." + std::to_string(l) + ".";
     Layer& L = layers_[l];
     L.attn_norm = upload_f32(f, p + "attn_norm.weight");
@@ -345,17 +347,17 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
 
 void Engine::enqueue_decode(hipStream_t s) {
   embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
-  for (int l = 0; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
   enqueue_head(x_, 1, s);
 }
 
-void Engine::enqueue_prefill(int T, int pos0, hipStream_t s) {
+void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
   const int d = hp_.n_embd, hd = hp_.head_dim;
   const bool tp = opt_.tp_size > 1;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   const int ncol = nq_ + 2 * nkvd_;
-  embed_rows(tok_embd_, tokens_, T, x_, s);
-  for (int l = 0; l < hp_.n_layer; ++l) {
+  if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
     const Layer& L = layers_[l];
     rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s);
     GemmArgs g;
@@ -539,6 +541,17 @@ std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0)
   std::memcpy(h_tokens_, tokens.data(), sizeof(int) * T);
   HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
   enqueue_prefill(T, pos0, stream_);
+  enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
+  std::vector<float> out(hp_.n_vocab);
+  HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
+  if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_hidden: bad size");
+  HIPCHK(hipMemcpyAsync(x_, x, sizeof(float) * T * hp_.n_embd, hipMemcpyHostToDevice, stream_));
+  enqueue_prefill(T, pos0, stream_, /*embed=*/false);
   enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
   std::vector<float> out(hp_.n_vocab);
   HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));

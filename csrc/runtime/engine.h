@@ -37,6 +37,7 @@ struct EngineOptions {
   int tp_rank = 0;
   int tp_size = 1;
   std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1)
+  int layer_begin = 0;  // hybrid placement: layers [0, layer_begin) run on the CPU backend
   bool verbose = false;
 };
 
@@ -77,6 +78,8 @@ class Engine {
   // test hooks (numerics vs the reference model)
   std::vector<float> eval_logits(const std::vector<int>& tokens, int pos0);  // prefill path
   std::vector<float> decode_logits(int token, int pos);                      // decode path (eager)
+  // hybrid placement: hidden states [T][d] of layer `layer_begin` in, last-row logits out
+  std::vector<float> eval_hidden(const float* x, int T, int pos0);
   void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing
 
   const HParams& hparams() const { return hp_; }
@@ -86,6 +89,7 @@ class Engine {
   bool healthy() const { return healthy_; }
   std::string last_error() const { return last_error_; }
   int n_ctx() const { return opt_.n_ctx; }
+  int layer_begin() const { return opt_.layer_begin; }
 
  private:
   void* dalloc(size_t bytes);
@@ -101,7 +105,7 @@ class Engine {
   void allreduce_into(const float* send, float* recv, size_t n, hipStream_t s);
   void enqueue_layer_decode(int l, hipStream_t s);
   void enqueue_decode(hipStream_t s);
-  void enqueue_prefill(int T, int pos0, hipStream_t s);
+  void enqueue_prefill(int T, int pos0, hipStream_t s, bool embed = true);
   void enqueue_head(const float* xrow, int advance_pos, hipStream_t s);
   void launch_step();
   void check(hipError_t e, const char* what);

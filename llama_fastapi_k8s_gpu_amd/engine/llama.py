@@ -45,7 +45,7 @@ def _select_backend(reader, hp: LlamaHParams, n_gpu_layers: int, backend: Option
     try:
         import torch
         if torch.cuda.is_available():
-            return "hip"
+            return "hip" if n_gpu >= hp.n_layer else "hybrid"
     except Exception:
         pass
     logger.warning("no GPU visible: n_gpu_layers=%d falls back to the CPU backend", n_gpu_layers)
@@ -86,7 +86,12 @@ class Llama:
             self._backend = ReferenceBackend(reader, self._n_ctx)
         elif kind == "cpu":
             from ..runtime.cpu_backend import CpuBackend
-            self._backend = CpuBackend(model_path, self._n_ctx, n_threads=n_threads)
+            self._backend = CpuBackend(model_path, self._n_ctx, n_threads=n_threads, split_mode=split_mode,
+                                       tensor_split=tensor_split)
+        elif kind == "hybrid":
+            from ..runtime.hybrid_backend import HybridBackend
+            self._backend = HybridBackend(model_path, self.hparams, n_gpu_layers=n_gpu_layers, n_ctx=self._n_ctx,
+                                          main_gpu=main_gpu, n_threads=n_threads, n_batch=n_batch)
         elif kind == "hip":
             from ..runtime.hip_backend import HipBackend
             self._backend = HipBackend(model_path, self.hparams, n_ctx=self._n_ctx, n_gpu_layers=n_gpu_layers,

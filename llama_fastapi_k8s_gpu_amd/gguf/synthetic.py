@@ -92,6 +92,11 @@ SPECS: Dict[str, ModelSpec] = {
                                      n_ctx_train=1024),
     "tiny-mixtral-q4_k_m": ModelSpec("tiny-mixtral", 256, 3, 4, 2, 512, 0, 1e6, "spm", "q4_k_m",
                                      n_expert=4, n_expert_used=2, n_ctx_train=1024),
+    # tensor-parallel test shapes: per-rank head / FFN slices stay multiples of 256 at TP=2
+    "tiny-llama3-tp": ModelSpec("tiny-llama3-tp", 512, 2, 8, 4, 1024, 0, 500000.0, "bpe", "q4_k_m",
+                                n_ctx_train=1024),
+    "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", 512, 2, 8, 4, 1024, 0, 1e6, "spm", "q4_k_m",
+                                 n_expert=4, n_expert_used=2, n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

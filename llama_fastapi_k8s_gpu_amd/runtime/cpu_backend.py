@@ -25,14 +25,24 @@ def sampling_dict(p: SamplingParams) -> dict:
 class CpuBackend:
     name = "cpu"
 
-    def __init__(self, model_path: str, n_ctx: int = 512, n_threads: Optional[int] = None, n_batch: int = 64, **_):
+    def __init__(self, model_path: str, n_ctx: int = 512, n_threads: Optional[int] = None, n_batch: int = 64,
+                 split_mode: str = "none", tensor_split=None, **_):
         cpu = load_cpu()
         threads = int(n_threads or os.environ.get("N_THREADS", 0) or 0)
-        self.engine = cpu.CpuEngine(model_path, n_ctx=n_ctx, n_threads=threads, n_batch=min(n_batch, 128))
+        rank, size = 0, 1
+        if split_mode == "row":
+            from ..parallel.comm import tp_group_info
+            rank, size = tp_group_info(tensor_split)
+        self.engine = cpu.CpuEngine(model_path, n_ctx=n_ctx, n_threads=threads, n_batch=min(n_batch, 128),
+                                    tp_rank=rank, tp_size=size)
+        if size > 1:
+            from ..parallel.comm import host_collectives
+            self.engine.set_comm(*host_collectives())
+        self.tp_rank, self.tp_size = rank, size
         self.n_ctx = n_ctx
 
     def health(self):
-        return {"ok": True, "backend": self.name}
+        return {"ok": True, "backend": self.name, "tp": self.tp_size}
 
     def device_memory(self):
         return {}

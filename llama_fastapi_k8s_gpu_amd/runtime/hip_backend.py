@@ -29,24 +29,14 @@ logger = logging.getLogger(__name__)
 
 def _tp_setup(split_mode: str, tensor_split):
     """(tp_rank, tp_size, device, nccl_id) from torch.distributed (if initialised)."""
-    try:
-        import torch.distributed as dist
-        init = dist.is_available() and dist.is_initialized()
-    except Exception:
-        init = False
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if split_mode != "row" or not init or dist.get_world_size() == 1:
+    from ..parallel.comm import broadcast_nccl_id, local_rank, tp_group_info
+    local = local_rank()
+    if split_mode != "row":
         return 0, 1, local, b""
-    ws, rank = dist.get_world_size(), dist.get_rank()
-    if tensor_split:
-        ts = [float(v) for v in tensor_split if float(v) > 0]
-        if len(ts) != ws or max(ts) - min(ts) > 1e-6 * max(ts):
-            raise ValueError(f"tensor_split {tensor_split} must be uniform over the {ws} ranks "
-                             "(row-split ranks are symmetric)")
-    hip = load_hip()
-    obj = [hip.nccl_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    return rank, ws, local, obj[0]
+    rank, ws = tp_group_info(tensor_split)
+    if ws == 1:
+        return 0, 1, local, b""
+    return rank, ws, local, broadcast_nccl_id(lambda: load_hip().nccl_unique_id())
 
 
 class HipBackend:
@@ -58,7 +48,7 @@ class HipBackend:
         hip = load_hip()
         if 0 <= n_gpu_layers < hparams.n_layer:
             raise ValueError(f"n_gpu_layers={n_gpu_layers} < n_layer={hparams.n_layer}: partial offload runs on "
-                             "the hybrid backend (use backend='hybrid')")
+                             "the hybrid backend (backend='hybrid')")
         rank, size, local, nccl_id = _tp_setup(split_mode, tensor_split)
         device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)
         self.tp_rank, self.tp_size = rank, size

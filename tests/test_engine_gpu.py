@@ -88,3 +88,30 @@ def test_cancel_poll_stops_generation(models):
         return calls["n"] >= 3
     r = eng.generate([1, 2, 3], 0, 400, {"temperature": 1.0, "seed": 1}, [], poll, None)
     assert r["finish"] == "cancelled" and len(r["tokens"]) < 400
+
+
+@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
+def test_hybrid_partial_offload_matches_full_gpu(models, spec):
+    """n_gpu_layers < n_layer: CPU layers [0, k) + GPU layers [k, n) == all-GPU logits."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu, load_hip
+    path = models[spec]
+    full = _engine(path, graph=False)
+    rng = np.random.default_rng(5)
+    toks = [int(t) for t in rng.integers(3, 300, 24)]
+    want = full.eval_logits(toks, 0)
+    want_dec = full.decode_logits(9, 24)
+    cpu = load_cpu().CpuEngine(path, n_ctx=256, n_threads=4, n_batch=16, layer_end=1, load_head=False)
+    gpu = load_hip().Engine(path, n_ctx=256, n_batch=128, device=0, use_graph=False, layer_begin=1)
+    got = gpu.eval_hidden(cpu.eval_hidden(toks, 0), 0)
+    got_dec = gpu.eval_hidden(cpu.eval_hidden([9], 24), 24)
+    assert rel_err(got, want) < 3e-2
+    assert rel_err(got_dec, want_dec) < 3e-2
+
+
+def test_hybrid_backend_facade(models):
+    from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+    llm = Llama(models["tiny-llama3-q4_k_m"], n_gpu_layers=2, n_ctx=128, seed=4)
+    assert llm.backend_name == "hybrid"
+    out = llm.create_chat_completion([{"role": "user", "content": "hi"}], max_tokens=8, temperature=0.0)
+    assert 1 <= out["usage"]["completion_tokens"] <= 8
+    assert llm.health()["cpu_layers"] == 2
