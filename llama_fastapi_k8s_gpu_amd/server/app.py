@@ -242,6 +242,20 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             return JSONResponse(status_code=503, content=info)
         return info
 
+    @app.get("/health/live")
+    async def health_live(request: Request):
+        """Liveness: the process serves HTTP and the engine has not faulted (a model
+        still loading is alive; readiness is ``/health``)."""
+        eng = getattr(request.app.state, "engine", None)
+        if eng is not None and hasattr(eng, "health"):
+            try:
+                h = eng.health()
+                if not h.get("ok", True):
+                    return JSONResponse(status_code=503, content={"status": "unhealthy", "engine": h})
+            except Exception as e:
+                return JSONResponse(status_code=503, content={"status": "unhealthy", "error": str(e)})
+        return {"status": "alive"}
+
     @app.get("/metrics")
     async def metrics_endpoint(request: Request):
         from prometheus_client import CONTENT_TYPE_LATEST, generate_latest

@@ -1,0 +1,99 @@
+"""T8 deploy: Helm chart renders (Go-template subset renderer, no helm binary in the
+image) into valid manifests that fix the reference's deployment defects
+(SURVEY Appendix C1-C5, C11), and the container files are consistent."""
+import os
+import sys
+
+import pytest
+import yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from helm_render import render_chart  # noqa: E402
+
+CHART = os.path.join(ROOT, "helm")
+
+
+def _docs(overrides=()):
+    out = {}
+    for name, text in render_chart(CHART, list(overrides)).items():
+        docs = [d for d in yaml.safe_load_all(text) if d]
+        if docs:
+            out[name] = docs[0]
+    return out
+
+
+def _app_container(dep):
+    return dep["spec"]["template"]["spec"]["containers"][0]
+
+
+def _env(c):
+    return {e["name"]: e.get("value") for e in c["env"]}
+
+
+def test_chart_metadata_at_root():
+    assert os.path.exists(os.path.join(CHART, "Chart.yaml"))
+    assert not os.path.exists(os.path.join(CHART, "templates", "Chart.yaml"))   # C3
+    meta = yaml.safe_load(open(os.path.join(CHART, "Chart.yaml")))
+    assert meta["apiVersion"] == "v2" and meta["name"]
+
+
+def test_default_render():
+    d = _docs()
+    assert set(d) == {"deployment.yaml", "service.yaml", "ingress.yaml"}
+    dep = d["deployment.yaml"]
+    assert dep["kind"] == "Deployment" and dep["spec"]["replicas"] == 4
+    c = _app_container(dep)
+    assert c["resources"]["limits"]["amd.com/gpu"] == 1                         # C4
+    assert c["readinessProbe"]["httpGet"]["path"] == "/health"                  # C2
+    assert c["livenessProbe"]["httpGet"]["path"] == "/health/live"
+    env = _env(c)
+    init = dep["spec"]["template"]["spec"]["initContainers"][0]
+    # C1: the downloaded object and the served file are the same value
+    assert env["MODEL_FILE"] in init["args"][0] and env["MODEL_DIR"] in init["args"][0]
+    # C11: AWS credentials only in the initContainer
+    assert not any(e["name"].startswith("AWS_") for e in c["env"])
+    assert env["SPLIT_MODE"] == "layer"
+    tol = dep["spec"]["template"]["spec"]["tolerations"][0]
+    assert tol["key"] == "amd.com/gpu"
+    svc = d["service.yaml"]
+    assert svc["spec"]["selector"]["app"] == dep["spec"]["template"]["metadata"]["labels"]["app"]
+    assert svc["spec"]["ports"][0]["targetPort"] == 8000
+    ing = d["ingress.yaml"]
+    assert ing["spec"]["rules"][0]["http"]["paths"][0]["backend"]["service"]["name"] == svc["metadata"]["name"]
+
+
+def test_ingress_guard_and_tensor_parallel_pod():
+    d = _docs(["ingress.enabled=false", "gpu.perPod=8", "model.cache.type=pvc", "model.cache.pvcName=models"])
+    assert "ingress.yaml" not in d                                              # C5
+    dep = d["deployment.yaml"]
+    c = _app_container(dep)
+    assert c["resources"]["requests"]["amd.com/gpu"] == 8
+    env = _env(c)
+    assert env["SPLIT_MODE"] == "row" and env["GPUS_PER_POD"] == "8"
+    vol = dep["spec"]["template"]["spec"]["volumes"][0]
+    assert vol["persistentVolumeClaim"]["claimName"] == "models"
+
+
+def test_env_rendered_into_settings(monkeypatch):
+    from llama_fastapi_k8s_gpu_amd.config import Settings
+    c = _app_container(_docs()["deployment.yaml"])
+    for k, v in _env(c).items():
+        monkeypatch.setenv(k, v or "")
+    s = Settings.from_env()
+    assert s.model_path == "/app/models/Llama-3-8B-Instruct-Q4_K_M.gguf"
+    assert s.n_gpu_layers == -1 and s.n_ctx == 1024 and s.max_queue_size == 5 and s.timeout_seconds == 25
+    assert s.tensor_split is None and s.seed is None and s.chat_format is None
+
+
+def test_docker_files():
+    base = open(os.path.join(ROOT, "docker", "Dockerfile.base")).read()
+    code = "\n".join(l for l in base.splitlines() if not l.lstrip().startswith("#"))
+    assert "gfx950" in code and "runtime.build" in code and "cuda" not in code.lower()
+    app = open(os.path.join(ROOT, "docker", "Dockerfile.app")).read()
+    assert "entrypoint.sh" in app
+    ep = open(os.path.join(ROOT, "docker", "entrypoint.sh")).read()
+    assert "api:app" in ep and "torch.distributed.run" in ep and "127.0.0.1" in ep
+    reqs = [l.split(">=")[0] for l in open(os.path.join(ROOT, "docker", "requirements.txt")).read().splitlines()
+            if l and not l.startswith("#")]
+    assert "boto3" not in reqs and "fastapi" in reqs and "gunicorn" in reqs

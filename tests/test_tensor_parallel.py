@@ -88,3 +88,44 @@ def test_tensor_split_must_be_uniform():
         check_tensor_split([0.7, 0.3], 2)
     with pytest.raises(ValueError, match="uniform"):
         check_tensor_split([1, 1, 1], 2)
+
+
+def _serve_rank(rank, world, port, path, out_dir):
+    """rank 0: FastAPI app with the TP leader; rank 1: follower loop (CPU backend, gloo)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from llama_fastapi_k8s_gpu_amd.config import Settings
+    from llama_fastapi_k8s_gpu_amd.engine.factory import build_engine
+    from llama_fastapi_k8s_gpu_amd.parallel.tp_serve import TPLeader, follower_loop, init_tp
+    import torch.distributed as dist
+    s = Settings()
+    s.model_path_override = path
+    s.n_gpu_layers = 0
+    s.n_ctx = 256
+    r, w, ctrl = init_tp(s)
+    assert (r, w) == (rank, world) and s.split_mode == "row" and s.seed is not None
+    llm = build_engine(s)
+    assert llm.health()["tp"] == 2
+    if rank == 0:
+        from fastapi.testclient import TestClient
+        from llama_fastapi_k8s_gpu_amd.server.app import create_app
+        leader = TPLeader(llm, ctrl)
+        with TestClient(create_app(s, engine=leader)) as c:
+            body = {"bot_profile": {"name": "Ann.f", "appearance": "a, b, c, d"}, "user_profile": {"name": "u"},
+                    "context": [{"turn": "user", "message": "hello there"}]}
+            codes = [c.post("/response", json=body).status_code for _ in range(2)]
+        leader.close()
+        with open(os.path.join(out_dir, "codes.txt"), "w") as f:
+            f.write(",".join(map(str, codes)))
+    else:
+        follower_loop(llm, ctrl)
+        open(os.path.join(out_dir, "follower_done"), "w").close()
+    dist.destroy_process_group()
+
+
+def test_tp_serving_leader_follower(tmp_path):
+    path = write_synthetic_gguf("tiny-llama3-tp", str(tmp_path / "m.gguf"))
+    mp.start_processes(_serve_rank, args=(2, _free_port(), path, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    assert (tmp_path / "codes.txt").read_text() == "200,200"
+    assert (tmp_path / "follower_done").exists()
