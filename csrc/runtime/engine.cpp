@@ -1,6 +1,7 @@
 #include "engine.h"
 
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <chrono>
 #include <cmath>
@@ -13,6 +14,12 @@
 namespace lfk {
 
 #define HIPCHK(x) check((x), #x)
+
+// roctx ranges (visible with rocprofv3 --marker-trace): prefill chunks, decode loop
+struct RoctxRange {
+  explicit RoctxRange(const char* m) { roctxRangePushA(m); }
+  ~RoctxRange() { roctxRangePop(); }
+};
 
 static double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -476,6 +483,8 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
 
   // prefill in n_batch chunks
   int pos = n_keep;
+  {
+  RoctxRange prefill_range("lfk.prefill");
   while (pos < n_prompt) {
     const int T = std::min(opt_.n_batch, n_prompt - pos);
     std::memcpy(h_tokens_, prompt.data() + pos, sizeof(int) * T);
@@ -484,6 +493,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
     pos += T;
     if (pos == n_prompt) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
     HIPCHK(hipStreamSynchronize(stream_));  // h_tokens_ is reused by the next chunk
+  }
   }
   HIPCHK(hipGetLastError());
   const double t1 = now_s();
@@ -494,6 +504,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
     for (int s : stop_ids) if (s == t) return true;
     return false;
   };
+  RoctxRange decode_range("lfk.decode");
   int tok = h_ring_[0];
   out.tokens.push_back(tok);
   if (on_token) on_token(tok);

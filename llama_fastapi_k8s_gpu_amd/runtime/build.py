@@ -97,7 +97,7 @@ def build_hip(jobs: int = 8, verbose: bool = True) -> str:
     out = hip_so_path()
     tmp = out + ".tmp"
     cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs + \
-          ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-lamdhip64", "-lgomp", "-Wl,-rpath," + os.path.join(ROCM, "lib")]
+          ["-L" + os.path.join(ROCM, "lib"), "-lrccl", "-lamdhip64", "-lrocprofiler-sdk-roctx", "-lgomp", "-Wl,-rpath," + os.path.join(ROCM, "lib")]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
