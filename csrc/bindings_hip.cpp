@@ -162,8 +162,9 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gemv", [](uintptr_t w, int type, int rows, int K, uintptr_t x, uintptr_t norm, float eps, uintptr_t out,
                    int n_out, int epi, uintptr_t stream, int n_slots, uintptr_t ids, size_t expert_stride,
-                   int slot_stride, uintptr_t resid) {
+                   int slot_stride, uintptr_t resid, int debug) {
     GemvArgs a;
+    a.debug = debug;
     a.w = make_qmat(P<void>(w), type, rows, K, expert_stride);
     a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.out = P<float>(out); a.n_out = n_out;
     a.n_slots = n_slots; a.expert_ids = P<int>(ids); a.out_slot_stride = slot_stride; a.resid = P<float>(resid);
@@ -171,7 +172,8 @@ PYBIND11_MODULE(_hip, m) {
     hip_ok("gemv");
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("norm"), py::arg("eps"),
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
-     py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0);
+     py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
+     py::arg("debug") = 0);
 
   m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,
                        uintptr_t x, uintptr_t norm, float eps, uintptr_t q_out, uintptr_t kc, uintptr_t vc, int n_ctx,
@@ -213,15 +215,20 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
-                          int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters) {
+                          int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,
+                          int debug_stop, uintptr_t dbg_clk) {
     AttnDecodeArgs a;
+    a.debug_stop = debug_stop;
+    a.dbg_clk = P<long long>(dbg_clk);
     a.counters = P<int>(counters);
     a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.pos = P<int>(pos);
     a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
     a.part = P<float>(part); a.out = P<float>(out);
     attn_decode(a, S(stream));
     hip_ok("attn_decode");
-  });
+  }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("pos"), py::arg("n_ctx"), py::arg("n_head"), py::arg("n_kv"),
+     py::arg("hd"), py::arg("scale"), py::arg("part"), py::arg("out"), py::arg("stream"), py::arg("counters"),
+     py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0);
   m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
   m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
                            int hd, float scale, uintptr_t out, uintptr_t stream) {
@@ -239,6 +246,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rmsnorm_bf16", [](uintptr_t x, uintptr_t w, float eps, int T, int d, uintptr_t y, uintptr_t stream) {
     rmsnorm_bf16(P<float>(x), P<float>(w), eps, T, d, P<__hip_bfloat16>(y), S(stream));
     hip_ok("rmsnorm_bf16");
+  });
+  m.def("clock_probe", [](uintptr_t out, int iters, uintptr_t stream) {
+    clock_probe(P<long long>(out), iters, S(stream));
+    hip_ok("clock_probe");
   });
   m.def("sampler_blocks", &sampler_blocks);
   m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cv,

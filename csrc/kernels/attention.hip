@@ -18,199 +18,305 @@ namespace lfk {
 
 static constexpr int CH = 64;  // keys per split
 
-// One block = 64 keys of one kv head x all G query heads sharing it.
-//   1. every thread issues its K and V loads first (4 lanes per key, HD/4 dims
-//      per lane: 2-4 independent 16-B loads each), q goes to LDS meanwhile;
-//   2. partial dots -> 2 shuffles -> scores; block softmax over the 64 keys;
-//   3. V is staged through LDS and re-read as (head, dim-pair) per thread;
-//   4. partial (o, m, l) -> workspace; the LAST arriving block of this kv head
-//      (agent-scope release/acquire + counter, reset by that block) merges all
-//      splits, so no separate combine launch is needed.
-template <int HD>
-__global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
-  constexpr int DPL = HD / 4;  // dims per lane
-  constexpr int NLD = DPL / 8; // 16-B loads per lane per K (or V) row
-  const int kvh = blockIdx.x, split = blockIdx.y;
-  const int L = *a.pos + 1;
-  const int start = split * CH;
-  if (start >= L) return;
-  const int n = min(CH, L - start);
-  const int G = a.n_head / a.n_kv_head;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int key = tid >> 2, sub = tid & 3;
-  __shared__ float qs[8][HD];
-  __shared__ __attribute__((aligned(16))) __half vs[CH][HD + 8];
-  __shared__ float ps[8][CH];
-  __shared__ float red[8][4];
-  __shared__ float mstat[8][2];
-  __shared__ int last;
-  (void)mstat;
+// L2-coherent 4-B store / load (global_store/load ... sc1): the cross-block
+// hand-off of split partials needs no agent-scope fence when every byte of it
+// goes through these (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-  // ---- 1. issue K/V row loads (clamped to the last valid key)
-  const int kk = min(key, n - 1);
-  const size_t row = ((size_t)kvh * a.n_ctx + start + kk) * HD + sub * DPL;
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+
+// Cross-lane helpers without the LDS crossbar: DPP within a row of 16 lanes,
+// v_readlane across rows (the reduction trees below are 2-4 steps, each a few
+// cycles instead of a ds_bpermute round trip).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_sum(float v) {  // sum over the 4 lanes of a quad
+  v += dpp<0xB1>(v);                                   // quad_perm [1,0,3,2]
+  return v + dpp<0x4E>(v);                             // quad_perm [2,3,0,1]
+}
+__device__ __forceinline__ float rowq_max(float v) {  // max over lanes i, i+4, i+8, i+12 of a row
+  v = fmaxf(v, dpp<0x124>(v));                         // row_ror:4
+  return fmaxf(v, dpp<0x128>(v));                      // row_ror:8
+}
+__device__ __forceinline__ float rowq_sum(float v) {
+  v += dpp<0x124>(v);
+  return v + dpp<0x128>(v);
+}
+__device__ __forceinline__ float rows_max(float v) {  // combine the 4 rows (wave-uniform result)
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+__device__ __forceinline__ float rows_sum(float v) {
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
+// One block = 64 keys of one kv head x all G query heads sharing it; 4 waves of
+// 16 keys, lane = (key = lane/4, sub = lane%4) holding HD/4 dims of its key.
+//   1. K/V row loads go out first, clamped to the cache (speculative: they do
+//      not wait for the device-resident position), q goes to LDS;
+//   2. per wave: scores (quad DPP reduce), wave-local softmax (DPP + readlane),
+//      P.V over the wave's 16 keys from LDS - no block barrier;
+//   3. the 4 wave partials meet in LDS (one barrier) -> block partial;
+//   4. single split: normalise and store. Otherwise the partial goes out with
+//      sc1 stores and the last-arriving block of the kv head merges all splits
+//      (sc1 loads; no cache-maintenance fences).
+template <int HD, int G, bool TL>
+__global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
+  constexpr int DPL = HD / 4;   // dims per lane in QK
+  constexpr int NLD = DPL / 8;  // 16-B loads per lane per K (or V) row
+  constexpr int KPW = 16;       // keys per wave
+  // TL: timeline instrumentation (microbenchmarks; a separate instantiation so
+  // the production kernel's code generation is untouched)
+  const long long t_entry = TL ? wall_clock64() : 0;
+  const bool stamp = TL && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
+#define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) a.dbg_clk[i] = wall_clock64() - t_entry; } } while (0)
+  const int kvh = blockIdx.x, split = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kw = lane >> 2, sub = lane & 3;
+  const int start = split * CH;
+  const int key = start + wave * KPW + kw;
+
+  __shared__ __attribute__((aligned(16))) h2v qs[G][HD / 2];   // q * scale in f16 pairs
+  __shared__ __attribute__((aligned(16))) __half vs[4][KPW][HD + 8];
+  __shared__ float ps[4][G][KPW];
+  __shared__ float wm[4][G], wl[4][G];
+  __shared__ __attribute__((aligned(16))) float wo[4][G][HD];
+  __shared__ int last;
+
+  // ---- 1. loads (speculative), then the position
+  const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
   uint4 kr[NLD], vr[NLD];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) kr[i] = *reinterpret_cast<const uint4*>(a.k_cache + row + 8 * i);
 #pragma unroll
   for (int i = 0; i < NLD; ++i) vr[i] = *reinterpret_cast<const uint4*>(a.v_cache + row + 8 * i);
-  for (int i = tid; i < G * HD; i += 256) qs[i / HD][i % HD] = a.q[(size_t)(kvh * G) * HD + i] * a.scale;
-#pragma unroll
-  for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[key][sub * DPL + 8 * i]) = vr[i];
-  __syncthreads();
+  for (int i = tid; i < G * HD / 2; i += 256) {
+    const float2 qv = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
+    qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv.x * a.scale), (_Float16)(qv.y * a.scale)};
+  }
+  const int L = *a.pos + 1;
+  LFK_STAMP(0);
+  if (start >= L || a.debug_stop == 1) return;
 
-  // ---- 2. scores
-  float kf[DPL];
-#pragma unroll
-  for (int i = 0; i < NLD; ++i) {
-    const unsigned w[4] = {kr[i].x, kr[i].y, kr[i].z, kr[i].w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      kf[8 * i + 2 * j] = h2f(w[j] & 0xFFFF);
-      kf[8 * i + 2 * j + 1] = h2f(w[j] >> 16);
-    }
-  }
-  float sc[8];
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    float p = 0.f;
-    if (g < G) {
-      const float4* q4 = reinterpret_cast<const float4*>(&qs[g][sub * DPL]);
-#pragma unroll
-      for (int i = 0; i < DPL / 4; ++i) {
-        const float4 q = q4[i];
-        p += q.x * kf[4 * i] + q.y * kf[4 * i + 1] + q.z * kf[4 * i + 2] + q.w * kf[4 * i + 3];
-      }
-    }
-    p += __shfl_xor(p, 1);
-    p += __shfl_xor(p, 2);
-    sc[g] = key < n ? p : -FLT_MAX;
-  }
-  // block max / sum per head: wave-reduce over its 16 keys, then across the 4 waves
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    if (g < G) {
-      float m = sc[g];
-#pragma unroll
-      for (int o = 4; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o));
-      if (lane == 0) red[g][wave] = m;
-    }
-  }
-  __syncthreads();
-  __shared__ float red2[8][4];
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    if (g < G) {
-      const float M = fmaxf(fmaxf(red[g][0], red[g][1]), fmaxf(red[g][2], red[g][3]));
-      const float e = key < n ? __expf(sc[g] - M) : 0.f;
-      if (sub == 0) ps[g][key] = e;
-      float l = sub == 0 ? e : 0.f;
-#pragma unroll
-      for (int o = 4; o < 64; o <<= 1) l += __shfl_xor(l, o);
-      l += __shfl_xor(l, 1);
-      l += __shfl_xor(l, 2);
-      if (lane == 0) red2[g][wave] = l;
-    }
-  }
-  __syncthreads();
-  if (tid < G) {
-    mstat[tid][0] = fmaxf(fmaxf(red[tid][0], red[tid][1]), fmaxf(red[tid][2], red[tid][3]));
-    mstat[tid][1] = red2[tid][0] + red2[tid][1] + red2[tid][2] + red2[tid][3];
-  }
-
-  // ---- 3. PV: thread -> (head g, dim pair)
-  const int npairs = G * (HD / 2);
-  for (int pi = tid; pi < npairs; pi += 256) {
-    const int g = pi / (HD / 2), dp = pi % (HD / 2);
-    float o0 = 0.f, o1 = 0.f;
-#pragma unroll 8
-    for (int k = 0; k < n; ++k) {
-      const float p = ps[g][k];
-      const __half2 v = *reinterpret_cast<const __half2*>(&vs[k][2 * dp]);
-      o0 += p * __low2float(v);
-      o1 += p * __high2float(v);
-    }
-    float* dst = a.part + ((size_t)split * a.n_head + kvh * G + g) * (HD + 2);
-    dst[2 * dp] = o0;
-    dst[2 * dp + 1] = o1;
-  }
-  __syncthreads();
-  if (tid < G) {
-    float* dst = a.part + ((size_t)split * a.n_head + kvh * G + tid) * (HD + 2);
-    dst[HD] = mstat[tid][0];
-    dst[HD + 1] = mstat[tid][1];
-  }
-
-  // ---- 4. last arriver merges the splits of this kv head
   const int ns = (L + CH - 1) / CH;
-  if (ns == 1) {
-    // single split: normalise in place
-    __syncthreads();
-    for (int pi = tid; pi < G * HD; pi += 256) {
-      const int g = pi / HD, d = pi % HD;
-      const float* src = a.part + ((size_t)kvh * G + g) * (HD + 2);
-      a.out[(size_t)(kvh * G + g) * HD + d] = src[d] / src[HD + 1];
-    }
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = vr[i];
+  __syncthreads();  // qs (and this wave's vs rows)
+  LFK_STAMP(1);
+  if (a.debug_stop == 2) {
+    if (__half2float(vs[wave][kw][sub]) == 1234.f) a.out[tid] = 1.f;
     return;
   }
+
+  // ---- 2a. scores
+  const bool valid = key < L;
+  // K row slice as f16 pairs, dotted with f16 q on v_dot2_f32_f16 (f32 accumulate)
+  h2v kh[DPL / 2];
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) {
+    kh[4 * i] = __builtin_bit_cast(h2v, kr[i].x);
+    kh[4 * i + 1] = __builtin_bit_cast(h2v, kr[i].y);
+    kh[4 * i + 2] = __builtin_bit_cast(h2v, kr[i].z);
+    kh[4 * i + 3] = __builtin_bit_cast(h2v, kr[i].w);
+  }
+  float sc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint4* q4 = reinterpret_cast<const uint4*>(&qs[g][sub * (DPL / 2)]);
+    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      const uint4 qq = q4[i];
+      p0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, qq.x), kh[4 * i], p0, false);
+      p1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, qq.y), kh[4 * i + 1], p1, false);
+      p0 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, qq.z), kh[4 * i + 2], p0, false);
+      p1 = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, qq.w), kh[4 * i + 3], p1, false);
+    }
+    sc[g] = quad_sum(p0 + p1);
+  }
+  // ---- 2b. wave-local softmax over the wave's 16 keys
+  float mw[G], lw[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float s = valid ? sc[g] : -FLT_MAX;
+    mw[g] = rows_max(rowq_max(s));
+    const float e = valid ? __expf(s - mw[g]) : 0.f;
+    sc[g] = e;
+    lw[g] = rows_sum(rowq_sum(e));
+  }
+  if (sub == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) ps[wave][g][kw] = sc[g];
+  }
+  LFK_STAMP(2);
+  // ---- 2c. P.V over this wave's keys (LDS written by this wave only)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr int DV = HD / 64;  // dims per lane in PV (1 or 2)
+  float o[G][DV];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < DV; ++j) o[g][j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < KPW; ++k) {
+    float v[DV];
+    if constexpr (DV == 2) {
+      const __half2 h2 = *reinterpret_cast<const __half2*>(&vs[wave][k][2 * lane]);
+      v[0] = __low2float(h2);
+      v[1] = __high2float(h2);
+    } else {
+      v[0] = __half2float(vs[wave][k][lane]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float p = ps[wave][g][k];
+#pragma unroll
+      for (int j = 0; j < DV; ++j) o[g][j] += p * v[j];
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int j = 0; j < DV; ++j) wo[wave][g][DV * lane + j] = o[g][j];
+    if (lane == 0) {
+      wm[wave][g] = mw[g];
+      wl[wave][g] = lw[g];
+    }
+  }
+  __syncthreads();
+  LFK_STAMP(3);
+  if (a.debug_stop == 3) {
+    if (tid < G) a.out[tid] = wl[0][tid];
+    return;
+  }
+  // ---- 3. block partial: element e = (g, d) per thread
+  for (int e = tid; e < G * HD; e += 256) {
+    const int g = e / HD, d = e % HD;
+    const float M = fmaxf(fmaxf(wm[0][g], wm[1][g]), fmaxf(wm[2][g], wm[3][g]));
+    float l = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = wm[w][g] == -FLT_MAX ? 0.f : __expf(wm[w][g] - M);
+      l += f * wl[w][g];
+      acc += f * wo[w][g][d];
+    }
+    if (ns == 1) {
+      a.out[(size_t)(kvh * G + g) * HD + d] = acc / l;
+    } else {
+      float* dst = a.part + ((size_t)split * a.n_head + kvh * G + g) * (HD + 2);
+      st_sc1(dst + d, acc);
+      if (d == 0) {
+        st_sc1(dst + HD, M);
+        st_sc1(dst + HD + 1, l);
+      }
+    }
+  }
+  LFK_STAMP(4);
+  if (ns == 1 || a.debug_stop == 4) return;
+
+  // ---- 4. hand-off: the last arriving block of this kv head merges all splits
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(a.counters + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = (prev == ns - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(a.counters + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (last) __hip_atomic_store(a.counters + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  LFK_STAMP(5);
+  if constexpr (TL) { if (last && threadIdx.x == 0) a.dbg_clk[8] = wall_clock64() - t_entry; }
   if (!last) return;
-  // merge: M and the denominator per head by a wave reduction over splits, then
-  // every output element sums its splits with independent (unrolled) loads
-  __shared__ float Ms[8], den_s[8];
-  for (int g = wave; g < G; g += 4) {
-    const int l = lane;
-    const int h = kvh * G + g;
-    float m = -FLT_MAX;
-    for (int s2 = l; s2 < ns; s2 += 64) m = fmaxf(m, a.part[((size_t)s2 * a.n_head + h) * (HD + 2) + HD]);
-    m = wave_max(m);
-    float den = 0.f;
-    for (int s2 = l; s2 < ns; s2 += 64) {
-      const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
-      den += __expf(p[HD] - m) * p[HD + 1];
+  // every element's split values and the split statistics are loaded in one
+  // batch of independent sc1 loads (one memory round trip per 16 splits)
+  constexpr int EPT = (G * HD + 255) / 256;
+  constexpr int NSB = 16;
+  float M[EPT], num[EPT], den[EPT];
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) { M[j] = -FLT_MAX; num[j] = 0.f; den[j] = 0.f; }
+  for (int s0 = 0; s0 < ns; s0 += NSB) {
+    float mv[EPT][NSB], lv[EPT][NSB], pv[EPT][NSB];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      const int e = min(tid + 256 * j, G * HD - 1);
+      const int h = kvh * G + e / HD, d = e % HD;
+#pragma unroll
+      for (int i = 0; i < NSB; ++i) {
+        const int s2 = min(s0 + i, ns - 1);
+        const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
+        mv[j][i] = ld_sc1(p + HD);
+        lv[j][i] = ld_sc1(p + HD + 1);
+        pv[j][i] = ld_sc1(p + d);
+      }
     }
-    den = wave_sum(den);
-    if (l == 0) { Ms[g] = m; den_s[g] = den; }
-  }
-  __syncthreads();
-  for (int pi = tid; pi < G * HD; pi += 256) {
-    const int g = pi / HD, d = pi % HD;
-    const int h = kvh * G + g;
-    const float M = Ms[g];
-    float num = 0.f;
-#pragma unroll 4
-    for (int s2 = 0; s2 < ns; ++s2) {
-      const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
-      num += __expf(p[HD] - M) * p[d];
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) {
+      float mb = M[j];
+#pragma unroll
+      for (int i = 0; i < NSB; ++i) mb = (s0 + i < ns) ? fmaxf(mb, mv[j][i]) : mb;
+      const float r = __expf(M[j] - mb);
+      num[j] *= r;
+      den[j] *= r;
+#pragma unroll
+      for (int i = 0; i < NSB; ++i) {
+        const float f = (s0 + i < ns) ? __expf(mv[j][i] - mb) : 0.f;
+        num[j] += f * pv[j][i];
+        den[j] += f * lv[j][i];
+      }
+      M[j] = mb;
     }
-    a.out[(size_t)h * HD + d] = num / den_s[g];
   }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    const int e = tid + 256 * j;
+    if (e < G * HD) a.out[(size_t)(kvh * G + e / HD) * HD + e % HD] = num[j] / den[j];
+  }
+  if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[9] = wall_clock64() - t_entry; }
+#undef LFK_STAMP
 }
 
 size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim) {
   return (size_t)((n_ctx + CH - 1) / CH) * n_head * (head_dim + 2);
 }
 
+template <int HD, bool TL>
+static void launch_attn_decode_tl(const AttnDecodeArgs& a, int G, dim3 grid, hipStream_t s) {
+  switch (G) {
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1, TL>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2, TL>), grid, dim3(256), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<HD, 4, TL>), grid, dim3(256), 0, s, a); break;
+    case 8: hipLaunchKernelGGL((attn_decode_kernel<HD, 8, TL>), grid, dim3(256), 0, s, a); break;
+    default: throw std::runtime_error("attn_decode: gqa group must be 1, 2, 4 or 8");
+  }
+}
+template <int HD>
+static void launch_attn_decode(const AttnDecodeArgs& a, int G, dim3 grid, hipStream_t s) {
+  if (a.dbg_clk) launch_attn_decode_tl<HD, true>(a, G, grid, s);
+  else launch_attn_decode_tl<HD, false>(a, G, grid, s);
+}
+
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
   const int G = a.n_head / a.n_kv_head;
-  if (G > 8 || a.n_head % a.n_kv_head) throw std::runtime_error("attn_decode: gqa group must be <= 8");
+  if (a.n_head % a.n_kv_head) throw std::runtime_error("attn_decode: n_head % n_kv_head");
   if (!a.counters) throw std::runtime_error("attn_decode: counters workspace missing");
   dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH);
-  if (a.head_dim == 128) hipLaunchKernelGGL(attn_decode_kernel<128>, grid, dim3(256), 0, s, a);
-  else if (a.head_dim == 64) hipLaunchKernelGGL(attn_decode_kernel<64>, grid, dim3(256), 0, s, a);
+  if (a.head_dim == 128) launch_attn_decode<128>(a, G, grid, s);
+  else if (a.head_dim == 64) launch_attn_decode<64>(a, G, grid, s);
   else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");
 }
 

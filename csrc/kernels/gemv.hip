@@ -13,6 +13,10 @@
 //
 // Geometry: 256-thread blocks (4 waves), grid-stride over row groups with the
 // grid capped at 4 blocks per CU so the prologue is amortised over many rows.
+#include <algorithm>
+#include <map>
+#include <mutex>
+
 #include "kernels.h"
 #include "qdot.h"
 
@@ -20,106 +24,151 @@ namespace lfk {
 
 static constexpr int kMaxBlocks = 1024;  // 256 CUs x 4
 
+// Block prologue: x (or x * w_norm) -> per-32 int8 + f32 scale in LDS.
+//
+// Split in two so its global loads are issued BEFORE the wave's first weight
+// loads (vmcnt retires in order: an x load queued behind a weight stream would
+// make the prologue wait for the weights):
+//   load()   : every thread issues its first NB float4 of x (and w_norm);
+//   finish() : per-32 amax on DPP, q8 -> LDS, sum of squares -> one barrier.
+// RMSNorm's 1/rms is a scalar, so q8(x * w) equals q8(x * w / rms) up to the
+// block scale: the kernel multiplies its final dot products by the returned
+// scale instead of making a second pass over x.
 template <bool NORM>
-__device__ __forceinline__ void quantize_x(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
-                                           int8_t* xq, float* xd, float* red) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float scale = 1.f;
-  if constexpr (NORM) {
+struct XPrologue {
+  static constexpr int NB = 4;
+  float4 v[NB], w[NB];
+  __device__ __forceinline__ void load_batch(const float* __restrict__ x, const float* __restrict__ nw, int K, int j0) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int i = ((j0 + b) << 10) + tid * 4;
+      v[b] = i < K ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (NORM) w[b] = i < K ? *reinterpret_cast<const float4*>(nw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ __forceinline__ void load(const float* __restrict__ x, const float* __restrict__ nw, int K) {
+    load_batch(x, nw, K, 0);
+  }
+  // returns the RMSNorm scale (1 without NORM)
+  __device__ __forceinline__ float finish(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
+                                          int8_t* xq, float* xd, float* red) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nj = (K + 1023) >> 10;
     float ss = 0.f;
-    for (int i = tid * 4; i < K; i += 1024) {
-      float4 v = *reinterpret_cast<const float4*>(x + i);
-      ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    for (int j0 = 0; j0 < nj; j0 += NB) {
+      if (j0 > 0) load_batch(x, nw, K, j0);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const int i = ((j0 + b) << 10) + tid * 4;
+        if (i < K) {
+          float4 t = v[b];
+          if constexpr (NORM) {
+            ss += t.x * t.x + t.y * t.y + t.z * t.z + t.w * t.w;
+            t.x *= w[b].x; t.y *= w[b].y; t.z *= w[b].z; t.w *= w[b].w;
+          }
+          const float amax = max8(fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w))));
+          const float d = amax * (1.f / 127.f);
+          const float id = d > 0.f ? 1.f / d : 0.f;
+          const int q0 = __float2int_rn(t.x * id), q1 = __float2int_rn(t.y * id);
+          const int q2 = __float2int_rn(t.z * id), q3 = __float2int_rn(t.w * id);
+          *reinterpret_cast<int*>(xq + i) =
+              (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
+          if ((tid & 7) == 0) xd[i >> 5] = d;
+        }
+      }
     }
-    ss = wave_sum(ss);
-    if (lane == 0) red[wave] = ss;
-    __syncthreads();
-    const float tot = red[0] + red[1] + red[2] + red[3];
-    scale = rsqrtf(tot / (float)K + eps);
-  }
-  for (int i = tid * 4; i < K; i += 1024) {
-    float4 v = *reinterpret_cast<const float4*>(x + i);
     if constexpr (NORM) {
-      float4 w = *reinterpret_cast<const float4*>(nw + i);
-      v.x *= scale * w.x; v.y *= scale * w.y; v.z *= scale * w.z; v.w *= scale * w.w;
+      ss = wave_sum_fast(ss);
+      if (lane == 0) red[wave] = ss;
     }
-    float amax = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    amax = fmaxf(amax, __shfl_xor(amax, 4));
-    const float d = amax * (1.f / 127.f);
-    const float id = d > 0.f ? 1.f / d : 0.f;
-    const int q0 = __float2int_rn(v.x * id), q1 = __float2int_rn(v.y * id);
-    const int q2 = __float2int_rn(v.z * id), q3 = __float2int_rn(v.w * id);
-    *reinterpret_cast<int*>(xq + i) = (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-    if ((tid & 7) == 0) xd[i >> 5] = d;
+    __syncthreads();
+    if constexpr (NORM) return rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+    return 1.f;
   }
-  __syncthreads();
+};
+
+// one-call form (MoE down, where there is no weight prefetch to order against)
+template <bool NORM>
+__device__ __forceinline__ float quantize_x(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
+                                            int8_t* xq, float* xd, float* red) {
+  XPrologue<NORM> xp;
+  xp.load(x, nw, K);
+  return xp.finish(x, nw, eps, K, xq, xd, red);
 }
 
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
-// NR rows of one matrix against the LDS-resident q8 x, K-slice `ks` of `wk`
-// (chunks ks*64 + lane + 64*wk*j). Loads for two passes of all NR rows are
-// issued before any math (2*NR independent 16-B loads per lane in flight);
-// out-of-range chunks are clamped (loaded, then ignored).
-template <int QT, int NR>
-__device__ __forceinline__ void load_pair(WRaw<QT> (&w)[2][NR], const RowPtr (&R)[NR], int c0, int step, int nchunks,
-                                          int lane) {
+// Weight stream of one wave item: NR rows x U passes of 64 chunks, all loads
+// issued before any math (NR*U independent 16-B loads per lane in flight).
+// Chunks past the row end are clamped (loaded from the last chunk, ignored).
+template <int QT, int NR, int U>
+struct WStream {
+  WRaw<QT> w[U][NR];
+  __device__ __forceinline__ void load(const RowPtr (&R)[NR], int c0, int nchunks, int lane) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = min(c0 + step * u + lane, nchunks - 1);
+    for (int u = 0; u < U; ++u) {
+      const int c = min(c0 + 64 * u + lane, nchunks - 1);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) wload<QT>(w[u][r], R[r], c);
-  }
-}
-
-template <int QT, int NR>
-__device__ __forceinline__ void dot_pair(const WRaw<QT> (&w)[2][NR], int c0, int step, int nchunks, const int8_t* xq,
-                                         const float* xd, float (&acc)[NR], int lane) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = c0 + step * u + lane;
-    if (c < nchunks) {
-      XChunk X;
-      load_x<QT>(X, xq, xd, c);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) acc[r] += wdot<QT>(w[u][r], X, c);
+      for (int r = 0; r < NR; ++r) wload<QT>(w[u][r], R[r], c);
     }
   }
-}
-
-template <int QT, int NR>
-__device__ __forceinline__ void dot_rows(const RowPtr (&R)[NR], int nchunks, const int8_t* xq, const float* xd,
-                                         float (&acc)[NR], int lane) {
-  for (int c0 = 0; c0 < nchunks; c0 += 128) {
-    WRaw<QT> w[2][NR];
-    load_pair<QT, NR>(w, R, c0, 64, nchunks, lane);
-    dot_pair<QT, NR>(w, c0, 64, nchunks, xq, xd, acc, lane);
-  }
+  __device__ __forceinline__ void dot(int c0, int nchunks, const int8_t* xq, const float* xd, float (&acc)[NR],
+                                      int lane) const {
 #pragma unroll
-  for (int r = 0; r < NR; ++r) acc[r] = wave_sum(acc[r]);
-}
-
-// rows per wave-item: enough independent loads in flight without dropping below
-// 2 waves/SIMD (Q6_K carries 4 loads per chunk, F16/F32 8)
-template <int QT>
-constexpr int rows_per_item() { return (QT == T_Q4_K || QT == T_Q8_0 || QT == T_Q5_K) ? 4 : 2; }
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + 64 * u + lane;
+      if (c < nchunks) {
+        XChunk X;
+        load_x<QT>(X, xq, xd, c);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc[r] += wdot<QT>(w[u][r], X, c);
+      }
+    }
+  }
+  // rest of the row after the first pass group was loaded by the caller
+  __device__ __forceinline__ void finish_rows(const RowPtr (&R)[NR], int nchunks, const int8_t* xq, const float* xd,
+                                              float (&acc)[NR], int lane) {
+    for (int c0 = 0;;) {
+      dot(c0, nchunks, xq, xd, acc, lane);
+      c0 += 64 * U;
+      if (c0 >= nchunks) break;
+      load(R, c0, nchunks, lane);
+    }
+  }
+};
 
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
-// pick acc[lane] for lanes < NR (every lane holds every reduced row)
+// Reduce NR per-lane partial sums over the wave so that lane l ends up with the
+// total of row (l % NR): a butterfly over offsets 32..NR, then a transposing
+// exchange for the last log2(NR) offsets (no dynamic register indexing).
 template <int NR>
-__device__ __forceinline__ float pick(const float (&acc)[NR], int lane) {
-  float v = acc[0];
+__device__ __forceinline__ float reduce_rows(float (&acc)[NR], int lane) {
 #pragma unroll
-  for (int r = 1; r < NR; ++r) v = lane == r ? acc[r] : v;
-  return v;
+  for (int o = 32; o >= NR; o >>= 1)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] += __shfl_xor(acc[r], o);
+  if constexpr (NR == 1) {
+    return acc[0];
+  } else if constexpr (NR == 2) {
+    const bool hi = lane & 1;
+    float z = hi ? acc[1] : acc[0];
+    const float w = hi ? acc[0] : acc[1];
+    return z + __shfl_xor(w, 1);
+  } else {
+    static_assert(NR == 4, "rows per item must be 1, 2 or 4");
+    const bool b1 = lane & 2;
+    float x0 = b1 ? acc[2] : acc[0], x1 = b1 ? acc[3] : acc[1];
+    const float y0 = b1 ? acc[0] : acc[2], y1 = b1 ? acc[1] : acc[3];
+    x0 += __shfl_xor(y0, 2);
+    x1 += __shfl_xor(y1, 2);
+    const bool b0 = lane & 1;
+    const float z = b0 ? x1 : x0, w = b0 ? x0 : x1;
+    return z + __shfl_xor(w, 1);
+  }
 }
 
-// K split over `wk` waves of the block (wk = 1, 2 or 4, chosen on the host so
-// every wave has >= one full 64-chunk pass): a block holds 4/wk row groups;
-// the wk partial sums of a group meet in LDS.
 template <int EPI, int NR>
 __device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups, RowPtr (&R)[NR], int& slot, int& f0) {
   constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
@@ -140,47 +189,62 @@ __device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups,
   }
 }
 
-// One wave = one row group of NR rows (NF outputs); 4 waves per block; grid
-// capped at 4 blocks/CU and strided over row groups. Measured on MI355X this
-// simple form (115 VGPRs for Q4_K, 4 waves/SIMD) beat variants that prefetch
-// across the prologue or split K across waves (170-200 VGPRs): occupancy wins.
-template <int QT, int EPI, int NR, bool NORM>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a, int /*unused*/) {
+// One wave = one item of NR rows (NF outputs); 4 waves per block; grid capped at
+// 4 blocks/CU and strided over items. Latency hiding: the first weight loads
+// of a wave go out BEFORE the block's x prologue (norm + q8 quantisation into
+// LDS), and the next item's first loads go out before the current item's
+// cross-lane reduction and epilogue.
+template <int QT, int EPI, int NR, int U, bool NORM>
+__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int K = a.w.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + K);
   float* red = xd + (K >> 5);
-  quantize_x<NORM>(a.x, a.norm_w, a.eps, K, xq, xd, red);
   const int wave = wave_id(), lane = threadIdx.x & 63;
   const int nchunks = K >> 5;
   constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
   const int groups = (a.n_out + NF - 1) / NF;
   const int total = groups * a.n_slots;
-  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
-    RowPtr R[NR];
-    int slot, f0;
+  const int stride = gridDim.x * 4;
+  int item = blockIdx.x * 4 + wave;
+  RowPtr R[NR];
+  int slot = 0, f0 = 0;
+  WStream<QT, NR, U> ws;
+  XPrologue<NORM> xp;
+  if (a.debug != 1) xp.load(a.x, a.norm_w, K);
+  if (item < total) {
     item_rows<EPI, NR>(a, item, groups, R, slot, f0);
+    ws.load(R, 0, nchunks, lane);
+  }
+  const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
+  if (a.debug == 2) {
+    if (threadIdx.x == 0) a.out[0] = (float)xq[5] * xs;
+    return;
+  }
+  while (item < total) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
-    dot_rows<QT, NR>(R, nchunks, xq, xd, acc, lane);
-    if (lane < NF && f0 + lane < a.n_out) {
-      float* o = a.out + (size_t)slot * a.out_slot_stride + f0 + lane;
-      if constexpr (EPI == EPI_SWIGLU) {
-        float g = acc[0], u = acc[NF];
-#pragma unroll
-        for (int r = 1; r < NF; ++r) {
-          g = lane == r ? acc[r] : g;
-          u = lane == r ? acc[NF + r] : u;
-        }
-        *o = silu(g) * u;
-      } else {
-        const float v = pick<NR>(acc, lane);
-        if constexpr (EPI == EPI_STORE) *o = a.resid ? v + a.resid[f0 + lane] : v;
-        else *o += v;
-      }
+    ws.finish_rows(R, nchunks, xq, xd, acc, lane);
+    const int cs = slot, cf = f0;
+    const int next = item + stride;
+    if (next < total) {
+      item_rows<EPI, NR>(a, next, groups, R, slot, f0);
+      ws.load(R, 0, nchunks, lane);
     }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] *= xs;
+    const float v = reduce_rows<NR>(acc, lane);        // lane l: row l % NR
+    if constexpr (EPI == EPI_SWIGLU) {
+      const float u = __shfl(v, (lane + NF) & 63);      // up row NF + r sits in lane NF + r
+      if (lane < NF && cf + lane < a.n_out) a.out[(size_t)cs * a.out_slot_stride + cf + lane] = silu(v) * u;
+    } else if (lane < NF && cf + lane < a.n_out) {
+      float* o = a.out + (size_t)cs * a.out_slot_stride + cf + lane;
+      if constexpr (EPI == EPI_STORE) *o = a.resid ? v + a.resid[cf + lane] : v;
+      else *o += v;
+    }
+    item = next;
   }
 }
 
@@ -200,17 +264,95 @@ static inline int grid_for(int items, int per_block = 4) {
   return b < 1 ? 1 : (b > kMaxBlocks ? kMaxBlocks : b);
 }
 
+// Blocks of `kern` that are resident at once on the device (occupancy x CUs):
+// the grid-stride GEMVs launch at most this many so no block waits for a second
+// dispatch wave (its x prologue would be exposed after the first wave drains).
+template <typename F>
+static int resident_blocks(F kern, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> cache;
+  const auto key = std::make_pair(reinterpret_cast<const void*>(kern), lds);
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per_cu = 0;
+  hipGetDevice(&dev);
+  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds);
+  const int r = std::max(1, per_cu) * std::max(1, cus);
+  cache[key] = r;
+  return r;
+}
+template <typename F>
+static dim3 gemv_grid(F kern, size_t lds, int items) {
+  const int want = std::max(1, (items + 3) / 4);
+  return dim3(std::min(want, resident_blocks(kern, lds)));
+}
+
+// (rows per item, passes per load group) for a weight type and shape.
+// Items: prefer >= 2048 (8 waves per CU) so the grid is latency-tolerant;
+// loads in flight per lane NR*U <= LB (register budget of the type's WRaw).
+struct GemvCfg {
+  int nr, u;
+};
+static int pow2_floor(int v) {
+  int p = 1;
+  while (p * 2 <= v) p *= 2;
+  return p;
+}
+static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
+  static const char* env = getenv("LFK_GEMV_CFG");  // "nr,u" override (tuning)
+  if (env && *env) {
+    GemvCfg c{4, 2};
+    if (sscanf(env, "%d,%d", &c.nr, &c.u) == 2 && c.nr >= min_nr) return c;
+  }
+  const int LB = (qt == T_F32) ? 2 : (qt == T_F16 ? 4 : 8);
+  int nr = (qt == T_F32 || qt == T_F16) ? 2 : 4;
+  while (nr > min_nr && rows / nr < 2048) nr /= 2;
+  const int passes = (nchunks + 63) / 64;
+  int u = pow2_floor(std::max(1, std::min(LB / nr, passes)));
+  if (nr * u > LB) u = std::max(1, LB / nr);
+  return {nr, u};
+}
+
+#define LFK_NRU_DISPATCH(NR_, U_, ...)                                              \
+  do {                                                                               \
+    if (NR_ == 4 && U_ >= 2) { constexpr int NR = 4, U = 2; __VA_ARGS__; }           \
+    else if (NR_ == 4) { constexpr int NR = 4, U = 1; __VA_ARGS__; }                 \
+    else if (NR_ == 2 && U_ >= 4) { constexpr int NR = 2, U = 4; __VA_ARGS__; }      \
+    else if (NR_ == 2 && U_ == 2) { constexpr int NR = 2, U = 2; __VA_ARGS__; }      \
+    else if (NR_ == 2) { constexpr int NR = 2, U = 1; __VA_ARGS__; }                 \
+    else if (U_ >= 8) { constexpr int NR = 1, U = 8; __VA_ARGS__; }                  \
+    else if (U_ == 4) { constexpr int NR = 1, U = 4; __VA_ARGS__; }                  \
+    else if (U_ == 2) { constexpr int NR = 1, U = 2; __VA_ARGS__; }                  \
+    else { constexpr int NR = 1, U = 1; __VA_ARGS__; }                               \
+  } while (0)
+
+template <int QT, int EPI, int NR, int U>
+static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
+  if constexpr (EPI == EPI_SWIGLU && NR < 2) {
+    throw std::runtime_error("gemv: swiglu needs >= 2 rows per item");
+  } else if constexpr ((QT == T_F32 || QT == T_F16) && NR * U > 4) {
+    throw std::runtime_error("gemv: config exceeds the F16/F32 register budget");
+  } else {
+    constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
+    const size_t lds = a.w.K + (a.w.K / 32) * 4 + 64;
+    const int items = (a.n_out + NF - 1) / NF * a.n_slots;
+    if (a.norm_w) {
+      auto k = gemv_kernel<QT, EPI, NR, U, true>;
+      hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+    } else {
+      auto k = gemv_kernel<QT, EPI, NR, U, false>;
+      hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+    }
+  }
+}
 
 template <int QT, int EPI>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
-  constexpr int NR = rows_per_item<QT>();
-  constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
-  const size_t lds = a.w.K + (a.w.K / 32) * 4 + 32 + 4 * NR * 4 + 64;
-  const int items = (a.n_out + NF - 1) / NF * a.n_slots;
-  dim3 grid(grid_for(items)), block(256);
-  const int wk = 1;
-  if (a.norm_w) hipLaunchKernelGGL((gemv_kernel<QT, EPI, NR, true>), grid, block, lds, s, a, wk);
-  else hipLaunchKernelGGL((gemv_kernel<QT, EPI, NR, false>), grid, block, lds, s, a, wk);
+  const int rows = (EPI == EPI_SWIGLU ? 2 * a.n_out : a.n_out) * a.n_slots;
+  const GemvCfg c = pick_cfg(QT, rows, a.w.K >> 5, EPI == EPI_SWIGLU ? 2 : 1);
+  LFK_NRU_DISPATCH(c.nr, c.u, (launch_gemv_cfg<QT, EPI, NR, U>(a, s)));
 }
 
 template <int QT>
@@ -265,79 +407,117 @@ struct QkvLaunch {
 
 // One launch per run of Q/K/V segments sharing a quant type (measured: mixing
 // two types in one kernel raised VGPRs past 200 and ran slower than 2 launches).
-template <int QT>
+// Items are NR (even) consecutive rows, so RoPE pairs (2j, 2j+1) meet in one
+// wave after the reduction.
+template <int QT, int NR>
+__device__ __forceinline__ void qkv_item(const QkvLaunch& a, int item, RowPtr (&R)[NR], int& si, int& r0) {
+  int it = item;
+  si = 0;
+  while (si < a.nseg - 1 && it >= a.seg[si].rows / NR) { it -= a.seg[si].rows / NR; ++si; }
+  r0 = it * NR;
+  const QkvSeg& sg = a.seg[si];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) R[r] = row_ptr(sg.base, sg.P, (unsigned)(r0 + r));
+}
+
+template <int QT, int NR, int U>
 __global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NR = rows_per_item<QT>();
   const int K = a.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + K);
   float* red = xd + (K >> 5);
-  if (a.norm_w) quantize_x<true>(a.x, a.norm_w, a.eps, K, xq, xd, red);
-  else quantize_x<false>(a.x, nullptr, a.eps, K, xq, xd, red);
   const int wave = wave_id(), lane = threadIdx.x & 63;
   int total = 0;
   for (int i = 0; i < a.nseg; ++i) total += a.seg[i].rows / NR;
   const int nchunks = K >> 5;
   const int hd = a.head_dim;
+  const int stride = gridDim.x * 4;
+  int item = blockIdx.x * 4 + wave;
+  RowPtr R[NR];
+  int si = 0, r0 = 0;
+  WStream<QT, NR, U> ws;
+  XPrologue<true> xp;   // QKV always follows the attention RMSNorm
+  xp.load(a.x, a.norm_w, K);
+  if (item < total) {
+    qkv_item<QT, NR>(a, item, R, si, r0);
+    ws.load(R, 0, nchunks, lane);
+  }
+  const float xs = xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red);
   const int pos = *a.pos;
-  for (int item = blockIdx.x * 4 + wave; item < total; item += gridDim.x * 4) {
-    int it = item, si = 0;
-    while (si < a.nseg - 1 && it >= a.seg[si].rows / NR) { it -= a.seg[si].rows / NR; ++si; }
-    const QkvSeg& sg = a.seg[si];
-    const int r0 = it * NR;
-    RowPtr R[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) R[r] = row_ptr(sg.base, sg.P, (unsigned)(r0 + r));
+  while (item < total) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
-    dot_rows<QT, NR>(R, nchunks, xq, xd, acc, lane);
-    float v = pick<NR>(acc, lane);
+    ws.finish_rows(R, nchunks, xq, xd, acc, lane);
+    const int csi = si, cr0 = r0;
+    const int next = item + stride;
+    if (next < total) {
+      qkv_item<QT, NR>(a, next, R, si, r0);
+      ws.load(R, 0, nchunks, lane);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] *= xs;
+    float v = reduce_rows<NR>(acc, lane);
     const float partner = __shfl_xor(v, 1);
+    const int kind = a.seg[csi].kind;
     if (lane < NR) {
-      const int r = r0 + lane;
+      const int r = cr0 + lane;
       const int dd = r % hd;
-      if (sg.kind < 2) {
+      if (kind < 2) {
         const float2 cs = a.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
         v = (lane & 1) ? partner * cs.y + v * cs.x : v * cs.x - partner * cs.y;
       }
-      if (sg.kind == 0) {
+      if (kind == 0) {
         a.q_out[r] = v;
       } else {
-        __half* c = (sg.kind == 1 ? a.k_cache : a.v_cache) + ((size_t)(r / hd) * a.n_ctx + pos) * hd + dd;
+        __half* c = (kind == 1 ? a.k_cache : a.v_cache) + ((size_t)(r / hd) * a.n_ctx + pos) * hd + dd;
         *c = __float2half(v);
       }
     }
+    item = next;
   }
+}
+
+template <int QT>
+static void launch_qkv(const QkvLaunch& L, int rows, hipStream_t s) {
+  const GemvCfg c = pick_cfg(QT, rows, L.K >> 5, 2);
+  const size_t lds = L.K + (L.K / 32) * 4 + 64;
+  LFK_NRU_DISPATCH(c.nr, c.u, ({
+    if constexpr (NR >= 2 && !((QT == T_F32 || QT == T_F16) && NR * U > 4)) {
+      auto k = gemv_qkv_kernel<QT, NR, U>;
+      hipLaunchKernelGGL(k, gemv_grid(k, lds, rows / NR), dim3(256), lds, s, L);
+    } else {
+      throw std::runtime_error("gemv_qkv: bad config");
+    }
+  }));
 }
 
 void gemv_qkv(const QkvArgs& a, hipStream_t s) {
   const int K = a.wq.K;
   if (K % 32 || a.wk.K != K || a.wv.K != K) throw std::runtime_error("gemv_qkv: K mismatch");
-  if (a.wq.rows % 4 || a.wk.rows % 4) throw std::runtime_error("gemv_qkv: rows must be multiples of 4");
+  if (!a.norm_w) throw std::runtime_error("gemv_qkv: the attention RMSNorm weight is required");
+  if (a.wq.rows % 4 || a.wk.rows % 4 || a.wv.rows % 4) throw std::runtime_error("gemv_qkv: rows must be multiples of 4");
   const QMat* m[3] = {&a.wq, &a.wk, &a.wv};
-  const size_t lds = K + (K / 32) * 4 + 64;
   for (int i = 0; i < 3;) {
     QkvLaunch L{};
     L.K = K; L.x = a.x; L.norm_w = a.norm_w; L.eps = a.eps; L.q_out = a.q_out; L.k_cache = a.k_cache;
     L.v_cache = a.v_cache; L.n_ctx = a.n_ctx; L.head_dim = a.head_dim; L.pos = a.pos; L.rope = a.rope;
     const int t = m[i]->type;
-    int items = 0;
+    int rows = 0;
     while (i < 3 && m[i]->type == t) {
       L.seg[L.nseg] = QkvSeg{m[i]->base, m[i]->P, m[i]->rows, i};
-      items += m[i]->rows / (t == T_Q4_K || t == T_Q5_K || t == T_Q8_0 ? 4 : 2);
+      rows += m[i]->rows;
       ++L.nseg;
       ++i;
     }
-    dim3 grid(grid_for(items)), block(256);
     switch (t) {
-      case T_Q4_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q4_K>, grid, block, lds, s, L); break;
-      case T_Q5_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q5_K>, grid, block, lds, s, L); break;
-      case T_Q6_K: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q6_K>, grid, block, lds, s, L); break;
-      case T_Q8_0: hipLaunchKernelGGL(gemv_qkv_kernel<T_Q8_0>, grid, block, lds, s, L); break;
-      case T_F16: hipLaunchKernelGGL(gemv_qkv_kernel<T_F16>, grid, block, lds, s, L); break;
-      case T_F32: hipLaunchKernelGGL(gemv_qkv_kernel<T_F32>, grid, block, lds, s, L); break;
+      case T_Q4_K: launch_qkv<T_Q4_K>(L, rows, s); break;
+      case T_Q5_K: launch_qkv<T_Q5_K>(L, rows, s); break;
+      case T_Q6_K: launch_qkv<T_Q6_K>(L, rows, s); break;
+      case T_Q8_0: launch_qkv<T_Q8_0>(L, rows, s); break;
+      case T_F16: launch_qkv<T_F16>(L, rows, s); break;
+      case T_F32: launch_qkv<T_F32>(L, rows, s); break;
       default: throw std::runtime_error("gemv_qkv: unsupported type");
     }
   }
@@ -370,12 +550,15 @@ __global__ __launch_bounds__(256) void gemv_moe_down_kernel(MoeDownArgs a) {
       float acc[NR];
 #pragma unroll
       for (int r = 0; r < NR; ++r) acc[r] = 0.f;
-      dot_rows<QT, NR>(R, nchunks, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), acc, lane);
+      WStream<QT, NR, (QT == T_F32 ? 1 : 2)> wstr;
+      wstr.load(R, 0, nchunks, lane);
+      wstr.finish_rows(R, nchunks, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), acc, lane);
       const float ws = a.expert_w[s];
 #pragma unroll
       for (int r = 0; r < NR; ++r) tot[r] += ws * acc[r];
     }
-    if (lane < NR && r0 + lane < a.w.rows) a.out[r0 + lane] += pick<NR>(tot, lane);
+    const float v = reduce_rows<NR>(tot, lane);
+    if (lane < NR && r0 + lane < a.w.rows) a.out[r0 + lane] += v;
   }
 }
 

@@ -45,6 +45,7 @@ struct GemvArgs {
   const int* expert_ids = nullptr; // [n_slots] expert index per slot (device)
   int out_slot_stride = 0;
   const float* resid = nullptr;    // EPI_STORE: out = acc + resid (TP rank 0 residual)
+  int debug = 0;                   // microbenchmarks only: 1 = skip the x prologue, 2 = prologue only
 };
 void gemv(const GemvArgs& a, int epi, hipStream_t s);
 
@@ -94,6 +95,8 @@ struct AttnDecodeArgs {
   float* part = nullptr;          // workspace [n_split][n_head][hd + 2]
   int* counters = nullptr;        // [n_kv_head] zero-initialised; each launch leaves them at 0
   float* out = nullptr;           // [n_head][hd]
+  int debug_stop = 0;             // microbenchmarks only: 1..4 = exit after stage N (0 = full kernel)
+  long long* dbg_clk = nullptr;   // microbenchmarks only: wall_clock64 stamps of block (0,0) / the merging block
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
 size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim);
@@ -136,6 +139,8 @@ void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int h
 // out[i] = x[i] (+) ... small helpers
 void add_inplace(float* x, const float* y, int n, hipStream_t s);
 void set_i32(int* p, int v, hipStream_t s);
+// microbenchmark: out[0] = shader cycles, out[1] = wall ticks (100 MHz) of `iters` dependent FMAs
+void clock_probe(long long* out, int iters, hipStream_t s);
 
 // ---------------------------------------------------------------- sampling
 // Sampling parameters live in DEVICE memory so a captured decode graph serves

@@ -176,3 +176,23 @@ void fill_random_planar(uint8_t* base, int type, size_t rows, size_t K, float st
 }
 
 }  // namespace lfk
+
+namespace lfk {
+// Clock probe (microbenchmarks): a dependent FMA chain timed in shader cycles
+// (clock64) and in constant-rate wall ticks (wall_clock64, 100 MHz), so the
+// ratio gives the shader clock the GPU actually ran at.
+__global__ void clock_probe_kernel(long long* out, int iters) {
+  const long long w0 = wall_clock64(), c0 = clock64();
+  float x = threadIdx.x * 1e-3f;
+  for (int i = 0; i < iters; ++i) x = fmaf(x, 0.999f, 0.5f);
+  const long long c1 = clock64(), w1 = wall_clock64();
+  if (threadIdx.x == 0) {
+    out[0] = c1 - c0;
+    out[1] = w1 - w0;
+    out[2] = (long long)x;
+  }
+}
+void clock_probe(long long* out, int iters, hipStream_t s) {
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, out, iters);
+}
+}  // namespace lfk

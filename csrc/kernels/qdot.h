@@ -45,6 +45,31 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// ---- cross-lane reductions without the LDS crossbar (DPP within 16-lane rows,
+// v_readlane across rows): a few cycles per step instead of a ds_bpermute trip.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float max8(float v) {   // max over each aligned group of 8 lanes
+  v = fmaxf(v, dpp_f<0xB1>(v));                      // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_f<0x4E>(v));                      // quad_perm [2,3,0,1]
+  return fmaxf(v, dpp_f<0x141>(v));                  // row_half_mirror
+}
+__device__ __forceinline__ float row_sum16(float v) {  // sum over each 16-lane row
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);                        // row_mirror
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {  // wave-uniform result
+  v = row_sum16(v);
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+
 // x operand of one chunk, read once from LDS and reused across the NR rows.
 struct XChunk {
   int lo[4];

@@ -198,7 +198,8 @@ def test_attn_decode(torch, hd, H, Hkv, L):
         hip().attn_decode(dq.data_ptr(), dK.data_ptr(), dV.data_ptr(), pos.data_ptr(), n_ctx, H, Hkv, hd, scale,
                           ws.data_ptr(), out.data_ptr(), stream(), cnt.data_ptr())
         torch.cuda.synchronize()
-        assert rel_err(out.cpu().numpy(), _attn_ref(q, K, V, L, scale)) < 1e-4
+        # q*scale is rounded to f16 for the v_dot2 score path (upstream's KQ is f16 too)
+        assert rel_err(out.cpu().numpy(), _attn_ref(q, K, V, L, scale)) < 3e-3
     assert int(cnt.abs().sum()) == 0
 
 

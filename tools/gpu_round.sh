@@ -21,6 +21,11 @@ for s in "$@"; do
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
     micro) step micro 300 python tools/launch_microbench.py ;;
+    gemvb) step gemvb 300 python tools/gemv_bench.py --debug ;;
+    sweep) step sweep 900 bash tools/gemv_sweep.sh ;;
+    profgemv) export TMPDIR=/tmp; step profgemv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profgemv -o gemv \
+            --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
+    opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
     prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o decode \
             --output-format csv -- python3 tools/decode_bench.py --steps 64 --no-graph ;;
