@@ -34,15 +34,16 @@ static constexpr int kMaxBlocks = 1024;  // 256 CUs x 4
 // RMSNorm's 1/rms is a scalar, so q8(x * w) equals q8(x * w / rms) up to the
 // block scale: the kernel multiplies its final dot products by the returned
 // scale instead of making a second pass over x.
-template <bool NORM>
+template <bool NORM, int BLOCK = 256>
 struct XPrologue {
   static constexpr int NB = 4;
+  static constexpr int SHIFT = (BLOCK == 1024) ? 12 : 10;  // log2(BLOCK * 4 floats per batch slot)
   float4 v[NB], w[NB];
   __device__ __forceinline__ void load_batch(const float* __restrict__ x, const float* __restrict__ nw, int K, int j0) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const int i = ((j0 + b) << 10) + tid * 4;
+      const int i = ((j0 + b) << SHIFT) + tid * 4;
       v[b] = i < K ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (NORM) w[b] = i < K ? *reinterpret_cast<const float4*>(nw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -54,13 +55,13 @@ struct XPrologue {
   __device__ __forceinline__ float finish(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
                                           int8_t* xq, float* xd, float* red) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nj = (K + 1023) >> 10;
+    const int nj = (K + (1 << SHIFT) - 1) >> SHIFT;
     float ss = 0.f;
     for (int j0 = 0; j0 < nj; j0 += NB) {
       if (j0 > 0) load_batch(x, nw, K, j0);
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        const int i = ((j0 + b) << 10) + tid * 4;
+        const int i = ((j0 + b) << SHIFT) + tid * 4;
         if (i < K) {
           float4 t = v[b];
           if constexpr (NORM) {
@@ -83,7 +84,12 @@ struct XPrologue {
       if (lane == 0) red[wave] = ss;
     }
     __syncthreads();
-    if constexpr (NORM) return rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+    if constexpr (NORM) {
+      float tot = 0.f;
+#pragma unroll
+      for (int i = 0; i < BLOCK / 64; ++i) tot += red[i];
+      return rsqrtf(tot / (float)K + eps);
+    }
     return 1.f;
   }
 };
@@ -194,8 +200,8 @@ __device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups,
 // of a wave go out BEFORE the block's x prologue (norm + q8 quantisation into
 // LDS), and the next item's first loads go out before the current item's
 // cross-lane reduction and epilogue.
-template <int QT, int EPI, int NR, int U, bool NORM>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
+template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int K = a.w.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
@@ -206,12 +212,13 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
   const int groups = (a.n_out + NF - 1) / NF;
   const int total = groups * a.n_slots;
-  const int stride = gridDim.x * 4;
-  int item = blockIdx.x * 4 + wave;
+  constexpr int WPB = BLOCK / 64;
+  const int stride = gridDim.x * WPB;
+  int item = blockIdx.x * WPB + wave;
   RowPtr R[NR];
   int slot = 0, f0 = 0;
   WStream<QT, NR, U> ws;
-  XPrologue<NORM> xp;
+  XPrologue<NORM, BLOCK> xp;
   if (a.debug != 1) xp.load(a.x, a.norm_w, K);
   if (item < total) {
     item_rows<EPI, NR>(a, item, groups, R, slot, f0);
@@ -268,25 +275,26 @@ static inline int grid_for(int items, int per_block = 4) {
 // the grid-stride GEMVs launch at most this many so no block waits for a second
 // dispatch wave (its x prologue would be exposed after the first wave drains).
 template <typename F>
-static int resident_blocks(F kern, size_t lds) {
+static int resident_blocks(F kern, size_t lds, int block = 256) {
   static std::mutex mu;
   static std::map<std::pair<const void*, size_t>, int> cache;
-  const auto key = std::make_pair(reinterpret_cast<const void*>(kern), lds);
+  const auto key = std::make_pair(reinterpret_cast<const void*>(kern), lds * 4096 + (size_t)block);
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int dev = 0, cus = 0, per_cu = 0;
   hipGetDevice(&dev);
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds);
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
   const int r = std::max(1, per_cu) * std::max(1, cus);
   cache[key] = r;
   return r;
 }
 template <typename F>
-static dim3 gemv_grid(F kern, size_t lds, int items) {
-  const int want = std::max(1, (items + 3) / 4);
-  return dim3(std::min(want, resident_blocks(kern, lds)));
+static dim3 gemv_grid(F kern, size_t lds, int items, int block = 256) {
+  const int wpb = block / 64;
+  const int want = std::max(1, (items + wpb - 1) / wpb);
+  return dim3(std::min(want, resident_blocks(kern, lds, block)));
 }
 
 // (rows per item, passes per load group) for a weight type and shape.
@@ -301,12 +309,19 @@ static int pow2_floor(int v) {
   return p;
 }
 static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
+  const int LB = (qt == T_F32) ? 2 : ((qt == T_F16 || nchunks > 128) ? 4 : 8);
   static const char* env = getenv("LFK_GEMV_CFG");  // "nr,u" override (tuning)
   if (env && *env) {
     GemvCfg c{4, 2};
-    if (sscanf(env, "%d,%d", &c.nr, &c.u) == 2 && c.nr >= min_nr) return c;
+    if (sscanf(env, "%d,%d", &c.nr, &c.u) == 2 && c.nr >= min_nr && c.nr * c.u <= LB) return c;
   }
-  const int LB = (qt == T_F32) ? 2 : (qt == T_F16 ? 4 : 8);
+  // measured on MI355X with weights streamed from HBM (tools/gemv_sweep.sh):
+  //   K > 4096 (FFN down)         : one row per wave, 4 passes (Q6_K: 2) in flight
+  //   >= 16384 rows (gate/up, head): 4 rows per wave, 1 pass
+  if (qt != T_F32 && qt != T_F16) {
+    if (nchunks > 128) return {std::max(1, min_nr), qt == T_Q6_K ? 2 : 4};
+    if (rows >= 16384) return {4, 1};
+  }
   int nr = (qt == T_F32 || qt == T_F16) ? 2 : 4;
   while (nr > min_nr && rows / nr < 2048) nr /= 2;
   const int passes = (nchunks + 63) / 64;
@@ -322,8 +337,7 @@ static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
     else if (NR_ == 2 && U_ >= 4) { constexpr int NR = 2, U = 4; __VA_ARGS__; }      \
     else if (NR_ == 2 && U_ == 2) { constexpr int NR = 2, U = 2; __VA_ARGS__; }      \
     else if (NR_ == 2) { constexpr int NR = 2, U = 1; __VA_ARGS__; }                 \
-    else if (U_ >= 8) { constexpr int NR = 1, U = 8; __VA_ARGS__; }                  \
-    else if (U_ == 4) { constexpr int NR = 1, U = 4; __VA_ARGS__; }                  \
+    else if (U_ >= 4) { constexpr int NR = 1, U = 4; __VA_ARGS__; }                  \
     else if (U_ == 2) { constexpr int NR = 1, U = 2; __VA_ARGS__; }                  \
     else { constexpr int NR = 1, U = 1; __VA_ARGS__; }                               \
   } while (0)
@@ -336,13 +350,28 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
     throw std::runtime_error("gemv: config exceeds the F16/F32 register budget");
   } else {
     constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
-    const size_t lds = a.w.K + (a.w.K / 32) * 4 + 64;
+    const size_t lds = a.w.K + (a.w.K / 32) * 4 + 128;
     const int items = (a.n_out + NF - 1) / NF * a.n_slots;
-    if (a.norm_w) {
-      auto k = gemv_kernel<QT, EPI, NR, U, true>;
+    // K > 4096 (FFN down, 70B): 1024-thread blocks so the x prologue is one batch
+    // of loads per thread (issued before the weights) and 16 waves share its LDS
+    // copy; 16 waves per CU cap the registers at 128, hence NR*U <= 4 there
+    if (a.w.K > 4096) {
+      if constexpr (NR * U <= 4) {
+        if (a.norm_w) {
+          auto k = gemv_kernel<QT, EPI, NR, U, true, 1024>;
+          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+        } else {
+          auto k = gemv_kernel<QT, EPI, NR, U, false, 1024>;
+          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+        }
+      } else {
+        throw std::runtime_error("gemv: K > 4096 needs rows*passes <= 4");
+      }
+    } else if (a.norm_w) {
+      auto k = gemv_kernel<QT, EPI, NR, U, true, 256>;
       hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
     } else {
-      auto k = gemv_kernel<QT, EPI, NR, U, false>;
+      auto k = gemv_kernel<QT, EPI, NR, U, false, 256>;
       hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
     }
   }
@@ -381,9 +410,13 @@ void gemv(const GemvArgs& a, int epi, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------ QKV + RoPE + KV append
-// One launch covers a run of Q/K/V segments that share a quant type (Q4_K_M:
-// usually Q+K together, V separately when it is Q6_K). Items are 4 rows = two
-// RoPE pairs, so the rotation happens between lanes (2j, 2j+1) after the reduce.
+// One launch for the Q, K and V projections. Their rows form at most two runs of
+// equal quant type (Q4_K_M: [Q,K] Q4_K + [V] Q6_K on the bumped layers; Mixtral:
+// [Q] Q4_K + [K,V] Q8_0); each run gets its own contiguous range of blocks, so a
+// block only ever executes one type's code (registers = max of the two paths,
+// not the sum, and one kernel boundary instead of two). Items are NR (even)
+// consecutive rows, so RoPE pairs (2j, 2j+1) meet in one wave after the
+// reduction; the RoPE (cos, sin) of an item is loaded with its weights.
 struct QkvSeg {
   const uint8_t* base;
   Planes P;
@@ -393,6 +426,8 @@ struct QkvSeg {
 struct QkvLaunch {
   QkvSeg seg[3];
   int nseg;
+  int g1;        // first segment of the second type run (== nseg: one run)
+  int blocks0;   // blocks given to the first run
   int K;
   const float* x;
   const float* norm_w;
@@ -405,15 +440,12 @@ struct QkvLaunch {
   const float2* rope;
 };
 
-// One launch per run of Q/K/V segments sharing a quant type (measured: mixing
-// two types in one kernel raised VGPRs past 200 and ran slower than 2 launches).
-// Items are NR (even) consecutive rows, so RoPE pairs (2j, 2j+1) meet in one
-// wave after the reduction.
 template <int QT, int NR>
-__device__ __forceinline__ void qkv_item(const QkvLaunch& a, int item, RowPtr (&R)[NR], int& si, int& r0) {
+__device__ __forceinline__ void qkv_item(const QkvLaunch& a, int s_lo, int s_hi, int item, RowPtr (&R)[NR], int& si,
+                                         int& r0) {
   int it = item;
-  si = 0;
-  while (si < a.nseg - 1 && it >= a.seg[si].rows / NR) { it -= a.seg[si].rows / NR; ++si; }
+  si = s_lo;
+  while (si < s_hi - 1 && it >= a.seg[si].rows / NR) { it -= a.seg[si].rows / NR; ++si; }
   r0 = it * NR;
   const QkvSeg& sg = a.seg[si];
 #pragma unroll
@@ -421,40 +453,38 @@ __device__ __forceinline__ void qkv_item(const QkvLaunch& a, int item, RowPtr (&
 }
 
 template <int QT, int NR, int U>
-__global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int K = a.K;
-  int8_t* xq = reinterpret_cast<int8_t*>(smem);
-  float* xd = reinterpret_cast<float*>(smem + K);
-  float* red = xd + (K >> 5);
+__device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, int blk, int nblk, int pos,
+                                        XPrologue<true>& xp, int8_t* xq, float* xd, float* red) {
   const int wave = wave_id(), lane = threadIdx.x & 63;
   int total = 0;
-  for (int i = 0; i < a.nseg; ++i) total += a.seg[i].rows / NR;
-  const int nchunks = K >> 5;
+  for (int i = s_lo; i < s_hi; ++i) total += a.seg[i].rows / NR;
+  const int nchunks = a.K >> 5;
   const int hd = a.head_dim;
-  const int stride = gridDim.x * 4;
-  int item = blockIdx.x * 4 + wave;
+  const int stride = nblk * 4;
+  int item = blk * 4 + wave;
   RowPtr R[NR];
-  int si = 0, r0 = 0;
+  int si = s_lo, r0 = 0;
   WStream<QT, NR, U> ws;
-  XPrologue<true> xp;   // QKV always follows the attention RMSNorm
-  xp.load(a.x, a.norm_w, K);
+  float2 cs = make_float2(1.f, 0.f);
+  auto rope_of = [&](int r) { return a.rope[(size_t)pos * (hd >> 1) + ((r % hd) >> 1)]; };
   if (item < total) {
-    qkv_item<QT, NR>(a, item, R, si, r0);
+    qkv_item<QT, NR>(a, s_lo, s_hi, item, R, si, r0);
     ws.load(R, 0, nchunks, lane);
+    if (lane < NR && a.seg[si].kind < 2) cs = rope_of(r0 + lane);
   }
-  const float xs = xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red);
-  const int pos = *a.pos;
+  const float xs = xp.finish(a.x, a.norm_w, a.eps, a.K, xq, xd, red);
   while (item < total) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
     ws.finish_rows(R, nchunks, xq, xd, acc, lane);
     const int csi = si, cr0 = r0;
+    const float2 ccs = cs;
     const int next = item + stride;
     if (next < total) {
-      qkv_item<QT, NR>(a, next, R, si, r0);
+      qkv_item<QT, NR>(a, s_lo, s_hi, next, R, si, r0);
       ws.load(R, 0, nchunks, lane);
+      if (lane < NR && a.seg[si].kind < 2) cs = rope_of(r0 + lane);
     }
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] *= xs;
@@ -464,10 +494,7 @@ __global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
     if (lane < NR) {
       const int r = cr0 + lane;
       const int dd = r % hd;
-      if (kind < 2) {
-        const float2 cs = a.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
-        v = (lane & 1) ? partner * cs.y + v * cs.x : v * cs.x - partner * cs.y;
-      }
+      if (kind < 2) v = (lane & 1) ? partner * ccs.y + v * ccs.x : v * ccs.x - partner * ccs.y;
       if (kind == 0) {
         a.q_out[r] = v;
       } else {
@@ -479,18 +506,51 @@ __global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
   }
 }
 
+template <int QT0, int NR0, int U0, int QT1, int NR1, int U1, bool TWO>
+__global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int8_t* xq = reinterpret_cast<int8_t*>(smem);
+  float* xd = reinterpret_cast<float*>(smem + a.K);
+  float* red = xd + (a.K >> 5);
+  const int pos = *a.pos;
+  XPrologue<true> xp;   // QKV always follows the attention RMSNorm
+  xp.load(a.x, a.norm_w, a.K);
+  if (!TWO || (int)blockIdx.x < a.blocks0) {
+    qkv_run<QT0, NR0, U0>(a, 0, a.g1, blockIdx.x, TWO ? a.blocks0 : gridDim.x, pos, xp, xq, xd, red);
+  } else if constexpr (TWO) {
+    qkv_run<QT1, NR1, U1>(a, a.g1, a.nseg, blockIdx.x - a.blocks0, gridDim.x - a.blocks0, pos, xp, xq, xd, red);
+  }
+}
+
+static size_t qkv_lds(int K) { return K + (K / 32) * 4 + 128; }
+
 template <int QT>
-static void launch_qkv(const QkvLaunch& L, int rows, hipStream_t s) {
+static void launch_qkv1(QkvLaunch L, int rows, hipStream_t s) {
   const GemvCfg c = pick_cfg(QT, rows, L.K >> 5, 2);
-  const size_t lds = L.K + (L.K / 32) * 4 + 64;
+  const size_t lds = qkv_lds(L.K);
+  L.g1 = L.nseg;
+  L.blocks0 = 0;
   LFK_NRU_DISPATCH(c.nr, c.u, ({
     if constexpr (NR >= 2 && !((QT == T_F32 || QT == T_F16) && NR * U > 4)) {
-      auto k = gemv_qkv_kernel<QT, NR, U>;
+      auto k = gemv_qkv_kernel<QT, NR, U, QT, NR, U, false>;
       hipLaunchKernelGGL(k, gemv_grid(k, lds, rows / NR), dim3(256), lds, s, L);
     } else {
       throw std::runtime_error("gemv_qkv: bad config");
     }
   }));
+}
+
+// two type runs in one launch: (2 rows, 2 passes) items for the first run and
+// (2 rows, 1 pass) for the second (keeps the combined kernel near 128 VGPRs)
+template <int QT0, int QT1>
+static void launch_qkv2(QkvLaunch L, int rows0, int rows1, hipStream_t s) {
+  const size_t lds = qkv_lds(L.K);
+  auto k = gemv_qkv_kernel<QT0, 2, 2, QT1, 2, 1, true>;
+  const int items = rows0 / 2 + rows1 / 2;
+  const int nb = (int)gemv_grid(k, lds, items).x;
+  const double b0 = (double)qbytes(QT0, rows0, L.K), b1 = (double)qbytes(QT1, rows1, L.K);
+  L.blocks0 = std::min(nb - 1, std::max(1, (int)std::lround(nb * b0 / (b0 + b1))));
+  hipLaunchKernelGGL(k, dim3(nb), dim3(256), lds, s, L);
 }
 
 void gemv_qkv(const QkvArgs& a, hipStream_t s) {
@@ -499,25 +559,50 @@ void gemv_qkv(const QkvArgs& a, hipStream_t s) {
   if (!a.norm_w) throw std::runtime_error("gemv_qkv: the attention RMSNorm weight is required");
   if (a.wq.rows % 4 || a.wk.rows % 4 || a.wv.rows % 4) throw std::runtime_error("gemv_qkv: rows must be multiples of 4");
   const QMat* m[3] = {&a.wq, &a.wk, &a.wv};
-  for (int i = 0; i < 3;) {
-    QkvLaunch L{};
-    L.K = K; L.x = a.x; L.norm_w = a.norm_w; L.eps = a.eps; L.q_out = a.q_out; L.k_cache = a.k_cache;
-    L.v_cache = a.v_cache; L.n_ctx = a.n_ctx; L.head_dim = a.head_dim; L.pos = a.pos; L.rope = a.rope;
-    const int t = m[i]->type;
-    int rows = 0;
-    while (i < 3 && m[i]->type == t) {
-      L.seg[L.nseg] = QkvSeg{m[i]->base, m[i]->P, m[i]->rows, i};
-      rows += m[i]->rows;
-      ++L.nseg;
-      ++i;
+  QkvLaunch L{};
+  L.K = K; L.x = a.x; L.norm_w = a.norm_w; L.eps = a.eps; L.q_out = a.q_out; L.k_cache = a.k_cache;
+  L.v_cache = a.v_cache; L.n_ctx = a.n_ctx; L.head_dim = a.head_dim; L.pos = a.pos; L.rope = a.rope;
+  // runs of equal type
+  int run_start[3], run_type[3], nrun = 0;
+  for (int i = 0; i < 3; ++i) {
+    if (i == 0 || m[i]->type != m[i - 1]->type) { run_start[nrun] = i; run_type[nrun] = m[i]->type; ++nrun; }
+  }
+  for (int i = 0; i < 3; ++i) L.seg[i] = QkvSeg{m[i]->base, m[i]->P, m[i]->rows, i};
+  L.nseg = 3;
+  auto rows_of = [&](int lo, int hi) { int r = 0; for (int i = lo; i < hi; ++i) r += m[i]->rows; return r; };
+  if (nrun == 1) {
+    switch (run_type[0]) {
+      case T_Q4_K: launch_qkv1<T_Q4_K>(L, rows_of(0, 3), s); return;
+      case T_Q5_K: launch_qkv1<T_Q5_K>(L, rows_of(0, 3), s); return;
+      case T_Q6_K: launch_qkv1<T_Q6_K>(L, rows_of(0, 3), s); return;
+      case T_Q8_0: launch_qkv1<T_Q8_0>(L, rows_of(0, 3), s); return;
+      case T_F16: launch_qkv1<T_F16>(L, rows_of(0, 3), s); return;
+      case T_F32: launch_qkv1<T_F32>(L, rows_of(0, 3), s); return;
+      default: throw std::runtime_error("gemv_qkv: unsupported type");
     }
-    switch (t) {
-      case T_Q4_K: launch_qkv<T_Q4_K>(L, rows, s); break;
-      case T_Q5_K: launch_qkv<T_Q5_K>(L, rows, s); break;
-      case T_Q6_K: launch_qkv<T_Q6_K>(L, rows, s); break;
-      case T_Q8_0: launch_qkv<T_Q8_0>(L, rows, s); break;
-      case T_F16: launch_qkv<T_F16>(L, rows, s); break;
-      case T_F32: launch_qkv<T_F32>(L, rows, s); break;
+  }
+  if (nrun == 2) {
+    L.g1 = run_start[1];
+    const int r0 = rows_of(0, L.g1), r1 = rows_of(L.g1, 3);
+    const int t0 = run_type[0], t1 = run_type[1];
+    if (t0 == T_Q4_K && t1 == T_Q6_K) return launch_qkv2<T_Q4_K, T_Q6_K>(L, r0, r1, s);
+    if (t0 == T_Q4_K && t1 == T_Q5_K) return launch_qkv2<T_Q4_K, T_Q5_K>(L, r0, r1, s);
+    if (t0 == T_Q4_K && t1 == T_Q8_0) return launch_qkv2<T_Q4_K, T_Q8_0>(L, r0, r1, s);
+    if (t0 == T_Q5_K && t1 == T_Q6_K) return launch_qkv2<T_Q5_K, T_Q6_K>(L, r0, r1, s);
+    if (t0 == T_Q6_K && t1 == T_Q4_K) return launch_qkv2<T_Q6_K, T_Q4_K>(L, r0, r1, s);
+  }
+  // any other mix: one launch per segment
+  for (int i = 0; i < 3; ++i) {
+    QkvLaunch Li = L;
+    Li.seg[0] = L.seg[i];
+    Li.nseg = 1;
+    switch (m[i]->type) {
+      case T_Q4_K: launch_qkv1<T_Q4_K>(Li, m[i]->rows, s); break;
+      case T_Q5_K: launch_qkv1<T_Q5_K>(Li, m[i]->rows, s); break;
+      case T_Q6_K: launch_qkv1<T_Q6_K>(Li, m[i]->rows, s); break;
+      case T_Q8_0: launch_qkv1<T_Q8_0>(Li, m[i]->rows, s); break;
+      case T_F16: launch_qkv1<T_F16>(Li, m[i]->rows, s); break;
+      case T_F32: launch_qkv1<T_F32>(Li, m[i]->rows, s); break;
       default: throw std::runtime_error("gemv_qkv: unsupported type");
     }
   }

@@ -127,8 +127,10 @@ def test_moe_route(torch):
     np.testing.assert_allclose(w.cpu().numpy(), (p[[1, 7]] / p[[1, 7]].sum()).numpy(), rtol=1e-5)
 
 
-@pytest.mark.parametrize("tq,tk,tv", [(GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q6_K),
-                                      (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0)])
+@pytest.mark.parametrize("tq,tk,tv", [(GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q6_K),   # two runs, one launch
+                                      (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0),
+                                      (GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q4_K),   # one run
+                                      (GGMLType.Q6_K, GGMLType.Q4_K, GGMLType.Q6_K)])  # three runs: per-segment
 def test_gemv_qkv_rope_kvstore(torch, tq, tk, tv):
     rng = np.random.default_rng(10)
     K, hd, nh, nkv, n_ctx, pos = 512, 64, 8, 2, 32, 5

@@ -67,6 +67,12 @@ def main():
     nw = torch.ones(F, device="cuda")
     out = torch.zeros(2 * F, device="cuda")
     bufs = []
+    # weights are cycled through enough copies (>= 600 MB) that every launch streams
+    # from HBM, as in a real decode step (a single re-read matrix would sit in the
+    # 256 MB infinity cache and flatter the kernel)
+    def copies(nb):
+        return max(1, min(32, (600 << 20) // nb + 1))
+
     for name, t, R, K, epi, norm in [
         ("wo_q4k_4096x4096_add", Q4_K, d, d, 1, False),
         ("gateup_q4k_28672x4096_swiglu", Q4_K, 2 * F, d, 2, True),
@@ -94,16 +100,23 @@ def main():
     q = torch.zeros(d, device="cuda")
     pos = torch.tensor([500], dtype=torch.int32, device="cuda")
     rope = torch.randn(n_ctx * hd // 2 * 2, device="cuda")
-    wq, nq_b = mat(Q4_K, d, d, 11)
-    wk, nk_b = mat(Q4_K, 1024, d, 12)
-    wv4, nv4 = mat(Q4_K, 1024, d, 13)
-    wv6, nv6 = mat(Q6_K, 1024, d, 14)
-    for name, wv, tv, nvb in [("qkv_q4k_all", wv4, Q4_K, nv4), ("qkv_q4k_v_q6k", wv6, Q6_K, nv6)]:
-        def fn(st=s, wv=wv, tv=tv):
-            hip.gemv_qkv(wq.data_ptr(), Q4_K, wk.data_ptr(), Q4_K, wv.data_ptr(), tv, d, 1024, d, x.data_ptr(),
-                         nw.data_ptr(), 1e-5, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), n_ctx, hd, pos.data_ptr(),
-                         rope.data_ptr(), st)
+    NC = 32
+    wqs = [mat(Q4_K, d, d, 100 + c)[0] for c in range(NC)]
+    wks = [mat(Q4_K, 1024, d, 200 + c)[0] for c in range(NC)]
+    wv4s = [mat(Q4_K, 1024, d, 300 + c)[0] for c in range(NC)]
+    wv6s = [mat(Q6_K, 1024, d, 400 + c)[0] for c in range(NC)]
+    nq_b, nk_b = hip.qbytes(Q4_K, d, d), hip.qbytes(Q4_K, 1024, d)
+    nv4, nv6 = hip.qbytes(Q4_K, 1024, d), hip.qbytes(Q6_K, 1024, d)
+    qctr = [0]
+    for name, wvs, tv, nvb in [("qkv_q4k_all", wv4s, Q4_K, nv4), ("qkv_q4k_v_q6k", wv6s, Q6_K, nv6)]:
+        def fn(st=s, wvs=wvs, tv=tv):
+            c = qctr[0] % NC
+            qctr[0] += 1
+            hip.gemv_qkv(wqs[c].data_ptr(), Q4_K, wks[c].data_ptr(), Q4_K, wvs[c].data_ptr(), tv, d, 1024, d,
+                         x.data_ptr(), nw.data_ptr(), 1e-5, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), n_ctx, hd,
+                         pos.data_ptr(), rope.data_ptr(), st)
         timed(name, fn, nq_b + nk_b + nvb)
+    del wqs, wks, wv4s, wv6s
 
     # decode attention, 32 q heads on 8 kv heads, hd 128, at a few KV lengths
     part = torch.empty(hip.attn_decode_workspace_floats(n_ctx, 32, hd), device="cuda")
@@ -134,7 +147,7 @@ def main():
           p1.data_ptr(), n_ctx, 32, 8, hd, 1.0, part.data_ptr(), ao.data_ptr(), st, cnt.data_ptr(), debug_stop=1), 1)
     # shader clock: alone, and right behind a heavy GEMV in the same stream
     clk = torch.zeros(3, dtype=torch.int64, device="cuda")
-    for label, pre in (("alone", None), ("after_gemv", bufs[1])):
+    for label, pre in (("alone", None), ("after_gemv", bufs[1])):  # bufs[1]: one gate/up copy
         vals = []
         for _ in range(5):
             if pre is not None:
