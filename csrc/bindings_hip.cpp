@@ -162,9 +162,10 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gemv", [](uintptr_t w, int type, int rows, int K, uintptr_t x, uintptr_t norm, float eps, uintptr_t out,
                    int n_out, int epi, uintptr_t stream, int n_slots, uintptr_t ids, size_t expert_stride,
-                   int slot_stride, uintptr_t resid, int debug) {
+                   int slot_stride, uintptr_t resid, int debug, uintptr_t dbg_clk) {
     GemvArgs a;
     a.debug = debug;
+    a.dbg_clk = P<long long>(dbg_clk);
     a.w = make_qmat(P<void>(w), type, rows, K, expert_stride);
     a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.out = P<float>(out); a.n_out = n_out;
     a.n_slots = n_slots; a.expert_ids = P<int>(ids); a.out_slot_stride = slot_stride; a.resid = P<float>(resid);
@@ -173,7 +174,7 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("norm"), py::arg("eps"),
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
      py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
-     py::arg("debug") = 0);
+     py::arg("debug") = 0, py::arg("dbg_clk") = 0);
 
   m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,
                        uintptr_t x, uintptr_t norm, float eps, uintptr_t q_out, uintptr_t kc, uintptr_t vc, int n_ctx,

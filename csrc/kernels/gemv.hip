@@ -200,9 +200,21 @@ __device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups,
 // of a wave go out BEFORE the block's x prologue (norm + q8 quantisation into
 // LDS), and the next item's first loads go out before the current item's
 // cross-lane reduction and epilogue.
-template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK>
+// SPLITK (EPI_ADD only): an item is NR rows x one group of 64*U chunks, and its
+// partial dot products are atomically added to the residual. Every item is a
+// single load round trip, so waves stream continuously instead of walking a
+// long row pass by pass (the FFN down projection, K = 14336).
+template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false>
 __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // TL: per-block timeline (wall_clock64 ticks, microbenchmarks only):
+  // [entry, prologue done, first item done, exit, items done by wave 0]
+  long long* tl = nullptr;
+  if constexpr (TL) {
+    tl = a.dbg_clk + (size_t)blockIdx.x * 5;
+    if (threadIdx.x == 0) tl[0] = wall_clock64();
+  }
+  int n_done = 0;
   const int K = a.w.K;
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + K);
@@ -211,7 +223,8 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   const int nchunks = K >> 5;
   constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
   const int groups = (a.n_out + NF - 1) / NF;
-  const int total = groups * a.n_slots;
+  const int kparts = SPLITK ? (nchunks + 64 * U - 1) / (64 * U) : 1;
+  const int total = groups * a.n_slots * kparts;
   constexpr int WPB = BLOCK / 64;
   const int stride = gridDim.x * WPB;
   int item = blockIdx.x * WPB + wave;
@@ -219,12 +232,18 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   int slot = 0, f0 = 0;
   WStream<QT, NR, U> ws;
   XPrologue<NORM, BLOCK> xp;
+  // The x prologue runs BEFORE the first weight loads: measured on MI355X, a
+  // prologue whose L2 reads queue behind a saturated weight stream (its own CU's
+  // or its neighbours') costs more than the latency its prefetch would hide.
   if (a.debug != 1) xp.load(a.x, a.norm_w, K);
-  if (item < total) {
-    item_rows<EPI, NR>(a, item, groups, R, slot, f0);
-    ws.load(R, 0, nchunks, lane);
-  }
   const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
+  int kp = 0;
+  if (item < total) {
+    item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0);
+    if constexpr (SPLITK) kp = item % kparts;
+    ws.load(R, kp * 64 * U, nchunks, lane);
+  }
+  if constexpr (TL) { if (threadIdx.x == 0) tl[1] = wall_clock64(); }
   if (a.debug == 2) {
     if (threadIdx.x == 0) a.out[0] = (float)xq[5] * xs;
     return;
@@ -233,12 +252,14 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
-    ws.finish_rows(R, nchunks, xq, xd, acc, lane);
+    if constexpr (SPLITK) ws.dot(kp * 64 * U, nchunks, xq, xd, acc, lane);
+    else ws.finish_rows(R, nchunks, xq, xd, acc, lane);
     const int cs = slot, cf = f0;
     const int next = item + stride;
     if (next < total) {
-      item_rows<EPI, NR>(a, next, groups, R, slot, f0);
-      ws.load(R, 0, nchunks, lane);
+      item_rows<EPI, NR>(a, SPLITK ? next / kparts : next, groups, R, slot, f0);
+      if constexpr (SPLITK) kp = next % kparts;
+      ws.load(R, kp * 64 * U, nchunks, lane);
     }
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] *= xs;
@@ -249,9 +270,17 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
     } else if (lane < NF && cf + lane < a.n_out) {
       float* o = a.out + (size_t)cs * a.out_slot_stride + cf + lane;
       if constexpr (EPI == EPI_STORE) *o = a.resid ? v + a.resid[cf + lane] : v;
+      else if constexpr (SPLITK) atomicAdd(o, v);
       else *o += v;
     }
     item = next;
+    if constexpr (TL) {
+      if (threadIdx.x == 0 && n_done == 0) tl[2] = wall_clock64();
+      ++n_done;
+    }
+  }
+  if constexpr (TL) {
+    if (threadIdx.x == 0) { tl[3] = wall_clock64(); tl[4] = n_done; }
   }
 }
 
@@ -355,7 +384,8 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
     // K > 4096 (FFN down, 70B): 1024-thread blocks so the x prologue is one batch
     // of loads per thread (issued before the weights) and 16 waves share its LDS
     // copy; 16 waves per CU cap the registers at 128, hence NR*U <= 4 there
-    if (a.w.K > 4096) {
+    static const bool force1024 = getenv("LFK_GEMV_BLOCK") && atoi(getenv("LFK_GEMV_BLOCK")) == 1024;
+    if (a.w.K > 4096 || (force1024 && NR * U <= 4)) {
       if constexpr (NR * U <= 4) {
         if (a.norm_w) {
           auto k = gemv_kernel<QT, EPI, NR, U, true, 1024>;
@@ -377,8 +407,61 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
   }
 }
 
+// microbenchmark: the heuristic's config, instrumented (TL) - Q4_K/Q6_K only
+template <int QT, int EPI>
+static void launch_gemv_tl(const GemvArgs& a, hipStream_t s) {
+  const int rows = (EPI == EPI_SWIGLU ? 2 * a.n_out : a.n_out) * a.n_slots;
+  const GemvCfg c = pick_cfg(QT, rows, a.w.K >> 5, EPI == EPI_SWIGLU ? 2 : 1);
+  LFK_NRU_DISPATCH(c.nr, c.u, ({
+    if constexpr (!(EPI == EPI_SWIGLU && NR < 2) && NR * U <= 4) {
+      constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
+      const size_t lds = a.w.K + (a.w.K / 32) * 4 + 128;
+      const int items = (a.n_out + NF - 1) / NF * a.n_slots;
+      if (a.w.K > 4096) {
+        auto k = gemv_kernel<QT, EPI, NR, U, false, 1024, true>;
+        hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+      } else if (a.norm_w) {
+        auto k = gemv_kernel<QT, EPI, NR, U, true, 256, true>;
+        hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+      } else {
+        auto k = gemv_kernel<QT, EPI, NR, U, false, 256, true>;
+        hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+      }
+    } else {
+      throw std::runtime_error("gemv timeline: config not instrumented");
+    }
+  }));
+}
+
+// split-K residual GEMV (EPI_ADD): 4 rows x 64 chunks per item
+template <int QT>
+static void launch_gemv_splitk(const GemvArgs& a, hipStream_t s) {
+  const size_t lds = a.w.K + (a.w.K / 32) * 4 + 128;
+  const int items = (a.n_out + 3) / 4 * a.n_slots * ((a.w.K / 32 + 63) / 64);
+  if (a.w.K > 4096) {  // long rows: 1024-thread blocks, one-batch x prologue
+    auto k = a.norm_w ? gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true>
+                      : gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true>;
+    hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+  } else if (a.norm_w) {
+    auto k = gemv_kernel<QT, EPI_ADD, 4, 1, true, 256, false, true>;
+    hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+  } else {
+    auto k = gemv_kernel<QT, EPI_ADD, 4, 1, false, 256, false, true>;
+    hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+  }
+}
+
 template <int QT, int EPI>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
+  if constexpr (EPI == EPI_ADD && (QT == T_Q4_K || QT == T_Q5_K || QT == T_Q6_K || QT == T_Q8_0)) {
+    static const char* sk = getenv("LFK_GEMV_SPLITK");  // "0" disables (A/B measurements)
+    const bool on = !(sk && sk[0] == '0');
+    if (on && !a.dbg_clk && a.w.K >= 4096 && !a.debug) return launch_gemv_splitk<QT>(a, s);
+  }
+  if (a.dbg_clk) {
+    if constexpr (QT == T_Q4_K || QT == T_Q6_K) return launch_gemv_tl<QT, EPI>(a, s);
+    else throw std::runtime_error("gemv timeline: Q4_K / Q6_K only");
+  }
   const int rows = (EPI == EPI_SWIGLU ? 2 * a.n_out : a.n_out) * a.n_slots;
   const GemvCfg c = pick_cfg(QT, rows, a.w.K >> 5, EPI == EPI_SWIGLU ? 2 : 1);
   LFK_NRU_DISPATCH(c.nr, c.u, (launch_gemv_cfg<QT, EPI, NR, U>(a, s)));

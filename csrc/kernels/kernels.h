@@ -45,7 +45,8 @@ struct GemvArgs {
   const int* expert_ids = nullptr; // [n_slots] expert index per slot (device)
   int out_slot_stride = 0;
   const float* resid = nullptr;    // EPI_STORE: out = acc + resid (TP rank 0 residual)
-  int debug = 0;                   // microbenchmarks only: 1 = skip the x prologue, 2 = prologue only
+  int debug = 0;                   // microbenchmarks only: 1 = skip the x prologue, 2 = prologue only, 3 = weights after it
+  long long* dbg_clk = nullptr;    // microbenchmarks only: per-block timeline [grid][5] (instrumented build)
 };
 void gemv(const GemvArgs& a, int epi, hipStream_t s);
 

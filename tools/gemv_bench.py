@@ -87,7 +87,7 @@ def main():
         n_out = R // 2 if epi == 2 else R
         big_out = torch.zeros(n_out, device="cuda")
 
-        for dbg in ((0, 1, 2) if args.debug else (0,)):
+        for dbg in ((0, 1, 2, 3) if args.debug else (0,)):
             def fn(st=s, w=w, t=t, R=R, K=K, epi=epi, norm=norm, n_out=n_out, big_out=big_out, dbg=dbg):
                 hip.gemv(w.data_ptr(), t, R, K, x.data_ptr(), nw.data_ptr() if norm else 0, 1e-5, big_out.data_ptr(),
                          n_out, epi, st, debug=dbg)

@@ -23,6 +23,8 @@ for s in "$@"; do
     micro) step micro 300 python tools/launch_microbench.py ;;
     gemvb) step gemvb 300 python tools/gemv_bench.py --debug ;;
     sweep) step sweep 900 bash tools/gemv_sweep.sh ;;
+    timeline) step timeline 300 python tools/gemv_timeline.py ;;
+    variants) step variants 900 bash tools/gemv_variants.sh ;;
     profgemv) export TMPDIR=/tmp; step profgemv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profgemv -o gemv \
             --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
