@@ -254,15 +254,19 @@ PYBIND11_MODULE(_hip, m) {
   });
   m.def("sampler_blocks", &sampler_blocks);
   m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cv,
-                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream, uintptr_t ct) {
+                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream, uintptr_t ct,
+                     uintptr_t dbg_clk) {
     SamplerArgs a;
+    a.dbg_clk = P<long long>(dbg_clk);
     a.cand_tau = P<unsigned>(ct);
     a.logits = P<float>(logits); a.V = V; a.p = P<SamplerParamsDev>(params); a.ring = P<int>(ring);
     a.state = P<int>(state); a.cand_val = P<float>(cv); a.cand_idx = P<int>(ci); a.out_tokens = P<int>(out_tokens);
     a.out_cap = out_cap; a.advance_pos = advance;
     sample(a, S(stream));
     hip_ok("sample");
-  });
+  }, py::arg("logits"), py::arg("V"), py::arg("params"), py::arg("ring"), py::arg("state"), py::arg("cv"),
+     py::arg("ci"), py::arg("out_tokens"), py::arg("out_cap"), py::arg("advance"), py::arg("stream"), py::arg("ct"),
+     py::arg("dbg_clk") = 0);
   m.def("sampler_params_bytes", [](int top_k, float top_p, float min_p, float temp, float rp, float fp, float pp,
                                    int last_n, unsigned long long seed, int greedy) {
     SamplerParamsDev p;

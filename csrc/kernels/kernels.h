@@ -167,7 +167,8 @@ struct SamplerArgs {
   float* logits_rw = nullptr;      // unused (penalties patch `logits` in place)
   float* cand_val = nullptr;       // workspace [sampler_blocks(V) * 64]
   int* cand_idx = nullptr;
-  unsigned* cand_tau = nullptr;    // workspace [sampler_blocks(V)]
+  unsigned* cand_tau = nullptr;    // workspace [2 * sampler_blocks(V)]: slice bounds, slice maxima
+  long long* dbg_clk = nullptr;    // microbenchmarks only: stage-2 timeline stamps (instrumented build)
   int* out_tokens = nullptr;       // optional device ring of sampled tokens [out_cap]
   int out_cap = 0;
   int advance_pos = 1;             // also bump state.pos (decode) after sampling

@@ -65,6 +65,13 @@ __device__ __forceinline__ float row_sum16(float v) {  // sum over each 16-lane 
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
+__device__ __forceinline__ float wave_max_fast(float v) {  // wave-uniform result
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
 __device__ __forceinline__ float wave_sum_fast(float v) {  // wave-uniform result
   v = row_sum16(v);
   return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));

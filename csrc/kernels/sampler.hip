@@ -3,13 +3,14 @@
 // draw - runs on the device, so only a 4-byte token id ever crosses to the host
 // (upstream copies 501 KiB of logits per token and samples on the CPU).
 //
-// Penalties: one wave patches the <= 64 penalised logits in place.
-// Stage 1 (one WAVE per 1K-logit slice, no LDS, no barrier): the slice's top-K
-// by an exact 32-step bisection on order-preserving integer keys (ballots).
-// Stage 2 (one block): candidates below the largest slice threshold are dropped
-// (they cannot be in the global top-K), the rest are selected exactly by one
-// wave, bitonic-sorted, then top-p / min-p / temperature / draw, and the device
-// state (token, position, RNG step, penalty ring) is updated.
+// Stage 1 (one WAVE per 1K-logit slice): penalties of the window tokens that
+// fall in the slice, then a top-K superset of the slice by an 8-way threshold
+// search (DPP reductions, ballots), plus the slice's lower bound of the global
+// K-th value.
+// Stage 2 (one block): candidates below the largest slice bound are dropped
+// (they cannot be in the global top-K), the survivors are compacted in LDS and
+// one wave selects, bitonic-sorts, applies top-p / min-p / temperature, draws,
+// and updates the device state (token, position, RNG step, penalty ring).
 //
 // The uniform draw is SplitMix64(seed ^ step*C) >> 40 - identical to
 // engine/sampling.py:philox_uniform and the CPU backend.
@@ -35,31 +36,6 @@ __device__ __forceinline__ int lanes_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
 }
 
-// Penalties, in place on the logits buffer (rewritten by the lm_head every step).
-// Lane i owns window entry i; only the first occurrence of a token applies it.
-__global__ __launch_bounds__(64) void sample_penalties(SamplerArgs a) {
-  const SamplerParamsDev& P = *a.p;
-  const int lane = threadIdx.x;
-  const int rlen = a.state[S_RING_LEN], rhead = a.state[S_RING_HEAD];
-  const int wn = min(rlen, P.last_n);
-  const int t = lane < wn ? a.ring[(rhead - wn + lane + 64) & 63] : -1;
-  int cnt = 0;
-  bool first = true;
-  for (int j = 0; j < 64; ++j) {
-    const int tj = __shfl(t, j);
-    if (tj == t) {
-      ++cnt;
-      if (j < lane) first = false;
-    }
-  }
-  if (t >= 0 && t < a.V && first) {
-    float l = a.logits[t];
-    l = l <= 0.f ? l * P.repeat_penalty : l / P.repeat_penalty;
-    l -= (float)cnt * P.freq_penalty + P.presence_penalty;
-    a.logits[t] = l;
-  }
-}
-
 // Superset selection by value bisection: find T with K <= count(v >= T) <= 64
 // (or the best effort after 40 halvings, ties), then every element >= T is a
 // candidate. A superset of the top-K is exact for the final selection: stage 2
@@ -72,22 +48,32 @@ __device__ __forceinline__ float wave_superset_threshold(const float (&v)[NE], i
     if (v[e] > -FLT_MAX) lo = fminf(lo, v[e]);
     hi = fmaxf(hi, v[e]);
   }
-  lo = -wave_max(-lo);
-  hi = wave_max(hi);
-  // invariant: count(>= T) >= K (T starts at the minimum); hi only ever lowers
+  lo = -wave_max_fast(-lo);
+  hi = wave_max_fast(hi);
+  // invariant: count(>= T) >= K (T starts at the minimum); hi only ever lowers.
+  // 8-way search per round (counts above 8 thresholds at once, DPP reductions).
   float T = lo;
   int cT = 0;
 #pragma unroll
   for (int e = 0; e < NE; ++e) cT += v[e] >= T;
-  cT = (int)wave_sum((float)cT);
-  for (int it = 0; it < 40 && cT > KMAX; ++it) {
-    const float mid = 0.5f * (T + hi);
-    if (!(mid > T) || !(mid < hi)) break;
-    int cm = 0;
+  cT = (int)wave_sum_fast((float)cT);
+  for (int it = 0; it < 16 && cT > KMAX; ++it) {
+    const float step = (hi - T) * (1.f / 9.f);
+    if (!(step > 0.f) || !(T + step > T)) break;
+    int best = -1, cbest = cT;
 #pragma unroll
-    for (int e = 0; e < NE; ++e) cm += v[e] >= mid;
-    cm = (int)wave_sum((float)cm);
-    if (cm >= K) { T = mid; cT = cm; } else { hi = mid; }
+    for (int j = 0; j < 8; ++j) {
+      const float t = T + step * (float)(j + 1);
+      int cm = 0;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) cm += v[e] >= t;
+      cm = (int)wave_sum_fast((float)cm);
+      if (cm >= K) { best = j; cbest = cm; }
+    }
+    const float newT = best >= 0 ? T + step * (float)(best + 1) : T;
+    hi = best < 7 ? T + step * (float)(best + 2) : hi;
+    T = newT;
+    cT = cbest;
   }
   return T;
 }
@@ -111,10 +97,16 @@ __device__ __forceinline__ int wave_collect(const float (&v)[NE], const int (&id
   return min(base, cap);
 }
 
+// Stage 1: one wave per 1024-logit slice. The repetition/frequency/presence
+// penalties of ring tokens that fall in this slice are applied here (the wave
+// stages its slice in LDS, lanes owning a first occurrence patch their entry),
+// then the slice's top-K superset is selected without LDS or barriers.
 __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
+  __shared__ float sl[SLICE];
   const int lane = threadIdx.x;
   const int lo = blockIdx.x * SLICE;
-  const int K = a.p->top_k;
+  const SamplerParamsDev& P = *a.p;
+  const int K = P.top_k;
   float v[NE1];
   int idx[NE1];
 #pragma unroll
@@ -123,6 +115,37 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
     v[e] = i < a.V ? a.logits[i] : -FLT_MAX;
     idx[e] = i;
   }
+  // ---- penalties (window = last min(ring_len, last_n) tokens)
+  const int rlen = a.state[S_RING_LEN], rhead = a.state[S_RING_HEAD];
+  const int wn = min(rlen, P.last_n);
+  const int t = lane < wn ? a.ring[(rhead - wn + lane + 64) & 63] : -1;
+  const bool mine = t >= lo && t < lo + SLICE && t < a.V;
+  if (__ballot(mine)) {  // wave-uniform: some window token lies in this slice
+#pragma unroll
+    for (int e = 0; e < NE1; ++e) sl[64 * e + lane] = v[e];
+    int cnt = 0;
+    bool first = true;
+    for (int j = 0; j < wn; ++j) {
+      const int tj = __builtin_amdgcn_readlane(t, j);
+      if (tj == t) {
+        ++cnt;
+        if (j < lane) first = false;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (mine && first) {
+      float l = sl[t - lo];
+      l = l <= 0.f ? l * P.repeat_penalty : l / P.repeat_penalty;
+      l -= (float)cnt * P.freq_penalty + P.presence_penalty;
+      sl[t - lo] = l;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int e = 0; e < NE1; ++e) v[e] = sl[64 * e + lane];
+  }
+  // ---- top-K superset of the slice
   const float T = wave_superset_threshold<NE1>(v, K);
   float* ov = a.cand_val + blockIdx.x * KMAX;
   int* oi = a.cand_idx + blockIdx.x * KMAX;
@@ -130,6 +153,17 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
   if (lane >= m) {
     ov[lane] = -FLT_MAX;
     oi[lane] = -1;
+  }
+  // this slice alone holds >= K values >= T, so the global K-th largest is >= T:
+  // stage 2 drops every candidate below the largest such slice bound
+  float vmax = -FLT_MAX;
+#pragma unroll
+  for (int e = 0; e < NE1; ++e) vmax = fmaxf(vmax, v[e]);
+  vmax = wave_max_fast(vmax);
+  if (lane == 0) {
+    const int nvalid = min(SLICE, a.V - lo);
+    a.cand_tau[blockIdx.x] = __float_as_uint(m >= K && nvalid >= K ? T : -FLT_MAX);
+    a.cand_tau[gridDim.x + blockIdx.x] = __float_as_uint(vmax);
   }
 }
 
@@ -145,73 +179,85 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
 // candidates (block-wide counts), collect <= 64 into LDS, then one wave sorts
 // (value desc, index asc), keeps K, applies top-p / min-p / temperature, draws,
 // and updates the device state.
-__device__ __forceinline__ int block_count(int c, int* red, int parity) {
-  c = (int)wave_sum((float)c);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[parity * 4 + wave] = c;
-  __syncthreads();
-  return red[parity * 4] + red[parity * 4 + 1] + red[parity * 4 + 2] + red[parity * 4 + 3];
-}
 
-template <int NE2>
+// Stage 2 (one 256-thread block): drop candidates below the largest slice
+// bound, compact the survivors into LDS (typically < 100), then ONE wave selects
+// a top-K superset of <= 64 from them (8-way threshold search, no barriers),
+// sorts (value desc, index asc), keeps K, applies top-p / min-p / temperature,
+// draws and updates the device state.
+static constexpr int CAP2 = 2048;  // survivors above the bounds (typically < 200)
+template <int NE2, bool TL = false>
 __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
+  long long t0 = 0;
+  if constexpr (TL) t0 = wall_clock64();
+#define LFK_ST(i) do { if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[i] = wall_clock64() - t0; } } while (0)
+  __shared__ float cval[CAP2];
+  __shared__ int cidx[CAP2];
   __shared__ float tval[KMAX];
   __shared__ int tidx[KMAX];
-  __shared__ int red[8];
-  __shared__ float redf[8];
+  __shared__ float redf[4];
   __shared__ int ncol;
   const int tid = threadIdx.x;
   const SamplerParamsDev& P = *a.p;
   const int K = P.top_k;
+  if (tid == 0) ncol = 0;
   float v[NE2];
   int idx[NE2];
 #pragma unroll
-  for (int e = 0; e < NE2; ++e) {
-    const int i = 256 * e + tid;
-    const bool ok = i < nb * KMAX;
-    const int id = ok ? a.cand_idx[i] : -1;
-    v[e] = (ok && id >= 0) ? a.cand_val[i] : -FLT_MAX;
-    idx[e] = id;
+  for (int e = 0; e < NE2; ++e) {  // independent loads (no value-dependent second load)
+    const int i = min(256 * e + tid, nb * KMAX - 1);
+    idx[e] = a.cand_idx[i];
+    v[e] = a.cand_val[i];
   }
-  // block min / max of the valid candidates
-  float lo = FLT_MAX, hi = -FLT_MAX;
-#pragma unroll
-  for (int e = 0; e < NE2; ++e) {
-    if (v[e] > -FLT_MAX) lo = fminf(lo, v[e]);
-    hi = fmaxf(hi, v[e]);
+  // Two lower bounds of the global K-th largest value: (a) each slice bound
+  // (that slice alone holds >= K values above it); (b) a superset threshold of
+  // the slice MAXIMA (>= K distinct slices have their maximum above it).
+  // (b) keeps the survivor count small even for flat (high-entropy) logits.
+  float lb = -FLT_MAX;
+  for (int b = tid; b < nb; b += 256) lb = fmaxf(lb, __uint_as_float(a.cand_tau[b]));
+  lb = wave_max_fast(lb);
+  if (tid < 64) {
+    float mx[2];
+    mx[0] = tid < nb ? __uint_as_float(a.cand_tau[nb + tid]) : -FLT_MAX;
+    mx[1] = tid + 64 < nb ? __uint_as_float(a.cand_tau[nb + 64 + tid]) : -FLT_MAX;
+    int valid = (mx[0] > -FLT_MAX) + (mx[1] > -FLT_MAX);
+    valid = (int)wave_sum_fast((float)valid);
+    if (valid >= K) lb = fmaxf(lb, wave_superset_threshold<2>(mx, K));
   }
-  lo = -wave_max(-lo);
-  hi = wave_max(hi);
-  if ((tid & 63) == 0) { redf[tid >> 6] = lo; redf[4 + (tid >> 6)] = hi; }
-  if (tid == 0) ncol = 0;
+  if ((tid & 63) == 0) redf[tid >> 6] = lb;
   __syncthreads();
-  lo = fminf(fminf(redf[0], redf[1]), fminf(redf[2], redf[3]));
-  hi = fmaxf(fmaxf(redf[4], redf[5]), fmaxf(redf[6], redf[7]));
-  float T = lo;
-  int c = 0;
-#pragma unroll
-  for (int e = 0; e < NE2; ++e) c += v[e] >= T && v[e] > -FLT_MAX;
-  int cT = block_count(c, red, 0);
-  for (int it = 0; it < 40 && cT > KMAX; ++it) {
-    const float mid = 0.5f * (T + hi);
-    if (!(mid > T) || !(mid < hi)) break;
-    c = 0;
-#pragma unroll
-    for (int e = 0; e < NE2; ++e) c += v[e] >= mid;
-    const int cm = block_count(c, red, (it + 1) & 1);
-    if (cm >= K) { T = mid; cT = cm; } else { hi = mid; }
-  }
+  lb = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
+  LFK_ST(0);
 #pragma unroll
   for (int e = 0; e < NE2; ++e) {
-    if (v[e] >= T && v[e] > -FLT_MAX) {
+    const bool ok = 256 * e + tid < nb * KMAX && idx[e] >= 0 && v[e] >= lb && v[e] > -FLT_MAX;
+    if (ok) {
       const int p = atomicAdd(&ncol, 1);
-      if (p < KMAX) { tval[p] = v[e]; tidx[p] = idx[e]; }
+      if (p < CAP2) { cval[p] = v[e]; cidx[p] = idx[e]; }
     }
   }
   __syncthreads();
+  LFK_ST(1);
   if (tid >= 64) return;
   const int lane = tid;
-  int m = min(ncol, KMAX);
+  const int n = min(ncol, CAP2);
+  constexpr int NW = CAP2 / 64;
+  float w[NW];
+  int wi[NW];
+#pragma unroll
+  for (int e = 0; e < NW; ++e) {
+    const int i = 64 * e + lane;
+    w[e] = i < n ? cval[i] : -FLT_MAX;
+    wi[e] = i < n ? cidx[i] : 0x7fffffff;
+  }
+  const float T = n > KMAX ? wave_superset_threshold<NW>(w, K) : -FLT_MAX;
+  if (lane == 0 && ncol > CAP2) a.state[S_NSTATE - 1] = ncol;  // overflow marker (diagnostics)
+  const int mcol = wave_collect<NW>(w, wi, T, KMAX, tval, tidx);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  LFK_ST(2);
+  int m = mcol;
   // ---- bitonic sort (descending value, ascending index) of <= 64 candidates
   float vv = lane < m ? tval[lane] : -FLT_MAX;
   int id = lane < m ? tidx[lane] : 0x7fffffff;
@@ -275,6 +321,7 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
     st[S_RING_HEAD] = (head + 1) & 63;
     st[S_RING_LEN] = min(st[S_RING_LEN] + 1, 64);
     if (a.out_tokens) a.out_tokens[st[S_NOUT] % a.out_cap] = tok;
+    LFK_ST(3);
     st[S_NOUT] += 1;
     st[S_STEP] += 1;
     if (a.advance_pos) st[S_POS] += 1;
@@ -285,11 +332,11 @@ int sampler_blocks(int V) { return (V + SLICE - 1) / SLICE; }
 
 void sample(const SamplerArgs& a, hipStream_t s) {
   const int nb = sampler_blocks(a.V);
-  hipLaunchKernelGGL(sample_penalties, dim3(1), dim3(64), 0, s, a);
   hipLaunchKernelGGL(sample_stage1, dim3(nb), dim3(64), 0, s, a);
   const int ncand = nb * KMAX;
-  if (ncand <= 256 * 8) hipLaunchKernelGGL(sample_stage2<8>, dim3(1), dim3(256), 0, s, a, nb);
-  else if (ncand <= 256 * 32) hipLaunchKernelGGL(sample_stage2<32>, dim3(1), dim3(256), 0, s, a, nb);
+  if (a.dbg_clk && ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, true>), dim3(1), dim3(256), 0, s, a, nb);
+  else if (ncand <= 256 * 8) hipLaunchKernelGGL((sample_stage2<8, false>), dim3(1), dim3(256), 0, s, a, nb);
+  else if (ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, false>), dim3(1), dim3(256), 0, s, a, nb);
   else throw std::runtime_error("GPU sampler: vocabulary too large (max 131072)");
 }
 

@@ -224,7 +224,7 @@ void Engine::alloc_buffers() {
   const int nb = sampler_blocks(hp_.n_vocab);
   cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
   cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
-  cand_tau_ = (unsigned*)dalloc(sizeof(unsigned) * nb);
+  cand_tau_ = (unsigned*)dalloc(sizeof(unsigned) * 2 * nb);  // slice bounds + slice maxima
   state_ = (int*)dalloc(sizeof(int) * S_NSTATE);
   ring_ = (int*)dalloc(sizeof(int) * 64);
   out_tokens_ = (int*)dalloc(sizeof(int) * 64);

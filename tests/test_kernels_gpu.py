@@ -306,7 +306,7 @@ def _run_sampler(torch, logits, ring_tokens, params, seed, step=0):
     nb = h.sampler_blocks(V)
     cv = torch.zeros(nb * 64, device="cuda")
     ci = torch.zeros(nb * 64, dtype=torch.int32, device="cuda")
-    ct = torch.zeros(nb, dtype=torch.int32, device="cuda")
+    ct = torch.zeros(2 * nb, dtype=torch.int32, device="cuda")
     h.sample(dl.data_ptr(), V, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), cv.data_ptr(), ci.data_ptr(), 0, 0, 1,
              stream(), ct.data_ptr())
     torch.cuda.synchronize()

@@ -24,6 +24,7 @@ for s in "$@"; do
     gemvb) step gemvb 300 python tools/gemv_bench.py --debug ;;
     sweep) step sweep 900 bash tools/gemv_sweep.sh ;;
     timeline) step timeline 300 python tools/gemv_timeline.py ;;
+    sampb) step sampb 300 python tools/sampler_bench.py ;;
     variants) step variants 900 bash tools/gemv_variants.sh ;;
     profgemv) export TMPDIR=/tmp; step profgemv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profgemv -o gemv \
             --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
