@@ -3,7 +3,8 @@
 //
 // Replaces upstream's "dequantise to f16 + cublasGemmEx" / MMQ with one kernel
 // and no vendor BLAS: each 256-thread block owns a 64 (tokens) x 128 (weight
-// rows) tile; per 64-deep K step the block
+// rows) tile (split over K when the tile grid is too small to fill the chip);
+// per 64-deep K step the block
 //   1. stages X (bf16) into LDS and
 //   2. decodes 128 x 64 quantised weights straight into a bf16 LDS tile
 //      (2 threads per weight row, 32 contiguous weights each),
@@ -30,13 +31,31 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return *reinterpret_cast<unsigned short*>(&b);
 }
 
-template <int QT, int EPI>
+__device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
+  uint4 p;
+  p.x = f2bf(w[0]) | ((unsigned)f2bf(w[1]) << 16);
+  p.y = f2bf(w[2]) | ((unsigned)f2bf(w[3]) << 16);
+  p.z = f2bf(w[4]) | ((unsigned)f2bf(w[5]) << 16);
+  p.w = f2bf(w[6]) | ((unsigned)f2bf(w[7]) << 16);
+  return p;
+}
+
+// Software pipeline (double-buffered LDS, one barrier per K step): the global
+// loads of step k+1 (X tile + raw quantised weights) are issued before step
+// k's MFMAs and decoded into the other LDS buffer after them. Split-K
+// (gridDim.z > 1) partitions the K steps; partial tiles are atomically added.
+// DB: double-buffered LDS (55 KB, 2 blocks/CU) for grids that fit the chip;
+// single-buffered (27 KB, up to 5 blocks/CU, one extra barrier per step) for
+// large grids where more resident blocks hide more latency.
+template <int QT, int EPI, bool DB>
 __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Xs[BM * PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned short Ws[BN * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short Xs[DB ? 2 : 1][BM * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short Ws[DB ? 2 : 1][BN * PITCH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int N = a.w.rows, K = a.w.K, T = a.T;
+  const int nk = K / BK, ks = (nk + gridDim.z - 1) / gridDim.z;
+  const int kb = blockIdx.z * ks, ke = min(nk, kb + ks);
   f32x16 acc[2];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -44,56 +63,68 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 
   const int wrow = tid >> 1, whalf = tid & 1;
+  const bool wvalid = n0 + wrow < N;
+  const size_t wr = (size_t)min(n0 + wrow, N - 1);
   const unsigned short* xg = reinterpret_cast<const unsigned short*>(a.x);
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // ---- stage X: 64 rows x 64 bf16 = 512 x 16 B
+  uint4 xr[2];
+  DqRaw<QT> raw;
+  auto load_step = [&](int k) {
+    const int k0 = k * BK;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, c = idx & 7;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (m0 + r < T) v = *reinterpret_cast<const uint4*>(xg + (size_t)(m0 + r) * K + k0 + 8 * c);
-      *reinterpret_cast<uint4*>(&Xs[r * PITCH + 8 * c]) = v;
+      xr[i] = make_uint4(0, 0, 0, 0);
+      if (m0 + r < T) xr[i] = *reinterpret_cast<const uint4*>(xg + (size_t)(m0 + r) * K + k0 + 8 * c);
     }
-    // ---- stage W: decode 32 weights per thread into bf16
-    {
-      float w[32];
-      if (n0 + wrow < N) {
-        dequant32<QT>(a.w.base, a.w.P, (size_t)(n0 + wrow), (k0 >> 5) + whalf, w);
-      } else {
+    dq_load<QT>(raw, a.w.base, a.w.P, wr, (k0 >> 5) + whalf);
+  };
+  auto store_step = [&](int k, int buf) {
 #pragma unroll
-        for (int i = 0; i < 32; ++i) w[i] = 0.f;
-      }
-      uint4* dst = reinterpret_cast<uint4*>(&Ws[wrow * PITCH + 32 * whalf]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        uint4 p;
-        p.x = f2bf(w[8 * i + 0]) | ((unsigned)f2bf(w[8 * i + 1]) << 16);
-        p.y = f2bf(w[8 * i + 2]) | ((unsigned)f2bf(w[8 * i + 3]) << 16);
-        p.z = f2bf(w[8 * i + 4]) | ((unsigned)f2bf(w[8 * i + 5]) << 16);
-        p.w = f2bf(w[8 * i + 6]) | ((unsigned)f2bf(w[8 * i + 7]) << 16);
-        dst[i] = p;
-      }
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx >> 3, c = idx & 7;
+      *reinterpret_cast<uint4*>(&Xs[buf][r * PITCH + 8 * c]) = xr[i];
     }
-    __syncthreads();
-    // ---- MFMA: 4 k-steps of 16
-    const int lr = lane & 31, lk = 8 * (lane >> 5);
+    float w[32];
+    dq_decode<QT>(raw, ((k * BK) >> 5) + whalf, w);
+    uint4* dst = reinterpret_cast<uint4*>(&Ws[buf][wrow * PITCH + 32 * whalf]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = wvalid ? pack_bf16x8(w + 8 * i) : make_uint4(0, 0, 0, 0);
+  };
+  if (kb < ke) {
+    load_step(kb);
+    store_step(kb, 0);
+  }
+  __syncthreads();
+  const int lr = lane & 31, lk = 8 * (lane >> 5);
+  for (int k = kb; k < ke; ++k) {
+    const int buf = DB ? ((k - kb) & 1) : 0;
+    const bool more = k + 1 < ke;
+    if (more) load_step(k + 1);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 16) {
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Ws[(32 * wave + lr) * PITCH + kk + lk]);
+      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&Ws[buf][(32 * wave + lr) * PITCH + kk + lk]);
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        const bf16x8 x = *reinterpret_cast<const bf16x8*>(&Xs[(32 * m + lr) * PITCH + kk + lk]);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, b, acc[m], 0, 0, 0);
+        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(&Xs[buf][(32 * m + lr) * PITCH + kk + lk]);
+        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xv, bw, acc[m], 0, 0, 0);
       }
     }
-    __syncthreads();
+    if constexpr (DB) {
+      if (more) store_step(k + 1, buf ^ 1);
+      __syncthreads();
+    } else {
+      __syncthreads();  // every wave is done reading the single buffer
+      if (more) store_step(k + 1, 0);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue. acc[m][r]: token = 32m + (r&3) + 8(r>>2) + 4(lane>>5), col = 32*wave + (lane&31)
   const int col = n0 + 32 * wave + (lane & 31);
   if constexpr (EPI == GEMM_SWIGLU) {
-    float* ex = reinterpret_cast<float*>(Ws);  // 2 odd waves x 2 x 16 x 64 floats = 16 KiB (fits Ws)
+    float* ex = reinterpret_cast<float*>(&Ws[0][0]);  // 2 odd waves x 2 x 16 x 64 floats = 16 KiB (fits Ws)
     if (wave & 1) {
 #pragma unroll
       for (int m = 0; m < 2; ++m)
@@ -125,8 +156,15 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
           const int t = m0 + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (t < T) {
             float* o = a.out + (size_t)t * a.ldo + col;
-            if constexpr (EPI == GEMM_ADD) *o += acc[m][r];
-            else *o = a.resid ? acc[m][r] + a.resid[(size_t)t * a.ldo + col] : acc[m][r];
+            if (gridDim.z > 1) {  // split-K: partial tiles meet by atomic add (STORE outputs pre-zeroed)
+              float v = acc[m][r];
+              if (EPI == GEMM_STORE && a.resid && blockIdx.z == 0) v += a.resid[(size_t)t * a.ldo + col];
+              atomicAdd(o, v);
+            } else if constexpr (EPI == GEMM_ADD) {
+              *o += acc[m][r];
+            } else {
+              *o = a.resid ? acc[m][r] + a.resid[(size_t)t * a.ldo + col] : acc[m][r];
+            }
           }
         }
     }
@@ -135,13 +173,31 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
 
 template <int QT>
 static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
-  dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BM - 1) / BM), block(256);
+  const int tiles = ((a.w.rows + BN - 1) / BN) * ((a.T + BM - 1) / BM);
+  const int nk = a.w.K / BK;
+  // split K until ~2 blocks per CU are busy, keeping >= 8 K steps per split
+  int split = 1;
+  if (epi != GEMM_SWIGLU) {
+    while (tiles * split < 512 && nk / (split * 2) >= 8) split *= 2;
+  }
+  if (split > 1 && epi == GEMM_STORE) {
+    const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
+    if (e != hipSuccess) throw std::runtime_error("gemm_dq: memset failed");
+  }
+  dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BM - 1) / BM, split), block(256);
+  const bool db = tiles * split <= 512;
+#define LFK_GEMM_LAUNCH(E)                                                   \
+  do {                                                                        \
+    if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false>), grid, block, 0, s, a);    \
+  } while (0)
   switch (epi) {
-    case GEMM_STORE: hipLaunchKernelGGL((gemm_dq_kernel<QT, GEMM_STORE>), grid, block, 0, s, a); break;
-    case GEMM_ADD: hipLaunchKernelGGL((gemm_dq_kernel<QT, GEMM_ADD>), grid, block, 0, s, a); break;
-    case GEMM_SWIGLU: hipLaunchKernelGGL((gemm_dq_kernel<QT, GEMM_SWIGLU>), grid, block, 0, s, a); break;
+    case GEMM_STORE: LFK_GEMM_LAUNCH(GEMM_STORE); break;
+    case GEMM_ADD: LFK_GEMM_LAUNCH(GEMM_ADD); break;
+    case GEMM_SWIGLU: LFK_GEMM_LAUNCH(GEMM_SWIGLU); break;
     default: throw std::runtime_error("gemm_dq: bad epilogue");
   }
+#undef LFK_GEMM_LAUNCH
 }
 
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s) {

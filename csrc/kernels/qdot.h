@@ -448,6 +448,117 @@ __device__ __forceinline__ void dequant32(const uint8_t* __restrict__ base, cons
   }
 }
 
+// ---------------------------------------------------------------------------
+// Split form of dequant32 for software-pipelined GEMM staging: dq_load issues
+// the raw loads of one 32-weight run (registers), dq_decode turns them into 32
+// floats later, so the loads of K-step k+1 fly while step k's MFMAs run.
+template <int T> struct DqRaw;
+template <> struct DqRaw<T_Q4_K> { int4 a, b, m; };
+template <> struct DqRaw<T_Q5_K> { int4 a, b, m, h0, h1; };
+template <> struct DqRaw<T_Q6_K> { int4 la, lb, ha, hb, sc; unsigned d; };
+template <> struct DqRaw<T_Q8_0> { int4 a, b; unsigned d; };
+template <> struct DqRaw<T_F16> { uint4 w[4]; };
+template <> struct DqRaw<T_F32> { float4 w[8]; };
+
+template <int T>
+__device__ __forceinline__ void dq_load(DqRaw<T>& r, const uint8_t* __restrict__ base, const Planes& P, size_t row,
+                                        int q) {
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+    const int sb = q >> 3, g = (q & 7) >> 1;
+    const int4* qs = reinterpret_cast<const int4*>(base + P.p0 + row * P.s0 + sb * 128 + 32 * g);
+    r.a = qs[0];
+    r.b = qs[1];
+    if constexpr (T == T_Q4_K) {
+      r.m = *reinterpret_cast<const int4*>(base + P.p1 + row * P.s1 + sb * 16);
+    } else {
+      const int4* qh = reinterpret_cast<const int4*>(base + P.p1 + row * P.s1 + sb * 32);
+      r.h0 = qh[0];
+      r.h1 = qh[1];
+      r.m = *reinterpret_cast<const int4*>(base + P.p2 + row * P.s2 + sb * 16);
+    }
+  } else if constexpr (T == T_Q6_K) {
+    const int sb = q >> 3, rr = q & 7, n = rr >> 2, half = rr & 1;
+    const int4* l = reinterpret_cast<const int4*>(base + P.p0 + row * P.s0 + sb * 128 + 64 * n + 32 * half);
+    const int4* h = reinterpret_cast<const int4*>(base + P.p1 + row * P.s1 + sb * 64 + 32 * n);
+    r.la = l[0]; r.lb = l[1];
+    r.ha = h[0]; r.hb = h[1];
+    r.sc = *reinterpret_cast<const int4*>(base + P.p2 + row * P.s2 + sb * 16);
+    r.d = *reinterpret_cast<const unsigned short*>(base + P.p3 + row * P.s3 + sb * 2);
+  } else if constexpr (T == T_Q8_0) {
+    const int4* qp = reinterpret_cast<const int4*>(base + P.p0 + row * P.s0 + 32 * q);
+    r.a = qp[0];
+    r.b = qp[1];
+    r.d = *reinterpret_cast<const unsigned short*>(base + P.p1 + row * P.s1 + 2 * q);
+  } else if constexpr (T == T_F16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r.w[i] = reinterpret_cast<const uint4*>(base + row * P.s0 + 64 * q)[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = reinterpret_cast<const float4*>(base + row * P.s0 + 128 * q)[i];
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void dq_decode(const DqRaw<T>& r, int q, float* out) {
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+    const int s = q & 7, g = s >> 1, hi = s & 1;
+    const float d = h2f((unsigned)r.m.x & 0xFFFF), dmin = h2f((unsigned)r.m.x >> 16);
+    float sc_lo, m_lo, sc_hi, m_hi;
+    scale_min_pair(g, (unsigned)r.m.y, (unsigned)r.m.z, (unsigned)r.m.w, sc_lo, m_lo, sc_hi, m_hi);
+    const float scl = d * (hi ? sc_hi : sc_lo), mn = dmin * (hi ? m_hi : m_lo);
+    const int qv[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int v = hi ? ((qv[i] >> 4) & 0x0F0F0F0F) : (qv[i] & 0x0F0F0F0F);
+      if constexpr (T == T_Q5_K) {
+        const int hv = i < 4 ? (i == 0 ? r.h0.x : i == 1 ? r.h0.y : i == 2 ? r.h0.z : r.h0.w)
+                             : (i == 4 ? r.h1.x : i == 5 ? r.h1.y : i == 6 ? r.h1.z : r.h1.w);
+        v |= ((hv >> s) & 0x01010101) << 4;
+      }
+#pragma unroll
+      for (int b8 = 0; b8 < 4; ++b8) out[4 * i + b8] = scl * (float)((v >> (8 * b8)) & 0xFF) - mn;
+    }
+  } else if constexpr (T == T_Q6_K) {
+    const int rr = q & 7, n = rr >> 2, qq = (rr >> 1) & 1, half = rr & 1;
+    const float d = h2f(r.d & 0xFFFF);
+    const int scw[4] = {r.sc.x, r.sc.y, r.sc.z, r.sc.w};
+    const int si = 8 * n + 2 * (2 * qq + half);
+    const float s0 = d * (float)(signed char)((scw[si >> 2] >> (8 * (si & 3))) & 0xFF);
+    const float s1 = d * (float)(signed char)((scw[(si + 1) >> 2] >> (8 * ((si + 1) & 3))) & 0xFF);
+    const int lv[8] = {r.la.x, r.la.y, r.la.z, r.la.w, r.lb.x, r.lb.y, r.lb.z, r.lb.w};
+    const int hv[8] = {r.ha.x, r.ha.y, r.ha.z, r.ha.w, r.hb.x, r.hb.y, r.hb.z, r.hb.w};
+    const int hs = 2 * (2 * qq + half);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int v = ((lv[i] >> (4 * qq)) & 0x0F0F0F0F) | (((hv[i] >> hs) & 0x03030303) << 4);
+#pragma unroll
+      for (int b8 = 0; b8 < 4; ++b8) out[4 * i + b8] = (i < 4 ? s0 : s1) * (float)(((v >> (8 * b8)) & 0xFF) - 32);
+    }
+  } else if constexpr (T == T_Q8_0) {
+    const float d = h2f(r.d & 0xFFFF);
+    const int qv[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int b8 = 0; b8 < 4; ++b8) out[4 * i + b8] = d * (float)(signed char)((qv[i] >> (8 * b8)) & 0xFF);
+  } else if constexpr (T == T_F16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned w[4] = {r.w[i].x, r.w[i].y, r.w[i].z, r.w[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        out[8 * i + 2 * j] = h2f(w[j] & 0xFFFF);
+        out[8 * i + 2 * j + 1] = h2f(w[j] >> 16);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      out[4 * i] = r.w[i].x; out[4 * i + 1] = r.w[i].y; out[4 * i + 2] = r.w[i].z; out[4 * i + 3] = r.w[i].w;
+    }
+  }
+}
+
 // Dispatch helper: call F.template operator()<T>() for the runtime type (wave-uniform).
 #define LFK_DISPATCH_TYPE(t, ...)                          \
   switch (t) {                                             \
