@@ -207,8 +207,123 @@ void decode_chunk(const CpuMat& W, const uint8_t* base, size_t row, int c, Chunk
   }
 }
 
+// ---- AVX2 path for the block-quantised types: one 32-weight chunk is unpacked
+// into a 256-bit vector (lo 16 | hi 16, unsigned for the K-quants, signed for
+// Q8_0) and dotted with the q8 activations of every token on
+// vpmaddubsw/vpmaddwd; per-chunk scales are applied in float lanes (lo 4 | hi 4)
+// so no horizontal sum happens until the end of the row.
+template <int QT>
+inline __m256i chunk_w(const CpuMat& W, const uint8_t* base, size_t row, int c, float& s_lo, float& m_lo, float& s_hi,
+                       float& m_hi, int& off_lo, int& off_hi) {
+  const Planes& P = W.P;
+  const int sb = c >> 3, j = c & 7;
+  const __m128i m4 = _mm_set1_epi8(0x0F);
+  if constexpr (QT == T_Q4_K || QT == T_Q5_K) {
+    const int g = j >> 1, h = j & 1;
+    const __m128i q = _mm_loadu_si128(reinterpret_cast<const __m128i*>(base + P.p0 + row * P.s0 + 16 * c));
+    __m128i lo = _mm_and_si128(q, m4), hi = _mm_and_si128(_mm_srli_epi16(q, 4), m4);
+    const uint8_t* meta = base + (QT == T_Q4_K ? P.p1 + row * P.s1 : P.p2 + row * P.s2) + 16 * sb;
+    if constexpr (QT == T_Q5_K) {
+      const __m128i qh = _mm_loadu_si128(reinterpret_cast<const __m128i*>(base + P.p1 + row * P.s1 + 32 * sb + 16 * h));
+      const __m128i one = _mm_set1_epi8(1);
+      lo = _mm_or_si128(lo, _mm_slli_epi16(_mm_and_si128(_mm_srl_epi16(qh, _mm_cvtsi32_si128(2 * g)), one), 4));
+      hi = _mm_or_si128(hi, _mm_slli_epi16(_mm_and_si128(_mm_srl_epi16(qh, _mm_cvtsi32_si128(2 * g + 1)), one), 4));
+    }
+    const float d = hf(meta), dmin = hf(meta + 2);
+    int sc0, mm0, sc1, mm1;
+    scale_min_k4(2 * g, meta + 4, sc0, mm0);
+    scale_min_k4(2 * g + 1, meta + 4, sc1, mm1);
+    s_lo = d * sc0; m_lo = dmin * mm0; s_hi = d * sc1; m_hi = dmin * mm1;
+    off_lo = sb * 256 + 64 * g + 16 * h;
+    off_hi = off_lo + 32;
+    return _mm256_set_m128i(hi, lo);
+  } else if constexpr (QT == T_Q6_K) {
+    const int n = j >> 2, o = 16 * (j & 3);
+    const __m128i ql = _mm_loadu_si128(reinterpret_cast<const __m128i*>(base + P.p0 + row * P.s0 + 16 * c));
+    const __m128i qh =
+        _mm_loadu_si128(reinterpret_cast<const __m128i*>(base + P.p1 + row * P.s1 + 64 * sb + 32 * n + (o & 31)));
+    const int sh = o >= 32 ? 2 : 0;
+    const __m128i m3 = _mm_set1_epi8(3);
+    const __m128i lo = _mm_or_si128(_mm_and_si128(ql, m4),
+                                    _mm_slli_epi16(_mm_and_si128(_mm_srl_epi16(qh, _mm_cvtsi32_si128(sh)), m3), 4));
+    const __m128i hi = _mm_or_si128(_mm_and_si128(_mm_srli_epi16(ql, 4), m4),
+                                    _mm_slli_epi16(_mm_and_si128(_mm_srl_epi16(qh, _mm_cvtsi32_si128(sh + 4)), m3), 4));
+    const int8_t* sc = reinterpret_cast<const int8_t*>(base + P.p2 + row * P.s2 + 16 * sb);
+    const float d = hf(base + P.p3 + row * P.s3 + 2 * sb);
+    const int si = 8 * n + (o >> 4);
+    s_lo = d * sc[si]; m_lo = 32.f * s_lo;
+    s_hi = d * sc[si + 4]; m_hi = 32.f * s_hi;
+    off_lo = sb * 256 + 128 * n + o;
+    off_hi = off_lo + 64;
+    return _mm256_set_m128i(hi, lo);
+  } else {  // Q8_0 (signed)
+    const float d = hf(base + P.p1 + row * P.s1 + 2 * c);
+    s_lo = s_hi = d;
+    m_lo = m_hi = 0.f;
+    off_lo = 32 * c;
+    off_hi = 32 * c + 16;
+    return _mm256_loadu_si256(reinterpret_cast<const __m256i*>(base + P.p0 + row * P.s0 + 32 * c));
+  }
+}
+
+template <int QT>
+void gemm_rows_avx2(const CpuMat& W, const uint8_t* base, const Q8& xq, int T, float* y, int ldy, bool add) {
+  const int K = W.K, nchunks = K / 32, nb = K / 32, n16 = K / 16;
+  const __m256i ones = _mm256_set1_epi16(1);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < W.rows; ++r) {
+    __m256 acc[128];
+    float mterm[128];
+    for (int t = 0; t < T; ++t) { acc[t] = _mm256_setzero_ps(); mterm[t] = 0.f; }
+    for (int c = 0; c < nchunks; ++c) {
+      float s_lo, m_lo, s_hi, m_hi;
+      int off_lo, off_hi;
+      __m256i w = chunk_w<QT>(W, base, (size_t)r, c, s_lo, m_lo, s_hi, m_hi, off_lo, off_hi);
+      __m256i wa = w;
+      if constexpr (QT == T_Q8_0) wa = _mm256_sign_epi8(w, w);  // |w| (unsigned operand of vpmaddubsw)
+      const int blo = off_lo >> 5, bhi = off_hi >> 5;
+      for (int t = 0; t < T; ++t) {
+        const int8_t* x = xq.q.data() + (size_t)t * K;
+        __m256i xv = _mm256_set_m128i(_mm_loadu_si128(reinterpret_cast<const __m128i*>(x + off_hi)),
+                                      _mm_loadu_si128(reinterpret_cast<const __m128i*>(x + off_lo)));
+        if constexpr (QT == T_Q8_0) xv = _mm256_sign_epi8(xv, w);
+        const __m256i p = _mm256_madd_epi16(_mm256_maddubs_epi16(wa, xv), ones);
+        const float* xd = xq.d.data() + (size_t)t * nb;
+        const float xl = xd[blo], xh = xd[bhi];
+        const __m256 sv = _mm256_set_m128(_mm_set1_ps(s_hi * xh), _mm_set1_ps(s_lo * xl));
+        acc[t] = _mm256_fmadd_ps(_mm256_cvtepi32_ps(p), sv, acc[t]);
+        if constexpr (QT != T_Q8_0) {
+          const int* s16 = xq.s16.data() + (size_t)t * n16;
+          mterm[t] += m_lo * xl * (float)s16[off_lo >> 4] + m_hi * xh * (float)s16[off_hi >> 4];
+        }
+      }
+    }
+    for (int t = 0; t < T; ++t) {
+      const __m128 h = _mm_add_ps(_mm256_castps256_ps128(acc[t]), _mm256_extractf128_ps(acc[t], 1));
+      const __m128 h2 = _mm_add_ps(h, _mm_movehl_ps(h, h));
+      const float v = _mm_cvtss_f32(_mm_add_ss(h2, _mm_shuffle_ps(h2, h2, 1))) - mterm[t];
+      float* o = y + (size_t)t * ldy + r;
+      *o = add ? *o + v : v;
+    }
+  }
+}
+
+void gemm_rows_scalar(const CpuMat& W, const uint8_t* base, const Q8& xq, int T, float* y, int ldy, bool add);
+
 // y[t][r] (+)= W[r] . x_t for rows r of a (possibly expert-offset) matrix
 void gemm_rows(const CpuMat& W, const uint8_t* base, const Q8& xq, int T, float* y, int ldy, bool add) {
+  if (T > 128) throw std::runtime_error("cpu gemm: at most 128 tokens per call");
+  switch (W.type) {
+    case T_Q4_K: return gemm_rows_avx2<T_Q4_K>(W, base, xq, T, y, ldy, add);
+    case T_Q5_K: return gemm_rows_avx2<T_Q5_K>(W, base, xq, T, y, ldy, add);
+    case T_Q6_K: return gemm_rows_avx2<T_Q6_K>(W, base, xq, T, y, ldy, add);
+    case T_Q8_0: return gemm_rows_avx2<T_Q8_0>(W, base, xq, T, y, ldy, add);
+    default: return gemm_rows_scalar(W, base, xq, T, y, ldy, add);
+  }
+}
+
+// portable path (F16/F32 and the numerics reference of the AVX2 path)
+void gemm_rows_scalar(const CpuMat& W, const uint8_t* base, const Q8& xq, int T, float* y, int ldy, bool add) {
   const int K = W.K, nchunks = K / 32, nb = K / 32, n16 = K / 16;
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < W.rows; ++r) {
@@ -334,6 +449,7 @@ CpuEngine::CpuEngine(const std::string& path, const CpuOptions& o)
   const GGUFTensor* emb = f.find("token_embd.weight");
   if (!emb) throw std::runtime_error("missing token_embd.weight");
   n_vocab_ = (int)emb->ne[1];
+  if (head_dim_ % 32) throw std::runtime_error("cpu backend: head_dim must be a multiple of 32");
   sp_ = make_shard_plan(n_head_, n_head_kv_, head_dim_, n_ff_, n_vocab_, o.tp_size, o.tp_rank);
   layer_end_ = o.layer_end < 0 ? n_layer_ : std::min(o.layer_end, n_layer_);
   tok_embd_ = load_mat(f, "token_embd.weight");
@@ -414,7 +530,8 @@ void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) co
   const float scale = 1.f / std::sqrt((float)hd);
   const uint16_t* kc = kc_.data() + (size_t)l * nkv * n_ctx_ * hd;
   const uint16_t* vc = vc_.data() + (size_t)l * nkv * n_ctx_ * hd;
-#pragma omp parallel for collapse(2) schedule(static)
+  // f16 rows are widened 8 at a time (F16C) and dotted / accumulated on FMA
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
   for (int t = 0; t < T; ++t)
     for (int h = 0; h < nh; ++h) {
       const int L = pos0 + t + 1, kvh = h / G;
@@ -423,19 +540,34 @@ void CpuEngine::attention(int l, const float* q, int T, int pos0, float* out) co
       float m = -INFINITY;
       for (int j = 0; j < L; ++j) {
         const uint16_t* kr = kc + ((size_t)kvh * n_ctx_ + j) * hd;
-        float a = 0.f;
-        for (int i = 0; i < hd; ++i) a += qh[i] * h2f(kr[i]);
-        s[j] = a * scale;
+        __m256 a = _mm256_setzero_ps();
+        for (int i = 0; i < hd; i += 8) {
+          const __m256 kf = _mm256_cvtph_ps(_mm_loadu_si128(reinterpret_cast<const __m128i*>(kr + i)));
+          a = _mm256_fmadd_ps(_mm256_loadu_ps(qh + i), kf, a);
+        }
+        const __m128 h4 = _mm_add_ps(_mm256_castps256_ps128(a), _mm256_extractf128_ps(a, 1));
+        const __m128 h2 = _mm_add_ps(h4, _mm_movehl_ps(h4, h4));
+        s[j] = _mm_cvtss_f32(_mm_add_ss(h2, _mm_shuffle_ps(h2, h2, 1))) * scale;
         m = std::max(m, s[j]);
       }
       float den = 0.f;
       for (int j = 0; j < L; ++j) { s[j] = std::exp(s[j] - m); den += s[j]; }
+      const float inv = 1.f / den;
       float* o = out + ((size_t)t * nh + h) * hd;
-      for (int i = 0; i < hd; ++i) o[i] = 0.f;
-      for (int j = 0; j < L; ++j) {
-        const uint16_t* vr = vc + ((size_t)kvh * n_ctx_ + j) * hd;
-        const float p = s[j] / den;
-        for (int i = 0; i < hd; ++i) o[i] += p * h2f(vr[i]);
+      for (int i0 = 0; i0 < hd; i0 += 32) {  // 4 accumulators of 8 dims
+        __m256 o0 = _mm256_setzero_ps(), o1 = o0, o2 = o0, o3 = o0;
+        for (int j = 0; j < L; ++j) {
+          const uint16_t* vr = vc + ((size_t)kvh * n_ctx_ + j) * hd + i0;
+          const __m256 p = _mm256_set1_ps(s[j] * inv);
+          o0 = _mm256_fmadd_ps(p, _mm256_cvtph_ps(_mm_loadu_si128(reinterpret_cast<const __m128i*>(vr))), o0);
+          o1 = _mm256_fmadd_ps(p, _mm256_cvtph_ps(_mm_loadu_si128(reinterpret_cast<const __m128i*>(vr + 8))), o1);
+          o2 = _mm256_fmadd_ps(p, _mm256_cvtph_ps(_mm_loadu_si128(reinterpret_cast<const __m128i*>(vr + 16))), o2);
+          o3 = _mm256_fmadd_ps(p, _mm256_cvtph_ps(_mm_loadu_si128(reinterpret_cast<const __m128i*>(vr + 24))), o3);
+        }
+        _mm256_storeu_ps(o + i0, o0);
+        _mm256_storeu_ps(o + i0 + 8, o1);
+        _mm256_storeu_ps(o + i0 + 16, o2);
+        _mm256_storeu_ps(o + i0 + 24, o3);
       }
     }
 }

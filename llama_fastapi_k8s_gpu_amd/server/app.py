@@ -105,6 +105,8 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
                               temperature=sampling.temperature, top_p=sampling.top_p,
                               frequency_penalty=sampling.frequency_penalty,
                               presence_penalty=sampling.presence_penalty)
+                if sampling.max_tokens is not None:  # parity default None: generate to EOS / context end
+                    kwargs["max_tokens"] = sampling.max_tokens
                 if settings.cooperative_cancel and getattr(eng, "supports_cancel", False):
                     kwargs["cancel_event"] = cancel_event
                 metrics.in_flight.inc()
