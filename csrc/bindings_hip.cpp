@@ -125,6 +125,7 @@ PYBIND11_MODULE(_hip, m) {
            })
       .def_property_readonly("device_bytes", &Engine::device_bytes)
       .def_property_readonly("healthy", &Engine::healthy)
+      .def_property_readonly("ffn_fused", &Engine::ffn_fused)
       .def_property_readonly("last_error", &Engine::last_error)
       .def_property_readonly("n_ctx", &Engine::n_ctx)
       .def_property_readonly("tp_rank", &Engine::tp_rank)
@@ -175,6 +176,22 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
      py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
      py::arg("debug") = 0, py::arg("dbg_clk") = 0);
+
+  m.def("ffn_fused", [](uintptr_t wgu, int tgu, uintptr_t wdn, int tdn, int d, int F, uintptr_t x, uintptr_t norm,
+                        float eps, uintptr_t h, uintptr_t ctr, uintptr_t ctr_clear, uintptr_t err, uintptr_t stream,
+                        uintptr_t dbg_clk) {
+    FfnFusedArgs a;
+    a.w_gu = make_qmat(P<void>(wgu), tgu, 2 * F, d);
+    a.w_down = make_qmat(P<void>(wdn), tdn, d, F);
+    a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.h = P<float>(h); a.F = F;
+    a.counters = P<int>(ctr); a.counters_clear = P<int>(ctr_clear); a.err = P<int>(err);
+    a.dbg_clk = P<long long>(dbg_clk);
+    if (!ffn_fused_supported(a)) throw std::runtime_error("ffn_fused: unsupported shape/types");
+    ffn_fused(a, S(stream));
+    hip_ok("ffn_fused");
+  }, py::arg("wgu"), py::arg("tgu"), py::arg("wdn"), py::arg("tdn"), py::arg("d"), py::arg("F"), py::arg("x"),
+     py::arg("norm"), py::arg("eps"), py::arg("h"), py::arg("ctr"), py::arg("ctr_clear"), py::arg("err"),
+     py::arg("stream"), py::arg("dbg_clk") = 0);
 
   m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,
                        uintptr_t x, uintptr_t norm, float eps, uintptr_t q_out, uintptr_t kc, uintptr_t vc, int n_ctx,
@@ -247,6 +264,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("rmsnorm_bf16", [](uintptr_t x, uintptr_t w, float eps, int T, int d, uintptr_t y, uintptr_t stream) {
     rmsnorm_bf16(P<float>(x), P<float>(w), eps, T, d, P<__hip_bfloat16>(y), S(stream));
     hip_ok("rmsnorm_bf16");
+  });
+  m.def("launch_probe", [](int threads, int blocks, size_t lds, int iters, uintptr_t out, uintptr_t stream) {
+    launch_probe(threads, blocks, lds, iters, P<float>(out), S(stream));
   });
   m.def("clock_probe", [](uintptr_t out, int iters, uintptr_t stream) {
     clock_probe(P<long long>(out), iters, S(stream));

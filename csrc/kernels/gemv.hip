@@ -17,183 +17,9 @@
 #include <map>
 #include <mutex>
 
-#include "kernels.h"
-#include "qdot.h"
+#include "gemv_dev.h"
 
 namespace lfk {
-
-static constexpr int kMaxBlocks = 1024;  // 256 CUs x 4
-
-// Block prologue: x (or x * w_norm) -> per-32 int8 + f32 scale in LDS.
-//
-// Split in two so its global loads are issued BEFORE the wave's first weight
-// loads (vmcnt retires in order: an x load queued behind a weight stream would
-// make the prologue wait for the weights):
-//   load()   : every thread issues its first NB float4 of x (and w_norm);
-//   finish() : per-32 amax on DPP, q8 -> LDS, sum of squares -> one barrier.
-// RMSNorm's 1/rms is a scalar, so q8(x * w) equals q8(x * w / rms) up to the
-// block scale: the kernel multiplies its final dot products by the returned
-// scale instead of making a second pass over x.
-template <bool NORM, int BLOCK = 256>
-struct XPrologue {
-  static constexpr int NB = 4;
-  static constexpr int SHIFT = (BLOCK == 1024) ? 12 : 10;  // log2(BLOCK * 4 floats per batch slot)
-  float4 v[NB], w[NB];
-  __device__ __forceinline__ void load_batch(const float* __restrict__ x, const float* __restrict__ nw, int K, int j0) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int i = ((j0 + b) << SHIFT) + tid * 4;
-      v[b] = i < K ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (NORM) w[b] = i < K ? *reinterpret_cast<const float4*>(nw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-  __device__ __forceinline__ void load(const float* __restrict__ x, const float* __restrict__ nw, int K) {
-    load_batch(x, nw, K, 0);
-  }
-  // returns the RMSNorm scale (1 without NORM)
-  __device__ __forceinline__ float finish(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
-                                          int8_t* xq, float* xd, float* red) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nj = (K + (1 << SHIFT) - 1) >> SHIFT;
-    float ss = 0.f;
-    for (int j0 = 0; j0 < nj; j0 += NB) {
-      if (j0 > 0) load_batch(x, nw, K, j0);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        const int i = ((j0 + b) << SHIFT) + tid * 4;
-        if (i < K) {
-          float4 t = v[b];
-          if constexpr (NORM) {
-            ss += t.x * t.x + t.y * t.y + t.z * t.z + t.w * t.w;
-            t.x *= w[b].x; t.y *= w[b].y; t.z *= w[b].z; t.w *= w[b].w;
-          }
-          const float amax = max8(fmaxf(fmaxf(fabsf(t.x), fabsf(t.y)), fmaxf(fabsf(t.z), fabsf(t.w))));
-          const float d = amax * (1.f / 127.f);
-          const float id = d > 0.f ? 1.f / d : 0.f;
-          const int q0 = __float2int_rn(t.x * id), q1 = __float2int_rn(t.y * id);
-          const int q2 = __float2int_rn(t.z * id), q3 = __float2int_rn(t.w * id);
-          *reinterpret_cast<int*>(xq + i) =
-              (q0 & 0xFF) | ((q1 & 0xFF) << 8) | ((q2 & 0xFF) << 16) | ((q3 & 0xFF) << 24);
-          if ((tid & 7) == 0) xd[i >> 5] = d;
-        }
-      }
-    }
-    if constexpr (NORM) {
-      ss = wave_sum_fast(ss);
-      if (lane == 0) red[wave] = ss;
-    }
-    __syncthreads();
-    if constexpr (NORM) {
-      float tot = 0.f;
-#pragma unroll
-      for (int i = 0; i < BLOCK / 64; ++i) tot += red[i];
-      return rsqrtf(tot / (float)K + eps);
-    }
-    return 1.f;
-  }
-};
-
-// one-call form (MoE down, where there is no weight prefetch to order against)
-template <bool NORM>
-__device__ __forceinline__ float quantize_x(const float* __restrict__ x, const float* __restrict__ nw, float eps, int K,
-                                            int8_t* xq, float* xd, float* red) {
-  XPrologue<NORM> xp;
-  xp.load(x, nw, K);
-  return xp.finish(x, nw, eps, K, xq, xd, red);
-}
-
-__device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
-
-// Weight stream of one wave item: NR rows x U passes of 64 chunks, all loads
-// issued before any math (NR*U independent 16-B loads per lane in flight).
-// Chunks past the row end are clamped (loaded from the last chunk, ignored).
-template <int QT, int NR, int U>
-struct WStream {
-  WRaw<QT> w[U][NR];
-  __device__ __forceinline__ void load(const RowPtr (&R)[NR], int c0, int nchunks, int lane) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int c = min(c0 + 64 * u + lane, nchunks - 1);
-#pragma unroll
-      for (int r = 0; r < NR; ++r) wload<QT>(w[u][r], R[r], c);
-    }
-  }
-  __device__ __forceinline__ void dot(int c0, int nchunks, const int8_t* xq, const float* xd, float (&acc)[NR],
-                                      int lane) const {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int c = c0 + 64 * u + lane;
-      if (c < nchunks) {
-        XChunk X;
-        load_x<QT>(X, xq, xd, c);
-#pragma unroll
-        for (int r = 0; r < NR; ++r) acc[r] += wdot<QT>(w[u][r], X, c);
-      }
-    }
-  }
-  // rest of the row after the first pass group was loaded by the caller
-  __device__ __forceinline__ void finish_rows(const RowPtr (&R)[NR], int nchunks, const int8_t* xq, const float* xd,
-                                              float (&acc)[NR], int lane) {
-    for (int c0 = 0;;) {
-      dot(c0, nchunks, xq, xd, acc, lane);
-      c0 += 64 * U;
-      if (c0 >= nchunks) break;
-      load(R, c0, nchunks, lane);
-    }
-  }
-};
-
-__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
-
-// Reduce NR per-lane partial sums over the wave so that lane l ends up with the
-// total of row (l % NR): a butterfly over offsets 32..NR, then a transposing
-// exchange for the last log2(NR) offsets (no dynamic register indexing).
-template <int NR>
-__device__ __forceinline__ float reduce_rows(float (&acc)[NR], int lane) {
-#pragma unroll
-  for (int o = 32; o >= NR; o >>= 1)
-#pragma unroll
-    for (int r = 0; r < NR; ++r) acc[r] += __shfl_xor(acc[r], o);
-  if constexpr (NR == 1) {
-    return acc[0];
-  } else if constexpr (NR == 2) {
-    const bool hi = lane & 1;
-    float z = hi ? acc[1] : acc[0];
-    const float w = hi ? acc[0] : acc[1];
-    return z + __shfl_xor(w, 1);
-  } else {
-    static_assert(NR == 4, "rows per item must be 1, 2 or 4");
-    const bool b1 = lane & 2;
-    float x0 = b1 ? acc[2] : acc[0], x1 = b1 ? acc[3] : acc[1];
-    const float y0 = b1 ? acc[0] : acc[2], y1 = b1 ? acc[1] : acc[3];
-    x0 += __shfl_xor(y0, 2);
-    x1 += __shfl_xor(y1, 2);
-    const bool b0 = lane & 1;
-    const float z = b0 ? x1 : x0, w = b0 ? x0 : x1;
-    return z + __shfl_xor(w, 1);
-  }
-}
-
-template <int EPI, int NR>
-__device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups, RowPtr (&R)[NR], int& slot, int& f0) {
-  constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
-  slot = it / groups;
-  f0 = (it - slot * groups) * NF;
-  const uint8_t* base = a.w.base;
-  if (a.expert_ids) base += (size_t)a.expert_ids[slot] * a.w.expert_stride;
-#pragma unroll
-  for (int r = 0; r < NF; ++r) {
-    if constexpr (EPI == EPI_SWIGLU) {
-      const int f = f0 + r;
-      const unsigned gr = (unsigned)((f >> 5) * 64 + (f & 31));
-      R[r] = row_ptr(base, a.w.P, gr);
-      R[NF + r] = row_ptr(base, a.w.P, gr + 32);
-    } else {
-      R[r] = row_ptr(base, a.w.P, (unsigned)min(f0 + r, a.n_out - 1));
-    }
-  }
-}
 
 // One wave = one item of NR rows (NF outputs); 4 waves per block; grid capped at
 // 4 blocks/CU and strided over items. Latency hiding: the first weight loads
@@ -204,7 +30,12 @@ __device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups,
 // partial dot products are atomically added to the residual. Every item is a
 // single load round trip, so waves stream continuously instead of walking a
 // long row pass by pass (the FFN down projection, K = 14336).
-template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false>
+// EARLY (1024-thread blocks, one per CU): the first weight loads go out right
+// after the x loads and BEFORE the prologue waits for x, so the weight stream
+// starts at block entry; with one block per CU no other block's weight stream
+// sits in front of this CU's x loads (in-order returns per CU).
+template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false,
+          bool EARLY = false>
 __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // TL: per-block timeline (wall_clock64 ticks, microbenchmarks only):
@@ -236,12 +67,20 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   // prologue whose L2 reads queue behind a saturated weight stream (its own CU's
   // or its neighbours') costs more than the latency its prefetch would hide.
   if (a.debug != 1) xp.load(a.x, a.norm_w, K);
-  const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
   int kp = 0;
-  if (item < total) {
-    item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0);
-    if constexpr (SPLITK) kp = item % kparts;
+  if constexpr (EARLY) {  // unconditional (clamped) so no control-flow join sits between these loads and finish()
+    const int it0 = min(item, total - 1);
+    item_rows<EPI, NR>(a, SPLITK ? it0 / kparts : it0, groups, R, slot, f0);
+    if constexpr (SPLITK) kp = it0 % kparts;
     ws.load(R, kp * 64 * U, nchunks, lane);
+  }
+  const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
+  if constexpr (!EARLY) {
+    if (item < total) {
+      item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0);
+      if constexpr (SPLITK) kp = item % kparts;
+      ws.load(R, kp * 64 * U, nchunks, lane);
+    }
   }
   if constexpr (TL) { if (threadIdx.x == 0) tl[1] = wall_clock64(); }
   if (a.debug == 2) {
@@ -359,6 +198,38 @@ static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
   return {nr, u};
 }
 
+// EARLY launches: 1024-thread blocks pinned to one per CU by their LDS request
+// (> half of the 160 KiB), so the grid is exactly one block per CU.
+static constexpr size_t kOnePerCuLds = 80 * 1024 + 256;
+// classes (bit mask, env LFK_GEMV_EARLY overrides the default)
+enum EarlyCls : int { EC_SWIGLU = 1, EC_SPLITK_LONG = 2, EC_SPLITK = 4, EC_STORE = 8, EC_QKV = 16 };
+static bool gemv_early(int cls) {
+  static const int mask = [] {
+    const char* e = getenv("LFK_GEMV_EARLY");
+    return e ? atoi(e) : (EC_SWIGLU | EC_SPLITK_LONG);  // measured in-situ (decode step) on MI355X
+  }();
+  return (mask & cls) != 0;
+}
+// LFK_GEMV_PIN: same class mask; 1024-thread blocks pinned one per CU, x loaded
+// and quantised BEFORE the first weight loads (the classic order)
+static bool gemv_pin(int cls) {
+  static const int mask = [] {
+    const char* e = getenv("LFK_GEMV_PIN");
+    return e ? atoi(e) : 0;
+  }();
+  return (mask & cls) != 0;
+}
+static int early_cls(int epi, int K) {
+  if (epi == EPI_SWIGLU) return EC_SWIGLU;
+  if (epi == EPI_ADD) return K > 4096 ? EC_SPLITK_LONG : EC_SPLITK;
+  return EC_STORE;
+}
+template <typename F>
+static void launch_early(F kern, size_t lds, int items, const GemvArgs& a, hipStream_t s) {
+  const size_t l = std::max(lds, kOnePerCuLds);
+  hipLaunchKernelGGL(kern, gemv_grid(kern, l, items, 1024), dim3(1024), l, s, a);
+}
+
 #define LFK_NRU_DISPATCH(NR_, U_, ...)                                              \
   do {                                                                               \
     if (NR_ == 4 && U_ >= 2) { constexpr int NR = 4, U = 2; __VA_ARGS__; }           \
@@ -385,6 +256,18 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
     // of loads per thread (issued before the weights) and 16 waves share its LDS
     // copy; 16 waves per CU cap the registers at 128, hence NR*U <= 4 there
     static const bool force1024 = getenv("LFK_GEMV_BLOCK") && atoi(getenv("LFK_GEMV_BLOCK")) == 1024;
+    if constexpr (NR * U <= 4) {
+      if (gemv_early(early_cls(EPI, a.w.K))) {
+        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, true>, lds, items, a, s);
+        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, false, false, true>, lds, items, a, s);
+        return;
+      }
+      if (gemv_pin(early_cls(EPI, a.w.K))) {
+        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, false>, lds, items, a, s);
+        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, false, false, false>, lds, items, a, s);
+        return;
+      }
+    }
     if (a.w.K > 4096 || (force1024 && NR * U <= 4)) {
       if constexpr (NR * U <= 4) {
         if (a.norm_w) {
@@ -417,7 +300,13 @@ static void launch_gemv_tl(const GemvArgs& a, hipStream_t s) {
       constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
       const size_t lds = a.w.K + (a.w.K / 32) * 4 + 128;
       const int items = (a.n_out + NF - 1) / NF * a.n_slots;
-      if (a.w.K > 4096) {
+      if (gemv_early(early_cls(EPI, a.w.K))) {
+        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, true, false, true>, lds, items, a, s);
+        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, true, false, true>, lds, items, a, s);
+      } else if (gemv_pin(early_cls(EPI, a.w.K))) {
+        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, true, false, false>, lds, items, a, s);
+        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, true, false, false>, lds, items, a, s);
+      } else if (a.w.K > 4096) {
         auto k = gemv_kernel<QT, EPI, NR, U, false, 1024, true>;
         hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
       } else if (a.norm_w) {
@@ -438,6 +327,16 @@ template <int QT>
 static void launch_gemv_splitk(const GemvArgs& a, hipStream_t s) {
   const size_t lds = a.w.K + (a.w.K / 32) * 4 + 128;
   const int items = (a.n_out + 3) / 4 * a.n_slots * ((a.w.K / 32 + 63) / 64);
+  if (gemv_early(early_cls(EPI_ADD, a.w.K))) {
+    if (a.norm_w) launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true, true>, lds, items, a, s);
+    else launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true, true>, lds, items, a, s);
+    return;
+  }
+  if (gemv_pin(early_cls(EPI_ADD, a.w.K))) {
+    if (a.norm_w) launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true, false>, lds, items, a, s);
+    else launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true, false>, lds, items, a, s);
+    return;
+  }
   if (a.w.K > 4096) {  // long rows: 1024-thread blocks, one-batch x prologue
     auto k = a.norm_w ? gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true>
                       : gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true>;
@@ -535,23 +434,24 @@ __device__ __forceinline__ void qkv_item(const QkvLaunch& a, int s_lo, int s_hi,
   for (int r = 0; r < NR; ++r) R[r] = row_ptr(sg.base, sg.P, (unsigned)(r0 + r));
 }
 
-template <int QT, int NR, int U>
+template <int QT, int NR, int U, int BLOCK>
 __device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, int blk, int nblk, int pos,
-                                        XPrologue<true>& xp, int8_t* xq, float* xd, float* red) {
+                                        XPrologue<true, BLOCK>& xp, int8_t* xq, float* xd, float* red) {
   const int wave = wave_id(), lane = threadIdx.x & 63;
   int total = 0;
   for (int i = s_lo; i < s_hi; ++i) total += a.seg[i].rows / NR;
   const int nchunks = a.K >> 5;
   const int hd = a.head_dim;
-  const int stride = nblk * 4;
-  int item = blk * 4 + wave;
+  constexpr int WPB = BLOCK / 64;
+  const int stride = nblk * WPB;
+  int item = blk * WPB + wave;
   RowPtr R[NR];
   int si = s_lo, r0 = 0;
   WStream<QT, NR, U> ws;
   float2 cs = make_float2(1.f, 0.f);
   auto rope_of = [&](int r) { return a.rope[(size_t)pos * (hd >> 1) + ((r % hd) >> 1)]; };
-  if (item < total) {
-    qkv_item<QT, NR>(a, s_lo, s_hi, item, R, si, r0);
+  {  // unconditional (clamped item): no control-flow join between these loads and finish()'s x wait
+    qkv_item<QT, NR>(a, s_lo, s_hi, min(item, total - 1), R, si, r0);
     ws.load(R, 0, nchunks, lane);
     if (lane < NR && a.seg[si].kind < 2) cs = rope_of(r0 + lane);
   }
@@ -589,19 +489,20 @@ __device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, 
   }
 }
 
-template <int QT0, int NR0, int U0, int QT1, int NR1, int U1, bool TWO>
-__global__ __launch_bounds__(256) void gemv_qkv_kernel(QkvLaunch a) {
+template <int QT0, int NR0, int U0, int QT1, int NR1, int U1, bool TWO, int BLOCK = 256>
+__global__ __launch_bounds__(BLOCK) void gemv_qkv_kernel(QkvLaunch a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + a.K);
   float* red = xd + (a.K >> 5);
   const int pos = *a.pos;
-  XPrologue<true> xp;   // QKV always follows the attention RMSNorm
+  XPrologue<true, BLOCK> xp;   // QKV always follows the attention RMSNorm
   xp.load(a.x, a.norm_w, a.K);
   if (!TWO || (int)blockIdx.x < a.blocks0) {
-    qkv_run<QT0, NR0, U0>(a, 0, a.g1, blockIdx.x, TWO ? a.blocks0 : gridDim.x, pos, xp, xq, xd, red);
+    qkv_run<QT0, NR0, U0, BLOCK>(a, 0, a.g1, blockIdx.x, TWO ? a.blocks0 : gridDim.x, pos, xp, xq, xd, red);
   } else if constexpr (TWO) {
-    qkv_run<QT1, NR1, U1>(a, a.g1, a.nseg, blockIdx.x - a.blocks0, gridDim.x - a.blocks0, pos, xp, xq, xd, red);
+    qkv_run<QT1, NR1, U1, BLOCK>(a, a.g1, a.nseg, blockIdx.x - a.blocks0, gridDim.x - a.blocks0, pos, xp, xq, xd,
+                                 red);
   }
 }
 
@@ -614,6 +515,14 @@ static void launch_qkv1(QkvLaunch L, int rows, hipStream_t s) {
   L.g1 = L.nseg;
   L.blocks0 = 0;
   LFK_NRU_DISPATCH(c.nr, c.u, ({
+    if constexpr (NR >= 2 && NR * U <= 4) {
+      if (gemv_early(EC_QKV)) {
+        auto k = gemv_qkv_kernel<QT, NR, U, QT, NR, U, false, 1024>;
+        const size_t l = std::max(lds, kOnePerCuLds);
+        hipLaunchKernelGGL(k, gemv_grid(k, l, rows / NR, 1024), dim3(1024), l, s, L);
+        return;
+      }
+    }
     if constexpr (NR >= 2 && !((QT == T_F32 || QT == T_F16) && NR * U > 4)) {
       auto k = gemv_qkv_kernel<QT, NR, U, QT, NR, U, false>;
       hipLaunchKernelGGL(k, gemv_grid(k, lds, rows / NR), dim3(256), lds, s, L);
@@ -627,11 +536,19 @@ static void launch_qkv1(QkvLaunch L, int rows, hipStream_t s) {
 // (2 rows, 1 pass) for the second (keeps the combined kernel near 128 VGPRs)
 template <int QT0, int QT1>
 static void launch_qkv2(QkvLaunch L, int rows0, int rows1, hipStream_t s) {
+  const double b0 = (double)qbytes(QT0, rows0, L.K), b1 = (double)qbytes(QT1, rows1, L.K);
+  const int items = rows0 / 2 + rows1 / 2;
+  if (gemv_early(EC_QKV)) {
+    auto k = gemv_qkv_kernel<QT0, 2, 2, QT1, 2, 1, true, 1024>;
+    const size_t l = std::max(qkv_lds(L.K), kOnePerCuLds);
+    const int nb = (int)gemv_grid(k, l, items, 1024).x;
+    L.blocks0 = std::min(nb - 1, std::max(1, (int)std::lround(nb * b0 / (b0 + b1))));
+    hipLaunchKernelGGL(k, dim3(nb), dim3(1024), l, s, L);
+    return;
+  }
   const size_t lds = qkv_lds(L.K);
   auto k = gemv_qkv_kernel<QT0, 2, 2, QT1, 2, 1, true>;
-  const int items = rows0 / 2 + rows1 / 2;
   const int nb = (int)gemv_grid(k, lds, items).x;
-  const double b0 = (double)qbytes(QT0, rows0, L.K), b1 = (double)qbytes(QT1, rows1, L.K);
   L.blocks0 = std::min(nb - 1, std::max(1, (int)std::lround(nb * b0 / (b0 + b1))));
   hipLaunchKernelGGL(k, dim3(nb), dim3(256), lds, s, L);
 }

@@ -66,6 +66,24 @@ struct QkvArgs {
 };
 void gemv_qkv(const QkvArgs& a, hipStream_t s);
 
+// Fused dense FFN (decode): x += W_down * (silu(W_gate n) * (W_up n)), n = RMSNorm(x) * norm_w.
+// One launch, one workgroup per CU; see ffn_fused.hip for the in-launch hand-off.
+struct FfnFusedArgs {
+  QMat w_gu;                       // [2F][d], gate/up interleaved in 32-row groups
+  QMat w_down;                     // [d][F]
+  float* x = nullptr;              // [d] residual: input, and output (accumulated)
+  const float* norm_w = nullptr;
+  float eps = 1e-5f;
+  float* h = nullptr;              // [F] scratch (SwiGLU output)
+  int F = 0;
+  int* counters = nullptr;         // this layer's 32 hand-off words (zero on entry)
+  int* counters_clear = nullptr;   // 32 words the launch zeroes (the previous layer's), or null
+  int* err = nullptr;              // set non-zero if a bounded wait timed out
+  long long* dbg_clk = nullptr;    // microbenchmarks only: per-workgroup wall-clock stamps [grid][8]
+};
+bool ffn_fused_supported(const FfnFusedArgs& a);  // shape/type/residency check (host)
+void ffn_fused(const FfnFusedArgs& a, hipStream_t s);
+
 // MoE down projection: out[r] += sum_s w[s] * dot(W_{ids[s]}[r], h_s)
 struct MoeDownArgs {
   QMat w;
@@ -140,6 +158,8 @@ void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int h
 // out[i] = x[i] (+) ... small helpers
 void add_inplace(float* x, const float* y, int n, hipStream_t s);
 void set_i32(int* p, int v, hipStream_t s);
+// microbenchmark: trivial kernel of a given launch shape (per-launch cost of the shape)
+void launch_probe(int threads, int blocks, size_t lds, int iters, float* out, hipStream_t s);
 // microbenchmark: out[0] = shader cycles, out[1] = wall ticks (100 MHz) of `iters` dependent FMAs
 void clock_probe(long long* out, int iters, hipStream_t s);
 

@@ -196,3 +196,26 @@ void clock_probe(long long* out, int iters, hipStream_t s) {
   hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, s, out, iters);
 }
 }  // namespace lfk
+
+namespace lfk {
+// ---------------------------------------------------------------- launch-shape probe (microbenchmarks)
+// A trivial kernel of the given geometry: every thread spins `iters` dependent
+// FMAs, one lane per block writes. Timing a graph chain of these separates the
+// per-launch cost of a workgroup shape (256 vs 1024 threads, LDS request) from
+// any real kernel body.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void launch_probe_kernel(float* out, int iters) {
+  extern __shared__ float lds_probe[];
+  float v = (float)threadIdx.x;
+  for (int i = 0; i < iters; ++i) v = v * 0.999f + 0.5f;
+  if (threadIdx.x == 0) {
+    lds_probe[0] = v;
+    out[blockIdx.x & 1023] = lds_probe[0];
+  }
+}
+void launch_probe(int threads, int blocks, size_t lds, int iters, float* out, hipStream_t s) {
+  if (threads == 1024) hipLaunchKernelGGL(launch_probe_kernel<1024>, dim3(blocks), dim3(1024), lds, s, out, iters);
+  else if (threads == 512) hipLaunchKernelGGL(launch_probe_kernel<512>, dim3(blocks), dim3(512), lds, s, out, iters);
+  else hipLaunchKernelGGL(launch_probe_kernel<256>, dim3(blocks), dim3(256), lds, s, out, iters);
+}
+}  // namespace lfk

@@ -97,6 +97,7 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   load(f);
   alloc_buffers();
   build_rope();
+  setup_ffn_fused();
   HIPCHK(hipStreamSynchronize(stream_));
 }
 
@@ -238,8 +239,36 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(state_, 0, sizeof(int) * S_NSTATE));
   HIPCHK(hipMemset(ring_, 0, sizeof(int) * 64));
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
+  ffn_cnt_ = (int*)dalloc(sizeof(int) * 32 * std::max(1, hp_.n_layer));
+  HIPCHK(hipMemset(ffn_cnt_, 0, sizeof(int) * 32 * std::max(1, hp_.n_layer)));
+  dev_err_ = (int*)dalloc(sizeof(int) * 4);
+  HIPCHK(hipMemset(dev_err_, 0, sizeof(int) * 4));
   HIPCHK(hipHostMalloc((void**)&h_ring_, sizeof(int) * 64, hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&h_tokens_, sizeof(int) * B, hipHostMallocDefault));
+}
+
+// The fused decode FFN needs: one rank (the TP path all-reduces the down
+// projection), a dense FFN, >= 2 GPU layers (each launch zeroes the previous
+// layer's counters), and every layer's gate/up + down type pair supported.
+void Engine::setup_ffn_fused() {
+  ffn_fused_ = false;
+  if (opt_.tp_size > 1 || hp_.n_expert > 0 || hp_.n_layer - opt_.layer_begin < 2) return;
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
+    FfnFusedArgs f;
+    f.w_gu = layers_[l].w_gu; f.w_down = layers_[l].w_down; f.F = F_l_;
+    if (!ffn_fused_supported(f)) return;
+  }
+  ffn_fused_ = true;
+}
+
+void Engine::check_device_err() {
+  int e = 0;
+  HIPCHK(hipMemcpy(&e, dev_err_, sizeof(int), hipMemcpyDeviceToHost));
+  if (e != 0) {
+    healthy_ = false;
+    last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
+    throw std::runtime_error(last_error_);
+  }
 }
 
 void Engine::build_rope() {
@@ -317,6 +346,16 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
       allreduce_into(tmp_, x_, d, s);
     }
   } else {
+    if (ffn_fused_) {
+      FfnFusedArgs f;
+      f.w_gu = L.w_gu; f.w_down = L.w_down; f.x = x_; f.norm_w = L.ffn_norm; f.eps = hp_.rms_eps;
+      f.h = hf_; f.F = F_l_;
+      f.counters = ffn_cnt_ + 32 * l;
+      f.counters_clear = ffn_cnt_ + 32 * (l == opt_.layer_begin ? hp_.n_layer - 1 : l - 1);
+      f.err = dev_err_;
+      ::lfk::ffn_fused(f, s);
+      return;
+    }
     GemvArgs g;
     g.w = L.w_gu; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
     g.out = hf_; g.n_out = F_l_;
@@ -536,6 +575,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   }
   HIPCHK(hipGetLastError());
   out.decode_s = now_s() - t1;
+  check_device_err();
   out.n_evaluated = n_prompt + (int)out.tokens.size() - 1;
   return out;
 }
@@ -583,6 +623,7 @@ std::vector<float> Engine::decode_logits(int token, int pos) {
   std::vector<float> out(hp_.n_vocab);
   HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
+  check_device_err();
   return out;
 }
 
@@ -601,6 +642,7 @@ void Engine::bench_decode(int n_steps, int pos0, double* ms_per_step) {
   for (int i = 0; i < n_steps; ++i) launch_step();
   HIPCHK(hipStreamSynchronize(stream_));
   *ms_per_step = (now_s() - t0) * 1e3 / n_steps;
+  check_device_err();
 }
 
 }  // namespace lfk

@@ -87,6 +87,7 @@ class Engine {
   int tp_rank() const { return opt_.tp_rank; }
   int tp_size() const { return opt_.tp_size; }
   bool healthy() const { return healthy_; }
+  bool ffn_fused() const { return ffn_fused_; }
   std::string last_error() const { return last_error_; }
   int n_ctx() const { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
@@ -109,6 +110,8 @@ class Engine {
   void enqueue_head(const float* xrow, int advance_pos, hipStream_t s);
   void launch_step();
   void check(hipError_t e, const char* what);
+  void check_device_err();
+  void setup_ffn_fused();
 
   HParams hp_;
   EngineOptions opt_;
@@ -157,6 +160,9 @@ class Engine {
   float* moe_y_ = nullptr;          // [n_batch][d] one expert's output (prefill)
   int* moe_ids_ = nullptr;
   float* moe_w_ = nullptr;
+  int* ffn_cnt_ = nullptr;    // [n_layer][32] fused-FFN hand-off counters (zero between launches)
+  int* dev_err_ = nullptr;    // device error word (bounded in-kernel waits that timed out)
+  bool ffn_fused_ = false;    // dense decode FFN as one fused launch (ffn_fused.hip)
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 

@@ -97,6 +97,9 @@ SPECS: Dict[str, ModelSpec] = {
                                 n_ctx_train=1024),
     "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", 512, 2, 8, 4, 1024, 0, 1e6, "spm", "q4_k_m",
                                  n_expert=4, n_expert_used=2, n_ctx_train=1024),
+    # wide enough for several 2048-feature FFN slices (fused decode FFN hand-off), partial last slice
+    "tiny-llama3-wide": ModelSpec("tiny-llama3-wide", 1024, 3, 8, 2, 5120, 0, 500000.0, "bpe", "q4_k_m",
+                                  n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

@@ -9,7 +9,8 @@ from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
 
 pytestmark = pytest.mark.gpu
 
-SPECS = ["tiny-llama3-q4_k_m", "tiny-llama3-mixed", "tiny-tinyllama-q8_0", "tiny-mixtral-q4_k_m", "tiny-llama3-f32"]
+SPECS = ["tiny-llama3-q4_k_m", "tiny-llama3-mixed", "tiny-tinyllama-q8_0", "tiny-mixtral-q4_k_m", "tiny-llama3-f32",
+         "tiny-llama3-wide"]
 
 
 @pytest.fixture(scope="module")
@@ -42,6 +43,27 @@ def test_prefill_and_decode_logits_match_reference(models, spec):
     assert rel_err(got_dec, ref_dec) < 5e-2, spec
     assert np.argmax(got_dec) == np.argmax(ref_dec) or \
         ref_dec[np.argmax(got_dec)] > ref_dec.max() - 0.05 * np.abs(ref_dec).max()
+
+
+@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-llama3-wide"])
+def test_fused_ffn_matches_unfused(models, spec, monkeypatch):
+    """ffn_fused.hip (one launch, in-launch slice hand-off) == gate/up + down GEMV launches."""
+    path = models[spec]
+    monkeypatch.setenv("LFK_FFN_FUSED", "1")   # opt-in path
+    eng_f = _engine(path)
+    assert eng_f.ffn_fused, "fused decode FFN not selected on a supported model"
+    monkeypatch.setenv("LFK_FFN_FUSED", "0")
+    eng_u = _engine(path)
+    assert not eng_u.ffn_fused
+    toks = [int(t) for t in np.random.default_rng(1).integers(0, 1000, 24)]
+    for i in range(20, 24):   # one decode step from an identical prefilled state, several graph replays
+        for e in (eng_f, eng_u):
+            e.eval_logits(toks[:i], 0)
+        a = eng_f.decode_logits(toks[i], i)
+        b = eng_u.decode_logits(toks[i], i)
+        # same math; only the fp32 order of the split-K atomics differs, which can flip a q8 rounding
+        assert rel_err(a, b) < 1e-2, (spec, i, rel_err(a, b))
+    assert eng_f.healthy
 
 
 def test_graph_equals_eager(models):

@@ -82,16 +82,23 @@ def main():
         ("wq_q4k_4096x4096_norm", Q4_K, d, d, 0, True),
         ("wv_q6k_1024x4096_norm", Q6_K, 1024, d, 0, True),
     ]:
-        w, nb = mat(t, R, K, len(bufs) + 1)
-        bufs.append(w)
+        if args.only and args.only not in name:
+            continue
+        nb = hip.qbytes(t, R, K)
+        ws = [mat(t, R, K, 1000 * len(bufs) + c + 1)[0] for c in range(copies(nb))]
+        bufs.append(ws[0])
         n_out = R // 2 if epi == 2 else R
         big_out = torch.zeros(n_out, device="cuda")
+        ctr = [0]
 
         for dbg in ((0, 1, 2, 3) if args.debug else (0,)):
-            def fn(st=s, w=w, t=t, R=R, K=K, epi=epi, norm=norm, n_out=n_out, big_out=big_out, dbg=dbg):
+            def fn(st=s, ws=ws, t=t, R=R, K=K, epi=epi, norm=norm, n_out=n_out, big_out=big_out, dbg=dbg, ctr=ctr):
+                w = ws[ctr[0] % len(ws)]
+                ctr[0] += 1
                 hip.gemv(w.data_ptr(), t, R, K, x.data_ptr(), nw.data_ptr() if norm else 0, 1e-5, big_out.data_ptr(),
                          n_out, epi, st, debug=dbg)
             timed(name + ("" if dbg == 0 else f"_dbg{dbg}"), fn, nb)
+        del ws[1:]
 
     # fused QKV + RoPE + KV append (Q/K Q4_K, V Q6_K as in the bumped layers; and all-Q4_K)
     n_ctx, hd = 1024, 128
@@ -147,7 +154,7 @@ def main():
           p1.data_ptr(), n_ctx, 32, 8, hd, 1.0, part.data_ptr(), ao.data_ptr(), st, cnt.data_ptr(), debug_stop=1), 1)
     # shader clock: alone, and right behind a heavy GEMV in the same stream
     clk = torch.zeros(3, dtype=torch.int64, device="cuda")
-    for label, pre in (("alone", None), ("after_gemv", bufs[1])):  # bufs[1]: one gate/up copy
+    for label, pre in (("alone", None), ("after_gemv", bufs[1] if len(bufs) > 1 else None)):
         vals = []
         for _ in range(5):
             if pre is not None:
