@@ -16,6 +16,8 @@
 // groups (the pair lives in adjacent waves; exchanged through LDS), bf16 out.
 #include <hip/hip_bf16.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 #include "qdot.h"
 
@@ -53,6 +55,14 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Ws[DB ? 2 : 1][BN * PITCH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  if (a.seg_dev) {  // grouped form: this expert's rows of the gathered buffers
+    const int r0 = a.seg_dev[0];
+    a.T = a.seg_dev[1] - r0;
+    if (m0 >= a.T) return;  // whole block, before any barrier
+    a.x += (size_t)r0 * a.w.K;
+    if (a.out) a.out += (size_t)r0 * a.ldo;
+    if (a.out_bf16) a.out_bf16 += (size_t)r0 * (a.w.rows >> 1);
+  }
   const int N = a.w.rows, K = a.w.K, T = a.T;
   const int nk = K / BK, ks = (nk + gridDim.z - 1) / gridDim.z;
   const int kb = blockIdx.z * ks, ke = min(nk, kb + ks);
@@ -173,19 +183,21 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
 
 template <int QT>
 static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
-  const int tiles = ((a.w.rows + BN - 1) / BN) * ((a.T + BM - 1) / BM);
+  const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
+  const int tiles = ((a.w.rows + BN - 1) / BN) * ((rows + BM - 1) / BM);
   const int nk = a.w.K / BK;
   // split K until ~2 blocks per CU are busy, keeping >= 8 K steps per split
   int split = 1;
   if (epi != GEMM_SWIGLU) {
     while (tiles * split < 512 && nk / (split * 2) >= 8) split *= 2;
   }
-  if (split > 1 && epi == GEMM_STORE) {
+  if (split > 1 && epi == GEMM_STORE && !a.seg_dev) {
     const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
     if (e != hipSuccess) throw std::runtime_error("gemm_dq: memset failed");
   }
   dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BM - 1) / BM, split), block(256);
   const bool db = tiles * split <= 512;
+  if (a.seg_dev && split > 1 && epi != GEMM_STORE) throw std::runtime_error("gemm_dq: grouped split-K needs STORE");
 #define LFK_GEMM_LAUNCH(E)                                                   \
   do {                                                                        \
     if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true>), grid, block, 0, s, a);  \

@@ -187,7 +187,10 @@ static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
   //   K > 4096 (FFN down)         : one row per wave, 4 passes (Q6_K: 2) in flight
   //   >= 16384 rows (gate/up, head): 4 rows per wave, 1 pass
   if (qt != T_F32 && qt != T_F16) {
-    if (nchunks > 128) return {std::max(1, min_nr), qt == T_Q6_K ? 2 : 4};
+    if (nchunks > 128) {  // long rows run on 1024-thread blocks: NR * U <= 4 (128 VGPRs)
+      const int nr = std::max(1, min_nr);
+      return {nr, std::max(1, (qt == T_Q6_K ? 2 : 4) / nr)};
+    }
     if (rows >= 16384) return {4, 1};
   }
   int nr = (qt == T_F32 || qt == T_F16) ? 2 : 4;
@@ -695,47 +698,6 @@ __global__ void moe_route_kernel(const float* logits, int E, int k, int* ids, fl
 void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s) {
   if (n_expert > 64 || k > n_expert) throw std::runtime_error("moe_route: n_expert must be <= 64");
   hipLaunchKernelGGL(moe_route_kernel, dim3(1), dim3(64), 0, s, logits, n_expert, k, ids, w);
-}
-
-// ------------------------------------------------------------------ MoE prefill helpers
-__global__ void moe_route_dense_kernel(const float* logits, int E, int k, float* wd) {
-  const int t = blockIdx.x, lane = threadIdx.x;
-  const float* lg = logits + (size_t)t * E;
-  float v = lane < E ? lg[lane] : -INFINITY;
-  const float m = wave_max(v);
-  float p = lane < E ? __expf(v - m) : 0.f;
-  p /= wave_sum(p);
-  float taken = lane < E ? p : -1.f, sel = 0.f, mine = 0.f;
-  for (int j = 0; j < k; ++j) {
-    float best = taken;
-    int bi = lane;
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    sel += best;
-    if (lane == bi) { mine = best; taken = -1.f; }
-  }
-  if (lane < E) wd[(size_t)t * E + lane] = mine / sel;
-}
-
-void moe_route_dense(const float* logits, int T, int n_expert, int k, float* w_dense, hipStream_t s) {
-  if (T <= 0) return;
-  if (n_expert > 64) throw std::runtime_error("moe_route_dense: n_expert must be <= 64");
-  hipLaunchKernelGGL(moe_route_dense_kernel, dim3(T), dim3(64), 0, s, logits, n_expert, k, w_dense);
-}
-
-__global__ void axpy_rows_kernel(float* acc, const float* y, const float* wd, int e, int E, int d) {
-  const int t = blockIdx.x;
-  const float w = wd[(size_t)t * E + e];
-  if (w == 0.f) return;
-  for (int i = threadIdx.x; i < d; i += blockDim.x) acc[(size_t)t * d + i] += w * y[(size_t)t * d + i];
-}
-
-void axpy_rows(float* acc, const float* y, const float* w_dense, int e, int E, int T, int d, hipStream_t s) {
-  if (T <= 0) return;
-  hipLaunchKernelGGL(axpy_rows_kernel, dim3(T), dim3(256), 0, s, acc, y, w_dense, e, E, d);
 }
 
 }  // namespace lfk

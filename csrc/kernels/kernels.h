@@ -97,10 +97,6 @@ void gemv_moe_down(const MoeDownArgs& a, hipStream_t s);
 
 // Router: softmax over n_expert logits, top-k, renormalise -> ids / weights (device).
 void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s);
-// Prefill router over T rows -> dense [T][E] weights (0 for unselected experts).
-void moe_route_dense(const float* logits, int T, int n_expert, int k, float* w_dense, hipStream_t s);
-// acc[t][:] += w_dense[t][e] * y[t][:]
-void axpy_rows(float* acc, const float* y, const float* w_dense, int e, int E, int T, int d, hipStream_t s);
 
 // ---------------------------------------------------------------- attention
 // Decode: split-L flash decoding over chunks of 64 keys, GQA-packed.
@@ -142,8 +138,21 @@ struct GemmArgs {
   __hip_bfloat16* out_bf16 = nullptr; // SWIGLU -> bf16 [T][N/2]
   int ldo = 0;
   const float* resid = nullptr;    // STORE: out = acc + resid[t][n] (TP rank 0)
+  // grouped (MoE) form: rows [seg_dev[0], seg_dev[1]) of x / out, read on the device;
+  // T is then only the launch bound (max rows) and rows_hint the expected count (split-K
+  // sizing). Split-K STORE partials are atomically added: the caller pre-zeroes `out`.
+  const int* seg_dev = nullptr;
+  int rows_hint = 0;
 };
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s);
+
+// ---------------------------------------------------------------- MoE prefill (grouped experts)
+// Device-side routing: per-expert row lists in ascending token order (moe.hip).
+void moe_route_group(const float* logits, int T, int n_expert, int k, int* sel, float* selw, int* cnt_off, int* tok,
+                     float* gw, int* pos, hipStream_t s);
+void gather_rows_bf16(const __hip_bfloat16* src, const int* tok, int n_rows, int d, __hip_bfloat16* dst,
+                      hipStream_t s);
+void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw, int T, int k, int d, hipStream_t s);
 
 // ---------------------------------------------------------------- elementwise / misc
 // x[t][:] = dequant(token_embd[tokens[t]][:])

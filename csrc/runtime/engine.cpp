@@ -232,10 +232,20 @@ void Engine::alloc_buffers() {
   tokens_ = (int*)dalloc(sizeof(int) * B);
   sparams_ = (SamplerParamsDev*)dalloc(sizeof(SamplerParamsDev));
   router_logits_ = (float*)dalloc(sizeof(float) * B * E);
-  route_w_ = (float*)dalloc(sizeof(float) * B * E);
   moe_ids_ = (int*)dalloc(sizeof(int) * KU);
   moe_w_ = (float*)dalloc(sizeof(float) * KU);
-  if (hp_.n_expert > 0) moe_y_ = (float*)dalloc(sizeof(float) * B * d);
+  if (hp_.n_expert > 0) {
+    const size_t R = (size_t)B * KU;
+    moe_sel_ = (int*)dalloc(sizeof(int) * R);
+    moe_selw_ = (float*)dalloc(sizeof(float) * R);
+    moe_off_ = (int*)dalloc(sizeof(int) * (E + 1));
+    moe_tok_ = (int*)dalloc(sizeof(int) * R);
+    moe_gw_ = (float*)dalloc(sizeof(float) * R);
+    moe_pos_ = (int*)dalloc(sizeof(int) * R);
+    moe_xg_ = (__hip_bfloat16*)dalloc(2 * R * d);
+    moe_hg_ = (__hip_bfloat16*)dalloc(2 * R * F_l_);
+    moe_yg_ = (float*)dalloc(sizeof(float) * R * d);
+  }
   HIPCHK(hipMemset(state_, 0, sizeof(int) * S_NSTATE));
   HIPCHK(hipMemset(ring_, 0, sizeof(int) * 64));
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
@@ -437,23 +447,29 @@ void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
       GemmArgs ra;
       ra.w = L.router; ra.x = xb_; ra.T = T; ra.out = router_logits_; ra.ldo = E;
       gemm_dq(ra, GEMM_STORE, s);
-      moe_route_dense(router_logits_, T, E, hp_.n_expert_used, route_w_, s);
+      const int KU = hp_.n_expert_used;
+      // device-side routing -> per-expert row lists; gather the routed rows once
+      moe_route_group(router_logits_, T, E, KU, moe_sel_, moe_selw_, moe_off_, moe_tok_, moe_gw_, moe_pos_, s);
+      gather_rows_bf16(xb_, moe_tok_, T * KU, d, moe_xg_, s);
       if (tp) {
         if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * T * d, hipMemcpyDeviceToDevice, s));
         else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * T * d, s));
       }
       float* acc = tp ? tmp_ : x_;
-      for (int e = 0; e < E; ++e) {
+      // split-K partials of the grouped down GEMMs meet by atomic add: zero the gathered output
+      HIPCHK(hipMemsetAsync(moe_yg_, 0, sizeof(float) * (size_t)T * KU * d, s));
+      const int hint = std::max(1, T * KU / E);
+      for (int e = 0; e < E; ++e) {  // each expert multiplies only its rows (count/offset read on the device)
         GemmArgs gu;
         gu.w = L.gu_exps; gu.w.base += L.gu_exps.expert_stride * e;
-        gu.x = xb_; gu.T = T; gu.out_bf16 = h_;
+        gu.x = moe_xg_; gu.T = T; gu.out_bf16 = moe_hg_; gu.seg_dev = moe_off_ + e; gu.rows_hint = hint;
         gemm_dq(gu, GEMM_SWIGLU, s);
         GemmArgs dn;
         dn.w = L.down_exps; dn.w.base += L.down_exps.expert_stride * e;
-        dn.x = h_; dn.T = T; dn.ldo = d; dn.out = moe_y_;
+        dn.x = moe_hg_; dn.T = T; dn.ldo = d; dn.out = moe_yg_; dn.seg_dev = moe_off_ + e; dn.rows_hint = hint;
         gemm_dq(dn, GEMM_STORE, s);
-        axpy_rows(acc, moe_y_, route_w_, e, E, T, d, s);
       }
+      moe_scatter_add(acc, moe_yg_, moe_pos_, moe_gw_, T, KU, d, s);
       if (tp) allreduce_into(tmp_, x_, (size_t)T * d, s);
     } else {
       GemmArgs gu;

@@ -156,8 +156,10 @@ class Engine {
   int* tokens_ = nullptr;     // [n_batch]
   SamplerParamsDev* sparams_ = nullptr;
   float* router_logits_ = nullptr;  // [n_batch][E]
-  float* route_w_ = nullptr;        // [n_batch][E] dense routing weights (prefill)
-  float* moe_y_ = nullptr;          // [n_batch][d] one expert's output (prefill)
+  // grouped MoE prefill (moe.hip): routing lists and gathered row buffers, [n_batch * k] rows
+  int* moe_sel_ = nullptr; float* moe_selw_ = nullptr; int* moe_off_ = nullptr; int* moe_tok_ = nullptr;
+  float* moe_gw_ = nullptr; int* moe_pos_ = nullptr;
+  __hip_bfloat16* moe_xg_ = nullptr; __hip_bfloat16* moe_hg_ = nullptr; float* moe_yg_ = nullptr;
   int* moe_ids_ = nullptr;
   float* moe_w_ = nullptr;
   int* ffn_cnt_ = nullptr;    // [n_layer][32] fused-FFN hand-off counters (zero between launches)

@@ -66,6 +66,20 @@ def test_fused_ffn_matches_unfused(models, spec, monkeypatch):
     assert eng_f.healthy
 
 
+def test_moe_grouped_prefill_chunked(models):
+    """Grouped expert prefill (device-side routing, per-expert row counts) is independent of
+    how the prompt is chunked: n_batch 16 (3 chunks, partial last) == n_batch 128 (one chunk)."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-mixtral-q4_k_m"]
+    prompt = [int(t) for t in np.random.default_rng(5).integers(3, 1000, 40)]
+    outs = []
+    for nb in (16, 128):
+        eng = load_hip().Engine(path, n_ctx=256, n_batch=nb, device=0, use_graph=True)
+        r = eng.generate(prompt, 0, 12, {"temperature": 0.0}, [], None, None)
+        outs.append(r["tokens"])
+    assert outs[0] == outs[1]
+
+
 def test_graph_equals_eager(models):
     path = models["tiny-llama3-q4_k_m"]
     outs = []

@@ -37,9 +37,10 @@ def test_gemv_types(torch, t, R, K):
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
-def test_gemv_norm_add_and_resid(torch, t):
+@pytest.mark.parametrize("K", [4096, 8192, 28672])   # 8B, 70B d_model, 70B FFN (1024-thread launch paths)
+def test_gemv_norm_add_and_resid(torch, t, K):
     rng = np.random.default_rng(7)
-    R, K = 256, 4096
+    R = 256
     raw, W = make_matrix(t, R, K, rng)
     x = rng.standard_normal(K).astype(np.float32) * 3
     nw = (1 + 0.1 * rng.standard_normal(K)).astype(np.float32)
@@ -60,9 +61,9 @@ def test_gemv_norm_add_and_resid(torch, t):
     assert rel_err(out2.cpu().numpy() - y0, ref - y0) < 1e-3
 
 
-def test_gemv_swiglu_interleaved(torch):
+@pytest.mark.parametrize("F,K", [(96, 512), (256, 4096), (128, 8192)])
+def test_gemv_swiglu_interleaved(torch, F, K):
     rng = np.random.default_rng(8)
-    F, K = 96, 512
     t = GGMLType.Q4_K
     rg, Wg = make_matrix(t, F, K, rng)
     ru, Wu = make_matrix(t, F, K, rng)
