@@ -126,6 +126,13 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("device_bytes", &Engine::device_bytes)
       .def_property_readonly("healthy", &Engine::healthy)
       .def_property_readonly("ffn_fused", &Engine::ffn_fused)
+      .def("p2p_handle", [](Engine& e) { return py::bytes(e.p2p_handle()); })
+      .def("p2p_open", [](Engine& e, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.push_back(std::string(h));
+        e.p2p_open(v);
+      })
+      .def_property_readonly("p2p_ready", &Engine::p2p_ready)
       .def_property_readonly("last_error", &Engine::last_error)
       .def_property_readonly("n_ctx", &Engine::n_ctx)
       .def_property_readonly("tp_rank", &Engine::tp_rank)
@@ -176,6 +183,21 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
      py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
      py::arg("debug") = 0, py::arg("dbg_clk") = 0);
+
+  py::class_<P2PComm>(m, "P2PComm")
+      .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_n"), py::arg("device"))
+      .def("handle", [](const P2PComm& c) { return py::bytes(c.handle()); })
+      .def("open", [](P2PComm& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (const auto& h : hs) v.push_back(std::string(h));
+        c.open(v);
+      })
+      .def("allreduce", [](P2PComm& c, uintptr_t src, uintptr_t dst, int n, uintptr_t stream) {
+        c.allreduce(P<float>(src), P<float>(dst), n, S(stream));
+        hip_ok("p2p_allreduce");
+      })
+      .def("error", &P2PComm::error)
+      .def("reset_error", &P2PComm::reset_error);
 
   m.def("ffn_fused", [](uintptr_t wgu, int tgu, uintptr_t wdn, int tdn, int d, int F, uintptr_t x, uintptr_t norm,
                         float eps, uintptr_t h, uintptr_t ctr, uintptr_t ctr_clear, uintptr_t err, uintptr_t stream,

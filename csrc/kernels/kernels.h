@@ -98,6 +98,25 @@ void gemv_moe_down(const MoeDownArgs& a, hipStream_t s);
 // Router: softmax over n_expert logits, top-k, renormalise -> ids / weights (device).
 void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s);
 
+// ---------------------------------------------------------------- tensor-parallel all-reduce
+// One-shot push all-reduce over peer memory (p2p_allreduce.hip). Rank p's receive
+// region: data [2 slots][world][max_n] f32, then flags [2][world][kP2PMaxBlocks] i32.
+static constexpr int kP2PMaxRanks = 8;
+static constexpr int kP2PMaxBlocks = 64;
+struct P2PPeers {
+  float* data[kP2PMaxRanks] = {};
+  int* flags[kP2PMaxRanks] = {};
+};
+struct P2PAllreduceArgs {
+  P2PPeers peers;                  // every rank's region as mapped in THIS process (own one included)
+  const float* src = nullptr;      // [n] this rank's partial
+  float* dst = nullptr;            // [n] the sum (may alias nothing in the regions)
+  int n = 0, max_n = 0, rank = 0, world = 1, blocks = 16;
+  int* epochs = nullptr;           // [kP2PMaxBlocks] local, zero-initialised, advanced per launch
+  int* err = nullptr;              // set on a timed-out wait
+};
+void p2p_allreduce(const P2PAllreduceArgs& a, hipStream_t s);
+
 // ---------------------------------------------------------------- attention
 // Decode: split-L flash decoding over chunks of 64 keys, GQA-packed.
 struct AttnDecodeArgs {

@@ -274,6 +274,7 @@ void Engine::setup_ffn_fused() {
 void Engine::check_device_err() {
   int e = 0;
   HIPCHK(hipMemcpy(&e, dev_err_, sizeof(int), hipMemcpyDeviceToHost));
+  if (e == 0 && p2p_ && p2p_->ready()) e = p2p_->error();
   if (e != 0) {
     healthy_ = false;
     last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
@@ -294,7 +295,25 @@ void Engine::build_rope() {
 }
 
 // ------------------------------------------------------------------------ schedule
+std::string Engine::p2p_handle() {
+  if (opt_.tp_size < 2) throw std::runtime_error("p2p: tensor parallelism is off");
+  if (!p2p_) p2p_ = std::make_unique<P2PComm>(opt_.tp_rank, opt_.tp_size, hp_.n_embd, opt_.device);
+  return p2p_->handle();
+}
+
+void Engine::p2p_open(const std::vector<std::string>& handles) {
+  if (!p2p_) throw std::runtime_error("p2p: call p2p_handle() first");
+  if (graph_exec_) throw std::runtime_error("p2p: open the peers before the first decode step");
+  p2p_->open(handles);
+}
+
+// Decode-sized messages (one token's hidden state) take the one-shot P2P path when
+// the peers are open; prefill-sized ones (T x d) go to RCCL's ring/tree algorithms.
 void Engine::allreduce_into(const float* send, float* recv, size_t n, hipStream_t s) {
+  if (p2p_ && p2p_->ready() && n <= (size_t)p2p_->max_n()) {
+    p2p_->allreduce(send, recv, (int)n, s);
+    return;
+  }
   ncclchk(ncclAllReduce(send, recv, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s), "ncclAllReduce");
 }
 

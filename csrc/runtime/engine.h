@@ -19,6 +19,7 @@
 
 #include "../kernels/kernels.h"
 #include "gguf.h"
+#include "p2p.h"
 
 namespace lfk {
 
@@ -86,6 +87,11 @@ class Engine {
   size_t device_bytes() const { return dev_bytes_; }
   int tp_rank() const { return opt_.tp_rank; }
   int tp_size() const { return opt_.tp_size; }
+  // tensor parallelism: one-shot P2P all-reduce for decode-sized messages (p2p.h);
+  // the caller exchanges every rank's handle, then opens them (before the first decode)
+  std::string p2p_handle();
+  void p2p_open(const std::vector<std::string>& handles);
+  bool p2p_ready() const { return p2p_ && p2p_->ready(); }
   bool healthy() const { return healthy_; }
   bool ffn_fused() const { return ffn_fused_; }
   std::string last_error() const { return last_error_; }
@@ -117,6 +123,7 @@ class Engine {
   EngineOptions opt_;
   hipStream_t stream_ = nullptr;
   void* comm_ = nullptr;  // ncclComm_t
+  std::unique_ptr<P2PComm> p2p_;
   std::vector<void*> allocs_;
   size_t dev_bytes_ = 0;
   bool healthy_ = true;

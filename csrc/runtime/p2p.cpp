@@ -1,0 +1,83 @@
+#include "p2p.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace lfk {
+
+static void p2pchk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("p2p: ") + what + ": " + hipGetErrorString(e));
+}
+
+P2PComm::P2PComm(int rank, int world, int max_n, int device)
+    : rank_(rank), world_(world), max_n_(max_n), device_(device) {
+  if (world < 1 || world > kP2PMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("p2p: bad rank/world");
+  if (max_n <= 0) throw std::runtime_error("p2p: bad max_n");
+  p2pchk(hipSetDevice(device_), "hipSetDevice");
+  data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n;
+  data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
+  region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
+  p2pchk(hipMalloc(&region_, region_bytes_), "hipMalloc region");
+  p2pchk(hipMemset(region_, 0, region_bytes_), "hipMemset region");
+  p2pchk(hipMalloc((void**)&epochs_, sizeof(int) * kP2PMaxBlocks), "hipMalloc epochs");
+  p2pchk(hipMemset(epochs_, 0, sizeof(int) * kP2PMaxBlocks), "hipMemset epochs");
+  p2pchk(hipMalloc((void**)&err_, sizeof(int) * 4), "hipMalloc err");
+  p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "hipMemset err");
+  p2pchk(hipDeviceSynchronize(), "sync");
+}
+
+P2PComm::~P2PComm() {
+  for (void* p : imported_)
+    if (p) (void)hipIpcCloseMemHandle(p);
+  if (region_) (void)hipFree(region_);
+  if (epochs_) (void)hipFree(epochs_);
+  if (err_) (void)hipFree(err_);
+}
+
+std::string P2PComm::handle() const {
+  hipIpcMemHandle_t h;
+  p2pchk(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void P2PComm::open(const std::vector<std::string>& handles) {
+  if ((int)handles.size() != world_) throw std::runtime_error("p2p: need one handle per rank");
+  p2pchk(hipSetDevice(device_), "hipSetDevice");
+  for (int p = 0; p < world_; ++p) {
+    char* base = nullptr;
+    if (p == rank_) {
+      base = static_cast<char*>(region_);
+    } else {
+      if (handles[p].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("p2p: bad handle size");
+      hipIpcMemHandle_t h;
+      std::memcpy(&h, handles[p].data(), sizeof(h));
+      void* ptr = nullptr;
+      p2pchk(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+      imported_.push_back(ptr);
+      base = static_cast<char*>(ptr);
+    }
+    peers_.data[p] = reinterpret_cast<float*>(base);
+    peers_.flags[p] = reinterpret_cast<int*>(base + data_bytes_);
+  }
+  ready_ = true;
+}
+
+void P2PComm::allreduce(const float* src, float* dst, int n, hipStream_t s) {
+  if (!ready_) throw std::runtime_error("p2p: open() the peer handles first");
+  P2PAllreduceArgs a;
+  a.peers = peers_;
+  a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_;
+  a.blocks = std::min(kP2PMaxBlocks, std::max(1, (n + 255) / 256));
+  a.epochs = epochs_; a.err = err_;
+  p2p_allreduce(a, s);
+}
+
+int P2PComm::error() const {
+  int e = 0;
+  p2pchk(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost), "read err");
+  return e;
+}
+
+void P2PComm::reset_error() { p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "reset err"); }
+
+}  // namespace lfk

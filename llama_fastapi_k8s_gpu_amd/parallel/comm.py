@@ -56,6 +56,14 @@ def broadcast_nccl_id(make_id: Callable[[], bytes]) -> bytes:
     return obj[0]
 
 
+def allgather_bytes(b: bytes, group=None) -> list:
+    """Every rank's bytes object, in rank order (IPC handle exchange)."""
+    import torch.distributed as dist
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, b, group=group)
+    return out
+
+
 def _gloo_group():
     global _GLOO
     import torch.distributed as dist

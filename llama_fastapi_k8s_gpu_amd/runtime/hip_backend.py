@@ -56,6 +56,22 @@ class HipBackend:
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id)
         self.n_ctx = n_ctx
         self.device = device
+        if size > 1:
+            self._open_p2p()
+
+    def _open_p2p(self):
+        """Exchange the ranks' IPC handles so decode all-reduces take the one-shot
+        P2P kernel over xGMI (prefill-sized ones stay on RCCL). Any failure leaves
+        the engine on RCCL for everything."""
+        import os
+        if os.environ.get("LFK_P2P_ALLREDUCE", "1") == "0":
+            return
+        from ..parallel.comm import allgather_bytes
+        try:
+            handles = allgather_bytes(self.engine.p2p_handle())
+            self.engine.p2p_open(handles)
+        except Exception as e:  # pragma: no cover - depends on the node's IPC support
+            logger.warning("P2P all-reduce unavailable, using RCCL only: %s", e)
 
     def health(self):
         return {"ok": bool(self.engine.healthy), "backend": self.name, "tp": self.tp_size,

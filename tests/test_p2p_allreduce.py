@@ -1,0 +1,88 @@
+"""One-shot P2P all-reduce (kernels/p2p_allreduce.hip, runtime/p2p.cpp).
+
+Two processes share the ONE GPU of the test box: each exports its receive region
+with a hipIpc handle, the handles are exchanged over a gloo group, and the
+all-reduce runs exactly as on an 8-GPU node, minus the xGMI transport (the
+peer pointer is an IPC mapping of the same device's memory). Checked against
+the fp32 sum in rank order, over many epochs (slot reuse) and under hipGraph
+replay (epochs advance on the device)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N = 4096
+
+
+def _inputs(rank, it, n=N):
+    return np.random.default_rng(1000 * it + rank).standard_normal(n).astype(np.float32)
+
+
+def _worker(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        from llama_fastapi_k8s_gpu_amd.parallel.comm import allgather_bytes
+        from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+        hip = load_hip()
+        c = hip.P2PComm(rank, world, N, 0)
+        c.open(allgather_bytes(c.handle()))
+        s = torch.cuda.current_stream()
+        src = torch.empty(N, device="cuda")
+        dst = torch.empty(N, device="cuda")
+        worst = 0.0
+        for it in range(40):   # eager: 40 epochs, both slots reused 20 times
+            n = N if it % 3 else 1000 + it
+            src[:n].copy_(torch.from_numpy(_inputs(rank, it, n)))
+            dist.barrier()
+            c.allreduce(src.data_ptr(), dst.data_ptr(), n, s.cuda_stream)
+            torch.cuda.synchronize()
+            ref = sum(_inputs(r, it, n).astype(np.float32) for r in range(world))
+            worst = max(worst, float(np.abs(dst[:n].cpu().numpy() - ref).max()))
+        # graph replay: the captured launch advances its epochs on the device
+        g = torch.cuda.CUDAGraph()
+        cs = torch.cuda.Stream()
+        src.copy_(torch.from_numpy(_inputs(rank, 99)))
+        with torch.cuda.stream(cs):
+            with torch.cuda.graph(g):
+                c.allreduce(src.data_ptr(), dst.data_ptr(), N, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref = sum(_inputs(r, 99) for r in range(world))
+        for _ in range(10):
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            worst = max(worst, float(np.abs(dst.cpu().numpy() - ref).max()))
+        q.put((rank, worst, c.error(), dst[:8].cpu().numpy().tolist()))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, None, repr(e), None))
+
+
+@pytest.mark.timeout(240)
+def test_p2p_allreduce_two_processes_one_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=200) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    res.sort()
+    for rank, worst, err, head in res:
+        assert worst is not None, err
+        assert err == 0, f"rank {rank}: device error word {err}"
+        assert worst < 1e-5, (rank, worst)
+    assert res[0][3] == res[1][3]   # bit-identical on both ranks
