@@ -30,7 +30,7 @@ PYBIND11_MODULE(_cpu, m) {
   m.doc() = "C++ CPU backend (OpenMP): GGUF engine for n_gpu_layers = 0";
   py::class_<CpuEngine>(m, "CpuEngine")
       .def(py::init([](const std::string& path, int n_ctx, int n_threads, int n_batch, int tp_rank, int tp_size,
-                       int layer_end, bool load_head) {
+                       int layer_end, bool load_head, const std::vector<float>& tensor_split) {
              CpuOptions o;
              o.n_ctx = n_ctx;
              o.n_threads = n_threads;
@@ -39,11 +39,13 @@ PYBIND11_MODULE(_cpu, m) {
              o.tp_size = tp_size;
              o.layer_end = layer_end;
              o.load_head = load_head;
+             o.tensor_split = tensor_split;
              py::gil_scoped_release nogil;
              return std::make_unique<CpuEngine>(path, o);
            }),
            py::arg("path"), py::arg("n_ctx") = 512, py::arg("n_threads") = 0, py::arg("n_batch") = 64,
-           py::arg("tp_rank") = 0, py::arg("tp_size") = 1, py::arg("layer_end") = -1, py::arg("load_head") = true)
+           py::arg("tp_rank") = 0, py::arg("tp_size") = 1, py::arg("layer_end") = -1, py::arg("load_head") = true,
+           py::arg("tensor_split") = std::vector<float>{})
       .def("set_comm",
            [](CpuEngine& e, py::object allreduce, py::object allgather) {
              // callbacks get numpy views of the engine's buffers (no copy); they run with the GIL held

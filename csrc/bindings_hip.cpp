@@ -34,7 +34,7 @@ PYBIND11_MODULE(_hip, m) {
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
-                       int tp_size, py::bytes nccl_id, int layer_begin) {
+                       int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split) {
              EngineOptions o;
              o.layer_begin = layer_begin;
              o.n_ctx = n_ctx;
@@ -44,12 +44,14 @@ PYBIND11_MODULE(_hip, m) {
              o.tp_rank = tp_rank;
              o.tp_size = tp_size;
              o.nccl_id = std::string(nccl_id);
+             o.tensor_split = tensor_split;
              py::gil_scoped_release nogil;
              return std::make_unique<Engine>(path, o);
            }),
            py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
-           py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0)
+           py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0,
+           py::arg("tensor_split") = std::vector<float>{})
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,

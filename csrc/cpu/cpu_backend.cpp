@@ -450,7 +450,7 @@ CpuEngine::CpuEngine(const std::string& path, const CpuOptions& o)
   if (!emb) throw std::runtime_error("missing token_embd.weight");
   n_vocab_ = (int)emb->ne[1];
   if (head_dim_ % 32) throw std::runtime_error("cpu backend: head_dim must be a multiple of 32");
-  sp_ = make_shard_plan(n_head_, n_head_kv_, head_dim_, n_ff_, n_vocab_, o.tp_size, o.tp_rank);
+  sp_ = make_shard_plan(n_head_, n_head_kv_, head_dim_, n_ff_, n_vocab_, o.tp_size, o.tp_rank, o.tensor_split);
   layer_end_ = o.layer_end < 0 ? n_layer_ : std::min(o.layer_end, n_layer_);
   tok_embd_ = load_mat(f, "token_embd.weight");
   if (o.load_head) {

@@ -48,6 +48,7 @@ struct CpuGenOut {
 struct CpuOptions {
   int n_ctx = 512, n_threads = 0, n_batch = 64;
   int tp_rank = 0, tp_size = 1;   // tensor parallel (same shard plan as the GPU engine)
+  std::vector<float> tensor_split;  // per-rank weights (empty = even); see runtime/shard.h
   int layer_end = -1;             // hybrid placement: only layers [0, layer_end) are resident
   bool load_head = true;          // output norm + lm_head resident
 };

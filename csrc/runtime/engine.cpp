@@ -75,7 +75,11 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   GGUFFile f(path);
   hp_ = read_hparams(f);
   const int tp = opt_.tp_size, r = opt_.tp_rank;
-  const ShardPlan sp = make_shard_plan(hp_.n_head, hp_.n_head_kv, hp_.head_dim, hp_.n_ff, hp_.n_vocab, tp, r);
+  const ShardPlan sp =
+      make_shard_plan(hp_.n_head, hp_.n_head_kv, hp_.head_dim, hp_.n_ff, hp_.n_vocab, tp, r, opt_.tensor_split);
+  q0_ = sp.q_row0();
+  kv0_ = sp.kv_row0();
+  f0_ = sp.f0();
   nh_l_ = sp.nh_l;
   nkv_l_ = sp.nkv_l;
   nq_ = sp.nq;
@@ -181,18 +185,18 @@ void Engine::load(const GGUFFile& f) {
     Layer& L = layers_[l];
     L.attn_norm = upload_f32(f, p + "attn_norm.weight");
     L.ffn_norm = upload_f32(f, p + "ffn_norm.weight");
-    L.wq = upload_matrix(f, p + "attn_q.weight", (size_t)r * nq_, nq_, 0, d);
-    L.wk = upload_matrix(f, p + "attn_k.weight", (size_t)r * nkvd_, nkvd_, 0, d);
-    L.wv = upload_matrix(f, p + "attn_v.weight", (size_t)r * nkvd_, nkvd_, 0, d);
-    L.wo = upload_matrix(f, p + "attn_output.weight", 0, d, (size_t)r * nq_, nq_);
+    L.wq = upload_matrix(f, p + "attn_q.weight", q0_, nq_, 0, d);
+    L.wk = upload_matrix(f, p + "attn_k.weight", kv0_, nkvd_, 0, d);
+    L.wv = upload_matrix(f, p + "attn_v.weight", kv0_, nkvd_, 0, d);
+    L.wo = upload_matrix(f, p + "attn_output.weight", 0, d, q0_, nq_);
     if (hp_.n_expert > 0) {
       L.router = upload_matrix(f, p + "ffn_gate_inp.weight", 0, hp_.n_expert, 0, d);
-      L.gu_exps = upload_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", (size_t)r * F_l_, F_l_,
+      L.gu_exps = upload_gate_up(f, p + "ffn_gate_exps.weight", p + "ffn_up_exps.weight", f0_, F_l_,
                                  hp_.n_expert);
-      L.down_exps = upload_matrix(f, p + "ffn_down_exps.weight", 0, d, (size_t)r * F_l_, F_l_, hp_.n_expert);
+      L.down_exps = upload_matrix(f, p + "ffn_down_exps.weight", 0, d, f0_, F_l_, hp_.n_expert);
     } else {
-      L.w_gu = upload_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight", (size_t)r * F_l_, F_l_);
-      L.w_down = upload_matrix(f, p + "ffn_down.weight", 0, d, (size_t)r * F_l_, F_l_);
+      L.w_gu = upload_gate_up(f, p + "ffn_gate.weight", p + "ffn_up.weight", f0_, F_l_);
+      L.w_down = upload_matrix(f, p + "ffn_down.weight", 0, d, f0_, F_l_);
     }
     (void)hd;
   }

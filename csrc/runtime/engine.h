@@ -38,6 +38,7 @@ struct EngineOptions {
   int tp_rank = 0;
   int tp_size = 1;
   std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1)
+  std::vector<float> tensor_split;  // per-rank weights (empty = even); see shard.h
   int layer_begin = 0;  // hybrid placement: layers [0, layer_begin) run on the CPU backend
   bool verbose = false;
 };
@@ -131,6 +132,7 @@ class Engine {
 
   // local (per-rank) sizes
   int nh_l_ = 0, nkv_l_ = 0, nq_ = 0, nkvd_ = 0, F_l_ = 0, V_l_ = 0, V_pad_ = 0;
+  size_t q0_ = 0, kv0_ = 0, f0_ = 0;   // this rank's first q row / kv row / FFN feature
 
   // weights
   QMat tok_embd_, output_;

@@ -95,6 +95,9 @@ SPECS: Dict[str, ModelSpec] = {
     # tensor-parallel test shapes: per-rank head / FFN slices stay multiples of 256 at TP=2
     "tiny-llama3-tp": ModelSpec("tiny-llama3-tp", 512, 2, 8, 4, 1024, 0, 500000.0, "bpe", "q4_k_m",
                                 n_ctx_train=1024),
+    # 4 kv heads of 256 q columns each: uneven tensor_split ratios and TP=3 are representable
+    "tiny-llama3-tp4": ModelSpec("tiny-llama3-tp4", 1024, 2, 8, 4, 1024, 0, 500000.0, "bpe", "q4_k_m",
+                                 n_ctx_train=1024),
     "tiny-mixtral-tp": ModelSpec("tiny-mixtral-tp", 512, 2, 8, 4, 1024, 0, 1e6, "spm", "q4_k_m",
                                  n_expert=4, n_expert_used=2, n_ctx_train=1024),
     # wide enough for several 2048-feature FFN slices (fused decode FFN hand-off), partial last slice

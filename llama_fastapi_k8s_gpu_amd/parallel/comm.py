@@ -27,15 +27,21 @@ def dist_ready() -> bool:
         return False
 
 
-def check_tensor_split(tensor_split: Optional[Sequence[float]], world: int) -> None:
-    """Row-split ranks are symmetric: ``tensor_split`` may be omitted or uniform
-    over the ranks (upstream proportional splits are rejected loudly)."""
+def check_tensor_split(tensor_split: Optional[Sequence[float]], world: int) -> list:
+    """Per-rank weights for the row-split shard plan (runtime/shard.h): heads are
+    apportioned in whole kv heads, FFN features in 256-wide superblocks, by these
+    ratios (llama.cpp's ``tensor_split`` semantics: proportions, not sizes).
+    Trailing zeros (GPUs a node has but the group does not use) are dropped;
+    returns [] for an even split."""
     if not tensor_split:
-        return
-    ts = [float(v) for v in tensor_split if float(v) > 0]
-    if len(ts) != world or max(ts) - min(ts) > 1e-6 * max(ts):
-        raise ValueError(f"tensor_split {list(tensor_split)} must be uniform over the {world} ranks "
-                         "(row-split ranks are symmetric)")
+        return []
+    ts = [float(v) for v in tensor_split]
+    while ts and ts[-1] == 0:
+        ts.pop()
+    if len(ts) != world or any(v <= 0 for v in ts):
+        raise ValueError(f"tensor_split {list(tensor_split)} must give a positive weight to each of the {world} "
+                         "ranks")
+    return ts
 
 
 def tp_group_info(tensor_split: Optional[Sequence[float]] = None) -> Tuple[int, int]:

@@ -29,12 +29,13 @@ class CpuBackend:
                  split_mode: str = "none", tensor_split=None, **_):
         cpu = load_cpu()
         threads = int(n_threads or os.environ.get("N_THREADS", 0) or 0)
-        rank, size = 0, 1
+        rank, size, ts = 0, 1, []
         if split_mode == "row":
-            from ..parallel.comm import tp_group_info
+            from ..parallel.comm import check_tensor_split, tp_group_info
             rank, size = tp_group_info(tensor_split)
+            ts = check_tensor_split(tensor_split, size) if size > 1 else []
         self.engine = cpu.CpuEngine(model_path, n_ctx=n_ctx, n_threads=threads, n_batch=min(n_batch, 128),
-                                    tp_rank=rank, tp_size=size)
+                                    tp_rank=rank, tp_size=size, tensor_split=ts)
         if size > 1:
             from ..parallel.comm import host_collectives
             self.engine.set_comm(*host_collectives())

@@ -8,9 +8,10 @@ api.py:24-28) mapped onto one process per GPU:
     gather it on the GPU - SURVEY K1).
   * ``split_mode="row"`` + ``torch.distributed`` initialised with world size N:
     tensor parallelism over N ranks (one per GPU) - heads and FFN features are
-    sharded, RCCL all-reduces twice per layer over xGMI. ``tensor_split`` must
-    be uniform (ranks are symmetric; uneven ratios are rejected with a clear
-    error rather than silently ignored).
+    sharded, two all-reduces per layer over xGMI (decode: one-shot P2P kernel;
+    prefill: RCCL). ``tensor_split`` weights apportion kv heads / FFN superblocks
+    per rank (llama.cpp proportions; csrc/runtime/shard.h), the vocabulary
+    split stays even (the logit all-gather moves equal counts).
   * ``split_mode="none"/"layer"`` in one process: the model runs on
     ``main_gpu`` (one GPU holds any BASELINE model: 288 GB HBM).
 """
@@ -28,15 +29,16 @@ logger = logging.getLogger(__name__)
 
 
 def _tp_setup(split_mode: str, tensor_split):
-    """(tp_rank, tp_size, device, nccl_id) from torch.distributed (if initialised)."""
-    from ..parallel.comm import broadcast_nccl_id, local_rank, tp_group_info
+    """(tp_rank, tp_size, device, nccl_id, shard weights) from torch.distributed (if initialised)."""
+    from ..parallel.comm import broadcast_nccl_id, check_tensor_split, local_rank, tp_group_info
     local = local_rank()
     if split_mode != "row":
-        return 0, 1, local, b""
+        return 0, 1, local, b"", []
     rank, ws = tp_group_info(tensor_split)
     if ws == 1:
-        return 0, 1, local, b""
-    return rank, ws, local, broadcast_nccl_id(lambda: load_hip().nccl_unique_id())
+        return 0, 1, local, b"", []
+    return (rank, ws, local, broadcast_nccl_id(lambda: load_hip().nccl_unique_id()),
+            check_tensor_split(tensor_split, ws))
 
 
 class HipBackend:
@@ -49,11 +51,12 @@ class HipBackend:
         if 0 <= n_gpu_layers < hparams.n_layer:
             raise ValueError(f"n_gpu_layers={n_gpu_layers} < n_layer={hparams.n_layer}: partial offload runs on "
                              "the hybrid backend (backend='hybrid')")
-        rank, size, local, nccl_id = _tp_setup(split_mode, tensor_split)
+        rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split)
         device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)
         self.tp_rank, self.tp_size = rank, size
         self.engine = hip.Engine(model_path, n_ctx=n_ctx, n_batch=min(n_batch, n_ctx), device=device,
-                                 use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id)
+                                 use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
+                                 tensor_split=ts)
         self.n_ctx = n_ctx
         self.device = device
         if size > 1:

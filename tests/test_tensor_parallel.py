@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, path, tokens, out_dir):
+def _rank_main(rank, world, port, path, tokens, out_dir, split):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -34,13 +34,14 @@ def _rank_main(rank, world, port, path, tokens, out_dir):
     try:
         from llama_fastapi_k8s_gpu_amd.parallel.comm import host_collectives
         cpu = load_cpu()
-        eng = cpu.CpuEngine(path, n_ctx=64, n_threads=2, n_batch=8, tp_rank=rank, tp_size=world)
+        ts = list(split or [])
+        eng = cpu.CpuEngine(path, n_ctx=64, n_threads=2, n_batch=8, tp_rank=rank, tp_size=world, tensor_split=ts)
         eng.set_comm(*host_collectives())
         a = eng.eval_logits(tokens, 0)
         b = eng.eval_logits([5], len(tokens))      # one decode step on top of the prefill
         sp = {"top_k": 40, "top_p": 0.9, "min_p": 0.05, "temperature": 1.2, "repeat_penalty": 1.1,
               "frequency_penalty": 0.7, "presence_penalty": 0.8, "last_n": 64, "seed": 9}
-        eng2 = cpu.CpuEngine(path, n_ctx=64, n_threads=2, n_batch=8, tp_rank=rank, tp_size=world)
+        eng2 = cpu.CpuEngine(path, n_ctx=64, n_threads=2, n_batch=8, tp_rank=rank, tp_size=world, tensor_split=ts)
         eng2.set_comm(*host_collectives())
         g = eng2.generate(tokens, 0, 6, sp, [])
         np.save(os.path.join(out_dir, f"r{rank}_a.npy"), a)
@@ -50,8 +51,13 @@ def _rank_main(rank, world, port, path, tokens, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("model", ["tiny-llama3-tp", "tiny-mixtral-tp"])
-def test_tp2_matches_tp1(tmp_path, model):
+@pytest.mark.parametrize("model,world,split", [
+    ("tiny-llama3-tp", 2, None), ("tiny-mixtral-tp", 2, None),
+    ("tiny-llama3-tp4", 2, [3, 1]),     # llama.cpp tensor_split proportions: 3 of 4 kv heads / FFN superblocks
+    ("tiny-llama3-tp4", 2, [1, 2]),
+    ("tiny-llama3-tp4", 3, None),       # degree not dividing the heads: apportioned 2/1/1
+])
+def test_tp_matches_tp1(tmp_path, model, world, split):
     path = write_synthetic_gguf(model, str(tmp_path / f"{model}.gguf"))
     rng = np.random.default_rng(0)
     tokens = [int(t) for t in rng.integers(3, 400, 12)]
@@ -59,9 +65,9 @@ def test_tp2_matches_tp1(tmp_path, model):
     ref = cpu.CpuEngine(path, n_ctx=64, n_threads=2, n_batch=8)
     want_a = ref.eval_logits(tokens, 0)
     want_b = ref.eval_logits([5], len(tokens))
-    mp.start_processes(_rank_main, args=(2, _free_port(), path, tokens, str(tmp_path)), nprocs=2, join=True,
-                       start_method="spawn")
-    for r in range(2):
+    mp.start_processes(_rank_main, args=(world, _free_port(), path, tokens, str(tmp_path), split), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
         a = np.load(tmp_path / f"r{r}_a.npy")
         b = np.load(tmp_path / f"r{r}_b.npy")
         assert a.shape == want_a.shape
@@ -70,27 +76,33 @@ def test_tp2_matches_tp1(tmp_path, model):
         for got, want in ((a, want_a), (b, want_b)):
             assert np.linalg.norm(got - want) / np.linalg.norm(want) < 5e-3
             assert int(np.argmax(got)) == int(np.argmax(want))
-    # both ranks sample the same tokens (identical gathered logits + shared seed)
-    assert np.array_equal(np.load(tmp_path / "r0_g.npy"), np.load(tmp_path / "r1_g.npy"))
+    # every rank samples the same tokens (identical gathered logits + shared seed)
+    for r in range(1, world):
+        assert np.array_equal(np.load(tmp_path / "r0_g.npy"), np.load(tmp_path / f"r{r}_g.npy"))
 
 
 def test_shard_plan_rejects_bad_degree(tmp_path):
     path = write_synthetic_gguf("tiny-llama3-tp", str(tmp_path / "m.gguf"))
     cpu = load_cpu()
-    with pytest.raises(RuntimeError, match="must divide the head counts"):
+    with pytest.raises(RuntimeError, match="exceeds the kv-head count"):
+        cpu.CpuEngine(path, n_ctx=32, tp_rank=0, tp_size=5)
+    with pytest.raises(RuntimeError, match="superblock-aligned"):   # 4 kv heads of 128 q columns: pairs
         cpu.CpuEngine(path, n_ctx=32, tp_rank=0, tp_size=3)
+    with pytest.raises(RuntimeError, match="entries for"):
+        cpu.CpuEngine(path, n_ctx=32, tp_rank=0, tp_size=2, tensor_split=[1.0, 1.0, 1.0])
     with pytest.raises(RuntimeError, match="set_comm"):
         cpu.CpuEngine(path, n_ctx=32, tp_rank=0, tp_size=2).eval_logits([1, 2], 0)
 
 
-def test_tensor_split_must_be_uniform():
+def test_tensor_split_validation():
     from llama_fastapi_k8s_gpu_amd.parallel.comm import check_tensor_split
-    check_tensor_split(None, 2)
-    check_tensor_split([0.5, 0.5], 2)
-    with pytest.raises(ValueError, match="uniform"):
-        check_tensor_split([0.7, 0.3], 2)
-    with pytest.raises(ValueError, match="uniform"):
+    assert check_tensor_split(None, 2) == []
+    assert check_tensor_split([0.7, 0.3], 2) == [0.7, 0.3]
+    assert check_tensor_split([0.5, 0.5, 0, 0], 2) == [0.5, 0.5]   # trailing unused GPUs
+    with pytest.raises(ValueError, match="positive weight"):
         check_tensor_split([1, 1, 1], 2)
+    with pytest.raises(ValueError, match="positive weight"):
+        check_tensor_split([1, 0, 1], 3)
 
 
 def _serve_rank(rank, world, port, path, out_dir):
