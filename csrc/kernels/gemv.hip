@@ -57,8 +57,21 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   const int kparts = SPLITK ? (nchunks + 64 * U - 1) / (64 * U) : 1;
   const int total = groups * a.n_slots * kparts;
   constexpr int WPB = BLOCK / 64;
-  const int stride = gridDim.x * WPB;
-  int item = blockIdx.x * WPB + wave;
+  // EARLY launches are one block per CU: each block takes a contiguous range of
+  // items so every CU streams the same bytes (a grid-stride walk with 16 waves
+  // per block left the last quarter of the CUs with half the items of the rest).
+  int item, stride, item_end;
+  if constexpr (EARLY) {
+    const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int b0 = min(total, (int)blockIdx.x * per);
+    item = b0 + wave;
+    stride = WPB;
+    item_end = min(total, b0 + per);
+  } else {
+    item = blockIdx.x * WPB + wave;
+    stride = gridDim.x * WPB;
+    item_end = total;
+  }
   RowPtr R[NR];
   int slot = 0, f0 = 0;
   WStream<QT, NR, U> ws;
@@ -87,7 +100,7 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
     if (threadIdx.x == 0) a.out[0] = (float)xq[5] * xs;
     return;
   }
-  while (item < total) {
+  while (item < item_end) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
@@ -95,7 +108,7 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
     else ws.finish_rows(R, nchunks, xq, xd, acc, lane);
     const int cs = slot, cf = f0;
     const int next = item + stride;
-    if (next < total) {
+    if (next < item_end) {
       item_rows<EPI, NR>(a, SPLITK ? next / kparts : next, groups, R, slot, f0);
       if constexpr (SPLITK) kp = next % kparts;
       ws.load(R, kp * 64 * U, nchunks, lane);
