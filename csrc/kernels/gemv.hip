@@ -664,6 +664,8 @@ __global__ __launch_bounds__(256) void gemv_moe_down_kernel(MoeDownArgs a) {
 }
 
 void gemv_moe_down(const MoeDownArgs& a, hipStream_t s) {
+  static const bool splitk = !(getenv("LFK_MOE_SPLITK") && getenv("LFK_MOE_SPLITK")[0] == '0');
+  if (splitk && moe_down_splitk(a, s)) return;
   const int K = a.w.K;
   const size_t lds = (size_t)a.n_slots * (K + (K / 32) * 4) + 64;
   dim3 grid(grid_for((a.w.rows + 1) / 2)), block(256);

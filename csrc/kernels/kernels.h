@@ -94,6 +94,12 @@ struct MoeDownArgs {
   float* out = nullptr;            // [rows]
 };
 void gemv_moe_down(const MoeDownArgs& a, hipStream_t s);
+// split-K form (moe.hip), K-quant / Q8_0 experts; returns false if the shape/type is not covered
+bool moe_down_splitk(const MoeDownArgs& a, hipStream_t s);
+// decode router fused with the routing (F32 router weights, E <= 16): one launch
+bool moe_router_fused_ok(int router_type, int E, int d);
+void moe_router_fused(const float* x, const float* nw, float eps, const float* W, int d, int E, int k, float* logits,
+                      int* ids, float* w, hipStream_t s);
 
 // Router: softmax over n_expert logits, top-k, renormalise -> ids / weights (device).
 void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s);

@@ -8,7 +8,9 @@
 // read their row count and offset from device memory (GemmArgs::rows_dev), so
 // only the rows routed to an expert are multiplied - top-2 of 8 experts costs
 // 2/8 of the dense loop - and no host round trip is needed.
-#include "kernels.h"
+#include <algorithm>
+
+#include "gemv_dev.h"
 
 namespace lfk {
 
@@ -109,6 +111,167 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
                      hipStream_t s) {
   if (T <= 0) return;
   hipLaunchKernelGGL(moe_scatter_add_kernel, dim3(T), dim3(256), 0, s, acc, y, pos, gw, k, d);
+}
+
+// ------------------------------------------------------------------ decode: fused router
+// logits = W_r (F32 [E][d]) . (RMSNorm(x) * w_norm), softmax over E, top-k, renormalise.
+// One block of 1024 threads: replaces the router GEMV launch + the routing launch
+// (two kernel boundaries per MoE layer). The router stays in f32 end to end.
+static constexpr int kRouterMaxE = 16;
+
+__global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __restrict__ x, const float* __restrict__ nw,
+                                                                float eps, const float* __restrict__ W, int d, int E,
+                                                                int k, float* logits, int* ids, float* wout) {
+  __shared__ float red[16][kRouterMaxE + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float ss = 0.f, acc[kRouterMaxE];
+#pragma unroll
+  for (int e = 0; e < kRouterMaxE; ++e) acc[e] = 0.f;
+  for (int i = tid * 4; i < d; i += 4096) {
+    const float4 xv = *reinterpret_cast<const float4*>(x + i);
+    const float4 wv = *reinterpret_cast<const float4*>(nw + i);
+    ss += xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
+    const float4 n = make_float4(xv.x * wv.x, xv.y * wv.y, xv.z * wv.z, xv.w * wv.w);
+#pragma unroll
+    for (int e = 0; e < kRouterMaxE; ++e) {
+      if (e < E) {
+        const float4 r = *reinterpret_cast<const float4*>(W + (size_t)e * d + i);
+        acc[e] += n.x * r.x + n.y * r.y + n.z * r.z + n.w * r.w;
+      }
+    }
+  }
+  ss = wave_sum_fast(ss);
+#pragma unroll
+  for (int e = 0; e < kRouterMaxE; ++e) acc[e] = e < E ? wave_sum_fast(acc[e]) : 0.f;
+  if (lane == 0) {
+    red[wave][kRouterMaxE] = ss;
+#pragma unroll
+    for (int e = 0; e < kRouterMaxE; ++e) red[wave][e] = acc[e];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w][kRouterMaxE];
+  const float sc = rsqrtf(tot / (float)d + eps);
+  float v = -INFINITY;
+  if (lane < E) {
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) sum += red[w][lane];
+    v = sum * sc;
+    if (logits) logits[lane] = v;
+  }
+  // softmax + top-k (lowest index on ties) + renormalise: as moe_route_kernel
+  const float m = wave_max(v);
+  float p = lane < E ? __expf(v - m) : 0.f;
+  p /= wave_sum(p);
+  float taken = lane < E ? p : -1.f, sel_sum = 0.f, my_w = 0.f;
+  int my_id = 0;
+  for (int j = 0; j < k; ++j) {
+    float best = taken;
+    int bi = lane;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == j) { my_id = bi; my_w = best; }
+    sel_sum += best;
+    if (lane == bi) taken = -1.f;
+  }
+  if (lane < k) {
+    ids[lane] = my_id;
+    wout[lane] = my_w / sel_sum;
+  }
+}
+
+bool moe_router_fused_ok(int router_type, int E, int d) {
+  return router_type == T_F32 && E <= kRouterMaxE && E >= 1 && d % 4 == 0;
+}
+
+void moe_router_fused(const float* x, const float* nw, float eps, const float* W, int d, int E, int k, float* logits,
+                      int* ids, float* w, hipStream_t s) {
+  if (E > kRouterMaxE || k > E || d % 4) throw std::runtime_error("moe_router_fused: unsupported shape");
+  hipLaunchKernelGGL(moe_router_fused_kernel, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
+}
+
+// ------------------------------------------------------------------ decode: grouped down, split-K
+// out[r] += sum_s w_s * dot(W_{e_s}[r, :], h_s), as the dense down projection's EARLY
+// split-K GEMV (gemv.hip): one 1024-thread block per CU (LDS request > half the CU),
+// contiguous item ranges, the first weight loads issued before the h prologue's wait.
+// Items = (slot, 64-chunk part, 4-row group), part-major; the two slots' h vectors are
+// quantised as ONE vector of n_slots*K (slot boundaries fall on q8 blocks).
+static constexpr size_t kMoeOnePerCuLds = 80 * 1024 + 256;
+
+template <int QT>
+__global__ __launch_bounds__(1024) void moe_down_splitk_kernel(MoeDownArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NR = 4, WPB = 16;
+  const int K = a.w.K, S = a.n_slots, nch = K >> 5;
+  const int kps = (nch + 63) / 64;
+  const int RG = (a.w.rows + NR - 1) / NR;
+  const int total = RG * S * kps;
+  int8_t* xq = reinterpret_cast<int8_t*>(smem);
+  float* xd = reinterpret_cast<float*>(smem + (size_t)S * K);
+  float* red = xd + (size_t)S * (K >> 5);
+  const int wave = wave_id(), lane = threadIdx.x & 63;
+  const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = min(total, (int)blockIdx.x * per), i1 = min(total, i0 + per);
+  XPrologue<false, 1024> xp;
+  xp.load(a.h, nullptr, S * K);
+  RowPtr R[NR];
+  WStream<QT, NR, 1> ws;
+  int item = i0 + wave, s = 0, kpl = 0, rg = 0;
+  auto locate = [&](int it) {
+    const int p = it / RG;
+    rg = it - p * RG;
+    s = p / kps;
+    kpl = p - s * kps;
+    const uint8_t* base = a.w.base + (size_t)a.expert_ids[s] * a.w.expert_stride;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) R[r] = row_ptr(base, a.w.P, (unsigned)min(rg * NR + r, a.w.rows - 1));
+  };
+  locate(min(item, total - 1));  // unconditional: no control-flow join before the h wait
+  ws.load(R, kpl * 64, nch, lane);
+  xp.finish(a.h, nullptr, 0.f, S * K, xq, xd, red);
+  while (item < i1) {
+    float acc[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] = 0.f;
+    ws.dot(kpl * 64, nch, xq + (size_t)s * K, xd + (size_t)s * (K >> 5), acc, lane);
+    const int cs = s, crg = rg;
+    const int next = item + WPB;
+    if (next < i1) {
+      locate(next);
+      ws.load(R, kpl * 64, nch, lane);
+    }
+    const float wsl = a.expert_w[cs];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc[r] *= wsl;
+    const float v = reduce_rows<NR>(acc, lane);
+    if (lane < NR && crg * NR + lane < a.w.rows) atomicAdd(a.out + crg * NR + lane, v);
+    item = next;
+  }
+}
+
+bool moe_down_splitk(const MoeDownArgs& a, hipStream_t s) {
+  const int K = a.w.K;
+  if (K % 256 || a.n_slots < 1 || a.n_slots * (size_t)K > 64 * 1024) return false;
+  const size_t lds = std::max((size_t)a.n_slots * (K + (K / 32) * 4) + 128, kMoeOnePerCuLds);
+  static int cus = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return c > 0 ? c : 256;
+  }();
+  switch (a.w.type) {
+    case T_Q4_K: hipLaunchKernelGGL(moe_down_splitk_kernel<T_Q4_K>, dim3(cus), dim3(1024), lds, s, a); return true;
+    case T_Q5_K: hipLaunchKernelGGL(moe_down_splitk_kernel<T_Q5_K>, dim3(cus), dim3(1024), lds, s, a); return true;
+    case T_Q6_K: hipLaunchKernelGGL(moe_down_splitk_kernel<T_Q6_K>, dim3(cus), dim3(1024), lds, s, a); return true;
+    case T_Q8_0: hipLaunchKernelGGL(moe_down_splitk_kernel<T_Q8_0>, dim3(cus), dim3(1024), lds, s, a); return true;
+    default: return false;  // F16/F32 experts: the per-slot kernel (gemv.hip)
+  }
 }
 
 }  // namespace lfk

@@ -357,11 +357,16 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   }
 
   if (hp_.n_expert > 0) {
-    GemvArgs ra;
-    ra.w = L.router; ra.x = x_; ra.norm_w = L.ffn_norm; ra.eps = hp_.rms_eps;
-    ra.out = router_logits_; ra.n_out = hp_.n_expert;
-    gemv(ra, EPI_STORE, s);
-    moe_route(router_logits_, hp_.n_expert, hp_.n_expert_used, moe_ids_, moe_w_, s);
+    if (moe_router_fused_ok(L.router.type, hp_.n_expert, d)) {  // one launch: norm + f32 router + top-k
+      moe_router_fused(x_, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, hp_.n_expert,
+                       hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, s);
+    } else {
+      GemvArgs ra;
+      ra.w = L.router; ra.x = x_; ra.norm_w = L.ffn_norm; ra.eps = hp_.rms_eps;
+      ra.out = router_logits_; ra.n_out = hp_.n_expert;
+      gemv(ra, EPI_STORE, s);
+      moe_route(router_logits_, hp_.n_expert, hp_.n_expert_used, moe_ids_, moe_w_, s);
+    }
     GemvArgs g;
     g.w = L.gu_exps; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
     g.out = hf_; g.n_out = F_l_; g.n_slots = hp_.n_expert_used; g.expert_ids = moe_ids_; g.out_slot_stride = F_l_;
