@@ -119,40 +119,42 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 // (two kernel boundaries per MoE layer). The router stays in f32 end to end.
 static constexpr int kRouterMaxE = 16;
 
+template <int EM>
 __global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __restrict__ x, const float* __restrict__ nw,
                                                                 float eps, const float* __restrict__ W, int d, int E,
                                                                 int k, float* logits, int* ids, float* wout) {
-  __shared__ float red[16][kRouterMaxE + 1];
+  __shared__ float red[16][EM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  float ss = 0.f, acc[kRouterMaxE];
+  float ss = 0.f, acc[EM];
 #pragma unroll
-  for (int e = 0; e < kRouterMaxE; ++e) acc[e] = 0.f;
+  for (int e = 0; e < EM; ++e) acc[e] = 0.f;
   for (int i = tid * 4; i < d; i += 4096) {
     const float4 xv = *reinterpret_cast<const float4*>(x + i);
     const float4 wv = *reinterpret_cast<const float4*>(nw + i);
     ss += xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
     const float4 n = make_float4(xv.x * wv.x, xv.y * wv.y, xv.z * wv.z, xv.w * wv.w);
+    // every row load unconditional (clamped row, result masked): a load under a
+    // runtime `e < E` branch makes hipcc drain vmcnt per row (E dependent round trips)
+    float4 r[EM];
 #pragma unroll
-    for (int e = 0; e < kRouterMaxE; ++e) {
-      if (e < E) {
-        const float4 r = *reinterpret_cast<const float4*>(W + (size_t)e * d + i);
-        acc[e] += n.x * r.x + n.y * r.y + n.z * r.z + n.w * r.w;
-      }
-    }
+    for (int e = 0; e < EM; ++e) r[e] = *reinterpret_cast<const float4*>(W + (size_t)min(e, E - 1) * d + i);
+#pragma unroll
+    for (int e = 0; e < EM; ++e)
+      acc[e] += e < E ? n.x * r[e].x + n.y * r[e].y + n.z * r[e].z + n.w * r[e].w : 0.f;
   }
   ss = wave_sum_fast(ss);
 #pragma unroll
-  for (int e = 0; e < kRouterMaxE; ++e) acc[e] = e < E ? wave_sum_fast(acc[e]) : 0.f;
+  for (int e = 0; e < EM; ++e) acc[e] = e < E ? wave_sum_fast(acc[e]) : 0.f;
   if (lane == 0) {
-    red[wave][kRouterMaxE] = ss;
+    red[wave][EM] = ss;
 #pragma unroll
-    for (int e = 0; e < kRouterMaxE; ++e) red[wave][e] = acc[e];
+    for (int e = 0; e < EM; ++e) red[wave][e] = acc[e];
   }
   __syncthreads();
   if (wave != 0) return;
   float tot = 0.f;
 #pragma unroll
-  for (int w = 0; w < 16; ++w) tot += red[w][kRouterMaxE];
+  for (int w = 0; w < 16; ++w) tot += red[w][EM];
   const float sc = rsqrtf(tot / (float)d + eps);
   float v = -INFINITY;
   if (lane < E) {
@@ -193,7 +195,10 @@ bool moe_router_fused_ok(int router_type, int E, int d) {
 void moe_router_fused(const float* x, const float* nw, float eps, const float* W, int d, int E, int k, float* logits,
                       int* ids, float* w, hipStream_t s) {
   if (E > kRouterMaxE || k > E || d % 4) throw std::runtime_error("moe_router_fused: unsupported shape");
-  hipLaunchKernelGGL(moe_router_fused_kernel, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
+  if (E <= 8)  // rows padded to EM are loaded (clamped) and masked: size EM to the expert count
+    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
+  else
+    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
 }
 
 // ------------------------------------------------------------------ decode: grouped down, split-K
