@@ -49,7 +49,7 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
 // DB: double-buffered LDS (55 KB, 2 blocks/CU) for grids that fit the chip;
 // single-buffered (27 KB, up to 5 blocks/CU, one extra barrier per step) for
 // large grids where more resident blocks hide more latency.
-template <int QT, int EPI, bool DB>
+template <int QT, int EPI, bool DB, int D = 3>
 __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned short Xs[DB ? 2 : 1][BM * PITCH];
   __shared__ __attribute__((aligned(16))) unsigned short Ws[DB ? 2 : 1][BN * PITCH];
@@ -76,58 +76,70 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   const bool wvalid = n0 + wrow < N;
   const size_t wr = (size_t)min(n0 + wrow, N - 1);
   const unsigned short* xg = reinterpret_cast<const unsigned short*>(a.x);
-  uint4 xr[2];
-  DqRaw<QT> raw;
-  auto load_step = [&](int k) {
-    const int k0 = k * BK;
+  // D-deep register prefetch ring: the global loads of step k+D go out at the start
+  // of step k, so one step's load latency (~1-2 us under load) is spread over D
+  // steps of MFMA work (with one stage in flight every K step was latency-bound).
+  // Every load is unconditional (step and token row clamped, rows past T zeroed by
+  // a select after the load): a load under a runtime branch makes hipcc drain vmcnt
+  // at the join, which would serialise the ring.
+  uint4 xr[D][2];
+  DqRaw<QT> raw[D];
+  auto load_step = [&](int k, int st) {
+    const int k0 = min(k, ke - 1) * BK;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, c = idx & 7;
-      xr[i] = make_uint4(0, 0, 0, 0);
-      if (m0 + r < T) xr[i] = *reinterpret_cast<const uint4*>(xg + (size_t)(m0 + r) * K + k0 + 8 * c);
+      xr[st][i] = *reinterpret_cast<const uint4*>(xg + (size_t)min(m0 + r, T - 1) * K + k0 + 8 * c);
     }
-    dq_load<QT>(raw, a.w.base, a.w.P, wr, (k0 >> 5) + whalf);
+    dq_load<QT>(raw[st], a.w.base, a.w.P, wr, (k0 >> 5) + whalf);
   };
-  auto store_step = [&](int k, int buf) {
+  auto store_step = [&](int k, int st, int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(&Xs[buf][r * PITCH + 8 * c]) = xr[i];
+      *reinterpret_cast<uint4*>(&Xs[buf][r * PITCH + 8 * c]) = (m0 + r < T) ? xr[st][i] : make_uint4(0, 0, 0, 0);
     }
     float w[32];
-    dq_decode<QT>(raw, ((k * BK) >> 5) + whalf, w);
+    dq_decode<QT>(raw[st], ((k * BK) >> 5) + whalf, w);
     uint4* dst = reinterpret_cast<uint4*>(&Ws[buf][wrow * PITCH + 32 * whalf]);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[i] = wvalid ? pack_bf16x8(w + 8 * i) : make_uint4(0, 0, 0, 0);
   };
   if (kb < ke) {
-    load_step(kb);
-    store_step(kb, 0);
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_step(kb + j, j);
+    store_step(kb, 0, 0);
   }
   __syncthreads();
   const int lr = lane & 31, lk = 8 * (lane >> 5);
-  for (int k = kb; k < ke; ++k) {
-    const int buf = DB ? ((k - kb) & 1) : 0;
-    const bool more = k + 1 < ke;
-    if (more) load_step(k + 1);
+  for (int k0 = kb; k0 < ke; k0 += D) {
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 16) {
-      const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&Ws[buf][(32 * wave + lr) * PITCH + kk + lk]);
+    for (int j = 0; j < D; ++j) {
+      const int k = k0 + j;
+      load_step(k + D, j);  // stage j held step k, already in LDS: refill it (clamped past ke)
+      if (k < ke) {
+        const int buf = DB ? ((k - kb) & 1) : 0;
+        const bool more = k + 1 < ke;
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const bf16x8 xv = *reinterpret_cast<const bf16x8*>(&Xs[buf][(32 * m + lr) * PITCH + kk + lk]);
-        acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xv, bw, acc[m], 0, 0, 0);
+        for (int kk = 0; kk < BK; kk += 16) {
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&Ws[buf][(32 * wave + lr) * PITCH + kk + lk]);
+#pragma unroll
+          for (int m = 0; m < 2; ++m) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(&Xs[buf][(32 * m + lr) * PITCH + kk + lk]);
+            acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xv, bw, acc[m], 0, 0, 0);
+          }
+        }
+        if constexpr (DB) {
+          if (more) store_step(k + 1, (j + 1) % D, buf ^ 1);
+          __syncthreads();
+        } else {
+          __syncthreads();  // every wave is done reading the single buffer
+          if (more) store_step(k + 1, (j + 1) % D, 0);
+          __syncthreads();
+        }
       }
-    }
-    if constexpr (DB) {
-      if (more) store_step(k + 1, buf ^ 1);
-      __syncthreads();
-    } else {
-      __syncthreads();  // every wave is done reading the single buffer
-      if (more) store_step(k + 1, 0);
-      __syncthreads();
     }
   }
 
