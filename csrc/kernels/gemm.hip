@@ -49,12 +49,18 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
 // DB: double-buffered LDS (55 KB, 2 blocks/CU) for grids that fit the chip;
 // single-buffered (27 KB, up to 5 blocks/CU, one extra barrier per step) for
 // large grids where more resident blocks hide more latency.
-template <int QT, int EPI, bool DB, int D = 3>
+// BMT: tokens per tile (64, or 128 for longer prompts: twice the MFMA work per
+// decoded weight tile - the PMC profile showed 27 VALU instructions per MFMA at 64,
+// the kernel VALU-bound on the weight decode).
+template <int QT, int EPI, bool DB, int D = 3, int BMT = BM>
 __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned short Xs[DB ? 2 : 1][BM * PITCH];
-  __shared__ __attribute__((aligned(16))) unsigned short Ws[DB ? 2 : 1][BN * PITCH];
+  constexpr int NBUF = DB ? 2 : 1, MT = BMT / 32, XL = BMT / 32;  // XL: 16-B X loads per thread per step
+  // one LDS array (Xs buffers, then Ws buffers): the SwiGLU epilogue reuses it whole
+  __shared__ __attribute__((aligned(16))) unsigned short lds[NBUF * (BMT + BN) * PITCH];
+  auto Xs = [&](int b) { return lds + b * BMT * PITCH; };
+  auto Ws = [&](int b) { return lds + NBUF * BMT * PITCH + b * BN * PITCH; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BMT;
   if (a.seg_dev) {  // grouped form: this expert's rows of the gathered buffers
     const int r0 = a.seg_dev[0];
     a.T = a.seg_dev[1] - r0;
@@ -66,9 +72,9 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   const int N = a.w.rows, K = a.w.K, T = a.T;
   const int nk = K / BK, ks = (nk + gridDim.z - 1) / gridDim.z;
   const int kb = blockIdx.z * ks, ke = min(nk, kb + ks);
-  f32x16 acc[2];
+  f32x16 acc[MT];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 
@@ -82,12 +88,12 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   // Every load is unconditional (step and token row clamped, rows past T zeroed by
   // a select after the load): a load under a runtime branch makes hipcc drain vmcnt
   // at the join, which would serialise the ring.
-  uint4 xr[D][2];
+  uint4 xr[D][XL];
   DqRaw<QT> raw[D];
   auto load_step = [&](int k, int st) {
     const int k0 = min(k, ke - 1) * BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < XL; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, c = idx & 7;
       xr[st][i] = *reinterpret_cast<const uint4*>(xg + (size_t)min(m0 + r, T - 1) * K + k0 + 8 * c);
@@ -96,14 +102,14 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   };
   auto store_step = [&](int k, int st, int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < XL; ++i) {
       const int idx = tid + 256 * i;
       const int r = idx >> 3, c = idx & 7;
-      *reinterpret_cast<uint4*>(&Xs[buf][r * PITCH + 8 * c]) = (m0 + r < T) ? xr[st][i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(Xs(buf) + r * PITCH + 8 * c) = (m0 + r < T) ? xr[st][i] : make_uint4(0, 0, 0, 0);
     }
     float w[32];
     dq_decode<QT>(raw[st], ((k * BK) >> 5) + whalf, w);
-    uint4* dst = reinterpret_cast<uint4*>(&Ws[buf][wrow * PITCH + 32 * whalf]);
+    uint4* dst = reinterpret_cast<uint4*>(Ws(buf) + wrow * PITCH + 32 * whalf);
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[i] = wvalid ? pack_bf16x8(w + 8 * i) : make_uint4(0, 0, 0, 0);
   };
@@ -124,10 +130,10 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
         const bool more = k + 1 < ke;
 #pragma unroll
         for (int kk = 0; kk < BK; kk += 16) {
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(&Ws[buf][(32 * wave + lr) * PITCH + kk + lk]);
+          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(Ws(buf) + (32 * wave + lr) * PITCH + kk + lk);
 #pragma unroll
-          for (int m = 0; m < 2; ++m) {
-            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(&Xs[buf][(32 * m + lr) * PITCH + kk + lk]);
+          for (int m = 0; m < MT; ++m) {
+            const bf16x8 xv = *reinterpret_cast<const bf16x8*>(Xs(buf) + (32 * m + lr) * PITCH + kk + lk);
             acc[m] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xv, bw, acc[m], 0, 0, 0);
           }
         }
@@ -146,25 +152,28 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   // ---- epilogue. acc[m][r]: token = 32m + (r&3) + 8(r>>2) + 4(lane>>5), col = 32*wave + (lane&31)
   const int col = n0 + 32 * wave + (lane & 31);
   if constexpr (EPI == GEMM_SWIGLU) {
-    float* ex = reinterpret_cast<float*>(&Ws[0][0]);  // 2 odd waves x 2 x 16 x 64 floats = 16 KiB (fits Ws)
+    // 2 odd waves x MT x 16 x 64 floats (16 KiB at BMT 64, 32 KiB at 128) in the whole LDS array
+    static_assert(2 * MT * 16 * 64 * 4 <= NBUF * (BMT + BN) * PITCH * 2, "SwiGLU exchange does not fit");
+    float* ex = reinterpret_cast<float*>(lds);
+    __syncthreads();  // the last K step's MFMA reads of the tiles are done
     if (wave & 1) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ex[(((wave >> 1) * 2 + m) * 16 + r) * 64 + lane] = acc[m][r];
+        for (int r = 0; r < 16; ++r) ex[(((wave >> 1) * MT + m) * 16 + r) * 64 + lane] = acc[m][r];
     }
     __syncthreads();
     if (!(wave & 1)) {
       const int feat = ((n0 + 32 * wave) >> 6) * 32 + (lane & 31);
       const int F = N >> 1;
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int t = m0 + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
           if (t < T && feat < F) {
             const float g = acc[m][r];
-            const float u = ex[(((wave >> 1) * 2 + m) * 16 + r) * 64 + lane];
+            const float u = ex[(((wave >> 1) * MT + m) * 16 + r) * 64 + lane];
             a.out_bf16[(size_t)t * F + feat] = __float2bfloat16(g / (1.f + __expf(-g)) * u);
           }
         }
@@ -172,7 +181,7 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   } else {
     if (col < N) {
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int t = m0 + 32 * m + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
@@ -193,10 +202,10 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   }
 }
 
-template <int QT>
-static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
+template <int QT, int BMT>
+static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
   const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
-  const int tiles = ((a.w.rows + BN - 1) / BN) * ((rows + BM - 1) / BM);
+  const int tiles = ((a.w.rows + BN - 1) / BN) * ((rows + BMT - 1) / BMT);
   const int nk = a.w.K / BK;
   // split K until ~2 blocks per CU are busy, keeping >= 8 K steps per split
   int split = 1;
@@ -207,13 +216,13 @@ static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
     const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
     if (e != hipSuccess) throw std::runtime_error("gemm_dq: memset failed");
   }
-  dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BM - 1) / BM, split), block(256);
+  dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BMT - 1) / BMT, split), block(256);
   const bool db = tiles * split <= 512;
   if (a.seg_dev && split > 1 && epi != GEMM_STORE) throw std::runtime_error("gemm_dq: grouped split-K needs STORE");
-#define LFK_GEMM_LAUNCH(E)                                                   \
-  do {                                                                        \
-    if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true>), grid, block, 0, s, a);  \
-    else hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false>), grid, block, 0, s, a);    \
+#define LFK_GEMM_LAUNCH(E)                                                                   \
+  do {                                                                                        \
+    if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true, 3, BMT>), grid, block, 0, s, a);  \
+    else hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false, 3, BMT>), grid, block, 0, s, a);    \
   } while (0)
   switch (epi) {
     case GEMM_STORE: LFK_GEMM_LAUNCH(GEMM_STORE); break;
@@ -222,6 +231,16 @@ static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
     default: throw std::runtime_error("gemm_dq: bad epilogue");
   }
 #undef LFK_GEMM_LAUNCH
+}
+
+// 128-token tiles once a prompt chunk (or an expert's expected rows) exceeds 64 tokens
+template <int QT>
+static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
+  static const int force = getenv("LFK_GEMM_BM") ? atoi(getenv("LFK_GEMM_BM")) : 0;
+  const int rows = a.seg_dev ? (a.rows_hint > 0 ? a.rows_hint : a.T) : a.T;
+  const bool big = force ? force >= 128 : rows > 64;
+  if (big) launch_gemm_t<QT, 128>(a, epi, s);
+  else launch_gemm_t<QT, 64>(a, epi, s);
 }
 
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s) {

@@ -225,7 +225,7 @@ def test_attn_prefill(torch, hd, T, pos0):
 
 
 @pytest.mark.parametrize("t", QTYPES)
-@pytest.mark.parametrize("T,N,K", [(1, 128, 256), (33, 256, 512), (130, 384, 1024)])
+@pytest.mark.parametrize("T,N,K", [(1, 128, 256), (33, 256, 512), (130, 384, 1024), (300, 256, 2048)])
 def test_gemm_mfma(torch, t, T, N, K):
     rng = np.random.default_rng(T * N + int(t))
     raw, W = make_matrix(t, N, K, rng)
@@ -245,9 +245,10 @@ def test_gemm_mfma(torch, t, T, N, K):
     assert rel_err((acc - base).cpu().numpy(), ref.numpy()) < 5e-3
 
 
-def test_gemm_swiglu(torch):
+@pytest.mark.parametrize("T", [40, 70, 200])   # 64-token tiles, and 128-token tiles (one / two, partial)
+def test_gemm_swiglu(torch, T):
     rng = np.random.default_rng(11)
-    F, K, T = 128, 512, 70
+    F, K = 128, 512
     t = GGMLType.Q4_K
     rg, Wg = make_matrix(t, F, K, rng)
     ru, Wu = make_matrix(t, F, K, rng)
