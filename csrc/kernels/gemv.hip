@@ -459,8 +459,19 @@ __device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, 
   const int nchunks = a.K >> 5;
   const int hd = a.head_dim;
   constexpr int WPB = BLOCK / 64;
-  const int stride = nblk * WPB;
-  int item = blk * WPB + wave;
+  // one-CU blocks (BLOCK 1024): contiguous per-block item ranges (equal bytes per CU)
+  int stride, item, item_end;
+  if constexpr (BLOCK == 1024) {
+    const int per = (total + nblk - 1) / nblk;
+    const int b0 = min(total, blk * per);
+    item = b0 + wave;
+    stride = WPB;
+    item_end = min(total, b0 + per);
+  } else {
+    stride = nblk * WPB;
+    item = blk * WPB + wave;
+    item_end = total;
+  }
   RowPtr R[NR];
   int si = s_lo, r0 = 0;
   WStream<QT, NR, U> ws;
@@ -472,7 +483,7 @@ __device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, 
     if (lane < NR && a.seg[si].kind < 2) cs = rope_of(r0 + lane);
   }
   const float xs = xp.finish(a.x, a.norm_w, a.eps, a.K, xq, xd, red);
-  while (item < total) {
+  while (item < item_end) {
     float acc[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) acc[r] = 0.f;
@@ -480,7 +491,7 @@ __device__ __forceinline__ void qkv_run(const QkvLaunch& a, int s_lo, int s_hi, 
     const int csi = si, cr0 = r0;
     const float2 ccs = cs;
     const int next = item + stride;
-    if (next < total) {
+    if (next < item_end) {
       qkv_item<QT, NR>(a, s_lo, s_hi, next, R, si, r0);
       ws.load(R, 0, nchunks, lane);
       if (lane < NR && a.seg[si].kind < 2) cs = rope_of(r0 + lane);
