@@ -22,7 +22,7 @@ static constexpr int kMaxBlocks = 1024;  // 256 CUs x 4
 template <bool NORM, int BLOCK = 256>
 struct XPrologue {
   static constexpr int NB = 4;
-  static constexpr int SHIFT = (BLOCK == 1024) ? 12 : 10;  // log2(BLOCK * 4 floats per batch slot)
+  static constexpr int SHIFT = (BLOCK == 1024) ? 12 : (BLOCK == 512 ? 11 : 10);  // log2(BLOCK * 4 floats per slot)
   float4 v[NB], w[NB];
   __device__ __forceinline__ void load_batch(const float* __restrict__ x, const float* __restrict__ nw, int K, int j0) {
     const int tid = threadIdx.x;
