@@ -218,11 +218,11 @@ static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
 // (> half of the 160 KiB), so the grid is exactly one block per CU.
 static constexpr size_t kOnePerCuLds = 80 * 1024 + 256;
 // classes (bit mask, env LFK_GEMV_EARLY overrides the default)
-enum EarlyCls : int { EC_SWIGLU = 1, EC_SPLITK_LONG = 2, EC_SPLITK = 4, EC_STORE = 8, EC_QKV = 16 };
+enum EarlyCls : int { EC_SWIGLU = 1, EC_SPLITK_LONG = 2, EC_SPLITK = 4, EC_STORE = 8, EC_QKV = 16, EC_QKV_LONG = 32 };
 static bool gemv_early(int cls) {
   static const int mask = [] {
     const char* e = getenv("LFK_GEMV_EARLY");
-    return e ? atoi(e) : (EC_SWIGLU | EC_SPLITK_LONG);  // measured in-situ (decode step) on MI355X
+    return e ? atoi(e) : (EC_SWIGLU | EC_SPLITK_LONG | EC_QKV_LONG);  // measured in-situ (decode step) on MI355X
   }();
   return (mask & cls) != 0;
 }
@@ -543,7 +543,7 @@ static void launch_qkv1(QkvLaunch L, int rows, hipStream_t s) {
   L.blocks0 = 0;
   LFK_NRU_DISPATCH(c.nr, c.u, ({
     if constexpr (NR >= 2 && NR * U <= 4) {
-      if (gemv_early(EC_QKV)) {
+      if (gemv_early(L.K > 4096 ? EC_QKV_LONG : EC_QKV)) {
         auto k = gemv_qkv_kernel<QT, NR, U, QT, NR, U, false, 1024>;
         const size_t l = std::max(lds, kOnePerCuLds);
         hipLaunchKernelGGL(k, gemv_grid(k, l, rows / NR, 1024), dim3(1024), l, s, L);
@@ -565,7 +565,7 @@ template <int QT0, int QT1>
 static void launch_qkv2(QkvLaunch L, int rows0, int rows1, hipStream_t s) {
   const double b0 = (double)qbytes(QT0, rows0, L.K), b1 = (double)qbytes(QT1, rows1, L.K);
   const int items = rows0 / 2 + rows1 / 2;
-  if (gemv_early(EC_QKV)) {
+  if (gemv_early(L.K > 4096 ? EC_QKV_LONG : EC_QKV)) {
     auto k = gemv_qkv_kernel<QT0, 2, 2, QT1, 2, 1, true, 1024>;
     const size_t l = std::max(qkv_lds(L.K), kOnePerCuLds);
     const int nb = (int)gemv_grid(k, l, items, 1024).x;

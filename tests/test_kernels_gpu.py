@@ -132,9 +132,10 @@ def test_moe_route(torch):
                                       (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0),
                                       (GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q4_K),   # one run
                                       (GGMLType.Q6_K, GGMLType.Q4_K, GGMLType.Q6_K)])  # three runs: per-segment
-def test_gemv_qkv_rope_kvstore(torch, tq, tk, tv):
+@pytest.mark.parametrize("K", [512, 8192])   # 8192: the one-CU launch path (K > 4096, 70B)
+def test_gemv_qkv_rope_kvstore(torch, tq, tk, tv, K):
     rng = np.random.default_rng(10)
-    K, hd, nh, nkv, n_ctx, pos = 512, 64, 8, 2, 32, 5
+    hd, nh, nkv, n_ctx, pos = 64, 8, 2, 32, 5
     (rq, Wq), (rk, Wk), (rv, Wv) = make_matrix(tq, nh * hd, K, rng), make_matrix(tk, nkv * hd, K, rng), \
         make_matrix(tv, nkv * hd, K, rng)
     dq, dk, dv = (dev_bytes(to_planar(t, r, R, K)) for t, r, R in ((tq, rq, nh * hd), (tk, rk, nkv * hd), (tv, rv, nkv * hd)))
