@@ -28,17 +28,21 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 static constexpr int BM = 64, BN = 128, BK = 64, PITCH = BK + 8;  // bf16 elements
 
-__device__ __forceinline__ unsigned short f2bf(float f) {
-  __hip_bfloat16 b = __float2bfloat16(f);
-  return *reinterpret_cast<unsigned short*>(&b);
+// two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even); the scalar
+// __float2bfloat16 form costs a conversion per value plus the shift/or to pack
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
+  const f32x2_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
 }
 
 __device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
   uint4 p;
-  p.x = f2bf(w[0]) | ((unsigned)f2bf(w[1]) << 16);
-  p.y = f2bf(w[2]) | ((unsigned)f2bf(w[3]) << 16);
-  p.z = f2bf(w[4]) | ((unsigned)f2bf(w[5]) << 16);
-  p.w = f2bf(w[6]) | ((unsigned)f2bf(w[7]) << 16);
+  p.x = pk_bf16(w[0], w[1]);
+  p.y = pk_bf16(w[2], w[3]);
+  p.z = pk_bf16(w[4], w[5]);
+  p.w = pk_bf16(w[6], w[7]);
   return p;
 }
 
