@@ -273,14 +273,17 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0);
   m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
   m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
-                           int hd, float scale, uintptr_t out, uintptr_t stream) {
+                           int hd, float scale, uintptr_t out, uintptr_t stream, bool out_bf16) {
     AttnPrefillArgs a;
     a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.T = T; a.pos0 = pos0;
     a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
-    a.out = P<float>(out); a.out_stride = n_head * hd;
+    if (out_bf16) a.out_bf16 = P<__hip_bfloat16>(out);
+    else a.out = P<float>(out);
+    a.out_stride = n_head * hd;
     attn_prefill(a, S(stream));
     hip_ok("attn_prefill");
-  });
+  }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("T"), py::arg("pos0"), py::arg("n_ctx"), py::arg("n_head"),
+     py::arg("n_kv"), py::arg("hd"), py::arg("scale"), py::arg("out"), py::arg("stream"), py::arg("out_bf16") = false);
   m.def("embed", [](uintptr_t w, int type, int V, int d, uintptr_t tokens, int T, uintptr_t x, uintptr_t stream) {
     embed_rows(make_qmat(P<void>(w), type, V, d), P<int>(tokens), T, P<float>(x), S(stream));
     hip_ok("embed");

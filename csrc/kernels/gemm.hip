@@ -28,21 +28,12 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 static constexpr int BM = 64, BN = 128, BK = 64, PITCH = BK + 8;  // bf16 elements
 
-// two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even); the scalar
-// __float2bfloat16 form costs a conversion per value plus the shift/or to pack
-typedef float f32x2_t __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ unsigned pk_bf16(float a, float b) {
-  const f32x2_t v = {a, b};
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
-}
-
 __device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
   uint4 p;
-  p.x = pk_bf16(w[0], w[1]);
-  p.y = pk_bf16(w[2], w[3]);
-  p.z = pk_bf16(w[4], w[5]);
-  p.w = pk_bf16(w[6], w[7]);
+  p.x = pk_bf16_pair(w[0], w[1]);
+  p.y = pk_bf16_pair(w[2], w[3]);
+  p.z = pk_bf16_pair(w[4], w[5]);
+  p.w = pk_bf16_pair(w[6], w[7]);
   return p;
 }
 
@@ -221,12 +212,14 @@ static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
     if (e != hipSuccess) throw std::runtime_error("gemm_dq: memset failed");
   }
   dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BMT - 1) / BMT, split), block(256);
-  const bool db = tiles * split <= 512;
+  // 256-token tiles are always double-buffered (110 KB of LDS, one block per CU)
+  const bool db = BMT == 256 || tiles * split <= 512;
   if (a.seg_dev && split > 1 && epi != GEMM_STORE) throw std::runtime_error("gemm_dq: grouped split-K needs STORE");
 #define LFK_GEMM_LAUNCH(E)                                                                   \
   do {                                                                                        \
     if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true, 3, BMT>), grid, block, 0, s, a);  \
-    else hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false, 3, BMT>), grid, block, 0, s, a);    \
+    else if constexpr (BMT < 256)                                                             \
+      hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false, 3, BMT>), grid, block, 0, s, a);       \
   } while (0)
   switch (epi) {
     case GEMM_STORE: LFK_GEMM_LAUNCH(GEMM_STORE); break;
@@ -242,8 +235,9 @@ template <int QT>
 static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
   static const int force = getenv("LFK_GEMM_BM") ? atoi(getenv("LFK_GEMM_BM")) : 0;
   const int rows = a.seg_dev ? (a.rows_hint > 0 ? a.rows_hint : a.T) : a.T;
-  const bool big = force ? force >= 128 : rows > 64;
-  if (big) launch_gemm_t<QT, 128>(a, epi, s);
+  const int bm = force ? force : (rows > 64 ? 128 : 64);
+  if (bm >= 256) launch_gemm_t<QT, 256>(a, epi, s);
+  else if (bm >= 128) launch_gemm_t<QT, 128>(a, epi, s);
   else launch_gemm_t<QT, 64>(a, epi, s);
 }
 

@@ -148,7 +148,8 @@ struct AttnPrefillArgs {
   const __half* v_cache = nullptr;
   int T = 0, pos0 = 0, n_ctx = 0, n_head = 0, n_kv_head = 0, head_dim = 0;
   float scale = 1.f;
-  float* out = nullptr;           // [T][n_head][hd]
+  float* out = nullptr;           // [T][n_head][hd] f32, or
+  __hip_bfloat16* out_bf16 = nullptr;  // bf16 (the Wo GEMM's input; MFMA path only)
   int out_stride = 0;
 };
 void attn_prefill(const AttnPrefillArgs& a, hipStream_t s);

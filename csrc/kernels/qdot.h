@@ -20,6 +20,15 @@
 
 namespace lfk {
 
+// two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (round to nearest even); the scalar
+// __float2bfloat16 form costs a conversion per value plus the shift/or to pack
+typedef float f32x2_pk_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_pk_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned pk_bf16_pair(float a, float b) {
+  const f32x2_pk_t v = {a, b};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_pk_t));
+}
+
 __device__ __forceinline__ float h2f(unsigned short h) {
   return __half2float(__ushort_as_half(h));
 }

@@ -455,9 +455,8 @@ void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
     AttnPrefillArgs pa;
     pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
     pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
-    pa.out = attn_; pa.out_stride = nq_;
+    pa.out_bf16 = attnb_; pa.out_stride = nq_;  // bf16 straight into the Wo GEMM's input
     attn_prefill(pa, s);
-    to_bf16(attn_, T * nq_, attnb_, s);
     GemmArgs o;
     o.w = L.wo; o.x = attnb_; o.T = T; o.ldo = d;
     if (!tp) {
