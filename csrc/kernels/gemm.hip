@@ -47,15 +47,16 @@ __device__ __forceinline__ uint4 pack_bf16x8(const float* w) {
 // BMT: tokens per tile (64, or 128 for longer prompts: twice the MFMA work per
 // decoded weight tile - the PMC profile showed 27 VALU instructions per MFMA at 64,
 // the kernel VALU-bound on the weight decode).
-template <int QT, int EPI, bool DB, int D = 3, int BMT = BM>
-__global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
-  constexpr int NBUF = DB ? 2 : 1, MT = BMT / 32, XL = BMT / 32;  // XL: 16-B X loads per thread per step
+template <int QT, int EPI, bool DB, int D = 3, int BMT = BM, int BNT = BN>
+__global__ __launch_bounds__(2 * BNT) void gemm_dq_kernel(GemmArgs a) {
+  constexpr int NT = 2 * BNT;  // threads: 2 per weight row of the tile, wave w owns rows 32w..32w+31
+  constexpr int NBUF = DB ? 2 : 1, MT = BMT / 32, XL = BMT * 8 / NT;  // XL: 16-B X loads per thread per step
   // one LDS array (Xs buffers, then Ws buffers): the SwiGLU epilogue reuses it whole
-  __shared__ __attribute__((aligned(16))) unsigned short lds[NBUF * (BMT + BN) * PITCH];
+  __shared__ __attribute__((aligned(16))) unsigned short lds[NBUF * (BMT + BNT) * PITCH];
   auto Xs = [&](int b) { return lds + b * BMT * PITCH; };
-  auto Ws = [&](int b) { return lds + NBUF * BMT * PITCH + b * BN * PITCH; };
+  auto Ws = [&](int b) { return lds + NBUF * BMT * PITCH + b * BNT * PITCH; };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BMT;
+  const int n0 = blockIdx.x * BNT, m0 = blockIdx.y * BMT;
   if (a.seg_dev) {  // grouped form: this expert's rows of the gathered buffers
     const int r0 = a.seg_dev[0];
     a.T = a.seg_dev[1] - r0;
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
     for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
 
   const int wrow = tid >> 1, whalf = tid & 1;
-  const bool wvalid = n0 + wrow < N;
+  const unsigned wmask = n0 + wrow < N ? ~0u : 0u;
   const size_t wr = (size_t)min(n0 + wrow, N - 1);
   const unsigned short* xg = reinterpret_cast<const unsigned short*>(a.x);
   // D-deep register prefetch ring: the global loads of step k+D go out at the start
@@ -89,7 +90,7 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
     const int k0 = min(k, ke - 1) * BK;
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int r = idx >> 3, c = idx & 7;
       xr[st][i] = *reinterpret_cast<const uint4*>(xg + (size_t)min(m0 + r, T - 1) * K + k0 + 8 * c);
     }
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   auto store_step = [&](int k, int st, int buf) {
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int r = idx >> 3, c = idx & 7;
       *reinterpret_cast<uint4*>(Xs(buf) + r * PITCH + 8 * c) = (m0 + r < T) ? xr[st][i] : make_uint4(0, 0, 0, 0);
     }
@@ -106,7 +107,10 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
     dq_decode<QT>(raw[st], ((k * BK) >> 5) + whalf, w);
     uint4* dst = reinterpret_cast<uint4*>(Ws(buf) + wrow * PITCH + 32 * whalf);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dst[i] = wvalid ? pack_bf16x8(w + 8 * i) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {  // rows past N: AND with 0 (a select here compiles to a branch)
+      const uint4 p = pack_bf16x8(w + 8 * i);
+      dst[i] = make_uint4(p.x & wmask, p.y & wmask, p.z & wmask, p.w & wmask);
+    }
   };
   if (kb < ke) {
 #pragma unroll
@@ -147,8 +151,8 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   // ---- epilogue. acc[m][r]: token = 32m + (r&3) + 8(r>>2) + 4(lane>>5), col = 32*wave + (lane&31)
   const int col = n0 + 32 * wave + (lane & 31);
   if constexpr (EPI == GEMM_SWIGLU) {
-    // 2 odd waves x MT x 16 x 64 floats (16 KiB at BMT 64, 32 KiB at 128) in the whole LDS array
-    static_assert(2 * MT * 16 * 64 * 4 <= NBUF * (BMT + BN) * PITCH * 2, "SwiGLU exchange does not fit");
+    // BNT/64 odd waves x MT x 16 x 64 floats (16 KiB at 128 x 64, 64 KiB at 256 x 128) in the whole LDS array
+    static_assert((BNT / 64) * MT * 16 * 64 * 4 <= NBUF * (BMT + BNT) * PITCH * 2, "SwiGLU exchange does not fit");
     float* ex = reinterpret_cast<float*>(lds);
     __syncthreads();  // the last K step's MFMA reads of the tiles are done
     if (wave & 1) {
@@ -197,29 +201,32 @@ __global__ __launch_bounds__(256) void gemm_dq_kernel(GemmArgs a) {
   }
 }
 
-template <int QT, int BMT>
+template <int QT, int BMT, int BNT>
 static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
   const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
-  const int tiles = ((a.w.rows + BN - 1) / BN) * ((rows + BMT - 1) / BMT);
+  const int tiles = ((a.w.rows + BNT - 1) / BNT) * ((rows + BMT - 1) / BMT);
   const int nk = a.w.K / BK;
   // split K until ~2 blocks per CU are busy, keeping >= 8 K steps per split
+  const int target = BNT == 256 ? 256 : 512;
   int split = 1;
   if (epi != GEMM_SWIGLU) {
-    while (tiles * split < 512 && nk / (split * 2) >= 8) split *= 2;
+    while (tiles * split < target && nk / (split * 2) >= 8) split *= 2;
   }
-  if (split > 1 && epi == GEMM_STORE && !a.seg_dev) {
+  if (split > 1 && epi == GEMM_STORE && !a.seg_dev && !a.out_zeroed) {
     const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
     if (e != hipSuccess) throw std::runtime_error("gemm_dq: memset failed");
   }
-  dim3 grid((a.w.rows + BN - 1) / BN, (a.T + BMT - 1) / BMT, split), block(256);
-  // 256-token tiles are always double-buffered (110 KB of LDS, one block per CU)
-  const bool db = BMT == 256 || tiles * split <= 512;
+  dim3 grid((a.w.rows + BNT - 1) / BNT, (a.T + BMT - 1) / BMT, split), block(2 * BNT);
+  // 256-token or 256-row tiles are always double-buffered (110 KB of LDS, one block per CU)
+  static const int force_db = getenv("LFK_GEMM_DB") ? atoi(getenv("LFK_GEMM_DB")) : -1;
+  constexpr bool big = BMT == 256 || BNT == 256;
+  const bool db = big || (force_db >= 0 ? force_db > 0 : tiles * split <= 512);
   if (a.seg_dev && split > 1 && epi != GEMM_STORE) throw std::runtime_error("gemm_dq: grouped split-K needs STORE");
-#define LFK_GEMM_LAUNCH(E)                                                                   \
-  do {                                                                                        \
-    if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true, 3, BMT>), grid, block, 0, s, a);  \
-    else if constexpr (BMT < 256)                                                             \
-      hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false, 3, BMT>), grid, block, 0, s, a);       \
+#define LFK_GEMM_LAUNCH(E)                                                                        \
+  do {                                                                                             \
+    if (db) hipLaunchKernelGGL((gemm_dq_kernel<QT, E, true, 3, BMT, BNT>), grid, block, 0, s, a);  \
+    else if constexpr (!big)                                                                       \
+      hipLaunchKernelGGL((gemm_dq_kernel<QT, E, false, 3, BMT, BNT>), grid, block, 0, s, a);       \
   } while (0)
   switch (epi) {
     case GEMM_STORE: LFK_GEMM_LAUNCH(GEMM_STORE); break;
@@ -230,15 +237,21 @@ static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
 #undef LFK_GEMM_LAUNCH
 }
 
-// 128-token tiles once a prompt chunk (or an expert's expected rows) exceeds 64 tokens
+// 128-token tiles once a prompt chunk (or an expert's expected rows) exceeds 64 tokens;
 template <int QT>
 static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
   static const int force = getenv("LFK_GEMM_BM") ? atoi(getenv("LFK_GEMM_BM")) : 0;
+  static const int force_bn = getenv("LFK_GEMM_BN") ? atoi(getenv("LFK_GEMM_BN")) : 0;
   const int rows = a.seg_dev ? (a.rows_hint > 0 ? a.rows_hint : a.T) : a.T;
   const int bm = force ? force : (rows > 64 ? 128 : 64);
-  if (bm >= 256) launch_gemm_t<QT, 256>(a, epi, s);
-  else if (bm >= 128) launch_gemm_t<QT, 128>(a, epi, s);
-  else launch_gemm_t<QT, 64>(a, epi, s);
+  // 256-row tiles for the gate/up GEMM (measured: 124.6 -> 112.6 us at 256 tokens, 242 -> 239 at
+  // 512); the split-K residual projections stay on 128-row tiles (Q6_K down is slower at 256)
+  const bool wide = force_bn ? force_bn == 256 : epi == GEMM_SWIGLU;
+  if (bm >= 256) launch_gemm_t<QT, 256, 128>(a, epi, s);
+  else if (bm >= 128) {
+    if (wide) launch_gemm_t<QT, 128, 256>(a, epi, s);
+    else launch_gemm_t<QT, 128, 128>(a, epi, s);
+  } else launch_gemm_t<QT, 64, 128>(a, epi, s);
 }
 
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s) {

@@ -169,6 +169,7 @@ struct GemmArgs {
   // sizing). Split-K STORE partials are atomically added: the caller pre-zeroes `out`.
   const int* seg_dev = nullptr;
   int rows_hint = 0;
+  bool out_zeroed = false;         // STORE: the caller already zeroed `out` (no memset for split-K)
 };
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s);
 
@@ -184,7 +185,9 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 // x[t][:] = dequant(token_embd[tokens[t]][:])
 void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s);
 // y_bf16[t] = rmsnorm(x[t]) * w
-void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s);
+// zero (optional): also zero rows [T][zero_ld] f32 (the next split-K GEMM's output)
+void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s,
+                  float* zero = nullptr, int zero_ld = 0);
 // f32 activation [T][d] -> bf16 (for the next GEMM)
 void to_bf16(const float* x, int n, __hip_bfloat16* y, hipStream_t s);
 // prefill: rope q/k of QKV rows, write q (f32) and k/v to the caches at pos0+t

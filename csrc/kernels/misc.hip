@@ -32,7 +32,7 @@ void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t
 }
 
 __global__ __launch_bounds__(256) void rmsnorm_bf16_kernel(const float* x, const float* w, float eps, int d,
-                                                          __hip_bfloat16* y) {
+                                                          __hip_bfloat16* y, float* zero, int zero_ld) {
   const int t = blockIdx.x, tid = threadIdx.x;
   const float* xr = x + (size_t)t * d;
   __shared__ float red[4];
@@ -41,6 +41,10 @@ __global__ __launch_bounds__(256) void rmsnorm_bf16_kernel(const float* x, const
     float4 v = *reinterpret_cast<const float4*>(xr + i);
     ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
   }
+  if (zero) {  // the next GEMM's split-K partials meet in this row by atomic add
+    float4* zr = reinterpret_cast<float4*>(zero + (size_t)t * zero_ld);
+    for (int i = tid; i < zero_ld / 4; i += 256) zr[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
@@ -48,17 +52,17 @@ __global__ __launch_bounds__(256) void rmsnorm_bf16_kernel(const float* x, const
   for (int i = tid * 4; i < d; i += 1024) {
     float4 v = *reinterpret_cast<const float4*>(xr + i);
     float4 g = *reinterpret_cast<const float4*>(w + i);
-    __hip_bfloat16* yr = y + (size_t)t * d + i;
-    yr[0] = __float2bfloat16(v.x * sc * g.x);
-    yr[1] = __float2bfloat16(v.y * sc * g.y);
-    yr[2] = __float2bfloat16(v.z * sc * g.z);
-    yr[3] = __float2bfloat16(v.w * sc * g.w);
+    *reinterpret_cast<uint2*>(y + (size_t)t * d + i) =
+        make_uint2(pk_bf16_pair(v.x * sc * g.x, v.y * sc * g.y), pk_bf16_pair(v.z * sc * g.z, v.w * sc * g.w));
   }
 }
 
-void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s) {
+void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s,
+                  float* zero, int zero_ld) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(rmsnorm_bf16_kernel, dim3(T), dim3(256), 0, s, x, w, eps, d, y);
+  if (zero && (zero_ld % 4 || reinterpret_cast<uintptr_t>(zero) % 16))
+    throw std::runtime_error("rmsnorm_bf16: zeroed rows must be float4 aligned");
+  hipLaunchKernelGGL(rmsnorm_bf16_kernel, dim3(T), dim3(256), 0, s, x, w, eps, d, y, zero, zero_ld);
 }
 
 __global__ void to_bf16_kernel(const float* x, int n, __hip_bfloat16* y) {

@@ -510,11 +510,16 @@ __device__ __forceinline__ void dq_load(DqRaw<T>& r, const uint8_t* __restrict__
 template <int T>
 __device__ __forceinline__ void dq_decode(const DqRaw<T>& r, int q, float* out) {
   if constexpr (T == T_Q4_K || T == T_Q5_K) {
-    const int s = q & 7, g = s >> 1, hi = s & 1;
+    const int s = q & 7, hi = s & 1;
     const float d = h2f((unsigned)r.m.x & 0xFFFF), dmin = h2f((unsigned)r.m.x >> 16);
-    float sc_lo, m_lo, sc_hi, m_hi;
-    scale_min_pair(g, (unsigned)r.m.y, (unsigned)r.m.z, (unsigned)r.m.w, sc_lo, m_lo, sc_hi, m_hi);
-    const float scl = d * (hi ? sc_hi : sc_lo), mn = dmin * (hi ? m_hi : m_lo);
+    // this lane's one 6-bit (scale, min) pair, branch-free (s differs per lane; a branch here
+    // would also split the GEMM's MFMA/decode scheduling region)
+    const unsigned y = r.m.y, z = r.m.z, w = r.m.w;
+    const int sh = 8 * (s & 3);
+    const unsigned sc_a = (y >> sh) & 63, m_a = (z >> sh) & 63;
+    const unsigned sc_b = ((w >> sh) & 0xF) | (((y >> (sh + 6)) & 3) << 4);
+    const unsigned m_b = ((w >> (sh + 4)) & 0xF) | (((z >> (sh + 6)) & 3) << 4);
+    const float scl = d * (float)(s >= 4 ? sc_b : sc_a), mn = dmin * (float)(s >= 4 ? m_b : m_a);
     const int qv[8] = {r.a.x, r.a.y, r.a.z, r.a.w, r.b.x, r.b.y, r.b.z, r.b.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

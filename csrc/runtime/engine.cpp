@@ -443,9 +443,9 @@ void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
   if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
   for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
     const Layer& L = layers_[l];
-    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s);
+    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, qkv_, ncol);  // + zero the q|k|v rows
     GemmArgs g;
-    g.x = xb_; g.T = T; g.ldo = ncol;
+    g.x = xb_; g.T = T; g.ldo = ncol; g.out_zeroed = true;
     g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
