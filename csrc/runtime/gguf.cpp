@@ -16,23 +16,32 @@ namespace {
 
 enum VT : uint32_t { U8 = 0, I8, U16, I16, U32, I32, F32, BOOL, STR, ARR, U64, I64, F64 };
 
+// Every length read from the file is checked against the bytes that remain before it
+// is used (pointer arithmetic with an unchecked 64-bit length is undefined behaviour and
+// could wrap past `end`; found by the ASan/UBSan mutation test, tests/test_sanitizers.py).
 struct Cursor {
   const uint8_t* p;
   const uint8_t* end;
+  size_t left() const { return (size_t)(end - p); }
   template <class T>
   T rd() {
-    if (p + sizeof(T) > end) throw std::runtime_error("gguf: truncated file");
+    if (left() < sizeof(T)) throw std::runtime_error("gguf: truncated file");
     T v;
     std::memcpy(&v, p, sizeof(T));
     p += sizeof(T);
     return v;
   }
   std::string str() {
-    uint64_t n = rd<uint64_t>();
-    if (p + n > end) throw std::runtime_error("gguf: truncated string");
+    const uint64_t n = rd<uint64_t>();
+    if (n > left()) throw std::runtime_error("gguf: truncated string");
     std::string s(reinterpret_cast<const char*>(p), n);
     p += n;
     return s;
+  }
+  // an array of n elements of at least `min_bytes` each must fit in what is left
+  // (bounds the reserve() below: a corrupt count cannot allocate gigabytes)
+  void need(uint64_t n, size_t min_bytes) const {
+    if (n > left() / min_bytes) throw std::runtime_error("gguf: array length exceeds the file");
   }
 };
 
@@ -61,6 +70,9 @@ GGUFValue read_value(Cursor& c, uint32_t t) {
     case ARR: {
       uint32_t et = c.rd<uint32_t>();
       uint64_t n = c.rd<uint64_t>();
+      static const size_t kMinBytes[] = {1, 1, 2, 2, 4, 4, 4, 1, 8, 12, 8, 8, 8};
+      if (et > F64) throw std::runtime_error("gguf: bad array element type");
+      c.need(n, kMinBytes[et]);
       if (et == STR) {
         v.kind = GGUFValue::ARR_STRING;
         v.as.reserve(n);
@@ -110,19 +122,34 @@ GGUFFile::GGUFFile(const std::string& path) : path_(path) {
     GGUFTensor t;
     t.name = c.str();
     uint32_t nd = c.rd<uint32_t>();
-    for (uint32_t d = 0; d < nd; ++d) t.ne.push_back((int64_t)c.rd<uint64_t>());
+    if (nd == 0 || nd > 4) throw std::runtime_error("gguf: tensor " + t.name + " has " + std::to_string(nd) + " dims");
+    uint64_t count = 1;
+    for (uint32_t d = 0; d < nd; ++d) {
+      const uint64_t ne = c.rd<uint64_t>();
+      // each dim and the element count stay far below 2^63 (n_elements() is int64)
+      if (ne > (1ull << 40) || (ne && count > (1ull << 50) / ne))
+        throw std::runtime_error("gguf: tensor " + t.name + " has an implausible shape");
+      count *= ne;
+      t.ne.push_back((int64_t)ne);
+    }
     t.type = (int)c.rd<uint32_t>();
     uint64_t off = c.rd<uint64_t>();
     infos.push_back({t, off});
   }
-  uint64_t align = (uint64_t)get_int("general.alignment", 32);
+  const int64_t align_i = get_int("general.alignment", 32);
+  if (align_i <= 0 || align_i > (1 << 20) || (align_i & (align_i - 1)))
+    throw std::runtime_error("gguf: general.alignment must be a power of two");
+  const uint64_t align = (uint64_t)align_i;
   uint64_t pos = (uint64_t)(c.p - base_);
   uint64_t data_off = (pos + align - 1) / align * align;
   for (auto& [t, off] : infos) {
-    t.offset = data_off + off;
     const TypeInfo ti = type_info(t.type);
-    t.nbytes = (uint64_t)(t.n_elements() / ti.block) * ti.bytes;
-    if (t.offset + t.nbytes > size_) throw std::runtime_error("gguf: tensor " + t.name + " out of bounds");
+    const int64_t n = t.n_elements();
+    if (t.ne[0] % ti.block) throw std::runtime_error("gguf: tensor " + t.name + " rows are not whole blocks");
+    t.nbytes = (uint64_t)(n / ti.block) * ti.bytes;
+    if (off > size_ || data_off > size_ - off || t.nbytes > size_ - data_off - off)
+      throw std::runtime_error("gguf: tensor " + t.name + " out of bounds");
+    t.offset = data_off + off;
     index_[t.name] = tensors_.size();
     tensors_.push_back(t);
   }

@@ -60,7 +60,7 @@ def _compile(cmd_prefix: List[str], src: str, flags: List[str]) -> str:
     obj = os.path.join(BUILD, src.replace("/", "_") + "." + key + ".o")
     if not os.path.exists(obj):
         os.makedirs(BUILD, exist_ok=True)
-        tmp = obj + ".tmp"
+        tmp = f"{obj}.{os.getpid()}.tmp"  # concurrent builders (pytest-xdist) never share a temp
         cmd = cmd_prefix + flags + ["-c", path, "-o", tmp]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -115,6 +115,29 @@ def build_cpu(jobs: int = 8, verbose: bool = True) -> str:
     out = cpu_so_path()
     tmp = out + ".tmp"
     cmd = ["g++", "-shared", "-fPIC", "-fopenmp", "-o", tmp] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
+    if verbose:
+        print("built", out)
+    return out
+
+
+SANITIZE_SOURCES = ["cpu/cpu_backend.cpp", "runtime/gguf.cpp", "runtime/repack.cpp", "tools/sanitize_driver.cpp"]
+
+
+def build_sanitize_driver(jobs: int = 4, verbose: bool = False) -> str:
+    """Host-side ASan + UBSan build of the GGUF parser, repack and CPU engine with a
+    small driver (device code cannot run under a GPU sanitizer on the pool)."""
+    flags = ["-O1", "-g", "-std=c++17", "-fopenmp", "-mavx2", "-mfma", "-mf16c", "-DLFK_NO_HIP",
+             "-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined",
+             "-I" + CSRC]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(["g++"], s, flags), SANITIZE_SOURCES))
+    out = os.path.join(ROOT, "build", "sanitize_driver")
+    tmp = f"{out}.{os.getpid()}.tmp"
+    cmd = ["g++", "-fsanitize=address,undefined", "-fopenmp", "-o", tmp] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
