@@ -103,3 +103,36 @@ def test_cancel_poll_stops_generation(paths):
     ev.set()
     out = llm.create_completion("hi", max_tokens=20, temperature=0.0, cancel_event=ev)
     assert out["usage"]["completion_tokens"] == 0
+
+
+def test_sampler_distribution_chi2():
+    """T5 on the C++ CPU sampler: 4000 draws at independent (seed, step) follow the
+    filtered, temperature-scaled softmax of the host chain (chi-square)."""
+    from scipy.stats import chisquare
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import _softmax, filtered_candidates
+    cpu = load_cpu()
+    rng = np.random.default_rng(5)
+    logits = (rng.standard_normal(2000) - 20).astype(np.float32)
+    live = rng.choice(2000, 10, replace=False)
+    logits[live] = np.linspace(3.0, 0.0, 10).astype(np.float32)
+    hist = [int(live[0]), int(live[2]), 9]
+    p = SamplingParams(temperature=1.2, top_k=40, top_p=0.9, min_p=0.0, repeat_penalty=1.0,
+                       frequency_penalty=0.7, presence_penalty=0.8, last_n=64)
+    ids, vals = filtered_candidates(logits, hist, p)
+    probs = _softmax(vals.astype(np.float64))
+    index = {int(t): j for j, t in enumerate(ids)}
+    counts = np.zeros(len(ids))
+    n = 4000
+    for s in range(n):
+        sp = {"top_k": p.top_k, "top_p": p.top_p, "min_p": p.min_p, "temperature": p.temperature,
+              "repeat_penalty": p.repeat_penalty, "frequency_penalty": p.frequency_penalty,
+              "presence_penalty": p.presence_penalty, "last_n": p.last_n, "seed": 1000 + s}
+        tok = cpu.sample(logits, hist, sp, s)
+        assert tok in index
+        counts[index[tok]] += 1
+    exp = probs * n
+    keep = exp >= 5
+    f_obs, f_exp = counts[keep], exp[keep]
+    if (~keep).any():
+        f_obs, f_exp = np.append(f_obs, counts[~keep].sum()), np.append(f_exp, exp[~keep].sum())
+    assert chisquare(f_obs, f_exp * f_obs.sum() / f_exp.sum()).pvalue > 1e-3, (counts, exp)

@@ -354,3 +354,39 @@ def test_sampler_matches_host_chain(torch):
         agree += tok == sample_token(logits, hist[-64:], p, i)
     assert outside <= 2
     assert agree >= n - 3
+
+
+def _chi2_logits(V=32000):
+    # 12 live candidates with spread logits, the rest far below (top-p / top-k cut inside the live set)
+    rng = np.random.default_rng(21)
+    logits = np.full(V, -30.0, np.float32) + rng.standard_normal(V).astype(np.float32)
+    live = rng.choice(V, 12, replace=False)
+    logits[live] = np.linspace(4.0, 0.5, 12).astype(np.float32)
+    return logits, live
+
+
+def test_sampler_distribution_chi2(torch):
+    """T5: the GPU draw follows the host chain's distribution (penalties -> top-k -> top-p
+    -> min-p -> temperature) - chi-square over 3000 draws with independent Philox streams."""
+    from scipy.stats import chisquare
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams, _softmax, filtered_candidates
+    logits, live = _chi2_logits()
+    hist = [int(live[0]), int(live[0]), int(live[3]), 5, 6]
+    p = SamplingParams(temperature=1.2, top_k=40, top_p=0.95, min_p=0.0, repeat_penalty=1.0,
+                       frequency_penalty=0.7, presence_penalty=0.8)
+    ids, vals = filtered_candidates(logits, hist, p)
+    probs = _softmax(vals.astype(np.float64))
+    index = {int(t): j for j, t in enumerate(ids)}
+    counts = np.zeros(len(ids))
+    n = 3000
+    for s in range(n):
+        tok, _ = _run_sampler(torch, logits, hist, p, 7919 * s + 3, step=s)
+        assert tok in index, tok  # never outside the filtered set
+        counts[index[tok]] += 1
+    exp = probs * n
+    keep = exp >= 5  # standard chi-square validity; pool the thin tail
+    f_obs = np.append(counts[keep], counts[~keep].sum())
+    f_exp = np.append(exp[keep], exp[~keep].sum())
+    if f_exp[-1] == 0:
+        f_obs, f_exp = f_obs[:-1], f_exp[:-1]
+    assert chisquare(f_obs, f_exp * f_obs.sum() / f_exp.sum()).pvalue > 1e-3, (counts, exp)
