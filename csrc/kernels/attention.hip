@@ -86,6 +86,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   const long long t_entry = TL ? wall_clock64() : 0;
   const bool stamp = TL && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
 #define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) a.dbg_clk[i] = wall_clock64() - t_entry; } } while (0)
+  if (blockIdx.z == 1) {  // weight-touch plane (see AttnDecodeArgs::pf)
+    const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!a.pf[r]) continue;
+      const size_t nl = (a.pf_bytes[r] + 127) / 128, per = (nl + nb - 1) / nb;
+      const size_t beg = (size_t)b * per, end = min(nl, beg + per), last_dw = a.pf_bytes[r] / 4 - 1;
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(a.pf[r]);
+#pragma unroll 4
+      for (size_t i = beg + threadIdx.x; i < end; i += 256) acc ^= p[min(i * 32, last_dw)];
+    }
+    if (acc == 0x9E3779B9u) *a.pf_sink = (int)acc;
+    return;
+  }
   const int kvh = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kw = lane >> 2, sub = lane & 3;
@@ -316,7 +331,13 @@ void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
   const int G = a.n_head / a.n_kv_head;
   if (a.n_head % a.n_kv_head) throw std::runtime_error("attn_decode: n_head % n_kv_head");
   if (!a.counters) throw std::runtime_error("attn_decode: counters workspace missing");
-  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH);
+  bool touch = false;
+  for (int r = 0; r < 4; ++r) {
+    if (!a.pf[r]) continue;
+    if (!a.pf_sink || a.pf_bytes[r] < 4) throw std::runtime_error("attn_decode: weight touch needs pf_sink and >= 4 bytes");
+    touch = true;
+  }
+  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, touch ? 2 : 1);
   if (a.head_dim == 128) launch_attn_decode<128>(a, G, grid, s);
   else if (a.head_dim == 64) launch_attn_decode<64>(a, G, grid, s);
   else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");

@@ -27,6 +27,16 @@ struct QMat {
 
 QMat make_qmat(const void* base, int type, int rows, int K, size_t expert_stride = 0);
 
+// Bytes spanned by one (non-expert) planar matrix: the end of its last non-empty plane.
+inline size_t qmat_bytes(const QMat& m) {
+  const size_t R = (size_t)m.rows;
+  size_t e = m.P.p0 + R * m.P.s0;
+  if (m.P.s1) e = m.P.p1 + R * m.P.s1 > e ? m.P.p1 + R * m.P.s1 : e;
+  if (m.P.s2) e = m.P.p2 + R * m.P.s2 > e ? m.P.p2 + R * m.P.s2 : e;
+  if (m.P.s3) e = m.P.p3 + R * m.P.s3 > e ? m.P.p3 + R * m.P.s3 : e;
+  return e;
+}
+
 // ---------------------------------------------------------------- GEMV (decode, T = 1)
 enum GemvEpi : int {
   EPI_STORE = 0,   // out[row] = acc
@@ -137,6 +147,14 @@ struct AttnDecodeArgs {
   float* out = nullptr;           // [n_head][hd]
   int debug_stop = 0;             // microbenchmarks only: 1..4 = exit after stage N (0 = full kernel)
   long long* dbg_clk = nullptr;   // microbenchmarks only: wall_clock64 stamps of block (0,0) / the merging block
+  // optional: a second grid plane (blockIdx.z = 1) touches one dword per 128-B line of
+  // [pf, pf + pf_bytes) so the next projection's weights are in the memory-side
+  // cache when its GEMV starts (the attention blocks are latency bound and leave
+  // HBM idle). pf_sink: a 4-B device word the touch result is conditionally stored to.
+  // Up to 4 ranges; each is spread over all touch blocks.
+  const uint8_t* pf[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t pf_bytes[4] = {0, 0, 0, 0};
+  int* pf_sink = nullptr;
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
 size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim);

@@ -226,6 +226,7 @@ void Engine::alloc_buffers() {
   attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
+  if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = std::atoi(e);
   const int nb = sampler_blocks(hp_.n_vocab);
   cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
   cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
@@ -342,6 +343,17 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
+  if (attn_touch_ > 0 && nkv_l_ < 63) {  // Wo weights into the memory-side cache under the attention
+    aa.pf[0] = L.wo.base;
+    aa.pf_bytes[0] = qmat_bytes(L.wo);
+    aa.pf_sink = attn_cnt_ + 63;
+    if (attn_touch_ > 1 && l + 1 < hp_.n_layer) {  // ... and the next layer's QKV
+      const Layer& N = layers_[l + 1];
+      aa.pf[1] = N.wq.base; aa.pf_bytes[1] = qmat_bytes(N.wq);
+      aa.pf[2] = N.wk.base; aa.pf_bytes[2] = qmat_bytes(N.wk);
+      aa.pf[3] = N.wv.base; aa.pf_bytes[3] = qmat_bytes(N.wv);
+    }
+  }
   attn_decode(aa, s);
 
   GemvArgs o;

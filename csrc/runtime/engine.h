@@ -155,7 +155,10 @@ class Engine {
   __half* vc_ = nullptr;
   float2* rope_ = nullptr;
   float* attn_part_ = nullptr;
-  int* attn_cnt_ = nullptr;   // per-kv-head split counters (last-arriver combine)
+  int* attn_cnt_ = nullptr;
+  // LFK_ATTN_TOUCH: decode attention pre-touches weights into the memory-side cache:
+  // 0 off, 1 this layer's Wo, 2 Wo + the next layer's Wq/Wk/Wv
+  int attn_touch_ = 1;   // per-kv-head split counters (last-arriver combine)
   float* cand_val_ = nullptr;
   int* cand_idx_ = nullptr;
   unsigned* cand_tau_ = nullptr;

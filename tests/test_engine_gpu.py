@@ -66,6 +66,25 @@ def test_fused_ffn_matches_unfused(models, spec, monkeypatch):
     assert eng_f.healthy
 
 
+@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
+def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
+    """The decode attention's weight-touch plane (LFK_ATTN_TOUCH 1: Wo, 2: Wo + next QKV)
+    only reads weights: decode logits match the untouched launch up to the fp32 order of the
+    split-K atomics."""
+    path = models[spec]
+    toks = [int(t) for t in np.random.default_rng(3).integers(0, 1000, 24)]
+    logits = []
+    for mode in ("0", "1", "2"):
+        monkeypatch.setenv("LFK_ATTN_TOUCH", mode)
+        eng = _engine(path)
+        eng.eval_logits(toks[:20], 0)
+        logits.append([eng.decode_logits(toks[i], i) for i in range(20, 23)])
+        assert eng.healthy
+    for other in logits[1:]:
+        for a, b in zip(logits[0], other):
+            assert rel_err(a, b) < 1e-2, (spec, rel_err(a, b))
+
+
 def test_moe_grouped_prefill_chunked(models):
     """Grouped expert prefill (device-side routing, per-expert row counts) is independent of
     how the prompt is chunked: n_batch 16 (3 chunks, partial last) == n_batch 128 (one chunk)."""
