@@ -89,14 +89,17 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   if (blockIdx.z == 1) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < AttnDecodeArgs::kTouchRanges; ++r) {
       if (!a.pf[r]) continue;
-      const size_t nl = (a.pf_bytes[r] + 127) / 128, per = (nl + nb - 1) / nb;
+      const size_t lps = (a.pf_bytes[r] + 127) / 128;  // lines per segment
+      const size_t nl = lps * a.pf_nseg[r], per = (nl + nb - 1) / nb;
       const size_t beg = (size_t)b * per, end = min(nl, beg + per), last_dw = a.pf_bytes[r] / 4 - 1;
-      const uint32_t* p = reinterpret_cast<const uint32_t*>(a.pf[r]);
 #pragma unroll 4
-      for (size_t i = beg + threadIdx.x; i < end; i += 256) acc ^= p[min(i * 32, last_dw)];
+      for (size_t i = beg + threadIdx.x; i < end; i += 256) {
+        const size_t seg = i / lps;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(a.pf[r] + seg * a.pf_seg_stride[r]);
+        acc ^= p[min((i - seg * lps) * 32, last_dw)];
+      }
     }
     if (acc == 0x9E3779B9u) *a.pf_sink = (int)acc;
     return;
@@ -332,9 +335,9 @@ void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
   if (a.n_head % a.n_kv_head) throw std::runtime_error("attn_decode: n_head % n_kv_head");
   if (!a.counters) throw std::runtime_error("attn_decode: counters workspace missing");
   bool touch = false;
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < AttnDecodeArgs::kTouchRanges; ++r) {
     if (!a.pf[r]) continue;
-    if (!a.pf_sink || a.pf_bytes[r] < 4) throw std::runtime_error("attn_decode: weight touch needs pf_sink and >= 4 bytes");
+    if (!a.pf_sink || a.pf_bytes[r] < 4 || a.pf_nseg[r] < 1) throw std::runtime_error("attn_decode: weight touch needs pf_sink and >= 4 bytes");
     touch = true;
   }
   dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, touch ? 2 : 1);

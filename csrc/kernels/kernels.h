@@ -151,9 +151,13 @@ struct AttnDecodeArgs {
   // [pf, pf + pf_bytes) so the next projection's weights are in the memory-side
   // cache when its GEMV starts (the attention blocks are latency bound and leave
   // HBM idle). pf_sink: a 4-B device word the touch result is conditionally stored to.
-  // Up to 4 ranges; each is spread over all touch blocks.
-  const uint8_t* pf[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t pf_bytes[4] = {0, 0, 0, 0};
+  // Up to 6 ranges, each spread over all touch blocks. A range is pf_nseg segments of
+  // pf_bytes bytes, pf_seg_stride apart (nseg 1: one contiguous span).
+  static constexpr int kTouchRanges = 6;
+  const uint8_t* pf[kTouchRanges] = {};
+  size_t pf_bytes[kTouchRanges] = {};
+  int pf_nseg[kTouchRanges] = {1, 1, 1, 1, 1, 1};
+  size_t pf_seg_stride[kTouchRanges] = {};
   int* pf_sink = nullptr;
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);

@@ -227,6 +227,7 @@ void Engine::alloc_buffers() {
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = std::atoi(e);
+  if (const char* e = std::getenv("LFK_ATTN_TOUCH_GU_FRAC")) attn_touch_gu_frac_ = std::atof(e);
   const int nb = sampler_blocks(hp_.n_vocab);
   cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
   cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
@@ -343,15 +344,30 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
-  if (attn_touch_ > 0 && nkv_l_ < 63) {  // Wo weights into the memory-side cache under the attention
-    aa.pf[0] = L.wo.base;
-    aa.pf_bytes[0] = qmat_bytes(L.wo);
+  if (attn_touch_ > 0 && nkv_l_ < 63) {  // weights into the memory-side cache under the attention
     aa.pf_sink = attn_cnt_ + 63;
-    if (attn_touch_ > 1 && l + 1 < hp_.n_layer) {  // ... and the next layer's QKV
+    if (attn_touch_ & 1) {                // this layer's Wo
+      aa.pf[0] = L.wo.base;
+      aa.pf_bytes[0] = qmat_bytes(L.wo);
+    }
+    if ((attn_touch_ & 2) && l + 1 < hp_.n_layer) {  // the next layer's QKV
       const Layer& N = layers_[l + 1];
       aa.pf[1] = N.wq.base; aa.pf_bytes[1] = qmat_bytes(N.wq);
       aa.pf[2] = N.wk.base; aa.pf_bytes[2] = qmat_bytes(N.wk);
       aa.pf[3] = N.wv.base; aa.pf_bytes[3] = qmat_bytes(N.wv);
+    }
+    if ((attn_touch_ & 4) && hp_.n_expert == 0 && L.w_gu.base) {
+      // the rows each CU's gate/up GEMV block streams first: the one-CU launch gives
+      // block b a contiguous item range, ~rows [b, b + 1) * rows / 256 in memory order
+      const QMat& W = L.w_gu;
+      const size_t segR = ((size_t)W.rows + 255) / 256;
+      const size_t head = std::max<size_t>(1, (size_t)(segR * attn_touch_gu_frac_));
+      aa.pf[4] = W.base + W.P.p0; aa.pf_nseg[4] = 256;
+      aa.pf_seg_stride[4] = segR * W.P.s0; aa.pf_bytes[4] = head * W.P.s0;
+      if (W.P.s1) {
+        aa.pf[5] = W.base + W.P.p1; aa.pf_nseg[5] = 256;
+        aa.pf_seg_stride[5] = segR * W.P.s1; aa.pf_bytes[5] = head * W.P.s1;
+      }
     }
   }
   attn_decode(aa, s);

@@ -157,8 +157,10 @@ class Engine {
   float* attn_part_ = nullptr;
   int* attn_cnt_ = nullptr;
   // LFK_ATTN_TOUCH: decode attention pre-touches weights into the memory-side cache:
-  // 0 off, 1 this layer's Wo, 2 Wo + the next layer's Wq/Wk/Wv
-  int attn_touch_ = 1;   // per-kv-head split counters (last-arriver combine)
+  // bit mask: 1 this layer's Wo, 2 the next layer's Wq/Wk/Wv, 4 the head of every CU's
+  // gate/up range (LFK_ATTN_TOUCH_GU_FRAC of it)
+  int attn_touch_ = 1;
+  double attn_touch_gu_frac_ = 0.3;   // per-kv-head split counters (last-arriver combine)
   float* cand_val_ = nullptr;
   int* cand_idx_ = nullptr;
   unsigned* cand_tau_ = nullptr;
