@@ -68,13 +68,13 @@ def test_fused_ffn_matches_unfused(models, spec, monkeypatch):
 
 @pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
 def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
-    """The decode attention's weight-touch plane (LFK_ATTN_TOUCH 1: Wo, 2: Wo + next QKV)
+    """The decode attention's weight-touch plane (LFK_ATTN_TOUCH bits: 1 Wo, 2 next QKV, 4 gate/up heads)
     only reads weights: decode logits match the untouched launch up to the fp32 order of the
     split-K atomics."""
     path = models[spec]
     toks = [int(t) for t in np.random.default_rng(3).integers(0, 1000, 24)]
     logits = []
-    for mode in ("0", "1", "2"):
+    for mode in ("0", "1", "7"):
         monkeypatch.setenv("LFK_ATTN_TOUCH", mode)
         eng = _engine(path)
         eng.eval_logits(toks[:20], 0)
