@@ -359,15 +359,25 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
     if ((attn_touch_ & 4) && hp_.n_expert == 0 && L.w_gu.base) {
       // the rows each CU's gate/up GEMV block streams first: the one-CU launch gives
       // block b a contiguous item range, ~rows [b, b + 1) * rows / 256 in memory order
+      // Every touched byte stays inside the plane: rows need not divide by 256 (F = 8640 gives
+      // segR 68, and 255 * 68 > 2F), so the segment count is cut to the segments that start
+      // inside the plane and the head to what the LAST segment still holds.
       const QMat& W = L.w_gu;
-      const size_t segR = ((size_t)W.rows + 255) / 256;
-      const size_t head = std::max<size_t>(1, (size_t)(segR * attn_touch_gu_frac_));
-      aa.pf[4] = W.base + W.P.p0; aa.pf_nseg[4] = 256;
+      const size_t rows = (size_t)W.rows;
+      const size_t segR = (rows + 255) / 256;
+      const size_t nseg = std::min<size_t>(256, (rows + segR - 1) / segR);
+      const size_t last_rows = rows - (nseg - 1) * segR;
+      const double frac = std::min(1.0, std::max(0.0, attn_touch_gu_frac_));
+      const size_t head = std::min(last_rows, std::max<size_t>(1, (size_t)(segR * frac)));
+      aa.pf[4] = W.base + W.P.p0; aa.pf_nseg[4] = (int)nseg;
       aa.pf_seg_stride[4] = segR * W.P.s0; aa.pf_bytes[4] = head * W.P.s0;
       if (W.P.s1) {
-        aa.pf[5] = W.base + W.P.p1; aa.pf_nseg[5] = 256;
+        aa.pf[5] = W.base + W.P.p1; aa.pf_nseg[5] = (int)nseg;
         aa.pf_seg_stride[5] = segR * W.P.s1; aa.pf_bytes[5] = head * W.P.s1;
       }
+      for (int k = 4; k < 6; ++k)  // (nseg-1)*stride + bytes <= plane bytes
+        if (aa.pf[k] && (nseg - 1) * aa.pf_seg_stride[k] + aa.pf_bytes[k] > rows * (k == 4 ? W.P.s0 : W.P.s1))
+          throw std::runtime_error("attention touch range exceeds the gate/up plane");
     }
   }
   attn_decode(aa, s);

@@ -155,12 +155,14 @@ class Engine {
   __half* vc_ = nullptr;
   float2* rope_ = nullptr;
   float* attn_part_ = nullptr;
+  // [64] per-kv-head split counters (last-arriver combine); word 63 is reserved as the
+  // weight touch's pf_sink, which is why the touch needs nkv_l_ < 63
   int* attn_cnt_ = nullptr;
   // LFK_ATTN_TOUCH: decode attention pre-touches weights into the memory-side cache:
   // bit mask: 1 this layer's Wo, 2 the next layer's Wq/Wk/Wv, 4 the head of every CU's
-  // gate/up range (LFK_ATTN_TOUCH_GU_FRAC of it)
+  // gate/up range (LFK_ATTN_TOUCH_GU_FRAC of it, clamped to (0, 1])
   int attn_touch_ = 1;
-  double attn_touch_gu_frac_ = 0.3;   // per-kv-head split counters (last-arriver combine)
+  double attn_touch_gu_frac_ = 0.3;
   float* cand_val_ = nullptr;
   int* cand_idx_ = nullptr;
   unsigned* cand_tau_ = nullptr;

@@ -101,13 +101,33 @@ GGUFFile::GGUFFile(const std::string& path) : path_(path) {
   fd_ = ::open(path.c_str(), O_RDONLY);
   if (fd_ < 0) throw std::runtime_error("gguf: cannot open " + path);
   struct stat st;
-  if (fstat(fd_, &st) != 0) throw std::runtime_error("gguf: stat failed");
+  if (fstat(fd_, &st) != 0) {
+    ::close(fd_);
+    throw std::runtime_error("gguf: stat failed");
+  }
   size_ = (size_t)st.st_size;
   void* m = mmap(nullptr, size_, PROT_READ, MAP_SHARED, fd_, 0);
-  if (m == MAP_FAILED) throw std::runtime_error("gguf: mmap failed");
+  if (m == MAP_FAILED) {
+    ::close(fd_);
+    throw std::runtime_error("gguf: mmap failed");
+  }
   base_ = static_cast<const uint8_t*>(m);
+  // a constructor that throws never runs the destructor: release the mapping and the
+  // fd here on every rejected file (bad magic, truncation, bounds, alignment)
+  try {
+    parse();
+  } catch (...) {
+    munmap(const_cast<uint8_t*>(base_), size_);
+    ::close(fd_);
+    base_ = nullptr;
+    fd_ = -1;
+    throw;
+  }
+}
+
+void GGUFFile::parse() {
   Cursor c{base_, base_ + size_};
-  if (c.rd<uint32_t>() != 0x46554747u) throw std::runtime_error("gguf: bad magic in " + path);
+  if (c.rd<uint32_t>() != 0x46554747u) throw std::runtime_error("gguf: bad magic in " + path_);
   version_ = c.rd<uint32_t>();
   if (version_ < 2 || version_ > 3) throw std::runtime_error("gguf: unsupported version");
   uint64_t n_tensors = c.rd<uint64_t>();

@@ -55,6 +55,8 @@ class GGUFFile {
   void prefetch(const GGUFTensor& t) const;
 
  private:
+  void parse();  // header, KV pairs and tensor infos of the mapped file (throws on malformed input)
+
   std::string path_;
   int fd_ = -1;
   const uint8_t* base_ = nullptr;

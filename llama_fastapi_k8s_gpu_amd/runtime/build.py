@@ -41,14 +41,30 @@ def _includes() -> List[str]:
     return ["-I" + CSRC, "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
 
 
+def _local_includes(path: str, seen: set) -> None:
+    """Every csrc header reachable from `path` through #include "..." (recursive)."""
+    import re
+    with open(path, "r", errors="replace") as fh:
+        text = fh.read()
+    for inc in re.findall(r'^\s*#\s*include\s*"([^"]+)"', text, flags=re.M):
+        dep = os.path.normpath(os.path.join(os.path.dirname(path), inc))
+        if not os.path.exists(dep):
+            dep = os.path.normpath(os.path.join(CSRC, inc))
+        if os.path.exists(dep) and dep not in seen:
+            seen.add(dep)
+            _local_includes(dep, seen)
+
+
 def _hash(path: str, flags: List[str]) -> str:
     h = hashlib.sha1(" ".join(flags).encode())
-    # include the headers of csrc so an edit to a header rebuilds dependants
-    for root, _, files in os.walk(CSRC):
-        for f in sorted(files):
-            if f.endswith(".h"):
-                with open(os.path.join(root, f), "rb") as fh:
-                    h.update(fh.read())
+    # the csrc headers this source includes (transitively): an edit to one of them
+    # rebuilds its dependants and nothing else
+    deps: set = set()
+    _local_includes(path, deps)
+    for dep in sorted(deps):
+        h.update(dep.encode())
+        with open(dep, "rb") as fh:
+            h.update(fh.read())
     with open(path, "rb") as fh:
         h.update(fh.read())
     return h.hexdigest()[:16]

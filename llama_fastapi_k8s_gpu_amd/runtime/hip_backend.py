@@ -58,6 +58,7 @@ class HipBackend:
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
                                  tensor_split=ts)
         self.n_ctx = n_ctx
+        self.n_batch = min(n_batch, n_ctx)  # the engine's prefill chunk bound (eval_logits rejects T > n_batch)
         self.device = device
         if size > 1:
             self._open_p2p()
@@ -106,7 +107,7 @@ class HipBackend:
         logits = None
         pos = n_keep
         while pos < len(hist):
-            T = min(len(hist) - pos, 512)
+            T = min(len(hist) - pos, self.n_batch)
             logits = e.eval_logits(hist[pos:pos + T], pos)
             pos += T
         t1 = time.perf_counter()

@@ -10,7 +10,7 @@ from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
 pytestmark = pytest.mark.gpu
 
 SPECS = ["tiny-llama3-q4_k_m", "tiny-llama3-mixed", "tiny-tinyllama-q8_0", "tiny-mixtral-q4_k_m", "tiny-llama3-f32",
-         "tiny-llama3-wide"]
+         "tiny-llama3-wide", "tiny-q8-oddff"]
 
 
 @pytest.fixture(scope="module")
@@ -66,7 +66,7 @@ def test_fused_ffn_matches_unfused(models, spec, monkeypatch):
     assert eng_f.healthy
 
 
-@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
+@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m", "tiny-q8-oddff"])
 def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
     """The decode attention's weight-touch plane (LFK_ATTN_TOUCH bits: 1 Wo, 2 next QKV, 4 gate/up heads)
     only reads weights: decode logits match the untouched launch up to the fp32 order of the
@@ -74,6 +74,8 @@ def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
     path = models[spec]
     toks = [int(t) for t in np.random.default_rng(3).integers(0, 1000, 24)]
     logits = []
+    # tiny-q8-oddff: 2F = 1088 gate/up rows, not a multiple of 256 (segments clamp to the plane)
+    monkeypatch.setenv("LFK_ATTN_TOUCH_GU_FRAC", "1.5")   # clamped to 1
     for mode in ("0", "1", "7"):
         monkeypatch.setenv("LFK_ATTN_TOUCH", mode)
         eng = _engine(path)
