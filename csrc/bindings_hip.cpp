@@ -128,6 +128,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("device_bytes", &Engine::device_bytes)
       .def_property_readonly("healthy", &Engine::healthy)
       .def_property_readonly("ffn_fused", &Engine::ffn_fused)
+      .def_property_readonly("pdecode", &Engine::pdecode_status)
       .def("p2p_handle", [](Engine& e) { return py::bytes(e.p2p_handle()); })
       .def("p2p_open", [](Engine& e, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;

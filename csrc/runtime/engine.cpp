@@ -102,6 +102,7 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   alloc_buffers();
   build_rope();
   setup_ffn_fused();
+  pdec_status_ = setup_pdecode();
   HIPCHK(hipStreamSynchronize(stream_));
 }
 
@@ -469,7 +470,11 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
 
 void Engine::enqueue_decode(hipStream_t s) {
   embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
+  if (pdec_) {
+    pdecode(pda_, s);  // every layer in one launch
+  } else {
+    for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
+  }
   enqueue_head(x_, 1, s);
 }
 

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../kernels/kernels.h"
+#include "../kernels/pdecode.h"
 #include "gguf.h"
 #include "p2p.h"
 
@@ -95,6 +96,8 @@ class Engine {
   bool p2p_ready() const { return p2p_ && p2p_->ready(); }
   bool healthy() const { return healthy_; }
   bool ffn_fused() const { return ffn_fused_; }
+  // persistent decode step (kernels/pdecode.h): "on", or why it is off
+  const std::string& pdecode_status() const { return pdec_status_; }
   std::string last_error() const { return last_error_; }
   int n_ctx() const { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
@@ -119,6 +122,7 @@ class Engine {
   void check(hipError_t e, const char* what);
   void check_device_err();
   void setup_ffn_fused();
+  std::string setup_pdecode();  // returns the status string
 
   HParams hp_;
   EngineOptions opt_;
@@ -181,6 +185,9 @@ class Engine {
   int* ffn_cnt_ = nullptr;    // [n_layer][32] fused-FFN hand-off counters (zero between launches)
   int* dev_err_ = nullptr;    // device error word (bounded in-kernel waits that timed out)
   bool ffn_fused_ = false;    // dense decode FFN as one fused launch (ffn_fused.hip)
+  bool pdec_ = false;         // decode layers as ONE persistent launch (pdecode.hip)
+  PDecodeArgs pda_;
+  std::string pdec_status_;
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 

@@ -103,10 +103,17 @@ SPECS: Dict[str, ModelSpec] = {
     # wide enough for several 2048-feature FFN slices (fused decode FFN hand-off), partial last slice
     "tiny-llama3-wide": ModelSpec("tiny-llama3-wide", 1024, 3, 8, 2, 5120, 0, 500000.0, "bpe", "q4_k_m",
                                   n_ctx_train=1024),
-    # Q8_0 with n_ff = 544: 2F = 1088 gate/up rows is NOT a multiple of 256 (the attention
+    # Q8_0 with n_ff = 576: 2F = 1152 gate/up rows is NOT a multiple of 256 (the attention
     # weight touch's per-CU gate/up segments must clamp to the plane end)
-    "tiny-q8-oddff": ModelSpec("tiny-q8-oddff", 256, 2, 4, 2, 544, 0, 10000.0, "spm", "q8_0",
+    "tiny-q8-oddff": ModelSpec("tiny-q8-oddff", 256, 2, 4, 2, 576, 0, 10000.0, "spm", "q8_0",
                                n_ctx_train=1024),
+    # smallest shapes the persistent decode kernel takes on a 256-CU MI355X (d = 4096 rows split
+    # 16 per CU, kv heads onto CU groups): 4 layers (Q4_K_M mix: layers 0 and 3 bump V/down to
+    # Q6_K), GQA groups of 4 and of 8
+    "pd-llama-g4": ModelSpec("pd-llama-g4", 4096, 4, 32, 8, 2048, 0, 500000.0, "bpe", "q4_k_m",
+                             n_ctx_train=1024),
+    "pd-llama-g8": ModelSpec("pd-llama-g8", 4096, 4, 32, 4, 2048, 0, 500000.0, "bpe", "q4_k_m",
+                             n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

@@ -74,7 +74,7 @@ def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
     path = models[spec]
     toks = [int(t) for t in np.random.default_rng(3).integers(0, 1000, 24)]
     logits = []
-    # tiny-q8-oddff: 2F = 1088 gate/up rows, not a multiple of 256 (segments clamp to the plane)
+    # tiny-q8-oddff: 2F = 1152 gate/up rows, not a multiple of 256 (segments clamp to the plane)
     monkeypatch.setenv("LFK_ATTN_TOUCH_GU_FRAC", "1.5")   # clamped to 1
     for mode in ("0", "1", "7"):
         monkeypatch.setenv("LFK_ATTN_TOUCH", mode)
