@@ -129,6 +129,14 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("healthy", &Engine::healthy)
       .def_property_readonly("ffn_fused", &Engine::ffn_fused)
       .def_property_readonly("pdecode", &Engine::pdecode_status)
+      .def("pdecode_timeline", [](Engine& e) {
+        std::vector<long long> v = e.pdecode_timeline();
+        return py::array_t<long long>(v.size(), v.data());
+      })
+      .def("pdecode_dump", [](Engine& e) {
+        std::vector<float> v = e.pdecode_dump();
+        return py::array_t<float>(v.size(), v.data());
+      })
       .def("p2p_handle", [](Engine& e) { return py::bytes(e.p2p_handle()); })
       .def("p2p_open", [](Engine& e, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;

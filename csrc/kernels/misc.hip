@@ -11,7 +11,9 @@ namespace lfk {
 template <int QT>
 __device__ void embed_body(const QMat& e, const int* tokens, int T, float* x) {
   const int t = blockIdx.x;
-  const size_t row = (size_t)tokens[t];
+  // clamped: a token id can only come from the host (validated) or the sampler, but a
+  // corrupted id must not turn into an out-of-bounds read that faults the GPU
+  const size_t row = (size_t)min(max(tokens[t], 0), e.rows - 1);
   const int nq = e.K >> 5;
   for (int q = threadIdx.x; q < nq; q += blockDim.x) {
     float v[32];

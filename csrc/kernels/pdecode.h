@@ -75,8 +75,14 @@ struct PDecodeArgs {
   int act_bytes = 0, part_floats = 0, res_rows = 0;  // LDS carve sizes
   float eps = 1e-5f, attn_scale = 1.f;
   int* err = nullptr;                // [0] error code, [1] abort flag (device)
-  long long* dbg = nullptr;          // optional per-CU stamps (microbenchmarks)
+  // debugging: when set, every layer's intermediates are stored at dbg + l * pd_dump_stride():
+  // q (roped, unscaled) [nq] | k [nkv] | v [nkv] | attention output [nq] | x after Wo [d] |
+  // SwiGLU output [F] | x after down [d]
+  float* dbg = nullptr;
+  // timeline: wall_clock64 stamps [ncu][n_layer][kPdStamps] (consumer stage ends, loader issue)
+  long long* tl = nullptr;
 };
+static constexpr int kPdStamps = 12;
 
 size_t pdecode_lds_bytes(const PDecodeArgs& a);
 // every workgroup of the grid (one per CU) can be resident at once (host check)
@@ -86,6 +92,7 @@ void pdecode(const PDecodeArgs& a, hipStream_t s);
 // map ? map[i] : i) goes to CU i / rows_cu, slot i % rows_cu of the stage at stage_off
 void pd_pack_rows(uint8_t* region, uint32_t cu_bytes, uint32_t stage_off, int rows_cu, int ncu, const QMat& src,
                   const int* map_dev, hipStream_t s);
+LFK_HD size_t pd_dump_stride(const PDecodeArgs& a) { return (size_t)2 * a.nq + 2 * a.nkv + 2 * a.d + a.F; }
 // ring row format size of one row
 uint32_t pd_row_bytes(int type, int K);
 

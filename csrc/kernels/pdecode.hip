@@ -55,7 +55,10 @@ constexpr int kAttW = 4;                 // consumer waves that read keys (16 ke
 constexpr long long kSpinTicks = 4000000;  // 40 ms of the 100 MHz wall clock per wait
 
 // LDS control words (ints at the start of the dynamic region)
-enum Ctl : int { C_FILLED = 0, C_FREED = 1, C_CBAR = 2, C_ABORT = 3, C_RMS = 4, C_NWORDS = 16 };
+// C_FREED0 + slot: consumer-wave releases of that ring slot, cumulative. Per slot, not one sum:
+// with one sum a wave running several items ahead could make a slot look free while a slower
+// wave still reads it (the loader then overwrote live ring bytes: measured, stages of 8+ items)
+enum Ctl : int { C_FILLED = 0, C_CBAR = 2, C_ABORT = 3, C_FREED0 = 8, C_NWORDS = 16 };
 
 __device__ __forceinline__ void gst(u64* p, unsigned tag, unsigned v) {
   __hip_atomic_store((gu64*)p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -283,17 +286,21 @@ __device__ void loader(const PDecodeArgs& a, const Lds& S, int u) {
   for (int l = 0; l < a.n_layer; ++l) {
     const PdLayer Ly = layer_at(a, l);
     const uint8_t* span = Ly.wbase + (size_t)u * Ly.cu_bytes;
+    long long* tl = a.tl ? a.tl + ((size_t)u * a.n_layer + l) * kPdStamps : nullptr;
     for (int k = 0; k < Ly.nitems; ++k, ++n) {
+      if (tl && lane == 0 && (k == 0 || k == Ly.nitems - 1)) tl[k == 0 ? 10 : 11] = wall_clock64();
       const PdItem it = item_at(a, Ly.item0 + k);
       const int slot = n % a.nslot;
       if (n >= a.nslot) {
-        const int need = (n - a.nslot + 1) * kNCW;
-        if (lds_ld(ctl + C_FREED) < need) {
+        // every consumer wave has released every earlier item of this slot
+        int* freed = ctl + C_FREED0 + slot;
+        const int need = (n / a.nslot) * kNCW;
+        if (lds_ld(freed) < need) {
           // about to block on the consumers: land and publish what is in flight first
           vm_wait<0>();
           if (pend >= 0) { if (lane == 0) lds_st(ctl + C_FILLED, pend + 1); pend = -1; }
           const long long t0 = wall_clock64();
-          while (lds_ld(ctl + C_FREED) < need) {
+          while (lds_ld(freed) < need) {
             if (lds_ld(ctl + C_ABORT)) return;
             if (wall_clock64() - t0 > 4 * kSpinTicks) {  // consumers gone without a word: give up
               if (lane == 0) raise_abort(a.err, ctl, 91);
@@ -430,7 +437,7 @@ struct Cons {
       default: item_units<T_Q8_0>(slot, it, K, S.xq, S.xs, S.part, cw, lane); break;
     }
     // every LDS read of the slot has returned before the release (the add is a release)
-    if (lane == 0) lds_add(S.ctl + C_FREED, 1);
+    if (lane == 0) lds_add(S.ctl + C_FREED0 + n % a.nslot, 1);
     ++n;
     return true;
   }
@@ -711,6 +718,7 @@ __device__ bool merge_head(Cons& C, int l, int g, int j, int S_) {
   }
   const float ov = num / den;
   const int h = g * G + j;
+  if (a.dbg) a.dbg[(size_t)l * pd_dump_stride(a) + a.nq + 2 * a.nkv + h * HD + dd] = ov;
   u64* rec = gl + a.off_o + (size_t)h * (HD / 4 + HD / 8);
   // lane group of wave cw covers dims [64cw, 64cw + 64): int8x4 records 16cw.., scales 8cw..
   C.publish_q8(rec, ov, 64, C.cw * 16, C.cw * 8, HD / 4);
@@ -748,6 +756,9 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
   for (int l = 0; l < a.n_layer && C.ok; ++l) {
     const PdLayer Ly = layer_at(a, l);
     u64* gl = a.gran + (size_t)l * a.gran_layer;
+    long long* tl = (a.tl && C.cw == 0 && C.lane == 0) ? a.tl + ((size_t)u * a.n_layer + l) * kPdStamps : nullptr;
+#define PD_T(i) do { if (tl) tl[i] = wall_clock64(); } while (0)
+    PD_T(0);
     // item ranges of the stages (items are stage-ordered)
     int kq = 0, kw0 = 0, kg0 = 0, kd0 = 0;
     {
@@ -761,8 +772,10 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
     }
     // ---- QKV
     if (!gather_hx(C, gl + a.off_hx)) break;
+    PD_T(1);
     const float rms_a = hx_rms(C);
     if (!C.consume(Ly, kq, kw0)) break;
+    PD_T(2);
     if (C.cw == 0) {
       const int nrow = a.nqu + 2 * a.nku;
       const int nq2 = a.nqu / 2, nk2 = a.nku / 2;
@@ -778,6 +791,11 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
         if (isq || isk) {
           const float2 cs = a.rope[(size_t)pos * (a.hd / 2) + dim / 2];
           v = (dim & 1) ? partner * cs.y + v * cs.x : v * cs.x - partner * cs.y;
+        }
+        if (a.dbg && j < nrow) {
+          float* db = a.dbg + (size_t)l * pd_dump_stride(a);
+          const int di = isq ? grow : (isk ? a.nq + grow : a.nq + a.nkv + grow);
+          db[di] = v;
         }
         if (isq) v *= a.attn_scale;
         if (!isq && j < nrow) {
@@ -800,6 +818,7 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
     if (gi >= a.cpg - G) {
       if (!merge_head<G>(C, l, g, gi - (a.cpg - G), S_)) break;
     }
+    PD_T(3);
     // ---- Wo
     {
       const int hd = a.hd, n4 = hd / 4, n8 = hd / 8, rec = n4 + n8;
@@ -809,15 +828,21 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
           }))
         break;
     }
+    PD_T(4);
     if (!C.consume(Ly, kw0, kg0)) break;
+    PD_T(5);
     if (C.cw == 0) {
       for (int j = C.lane; j < nx; j += 64) S.xres[j] += C.row_total(j, a.nq);
+      if (a.dbg)
+        for (int j = C.lane; j < nx; j += 64) a.dbg[(size_t)l * pd_dump_stride(a) + 2 * a.nq + 2 * a.nkv + u * nx + j] = S.xres[j];
       publish_hx(C, gl + a.off_hx2, Ly.ffn_norm);
     }
     // ---- gate/up + SwiGLU
     if (!gather_hx(C, gl + a.off_hx2)) break;
+    PD_T(6);
     const float rms_f = hx_rms(C);
     if (!C.consume(Ly, kg0, kd0)) break;
+    PD_T(7);
     if (C.cw == 0) {
       const int nf = a.nfu;
       u64* rec = gl + a.off_hh + (size_t)u * (nf / 4 + nf / 8);
@@ -826,6 +851,7 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
         const int jj = min(j, nf - 1);
         const float gv = C.row_total(jj, a.d) * rms_f, uv = C.row_total(nf + jj, a.d) * rms_f;
         const float h = j < nf ? silu_f(gv) * uv : 0.f;
+        if (a.dbg && j < nf) a.dbg[(size_t)l * pd_dump_stride(a) + 2 * a.nq + 2 * a.nkv + a.d + u * nf + j] = h;
         C.publish_q8(rec, h, min(64, nf - j0), j0 / 4, j0 / 8, nf / 4);
       }
     }
@@ -838,9 +864,15 @@ __global__ __launch_bounds__(kThreads) void pdecode_kernel(PDecodeArgs a) {
           }))
         break;
     }
+    PD_T(8);
     if (!C.consume(Ly, kd0, Ly.nitems)) break;
+    PD_T(9);
+#undef PD_T
     if (C.cw == 0) {
       for (int j = C.lane; j < nx; j += 64) S.xres[j] += C.row_total(j, a.F);
+      if (a.dbg)
+        for (int j = C.lane; j < nx; j += 64)
+          a.dbg[(size_t)l * pd_dump_stride(a) + 2 * a.nq + 2 * a.nkv + a.d + a.F + u * nx + j] = S.xres[j];
       if (l + 1 < a.n_layer) {
         publish_hx(C, a.gran + (size_t)(l + 1) * a.gran_layer + a.off_hx, layer_at(a, l + 1).attn_norm);
       } else {

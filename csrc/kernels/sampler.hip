@@ -315,6 +315,7 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
   }
   if (lane == 0) {
     int* st = a.state;
+    tok = min(max(tok, 0), a.V - 1);  // non-finite logits must not leave an out-of-range id behind
     st[S_TOKEN] = tok;
     const int head = st[S_RING_HEAD];
     a.ring[head & 63] = tok;

@@ -98,6 +98,10 @@ class Engine {
   bool ffn_fused() const { return ffn_fused_; }
   // persistent decode step (kernels/pdecode.h): "on", or why it is off
   const std::string& pdecode_status() const { return pdec_status_; }
+  // LFK_PDECODE_DUMP=1: every layer's intermediates of the last persistent decode step
+  std::vector<float> pdecode_dump();
+  // LFK_PDECODE_TIMELINE=1: wall-clock stamps [CU][layer][kPdStamps] of the last step
+  std::vector<long long> pdecode_timeline();
   std::string last_error() const { return last_error_; }
   int n_ctx() const { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
@@ -188,6 +192,7 @@ class Engine {
   bool pdec_ = false;         // decode layers as ONE persistent launch (pdecode.hip)
   PDecodeArgs pda_;
   std::string pdec_status_;
+  size_t pd_dump_n_ = 0, pd_tl_n_ = 0;
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 

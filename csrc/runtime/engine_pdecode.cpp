@@ -87,7 +87,12 @@ std::string Engine::setup_pdecode() {
     for (const StageSpec& s : st) {
       const uint32_t rb = pd_row_bytes(s.m->type, s.m->K);
       if (rb == 0 || rb > (uint32_t)a.slot_bytes) return "row larger than a ring slot";
-      const int per_slot = a.slot_bytes / (int)rb;
+      // the loader keeps two items in flight and counts their transfers with vmcnt, a 6-bit
+      // counter: two items together must stay below 64 one-KiB transfers (measured: 32 + 32
+      // KiB items fed stale ring bytes to the consumers)
+      const int item_max = std::min(a.slot_bytes, 31 * 1024);
+      const int per_slot = item_max / (int)rb;
+      if (per_slot < 1) return "row larger than a ring item";
       const int nit = (s.rows_cu + per_slot - 1) / per_slot;
       for (int i = 0; i < nit; ++i) {
         const int r0 = (int)((long long)s.rows_cu * i / nit), r1 = (int)((long long)s.rows_cu * (i + 1) / nit);
@@ -99,7 +104,7 @@ std::string Engine::setup_pdecode() {
         it.dma_kb = (uint16_t)(((size_t)(r1 - r0) * rb + 1023) / 1024);
         it.stage = (uint8_t)s.stage;
         it.type = (uint8_t)s.m->type;
-        if (it.dma_kb * 1024 > a.slot_bytes || it.dma_kb > 47) return "item exceeds a ring slot";
+        if (it.dma_kb * 1024 > a.slot_bytes || it.dma_kb > 31) return "item exceeds a ring slot";
         items.push_back(it);
       }
       off += (size_t)s.rows_cu * rb;
@@ -175,6 +180,16 @@ std::string Engine::setup_pdecode() {
   a.pos = state_ + S_POS;
   a.err = dev_err_;
   if (!pdecode_resident(a)) return "one workgroup per CU is not resident";
+  if (const char* tm = std::getenv("LFK_PDECODE_TIMELINE"); tm && tm[0] == '1') {
+    pd_tl_n_ = (size_t)ncu * hp_.n_layer * kPdStamps;
+    a.tl = static_cast<long long*>(dalloc(sizeof(long long) * pd_tl_n_));
+    HIPCHK(hipMemsetAsync(a.tl, 0, sizeof(long long) * pd_tl_n_, stream_));
+  }
+  if (const char* dm = std::getenv("LFK_PDECODE_DUMP"); dm && dm[0] == '1') {
+    pd_dump_n_ = pd_dump_stride(a) * hp_.n_layer;
+    a.dbg = static_cast<float*>(dalloc(sizeof(float) * pd_dump_n_));
+    HIPCHK(hipMemsetAsync(a.dbg, 0, sizeof(float) * pd_dump_n_, stream_));
+  }
   HIPCHK(hipStreamSynchronize(stream_));
   pda_ = a;
   pdec_ = true;
@@ -182,6 +197,24 @@ std::string Engine::setup_pdecode() {
     std::fprintf(stderr, "[lfk] persistent decode: %d CUs, ring %d x %d KiB, %zu items, %.2f GB ring-format weights\n",
                  ncu, a.nslot, a.slot_bytes / 1024, items.size(), total / 1e9);
   return "on";
+}
+
+std::vector<long long> Engine::pdecode_timeline() {
+  std::vector<long long> out(pd_tl_n_);
+  if (pd_tl_n_) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(out.data(), pda_.tl, sizeof(long long) * pd_tl_n_, hipMemcpyDeviceToHost));
+  }
+  return out;
+}
+
+std::vector<float> Engine::pdecode_dump() {
+  std::vector<float> out(pd_dump_n_);
+  if (pd_dump_n_) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(out.data(), pda_.dbg, sizeof(float) * pd_dump_n_, hipMemcpyDeviceToHost));
+  }
+  return out;
 }
 
 }  // namespace lfk

@@ -112,6 +112,9 @@ SPECS: Dict[str, ModelSpec] = {
     # Q6_K), GQA groups of 4 and of 8
     "pd-llama-g4": ModelSpec("pd-llama-g4", 4096, 4, 32, 8, 2048, 0, 500000.0, "bpe", "q4_k_m",
                              n_ctx_train=1024),
+    # two layers of the exact Llama-3-8B layer shape (F = 14336: multi-item ring stages)
+    "pd-llama-8b2": ModelSpec("pd-llama-8b2", 4096, 2, 32, 8, 14336, 0, 500000.0, "bpe", "q4_k_m",
+                              n_ctx_train=1024),
     "pd-llama-g8": ModelSpec("pd-llama-g8", 4096, 4, 32, 4, 2048, 0, 500000.0, "bpe", "q4_k_m",
                              n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",

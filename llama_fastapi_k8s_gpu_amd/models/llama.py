@@ -134,8 +134,10 @@ class ReferenceLlama:
                 out[t] += w[t, j] * (L["ffn_down_exps"][e] @ g)
         return out
 
-    def forward(self, tokens, n_past: int, all_logits: bool = False):
-        """Evaluate ``tokens`` at positions n_past.. ; returns logits [T,V] or [V]."""
+    def forward(self, tokens, n_past: int, all_logits: bool = False, trace: Optional[List[Dict]] = None):
+        """Evaluate ``tokens`` at positions n_past.. ; returns logits [T,V] or [V].
+        ``trace`` (a list) receives per layer the last token's q / k / v (roped), the attention
+        output, x after the attention residual, the SwiGLU output and x after the FFN residual."""
         torch = self.torch
         hp = self.hp
         T = len(tokens)
@@ -159,7 +161,15 @@ class ReferenceLlama:
             a = torch.einsum("htl,lhd->thd", torch.softmax(s, -1), V).reshape(T, -1)
             x = x + a @ L["attn_output"].T
             h = self._rms(x, L["ffn_norm"])
+            if trace is not None and not self.hp.n_expert:
+                F = torch.nn.functional
+                hh = F.silu(h @ L["ffn_gate"].T) * (h @ L["ffn_up"].T)
+                trace.append({"q": q[-1].reshape(-1).clone(), "k": k[-1].reshape(-1).clone(),
+                              "v": v[-1].reshape(-1).clone(), "o": a[-1].clone(), "x_attn": x[-1].clone(),
+                              "h": hh[-1].clone()})
             x = x + self._ffn(L, h)
+            if trace is not None and not self.hp.n_expert:
+                trace[-1]["x_ffn"] = x[-1].clone()
         x = self._rms(x, self.out_norm)
         if all_logits:
             return x @ self.output.T

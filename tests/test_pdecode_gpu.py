@@ -15,7 +15,7 @@ from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
 
 pytestmark = pytest.mark.gpu
 
-SPECS = ["pd-llama-g4", "pd-llama-g8"]
+SPECS = ["pd-llama-g4", "pd-llama-g8", "pd-llama-8b2"]
 
 
 @pytest.fixture(scope="module")
@@ -67,7 +67,8 @@ def test_pdecode_matches_launch_path(models, spec, monkeypatch):
     toks = [int(t) for t in rng.integers(3, 1000, 300)]
     for n in (20, 64, 65, 200, 299):
         for e in (on, off):
-            e.eval_logits(toks[:n], 0)
+            for p0 in range(0, n, 128):   # prefill in n_batch chunks
+                e.eval_logits(toks[p0:min(n, p0 + 128)], p0)
         for i in range(2):
             a = on.decode_logits(toks[n], n)
             b = off.decode_logits(toks[n], n)

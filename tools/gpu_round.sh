@@ -28,7 +28,10 @@ for s in "$@"; do
     variants) step variants 900 bash tools/gemv_variants.sh ;;
     profgemv) export TMPDIR=/tmp; step profgemv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profgemv -o gemv \
             --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
-    pdtest) step pdtest 300 python -u -m pytest tests/test_pdecode_gpu.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    pdtest) step pdtest 400 python -u -m pytest tests/test_pdecode_gpu.py -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    pddebug) step pddebug 300 python -u tools/pdecode_debug.py ;;
+    pddebug4) step pddebug4 300 python -u tools/pdecode_debug.py --spec pd-llama-g4 --n 100 ;;
+    pdtl) step pdtl 300 python -u tools/pdecode_timeline.py ;;
     pdcheck) step pdcheck 300 python -u tools/pdecode_check.py ;;
     pdcheck70) step pdcheck70 600 python -u tools/pdecode_check.py --model llama3-70b-q4_k_m --steps 16 ;;
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
