@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include "kernels/kernels.h"
+#include "kernels/pdecode.h"
 #include "runtime/engine.h"
 #include "runtime/repack.h"
 
@@ -129,6 +130,10 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("healthy", &Engine::healthy)
       .def_property_readonly("ffn_fused", &Engine::ffn_fused)
       .def_property_readonly("pdecode", &Engine::pdecode_status)
+      .def("pdecode_acct", [](Engine& e) {
+        std::vector<long long> v = e.pdecode_acct();
+        return py::array_t<long long>(v.size(), v.data());
+      })
       .def("pdecode_timeline", [](Engine& e) {
         std::vector<long long> v = e.pdecode_timeline();
         return py::array_t<long long>(v.size(), v.data());
@@ -158,6 +163,10 @@ PYBIND11_MODULE(_hip, m) {
         return d;
       });
 
+  m.def("pd_item_bench", [](int type, int rows, int K, int iters, int blocks, uintptr_t out, uintptr_t stream) {
+    pd_item_bench(type, rows, K, iters, blocks, reinterpret_cast<long long*>(out), S(stream));
+    hip_ok("pd_item_bench");
+  });
   m.def("nccl_unique_id", []() {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");

@@ -5,9 +5,9 @@
 // ~26 us of a 46 us Llama-3-8B layer in kernel boundaries, x prologues and
 // launch ramps/tails while HBM idled; the weight stream could not cross a
 // dependency edge. Here every CU owns a fixed slice of every projection and
-// ONE loader wave per CU streams that CU's weights for the whole token into an
+// two loader waves per CU stream that CU's weights for the whole token into an
 // LDS ring (global_load_lds, non-temporal) in consumption order, independent
-// of the activations. Seven consumer waves wait for activations at the
+// of the activations. Six consumer waves wait for activations at the
 // dependency edges while the ring keeps filling, so the weight stream runs
 // across every edge.
 //
@@ -30,6 +30,11 @@
 #include "kernels.h"
 
 namespace lfk {
+
+// workgroup geometry (one per CU): loader waves stream the ring, consumer waves compute
+static constexpr int kPdThreads = 512;
+static constexpr int kPdLoaderWaves = 2;
+static constexpr int kPdConsumerWaves = kPdThreads / 64 - kPdLoaderWaves;
 
 enum PdStage : int { PD_Q = 0, PD_K = 1, PD_V = 2, PD_WO = 3, PD_GATE = 4, PD_UP = 5, PD_DOWN = 6 };
 
@@ -81,18 +86,33 @@ struct PDecodeArgs {
   float* dbg = nullptr;
   // timeline: wall_clock64 stamps [ncu][n_layer][kPdStamps] (consumer stage ends, loader issue)
   long long* tl = nullptr;
+  // item timeline of layer 2: [ncu][kPdItemStamps][8]: loader issue, -, consumer wait start,
+  // item available, item released
+  long long* tli = nullptr;
+  // cycle accounting (LFK_PDECODE_ACCT=1): [ncu][16] shader-clock totals kept in registers and
+  // stored once at the end (no memory traffic inside the step): consumer wave 0: 0 item code,
+  // 1 waiting for ring items, 2 consumer barriers, 3 granule sweeps, 4 items, 5 attention,
+  // 6 merge, 7 whole; loader wave 0: 8 blocked on free slots, 9 waiting for landings, 10 issue
+  long long* acct = nullptr;
+  // experiments only (LFK_PDECODE_DBG): 1 = consumers release ring items without computing,
+  // 2 = the loader publishes items without loading them
+  int dbg_mode = 0;
 };
 static constexpr int kPdStamps = 12;
+static constexpr int kPdItemStamps = 48;
 
 size_t pdecode_lds_bytes(const PDecodeArgs& a);
 // every workgroup of the grid (one per CU) can be resident at once (host check)
 bool pdecode_resident(const PDecodeArgs& a);
-void pdecode(const PDecodeArgs& a, hipStream_t s);
+// a: host copy (launch geometry), a_dev: the same struct in device memory (what the kernel reads)
+void pdecode(const PDecodeArgs& a, const PDecodeArgs* a_dev, hipStream_t s);
 // copy rows_cu * ncu rows of a planar matrix into the ring row format: row i (source row
 // map ? map[i] : i) goes to CU i / rows_cu, slot i % rows_cu of the stage at stage_off
 void pd_pack_rows(uint8_t* region, uint32_t cu_bytes, uint32_t stage_off, int rows_cu, int ncu, const QMat& src,
                   const int* map_dev, hipStream_t s);
 LFK_HD size_t pd_dump_stride(const PDecodeArgs& a) { return (size_t)2 * a.nq + 2 * a.nkv + 2 * a.d + a.F; }
+// microbenchmark of the consumer item code alone: out[block * 8 + wave] = cycles per item
+void pd_item_bench(int type, int rows, int K, int iters, int blocks, long long* out, hipStream_t s);
 // ring row format size of one row
 uint32_t pd_row_bytes(int type, int K);
 

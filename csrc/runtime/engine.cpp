@@ -471,7 +471,7 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
 void Engine::enqueue_decode(hipStream_t s) {
   embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
   if (pdec_) {
-    pdecode(pda_, s);  // every layer in one launch
+    pdecode(pda_, pda_dev_, s);  // every layer in one launch
   } else {
     for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
   }

@@ -102,6 +102,7 @@ class Engine {
   std::vector<float> pdecode_dump();
   // LFK_PDECODE_TIMELINE=1: wall-clock stamps [CU][layer][kPdStamps] of the last step
   std::vector<long long> pdecode_timeline();
+  std::vector<long long> pdecode_acct();  // LFK_PDECODE_ACCT=1: cycle totals [CU][16]
   std::string last_error() const { return last_error_; }
   int n_ctx() const { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
@@ -191,8 +192,9 @@ class Engine {
   bool ffn_fused_ = false;    // dense decode FFN as one fused launch (ffn_fused.hip)
   bool pdec_ = false;         // decode layers as ONE persistent launch (pdecode.hip)
   PDecodeArgs pda_;
+  PDecodeArgs* pda_dev_ = nullptr;
   std::string pdec_status_;
-  size_t pd_dump_n_ = 0, pd_tl_n_ = 0;
+  size_t pd_dump_n_ = 0, pd_tl_n_ = 0, pd_acct_n_ = 0;
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 

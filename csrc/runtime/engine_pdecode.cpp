@@ -48,7 +48,7 @@ std::string Engine::setup_pdecode() {
   for (int l = 0; l < hp_.n_layer; ++l) {
     const Layer& L = layers_[l];
     for (const QMat* m : {&L.wq, &L.wk, &L.wv, &L.wo, &L.w_gu, &L.w_down})
-      if (!pd_type_ok(m->type) || (m->type != T_Q8_0 && m->K % 256)) return "weight type";
+      if (!pd_type_ok(m->type) || m->K % 256) return "weight type";
   }
 
   PDecodeArgs a;
@@ -56,18 +56,27 @@ std::string Engine::setup_pdecode() {
   a.ncu = ncu; a.cpg = cpg; a.nxu = nxu; a.nqu = nqu; a.nku = nku; a.nfu = nfu;
   a.smax = cpg - G;
   a.eps = hp_.rms_eps; a.attn_scale = 1.f / std::sqrt((float)hd);
-  a.slot_bytes = 32 * 1024;
+  a.slot_bytes = 16 * 1024;
   // LDS carve
   const int actn = (std::max(std::max(d, nq), F) + 63) & ~63;
   const int act_norm = actn + actn / 2 + ncu * 4;
   const int act_att = G * hd * 2 + 2 * hd * 2 + 4 * 16 * (hd + 8) * 2 + 4 * G * 16 * 4 + 2 * 4 * G * 4 + 4 * G * hd * 4;
   a.act_bytes = (std::max(act_norm, act_att) + 15) & ~15;
-  auto nblk = [](int K) { return ((K / 32) + 63) / 64; };
-  a.part_floats = std::max({(nqu + 2 * nku) * nblk(d), nxu * nblk(nq), 2 * nfu * nblk(d), nxu * nblk(F)});
-  const size_t fixed = 64 + 256 + ((a.part_floats * 4 + 15) & ~15) + a.act_bytes;
+  // per-CU stage partials [row][block group] (kernel: stage_map)
+  auto ngroup = [](int K) {
+    const int nblk = ((K / 32) + 63) / 64;
+    const int wpb = std::max(1, kPdConsumerWaves / nblk);
+    return kPdConsumerWaves / wpb;
+  };
+  for (int K : {d, nq, F}) {
+    const int nblk = ((K / 32) + 63) / 64;
+    if (nblk > 2 * ngroup(K)) return "activation longer than two blocks per consumer wave";
+  }
+  a.part_floats = std::max({(nqu + 2 * nku) * ngroup(d), nxu * ngroup(nq), 2 * nfu * ngroup(d), nxu * ngroup(F)});
+  const size_t fixed = 128 + 256 + ((a.part_floats * 4 + 15) & ~15) + a.act_bytes;
   const size_t lds_max = 160 * 1024;
   if (fixed + 3 * (size_t)a.slot_bytes > lds_max) return "LDS";
-  a.nslot = (int)std::min<size_t>(6, (lds_max - fixed) / a.slot_bytes);
+  a.nslot = (int)std::min<size_t>(8, (lds_max - fixed) / a.slot_bytes);
   a.res_rows = 0;
 
   // ---- item tables + region layout
@@ -87,10 +96,9 @@ std::string Engine::setup_pdecode() {
     for (const StageSpec& s : st) {
       const uint32_t rb = pd_row_bytes(s.m->type, s.m->K);
       if (rb == 0 || rb > (uint32_t)a.slot_bytes) return "row larger than a ring slot";
-      // the loader keeps two items in flight and counts their transfers with vmcnt, a 6-bit
-      // counter: two items together must stay below 64 one-KiB transfers (measured: 32 + 32
-      // KiB items fed stale ring bytes to the consumers)
-      const int item_max = std::min(a.slot_bytes, 31 * 1024);
+      // the loader keeps up to four items in flight and counts their transfers with vmcnt, a
+      // 6-bit counter: together they must stay below 64 one-KiB transfers
+      const int item_max = std::min(a.slot_bytes, 15 * 1024);
       const int per_slot = item_max / (int)rb;
       if (per_slot < 1) return "row larger than a ring item";
       const int nit = (s.rows_cu + per_slot - 1) / per_slot;
@@ -104,7 +112,7 @@ std::string Engine::setup_pdecode() {
         it.dma_kb = (uint16_t)(((size_t)(r1 - r0) * rb + 1023) / 1024);
         it.stage = (uint8_t)s.stage;
         it.type = (uint8_t)s.m->type;
-        if (it.dma_kb * 1024 > a.slot_bytes || it.dma_kb > 31) return "item exceeds a ring slot";
+        if (it.dma_kb * 1024 > a.slot_bytes || it.dma_kb > 15) return "item exceeds a ring slot";
         items.push_back(it);
       }
       off += (size_t)s.rows_cu * rb;
@@ -180,9 +188,16 @@ std::string Engine::setup_pdecode() {
   a.pos = state_ + S_POS;
   a.err = dev_err_;
   if (!pdecode_resident(a)) return "one workgroup per CU is not resident";
+  if (const char* dm = std::getenv("LFK_PDECODE_DBG")) a.dbg_mode = std::atoi(dm);
+  if (const char* ac = std::getenv("LFK_PDECODE_ACCT"); ac && ac[0] == '1') {
+    pd_acct_n_ = (size_t)ncu * 16;
+    a.acct = static_cast<long long*>(dalloc(sizeof(long long) * pd_acct_n_));
+    HIPCHK(hipMemsetAsync(a.acct, 0, sizeof(long long) * pd_acct_n_, stream_));
+  }
   if (const char* tm = std::getenv("LFK_PDECODE_TIMELINE"); tm && tm[0] == '1') {
-    pd_tl_n_ = (size_t)ncu * hp_.n_layer * kPdStamps;
+    pd_tl_n_ = (size_t)ncu * hp_.n_layer * kPdStamps + (size_t)ncu * kPdItemStamps * 8;
     a.tl = static_cast<long long*>(dalloc(sizeof(long long) * pd_tl_n_));
+    a.tli = a.tl + (size_t)ncu * hp_.n_layer * kPdStamps;
     HIPCHK(hipMemsetAsync(a.tl, 0, sizeof(long long) * pd_tl_n_, stream_));
   }
   if (const char* dm = std::getenv("LFK_PDECODE_DUMP"); dm && dm[0] == '1') {
@@ -190,6 +205,8 @@ std::string Engine::setup_pdecode() {
     a.dbg = static_cast<float*>(dalloc(sizeof(float) * pd_dump_n_));
     HIPCHK(hipMemsetAsync(a.dbg, 0, sizeof(float) * pd_dump_n_, stream_));
   }
+  pda_dev_ = static_cast<PDecodeArgs*>(dalloc(sizeof(PDecodeArgs)));
+  HIPCHK(hipMemcpyAsync(pda_dev_, &a, sizeof(PDecodeArgs), hipMemcpyHostToDevice, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   pda_ = a;
   pdec_ = true;
@@ -197,6 +214,15 @@ std::string Engine::setup_pdecode() {
     std::fprintf(stderr, "[lfk] persistent decode: %d CUs, ring %d x %d KiB, %zu items, %.2f GB ring-format weights\n",
                  ncu, a.nslot, a.slot_bytes / 1024, items.size(), total / 1e9);
   return "on";
+}
+
+std::vector<long long> Engine::pdecode_acct() {
+  std::vector<long long> out(pd_acct_n_);
+  if (pd_acct_n_) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(out.data(), pda_.acct, sizeof(long long) * pd_acct_n_, hipMemcpyDeviceToHost));
+  }
+  return out;
 }
 
 std::vector<long long> Engine::pdecode_timeline() {
