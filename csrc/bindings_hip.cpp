@@ -67,6 +67,11 @@ PYBIND11_MODULE(_hip, m) {
             o.presence_penalty = sp.contains("presence_penalty") ? sp["presence_penalty"].cast<float>() : 0.f;
             o.last_n = sp.contains("last_n") ? sp["last_n"].cast<int>() : 64;
             o.seed = sp.contains("seed") ? sp["seed"].cast<unsigned long long>() : 0ull;
+            o.tfs_z = sp.contains("tfs_z") ? sp["tfs_z"].cast<float>() : 1.f;
+            o.typical_p = sp.contains("typical_p") ? sp["typical_p"].cast<float>() : 1.f;
+            if (sp.contains("logit_bias"))
+              for (auto kv : sp["logit_bias"].cast<py::dict>())
+                o.logit_bias.emplace_back(kv.first.cast<int>(), kv.second.cast<float>());
             std::function<bool()> pf;
             std::function<void(int)> tf;
             if (!poll.is_none()) pf = [poll]() { py::gil_scoped_acquire g; return poll().cast<bool>(); };
@@ -333,12 +338,21 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ci"), py::arg("out_tokens"), py::arg("out_cap"), py::arg("advance"), py::arg("stream"), py::arg("ct"),
      py::arg("dbg_clk") = 0);
   m.def("sampler_params_bytes", [](int top_k, float top_p, float min_p, float temp, float rp, float fp, float pp,
-                                   int last_n, unsigned long long seed, int greedy) {
+                                   int last_n, unsigned long long seed, int greedy, float tfs_z, float typical_p,
+                                   py::dict logit_bias) {
     SamplerParamsDev p;
     p.top_k = top_k; p.top_p = top_p; p.min_p = min_p; p.temp = temp; p.repeat_penalty = rp;
     p.freq_penalty = fp; p.presence_penalty = pp; p.last_n = last_n; p.seed = seed; p.greedy = greedy;
+    p.tfs_z = tfs_z; p.typical_p = typical_p;
+    for (auto kv : logit_bias) {
+      if (p.n_bias == kMaxLogitBias) throw std::runtime_error("at most 64 logit_bias entries");
+      p.bias_tok[p.n_bias] = kv.first.cast<int>();
+      p.bias_val[p.n_bias++] = kv.second.cast<float>();
+    }
     return py::bytes(reinterpret_cast<const char*>(&p), sizeof(p));
-  });
+  }, py::arg("top_k"), py::arg("top_p"), py::arg("min_p"), py::arg("temp"), py::arg("rp"), py::arg("fp"),
+     py::arg("pp"), py::arg("last_n"), py::arg("seed"), py::arg("greedy"), py::arg("tfs_z") = 1.f,
+     py::arg("typical_p") = 1.f, py::arg("logit_bias") = py::dict());
   m.def("fill_random", [](uintptr_t base, int type, size_t rows, size_t K, float std, unsigned long long seed,
                           uintptr_t stream) {
     fill_random_planar(P<uint8_t>(base), type, rows, K, std, seed, S(stream));

@@ -226,14 +226,18 @@ void clock_probe(long long* out, int iters, hipStream_t s);
 // ---------------------------------------------------------------- sampling
 // Sampling parameters live in DEVICE memory so a captured decode graph serves
 // every request unchanged (they are written once per request, before replay).
+static constexpr int kMaxLogitBias = 64;  // logit-bias entries applied by sampler stage 1
 struct SamplerParamsDev {
   int top_k = 40;
   int last_n = 64;
   int greedy = 0;
-  int pad = 0;
+  int n_bias = 0;                  // entries of bias_tok/bias_val in use (distinct tokens)
   float top_p = 0.95f, min_p = 0.05f, temp = 0.8f;
   float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
+  float tfs_z = 1.f, typical_p = 1.f;  // tail-free / locally-typical (1 = off)
   unsigned long long seed = 0;
+  int bias_tok[kMaxLogitBias] = {};
+  float bias_val[kMaxLogitBias] = {};
 };
 // Device state block (ints) shared by the decode kernels.
 enum StateIdx : int { S_TOKEN = 0, S_POS = 1, S_STEP = 2, S_RING_LEN = 3, S_RING_HEAD = 4, S_NOUT = 5, S_NSTATE = 8 };

@@ -115,14 +115,22 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
     v[e] = i < a.V ? a.logits[i] : -FLT_MAX;
     idx[e] = i;
   }
-  // ---- penalties (window = last min(ring_len, last_n) tokens)
+  // ---- logit bias (lane j holds entry j; distinct tokens), then the penalties
+  // (window = last min(ring_len, last_n) tokens) on the biased values
+  const int nbias = P.n_bias;
+  const int bt = lane < nbias ? P.bias_tok[lane] : -1;
+  const bool bmine = bt >= lo && bt < lo + SLICE && bt < a.V;
   const int rlen = a.state[S_RING_LEN], rhead = a.state[S_RING_HEAD];
   const int wn = min(rlen, P.last_n);
   const int t = lane < wn ? a.ring[(rhead - wn + lane + 64) & 63] : -1;
   const bool mine = t >= lo && t < lo + SLICE && t < a.V;
-  if (__ballot(mine)) {  // wave-uniform: some window token lies in this slice
+  if (__ballot(mine) | __ballot(bmine)) {  // wave-uniform: a window or bias token lies in this slice
 #pragma unroll
     for (int e = 0; e < NE1; ++e) sl[64 * e + lane] = v[e];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (bmine) sl[bt - lo] += P.bias_val[lane];
     int cnt = 0;
     bool first = true;
     for (int j = 0; j < wn; ++j) {
@@ -132,7 +140,9 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
         if (j < lane) first = false;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (mine && first) {
       float l = sl[t - lo];
       l = l <= 0.f ? l * P.repeat_penalty : l / P.repeat_penalty;
@@ -165,6 +175,65 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
     a.cand_tau[blockIdx.x] = __float_as_uint(m >= K && nvalid >= K ? T : -FLT_MAX);
     a.cand_tau[gridDim.x + blockIdx.x] = __float_as_uint(vmax);
   }
+}
+
+// inclusive wave prefix sum (64 lanes)
+__device__ __forceinline__ float wave_scan(float x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(x, o);
+    if (lane >= o) x += t;
+  }
+  return x;
+}
+
+// Tail-free (llama_sample_tail_free, min_keep 1) on m > 2 candidates held one per
+// lane, sorted by descending logit: normalised |second derivative| of the
+// temperature-1 probabilities; keep the first i tokens where i >= 1 is the first
+// index whose running sum exceeds z.
+__device__ __forceinline__ int tail_free_cut(float v, int m, float z) {
+  const int lane = threadIdx.x & 63;
+  const float v0 = __shfl(v, 0);
+  const float e = lane < m ? expf(v - v0) : 0.f;
+  const float p = e / wave_sum_fast(e);
+  const float p1 = __shfl(p, min(lane + 1, 63));
+  const float d1 = p - p1;                       // valid for lane < m-1
+  const float d1n = __shfl(d1, min(lane + 1, 63));
+  const bool ok = lane < m - 2;
+  float d2 = ok ? fabsf(d1 - d1n) : 0.f;
+  const float s = wave_sum_fast(d2);
+  d2 = ok ? (s > 1e-6f ? d2 / s : 1.f / (float)(m - 2)) : 0.f;
+  const float cum = wave_scan(d2);
+  const unsigned long long hit = __ballot(ok && lane >= 1 && cum > z);
+  return hit ? (int)__ffsll((long long)hit) - 1 : m;
+}
+
+// Locally typical (llama_sample_typical, min_keep 1): rank the m candidates by
+// |surprise - entropy| (ties by position), keep them in that order until the
+// kept mass exceeds tp; the kept set is compacted back into descending-logit
+// order in lanes [0, new m). Returns the new m.
+__device__ __forceinline__ int typical_keep(float& v, int& id, int m, float tp) {
+  const int lane = threadIdx.x & 63;
+  const float v0 = __shfl(v, 0);
+  const float e = lane < m ? expf(v - v0) : 0.f;
+  const float p = e / wave_sum_fast(e);
+  const float lp = lane < m ? logf(fmaxf(p, 1e-30f)) : 0.f;
+  const float ent = -wave_sum_fast(lane < m ? p * lp : 0.f);
+  const float sh = lane < m ? fabsf(-lp - ent) : FLT_MAX;
+  float before = 0.f;  // mass of the candidates ranked ahead of this one
+  for (int j = 0; j < m; ++j) {
+    const float sj = __shfl(sh, j);
+    const float pj = __shfl(p, j);
+    if (sj < sh || (sj == sh && j < lane)) before += pj;
+  }
+  const unsigned long long keep = __ballot(lane < m && before <= tp);
+  const int kept = __popcll(keep);
+  const bool k = (keep >> lane) & 1ull;
+  const int dst = k ? lanes_below(keep) : kept + lanes_below(~keep);
+  v = __int_as_float(__builtin_amdgcn_ds_permute(dst << 2, __float_as_int(v)));
+  id = __builtin_amdgcn_ds_permute(dst << 2, id);
+  return max(kept, 1);
 }
 
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
@@ -273,6 +342,8 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
     }
   }
   m = min(m, K);
+  if (!P.greedy && m > 2 && P.tfs_z < 1.f) m = tail_free_cut(vv, m, P.tfs_z);
+  if (!P.greedy && m > 1 && P.typical_p < 1.f) m = typical_keep(vv, id, m, P.typical_p);
   const float v_ = vv;
   int tok;
   if (P.greedy || m <= 1) {

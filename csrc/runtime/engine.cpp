@@ -594,6 +594,15 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   p.repeat_penalty = sp.repeat_penalty; p.freq_penalty = sp.freq_penalty; p.presence_penalty = sp.presence_penalty;
   p.last_n = std::min(sp.last_n, 64);
   p.seed = sp.seed;
+  p.tfs_z = sp.tfs_z; p.typical_p = sp.typical_p;
+  if ((int)sp.logit_bias.size() > kMaxLogitBias) throw std::runtime_error("GPU sampler: at most 64 logit_bias entries");
+  for (const auto& [t, b] : sp.logit_bias) {
+    if (t < 0 || t >= hp_.n_vocab) continue;  // out-of-vocabulary entries are ignored (as upstream)
+    for (int j = 0; j < p.n_bias; ++j)
+      if (p.bias_tok[j] == t) throw std::runtime_error("GPU sampler: duplicate logit_bias token");
+    p.bias_tok[p.n_bias] = t;
+    p.bias_val[p.n_bias++] = b;
+  }
   int hstate[S_NSTATE] = {0};
   int hring[64] = {0};
   const int rl = std::min(n_prompt, 64);

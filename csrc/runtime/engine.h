@@ -50,6 +50,8 @@ struct SamplingOpts {
   float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
   int last_n = 64;
   unsigned long long seed = 0;
+  float tfs_z = 1.f, typical_p = 1.f;
+  std::vector<std::pair<int, float>> logit_bias;  // distinct tokens, at most kMaxLogitBias
 };
 
 struct GenOut {

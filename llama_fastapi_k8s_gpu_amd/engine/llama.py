@@ -141,16 +141,8 @@ class Llama:
             c()
 
     # ------------------------------------------------------------ generation
-    def _generate(self, prompt_tokens: List[int], max_tokens: Optional[int], params: SamplingParams,
-                  stop: List[str], cancel_event: Optional[threading.Event], on_token=None):
-        n_prompt = len(prompt_tokens)
-        if n_prompt >= self._n_ctx:
-            raise ValueError(f"Requested tokens ({n_prompt}) exceed context window of {self._n_ctx}")
-        if max_tokens is None or max_tokens <= 0:
-            max_tokens = self._n_ctx - n_prompt
-        if max_tokens + n_prompt >= self._n_ctx:
-            max_tokens = self._n_ctx - n_prompt
-        # special-token stop strings become stop ids; the rest are matched on text
+    def _text_stops(self, stop: List[str]):
+        """Special-token stop strings become stop ids; the rest are matched on text."""
         stop_ids = set(self.tokenizer.eog_ids)
         text_stops = []
         for s in stop:
@@ -159,6 +151,19 @@ class Llama:
                 stop_ids.add(tid)
             elif s:
                 text_stops.append(s)
+        return stop_ids, text_stops
+
+    def _generate(self, prompt_tokens: List[int], max_tokens: Optional[int], params: SamplingParams,
+                  stop: List[str], cancel_event: Optional[threading.Event], on_token=None,
+                  stopping_criteria=None):
+        n_prompt = len(prompt_tokens)
+        if n_prompt >= self._n_ctx:
+            raise ValueError(f"Requested tokens ({n_prompt}) exceed context window of {self._n_ctx}")
+        if max_tokens is None or max_tokens <= 0:
+            max_tokens = self._n_ctx - n_prompt
+        if max_tokens + n_prompt >= self._n_ctx:
+            max_tokens = self._n_ctx - n_prompt
+        stop_ids, text_stops = self._text_stops(stop)
         # KV prefix reuse (must re-evaluate at least one prompt token for logits)
         n_keep = 0
         for a, b in zip(self._kv_tokens, prompt_tokens):
@@ -166,10 +171,38 @@ class Llama:
                 break
             n_keep += 1
         n_keep = min(n_keep, n_prompt - 1)
-        poll = cancel_event.is_set if cancel_event is not None else None
+        # upstream stops as soon as a stop string appears in the generated text (or a
+        # stopping criterion fires): watch the token stream and end the backend's loop
+        # through its cancel poll
+        hit = {"stop": False}
+        stops_b = [s.encode("utf-8") for s in text_stops]
+        maxlen = max((len(b) for b in stops_b), default=0)
+        buf = bytearray()
+        gen: List[int] = []
+
+        def watch(t: int):
+            gen.append(t)
+            if stops_b and t not in stop_ids:
+                piece = self.tokenizer.detokenize_bytes([t], False)
+                buf.extend(piece)
+                region = bytes(buf[max(0, len(buf) - len(piece) - maxlen + 1):])
+                if any(b in region for b in stops_b):
+                    hit["stop"] = True
+            if stopping_criteria is not None and not hit["stop"]:
+                import numpy as np
+                if stopping_criteria(np.asarray(list(prompt_tokens) + gen, np.int64), None):
+                    hit["stop"] = True
+            if on_token:
+                on_token(t)
+
+        def poll():
+            return hit["stop"] or (cancel_event is not None and cancel_event.is_set())
+        watched = bool(stops_b) or stopping_criteria is not None
         with self._lock:
-            res: GenerationResult = self._backend.generate(prompt_tokens, n_keep, max_tokens, params,
-                                                           sorted(stop_ids), poll=poll, on_token=on_token)
+            res: GenerationResult = self._backend.generate(
+                prompt_tokens, n_keep, max_tokens, params, sorted(stop_ids),
+                poll=poll if (watched or cancel_event is not None) else None,
+                on_token=watch if (watched or on_token) else None)
             hist = list(prompt_tokens) + list(res.tokens)
             self._kv_tokens = hist[:res.n_evaluated]
         toks = list(res.tokens)
@@ -177,123 +210,278 @@ class Llama:
         if toks and toks[-1] in stop_ids:
             toks = toks[:-1]
             reason = "stop"
+        if hit["stop"] and reason == "cancelled":
+            reason = "stop"
         text = self.detokenize(toks).decode("utf-8", errors="replace")
-        for s in text_stops:
-            i = text.find(s)
-            if i >= 0:
-                text = text[:i]
-                reason = "stop"
+        cut = min((i for i in (text.find(s) for s in text_stops) if i >= 0), default=-1)
+        if cut >= 0:
+            text = text[:cut]
+            reason = "stop"
         return text, toks, reason, res
 
     def _params(self, temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
-                frequency_penalty, presence_penalty, seed) -> SamplingParams:
+                frequency_penalty, presence_penalty, seed, logit_bias=None, mirostat_mode=0,
+                mirostat_tau=5.0, mirostat_eta=0.1, n_probs=0, logits_processor=None) -> SamplingParams:
         if seed is None:
             self._n_requests += 1
             seed = (self._seed * 1000003 + self._n_requests) & 0xFFFFFFFF
+        bias = {int(k): float(v) for k, v in (logit_bias or {}).items()}
         return SamplingParams(temperature=temperature, top_k=top_k, top_p=top_p, min_p=min_p,
                               typical_p=typical_p, tfs_z=tfs_z, repeat_penalty=repeat_penalty,
                               frequency_penalty=frequency_penalty, presence_penalty=presence_penalty,
-                              last_n=self.last_n_tokens_size, seed=int(seed))
+                              last_n=self.last_n_tokens_size, seed=int(seed), logit_bias=bias,
+                              mirostat_mode=int(mirostat_mode or 0), mirostat_tau=float(mirostat_tau),
+                              mirostat_eta=float(mirostat_eta), n_probs=int(n_probs or 0),
+                              logits_processor=logits_processor)
 
-    def create_completion(self, prompt: Union[str, List[int]], max_tokens: Optional[int] = 16,
-                          temperature: float = 0.8, top_p: float = 0.95, min_p: float = 0.05,
-                          typical_p: float = 1.0, stop: Optional[Union[str, List[str]]] = None,
+    @staticmethod
+    def logits_to_logprobs(logits, axis: int = -1):
+        """Natural-log softmax (``llama_cpp.Llama.logits_to_logprobs``)."""
+        import numpy as np
+        l = np.asarray(logits, np.float32)
+        m = np.max(l, axis=axis, keepdims=True)
+        return (l - m - np.log(np.sum(np.exp(l - m), axis=axis, keepdims=True))).astype(np.float32)
+
+    def _piece(self, t: int) -> str:
+        return self.detokenize([t]).decode("utf-8", errors="ignore")
+
+    def _completion_logprobs(self, prompt_tokens: List[int], toks: List[int], res: GenerationResult, echo: bool,
+                             prompt_text: str):
+        """The OpenAI / llama-cpp-python ``logprobs`` block. Generated tokens carry the
+        log-probabilities of the raw model logits; echoed prompt tokens carry None (the
+        engine keeps only the last prompt position's logits - upstream needs
+        ``logits_all=True`` for those)."""
+        entries = list(res.logprobs or [])[:len(toks)]
+        all_toks = (list(prompt_tokens) if echo else []) + list(toks)
+        strs = [self._piece(t) for t in all_toks]
+        offset = 0 if echo else len(prompt_text)
+        out = {"tokens": [], "text_offset": [], "token_logprobs": [], "top_logprobs": []}
+        n_echo = len(all_toks) - len(toks)
+        run = 0
+        for i, (t, ts) in enumerate(zip(all_toks, strs)):
+            if echo and i == 0 and t == self.tokenizer.bos_id:
+                continue
+            out["tokens"].append(ts)
+            out["text_offset"].append(offset + run)
+            run += len(ts)
+            if i < n_echo:
+                out["token_logprobs"].append(None)
+                out["top_logprobs"].append(None)
+                continue
+            lp, top = entries[i - n_echo] if i - n_echo < len(entries) else (None, [])
+            out["token_logprobs"].append(lp)
+            d = {self._piece(j): v for j, v in top}
+            if lp is not None:
+                d[ts] = lp
+            out["top_logprobs"].append(d)
+        return out
+
+    def create_completion(self, prompt: Union[str, List[int]], suffix: Optional[str] = None,
+                          max_tokens: Optional[int] = 16, temperature: float = 0.8, top_p: float = 0.95,
+                          min_p: float = 0.05, typical_p: float = 1.0, logprobs: Optional[int] = None,
+                          echo: bool = False, stop: Optional[Union[str, List[str]]] = None,
                           frequency_penalty: float = 0.0, presence_penalty: float = 0.0,
                           repeat_penalty: float = 1.1, top_k: int = 40, stream: bool = False,
-                          seed: Optional[int] = None, tfs_z: float = 1.0,
+                          seed: Optional[int] = None, tfs_z: float = 1.0, mirostat_mode: int = 0,
+                          mirostat_tau: float = 5.0, mirostat_eta: float = 0.1, model: Optional[str] = None,
+                          stopping_criteria=None, logits_processor=None, grammar=None,
+                          logit_bias: Optional[Dict[int, float]] = None,
                           cancel_event: Optional[threading.Event] = None, add_bos: bool = True,
                           **unused) -> Union[Dict[str, Any], Iterator[Dict[str, Any]]]:
+        if grammar is not None:
+            raise NotImplementedError("grammar-constrained sampling is not supported by this engine")
+        if suffix:
+            raise NotImplementedError("infill (suffix) is not supported by this engine")
         if isinstance(prompt, str):
+            prompt_text = prompt
             tokens = self.tokenize(prompt, add_bos=add_bos, special=True)
         else:
             tokens = list(prompt)
+            prompt_text = self.detokenize(tokens).decode("utf-8", errors="replace")
         stops = [stop] if isinstance(stop, str) else list(stop or [])
         params = self._params(temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
-                              frequency_penalty, presence_penalty, seed)
+                              frequency_penalty, presence_penalty, seed, logit_bias, mirostat_mode,
+                              mirostat_tau, mirostat_eta, logprobs, logits_processor)
         cid = f"cmpl-{uuid.uuid4()}"
+        mname = model or self.model_path
         if stream:
-            return self._stream(cid, tokens, max_tokens, params, stops, cancel_event)
-        text, toks, reason, res = self._generate(tokens, max_tokens, params, stops, cancel_event)
+            return self._stream(cid, tokens, max_tokens, params, stops, cancel_event, mname,
+                                echo_text=prompt_text if echo else None, stopping_criteria=stopping_criteria)
+        text, toks, reason, res = self._generate(tokens, max_tokens, params, stops, cancel_event,
+                                                 stopping_criteria=stopping_criteria)
+        lp = self._completion_logprobs(tokens, toks, res, echo, prompt_text) if params.n_probs > 0 else None
         return {"id": cid, "object": "text_completion", "created": int(time.time()),
-                "model": self.model_path,
-                "choices": [{"text": text, "index": 0, "logprobs": None, "finish_reason": reason}],
+                "model": mname,
+                "choices": [{"text": (prompt_text + text) if echo else text, "index": 0, "logprobs": lp,
+                             "finish_reason": reason}],
                 "usage": {"prompt_tokens": len(tokens), "completion_tokens": len(res.tokens),
                           "total_tokens": len(tokens) + len(res.tokens)},
                 "timings": {"prefill_s": res.prefill_s, "decode_s": res.decode_s,
                             "n_prefilled": res.n_prefilled}}
 
-    def _stream(self, cid, tokens, max_tokens, params, stops, cancel_event):
+    __call__ = create_completion
+
+    def _stream(self, cid, tokens, max_tokens, params, stops, cancel_event, mname=None, echo_text=None,
+                stopping_criteria=None):
+        """Chunks as tokens arrive. Text that could still become a stop string is held
+        back until it cannot (upstream behaviour); a stop string ends the stream and
+        the generation."""
         import queue as _q
+        mname = mname or self.model_path
         q: "_q.Queue" = _q.Queue()
         done = object()
         box = {}
+        stop_now = threading.Event()
+        ev = _AnyEvent(cancel_event, stop_now)
+        lps: List[Any] = []
+        if params.n_probs > 0:
+            params.logprob_cb = lps.append
 
         def run():
             try:
-                box["r"] = self._generate(tokens, max_tokens, params, stops, cancel_event,
-                                          on_token=lambda t: q.put(t))
+                box["r"] = self._generate(tokens, max_tokens, params, stops, ev, on_token=lambda t: q.put(t),
+                                          stopping_criteria=stopping_criteria)
             except BaseException as e:  # surfaced to the consumer
                 box["e"] = e
             q.put(done)
         th = threading.Thread(target=run, daemon=True)
         th.start()
+        _, text_stops = self._text_stops(stops)
+
+        def chunk(text, reason=None, lp=None):
+            return {"id": cid, "object": "text_completion", "created": int(time.time()), "model": mname,
+                    "choices": [{"text": text, "index": 0, "logprobs": lp, "finish_reason": reason}]}
+        if echo_text:
+            yield chunk(echo_text)
         pending: List[int] = []
-        emitted = ""
+        text_all, emitted, n_tok = "", 0, 0
+        stopped = False
         while True:
             t = q.get()
             if t is done:
                 break
-            if t in self.tokenizer.eog_ids:
+            if stopped or t in self.tokenizer.eog_ids:
                 continue
+            n_tok += 1
             pending.append(t)
-            text = self.detokenize(pending).decode("utf-8", errors="ignore")
-            if text and not text.endswith("�"):
-                emitted += text
-                pending = []
-                yield {"id": cid, "object": "text_completion", "created": int(time.time()),
-                       "model": self.model_path,
-                       "choices": [{"text": text, "index": 0, "logprobs": None, "finish_reason": None}]}
+            raw = self.detokenize(pending)
+            try:
+                piece = raw.decode("utf-8")
+            except UnicodeDecodeError:      # a multi-byte character split across tokens
+                if len(pending) < 4:
+                    continue
+                piece = raw.decode("utf-8", errors="replace")
+            pending = []
+            if not piece:
+                continue
+            text_all += piece
+            cut = min((i for i in (text_all.find(s) for s in text_stops) if i >= 0), default=-1)
+            if cut >= 0:
+                stopped = True
+                stop_now.set()
+                if cut > emitted:
+                    yield chunk(text_all[emitted:cut])
+                emitted = cut
+                continue
+            hold = 0   # longest suffix that is a proper prefix of some stop string
+            for s in text_stops:
+                for k in range(min(len(s) - 1, len(text_all)), 0, -1):
+                    if text_all.endswith(s[:k]):
+                        hold = max(hold, k)
+                        break
+            safe = len(text_all) - hold
+            if safe > emitted:
+                lp = None
+                if params.n_probs > 0 and n_tok <= len(lps):
+                    l, top = lps[n_tok - 1]
+                    lp = {"tokens": [piece], "text_offset": [emitted], "token_logprobs": [l],
+                          "top_logprobs": [{self._piece(j): v for j, v in top}]}
+                yield chunk(text_all[emitted:safe], lp=lp)
+                emitted = safe
         th.join()
         if "e" in box:
             raise box["e"]
         _, _, reason, _ = box["r"]
-        yield {"id": cid, "object": "text_completion", "created": int(time.time()), "model": self.model_path,
-               "choices": [{"text": "", "index": 0, "logprobs": None, "finish_reason": reason}]}
+        if stopped:
+            reason = "stop"
+        elif emitted < len(text_all):
+            yield chunk(text_all[emitted:])
+        yield chunk("", reason)
 
-    def create_chat_completion(self, messages: List[Dict[str, str]], temperature: float = 0.2,
+    def create_chat_completion(self, messages: List[Dict[str, str]], functions=None, function_call=None,
+                               tools=None, tool_choice=None, temperature: float = 0.2,
                                top_p: float = 0.95, top_k: int = 40, min_p: float = 0.05,
                                typical_p: float = 1.0, stream: bool = False,
                                stop: Optional[Union[str, List[str]]] = None, seed: Optional[int] = None,
-                               max_tokens: Optional[int] = None, presence_penalty: float = 0.0,
-                               frequency_penalty: float = 0.0, repeat_penalty: float = 1.1,
-                               tfs_z: float = 1.0, cancel_event: Optional[threading.Event] = None,
-                               **unused):
+                               response_format=None, max_tokens: Optional[int] = None,
+                               presence_penalty: float = 0.0, frequency_penalty: float = 0.0,
+                               repeat_penalty: float = 1.1, tfs_z: float = 1.0, mirostat_mode: int = 0,
+                               mirostat_tau: float = 5.0, mirostat_eta: float = 0.1, model: Optional[str] = None,
+                               logits_processor=None, grammar=None, logit_bias: Optional[Dict[int, float]] = None,
+                               logprobs: Optional[bool] = None, top_logprobs: Optional[int] = None,
+                               cancel_event: Optional[threading.Event] = None, **unused):
+        if grammar is not None:
+            raise NotImplementedError("grammar-constrained sampling is not supported by this engine")
+        if functions or tools:
+            raise NotImplementedError("function / tool calling needs a chat handler this engine does not ship")
         fr = self._formatter(messages)
         stops = [stop] if isinstance(stop, str) else list(stop or [])
         if fr.stop:
             stops += [fr.stop] if isinstance(fr.stop, str) else list(fr.stop)
         tokens = self.tokenize(fr.prompt, add_bos=not fr.added_special, special=True)
+        n_probs = (top_logprobs or 0) if logprobs else 0
+        if logprobs and not n_probs:
+            n_probs = 1   # the chosen token's log-probability is reported either way
         params = self._params(temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
-                              frequency_penalty, presence_penalty, seed)
+                              frequency_penalty, presence_penalty, seed, logit_bias, mirostat_mode,
+                              mirostat_tau, mirostat_eta, n_probs, logits_processor)
         cid = f"chatcmpl-{uuid.uuid4()}"
+        mname = model or self.model_path
         if stream:
             def gen():
                 first = True
-                for chunk in self._stream(cid, tokens, max_tokens, params, stops, cancel_event):
+                for chunk in self._stream(cid, tokens, max_tokens, params, stops, cancel_event, mname):
                     c = chunk["choices"][0]
                     delta = {"role": "assistant"} if first else {}
                     first = False
                     if c["text"]:
                         delta["content"] = c["text"]
                     yield {"id": cid, "object": "chat.completion.chunk", "created": chunk["created"],
-                           "model": self.model_path,
-                           "choices": [{"index": 0, "delta": delta, "finish_reason": c["finish_reason"]}]}
+                           "model": mname,
+                           "choices": [{"index": 0, "delta": delta, "logprobs": _chat_logprobs(c["logprobs"], top_logprobs),
+                                        "finish_reason": c["finish_reason"]}]}
             return gen()
         text, toks, reason, res = self._generate(tokens, max_tokens, params, stops, cancel_event)
-        return {"id": cid, "object": "chat.completion", "created": int(time.time()), "model": self.model_path,
+        lp = None
+        if logprobs:
+            lp = _chat_logprobs(self._completion_logprobs(tokens, toks, res, False, ""), top_logprobs)
+        return {"id": cid, "object": "chat.completion", "created": int(time.time()), "model": mname,
                 "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
-                             "logprobs": None, "finish_reason": reason}],
+                             "logprobs": lp, "finish_reason": reason}],
                 "usage": {"prompt_tokens": len(tokens), "completion_tokens": len(res.tokens),
                           "total_tokens": len(tokens) + len(res.tokens)},
                 "timings": {"prefill_s": res.prefill_s, "decode_s": res.decode_s,
                             "n_prefilled": res.n_prefilled}}
+
+
+def _chat_logprobs(lp: Optional[Dict[str, Any]], top_n: Optional[int]):
+    """Text-completion logprobs -> the chat ``{"content": [...]}`` form."""
+    if lp is None:
+        return None
+    content = []
+    for tok, l, top in zip(lp["tokens"], lp["token_logprobs"], lp["top_logprobs"]):
+        items = list((top or {}).items())[:max(0, int(top_n or 0))]
+        content.append({"token": tok, "bytes": list(tok.encode("utf-8")), "logprob": l,
+                        "top_logprobs": [{"token": t, "bytes": list(t.encode("utf-8")), "logprob": v}
+                                         for t, v in items]})
+    return {"content": content, "refusal": None}
+
+
+class _AnyEvent:
+    """``is_set()`` of either event (caller's cancel, or the stream's stop string)."""
+
+    def __init__(self, a: Optional[threading.Event], b: threading.Event):
+        self.a, self.b = a, b
+
+    def is_set(self) -> bool:
+        return self.b.is_set() or (self.a is not None and self.a.is_set())

@@ -11,9 +11,18 @@ from __future__ import annotations
 import os
 from typing import Callable, Optional, Sequence
 
-from ..engine.backends import GenerationResult
-from ..engine.sampling import SamplingParams, sample_token
+from ..engine.backends import GenerationResult, host_generate
+from ..engine.sampling import SamplingParams
 from . import load_cpu
+
+
+def native_sampling(p: SamplingParams) -> bool:
+    """Whether the C++ CPU sampler (csrc/cpu/cpu_backend.cpp:cpu_sample) implements
+    this chain: penalties, top-k, top-p, min-p, temperature - no tail-free, typical,
+    logit bias, mirostat or log-probabilities (those take the host loop)."""
+    return (p.tfs_z >= 1.0 and p.typical_p >= 1.0 and not p.logit_bias and p.n_probs <= 0
+            and p.logits_processor is None
+            and (p.mirostat_mode == 0 or p.greedy()))
 
 
 def sampling_dict(p: SamplingParams) -> dict:
@@ -54,35 +63,10 @@ class CpuBackend:
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
                  on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:
-        if params.tfs_z != 1.0 or params.typical_p != 1.0:
-            return self._generate_host_sampler(prompt, n_keep, max_new, params, stop_ids, poll, on_token)
+        if not native_sampling(params):
+            return host_generate(lambda toks, pos0: self.engine.eval_logits(list(toks), int(pos0)), prompt, n_keep,
+                                 max_new, params, stop_ids, self.n_ctx, poll, on_token)
         r = self.engine.generate(list(prompt), int(n_keep), int(max_new), sampling_dict(params), list(stop_ids),
                                  poll, on_token)
         return GenerationResult(list(r["tokens"]), r["finish"], int(r["n_evaluated"]), r["prefill_s"],
                                 r["decode_s"], int(r["n_prefilled"]))
-
-    def _generate_host_sampler(self, prompt, n_keep, max_new, params, stop_ids, poll, on_token):
-        import time
-        t0 = time.perf_counter()
-        hist = list(prompt)
-        logits = self.engine.eval_logits(hist[n_keep:], n_keep)
-        t1 = time.perf_counter()
-        out, reason = [], "length"
-        stops = set(stop_ids)
-        for step in range(max_new):
-            if poll is not None and poll():
-                reason = "cancelled"
-                break
-            tok = sample_token(logits, hist[-params.last_n:] if params.last_n else [], params, step)
-            out.append(tok)
-            hist.append(tok)
-            if on_token:
-                on_token(tok)
-            if tok in stops:
-                reason = "stop"
-                break
-            if step + 1 == max_new or len(hist) > self.n_ctx - 1:
-                break
-            logits = self.engine.eval_logits([tok], len(hist) - 1)
-        return GenerationResult(out, reason, len(prompt) + max(0, len(out) - 1), t1 - t0,
-                                time.perf_counter() - t1, len(prompt) - n_keep)

@@ -21,8 +21,8 @@ import logging
 import os
 from typing import Callable, Optional, Sequence
 
-from ..engine.backends import GenerationResult
-from ..engine.sampling import SamplingParams, sample_token
+from ..engine.backends import GenerationResult, host_generate
+from ..engine.sampling import SamplingParams
 from . import load_hip
 
 logger = logging.getLogger(__name__)
@@ -58,6 +58,7 @@ class HipBackend:
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
                                  tensor_split=ts)
         self.n_ctx = n_ctx
+        self.n_vocab = int(hparams.n_vocab)
         self.n_batch = min(n_batch, n_ctx)  # the engine's prefill chunk bound (eval_logits rejects T > n_batch)
         self.device = device
         if size > 1:
@@ -87,45 +88,26 @@ class HipBackend:
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
                  on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:
-        if not (0 <= params.top_k <= 64) or params.tfs_z != 1.0 or params.typical_p != 1.0:
-            return self._generate_host_sampler(prompt, n_keep, max_new, params, stop_ids, poll, on_token)
+        if not params.gpu_compatible(self.n_vocab):
+            return host_generate(self._forward, prompt, n_keep, max_new, params, stop_ids, self.n_ctx, poll,
+                                 on_token)
         sp = {"top_k": params.top_k, "top_p": params.top_p, "min_p": params.min_p,
               "temperature": params.temperature, "repeat_penalty": params.repeat_penalty,
               "frequency_penalty": params.frequency_penalty, "presence_penalty": params.presence_penalty,
-              "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF}
+              "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF, "tfs_z": params.tfs_z,
+              "typical_p": params.typical_p,
+              "logit_bias": {int(t): float(b) for t, b in params.logit_bias.items() if 0 <= int(t) < self.n_vocab}}
         r = self.engine.generate(list(prompt), int(n_keep), int(max_new), sp, list(stop_ids), poll, on_token)
         return GenerationResult(list(r["tokens"]), r["finish"], int(r["n_evaluated"]), r["prefill_s"],
                                 r["decode_s"], int(r["n_prefilled"]))
 
-    def _generate_host_sampler(self, prompt, n_keep, max_new, params, stop_ids, poll, on_token):
-        """Slow path for sampler settings the GPU kernel does not implement
-        (top_k outside [0, 64], tail-free, typical): logits come back to the host."""
-        import time
-        t0 = time.perf_counter()
-        hist = list(prompt)
-        e = self.engine
+    def _forward(self, tokens: Sequence[int], pos0: int):
+        """Evaluate tokens into the KV cache (prefill chunks of at most n_batch, the
+        engine's bound; the eager decode path for single tokens) -> last raw logits."""
+        tokens = list(tokens)
+        if len(tokens) == 1:
+            return self.engine.decode_logits(int(tokens[0]), int(pos0))
         logits = None
-        pos = n_keep
-        while pos < len(hist):
-            T = min(len(hist) - pos, self.n_batch)
-            logits = e.eval_logits(hist[pos:pos + T], pos)
-            pos += T
-        t1 = time.perf_counter()
-        out, reason = [], "length"
-        for step in range(max_new):
-            if poll is not None and poll():
-                reason = "cancelled"
-                break
-            tok = sample_token(logits, hist[-params.last_n:] if params.last_n else [], params, step)
-            out.append(tok)
-            hist.append(tok)
-            if on_token:
-                on_token(tok)
-            if tok in set(stop_ids):
-                reason = "stop"
-                break
-            if step + 1 == max_new or len(hist) > self.n_ctx - 1:
-                break
-            logits = e.decode_logits(tok, len(hist) - 1)
-        return GenerationResult(out, reason, len(prompt) + max(0, len(out) - 1), t1 - t0,
-                                time.perf_counter() - t1, len(prompt) - n_keep)
+        for p in range(0, len(tokens), self.n_batch):
+            logits = self.engine.eval_logits(tokens[p:p + self.n_batch], int(pos0 + p))
+        return logits

@@ -12,15 +12,14 @@ sampler chain as the CPU backend, bit-identical uniforms).
 """
 from __future__ import annotations
 
-import time
 from typing import Callable, Optional, Sequence
 
 import numpy as np
 
-from ..engine.backends import GenerationResult
-from ..engine.sampling import SamplingParams, sample_token
+from ..engine.backends import GenerationResult, host_generate
+from ..engine.sampling import SamplingParams
 from . import load_cpu, load_hip
-from .cpu_backend import sampling_dict
+from .cpu_backend import native_sampling, sampling_dict
 
 
 class HybridBackend:
@@ -62,31 +61,9 @@ class HybridBackend:
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
                  on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:
-        t0 = time.perf_counter()
-        hist = list(prompt)
-        n_keep = n_keep if 0 <= n_keep < len(hist) else 0
-        logits = self._forward(hist[n_keep:], n_keep)
-        t1 = time.perf_counter()
-        native = params.tfs_z == 1.0 and params.typical_p == 1.0
-        sp = sampling_dict(params)
-        out, reason = [], "length"
-        stops = set(stop_ids)
-        for step in range(max_new):
-            if poll is not None and poll():
-                reason = "cancelled"
-                break
-            window = hist[-params.last_n:] if params.last_n > 0 else []
-            tok = (self._cpu_mod.sample(logits, window, sp, step) if native
-                   else sample_token(logits, window, params, step))
-            out.append(tok)
-            hist.append(tok)
-            if on_token:
-                on_token(tok)
-            if tok in stops:
-                reason = "stop"
-                break
-            if step + 1 == max_new or len(hist) > self.n_ctx - 1:
-                break
-            logits = self._forward([tok], len(hist) - 1)
-        return GenerationResult(out, reason, len(prompt) + max(0, len(out) - 1), t1 - t0,
-                                time.perf_counter() - t1, len(prompt) - n_keep)
+        fn = None
+        if native_sampling(params):
+            sp = sampling_dict(params)
+            fn = lambda logits, window, step: self._cpu_mod.sample(logits, window, sp, step)  # noqa: E731
+        return host_generate(self._forward, prompt, n_keep, max_new, params, stop_ids, self.n_ctx, poll, on_token,
+                             sample_fn=fn)

@@ -172,3 +172,35 @@ def test_hybrid_backend_facade(models):
     out = llm.create_chat_completion([{"role": "user", "content": "hi"}], max_tokens=8, temperature=0.0)
     assert 1 <= out["usage"]["completion_tokens"] <= 8
     assert llm.health()["cpu_layers"] == 2
+
+
+def test_facade_sampler_options_on_gpu(models):
+    """The HIP backend's routing: logit bias / tail-free / typical stay on the device
+    sampler; mirostat, log-probabilities and unlimited top-k take the host loop over
+    the engine's logits; a stop string ends the device loop through its poll."""
+    from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+    llm = Llama(models["tiny-llama3-q4_k_m"], n_gpu_layers=-1, n_ctx=256, seed=3, verbose=False)
+    assert llm.backend_name == "hip"
+    forced = 77
+    out = llm.create_completion("hello", max_tokens=5, temperature=0.0, logit_bias={forced: 1e4})
+    assert llm.tokenize(out["choices"][0]["text"].encode(), add_bos=False) == [forced] * 5 or \
+        out["choices"][0]["text"] == llm.detokenize([forced] * 5).decode("utf-8", errors="replace")
+    for kw in ({"tfs_z": 0.9}, {"typical_p": 0.8}, {"mirostat_mode": 2}, {"top_k": 0, "top_p": 0.9},
+               {"logprobs": 2}):
+        r = llm.create_completion("a b c", max_tokens=6, temperature=0.9, seed=4, **kw)
+        assert 1 <= r["usage"]["completion_tokens"] <= 6, kw
+        if "logprobs" in kw:
+            lp = r["choices"][0]["logprobs"]
+            assert all(x <= 1e-6 for x in lp["token_logprobs"])
+    # host loop (greedy + logprobs) and device loop (greedy) produce the same tokens
+    a = llm.create_completion("the quick", max_tokens=8, temperature=0.0, logprobs=1)
+    b = llm.create_completion("the quick", max_tokens=8, temperature=0.0)
+    assert a["choices"][0]["text"] == b["choices"][0]["text"]
+    full = llm.create_completion("the quick", max_tokens=32, temperature=0.0)
+    text = full["choices"][0]["text"]
+    if len(text) >= 12:
+        stop = text[len(text) // 2: len(text) // 2 + 3]
+        r = llm.create_completion("the quick", max_tokens=32, temperature=0.0, stop=[stop])
+        assert r["choices"][0]["text"] == text[:text.find(stop)]
+        assert r["choices"][0]["finish_reason"] == "stop"
+        assert r["usage"]["completion_tokens"] < full["usage"]["completion_tokens"]

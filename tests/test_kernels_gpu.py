@@ -305,7 +305,8 @@ def _run_sampler(torch, logits, ring_tokens, params, seed, step=0):
     pb = np.frombuffer(h.sampler_params_bytes(params.top_k, params.top_p, params.min_p, params.temperature,
                                               params.repeat_penalty, params.frequency_penalty,
                                               params.presence_penalty, params.last_n, seed,
-                                              int(params.temperature <= 0)), np.uint8)
+                                              int(params.temperature <= 0), params.tfs_z, params.typical_p,
+                                              dict(params.logit_bias)), np.uint8)
     dp = torch.from_numpy(pb.copy()).cuda()
     ring = np.zeros(64, np.int32)
     rl = min(len(ring_tokens), 64)
@@ -390,3 +391,45 @@ def test_sampler_distribution_chi2(torch):
     if f_exp[-1] == 0:
         f_obs, f_exp = f_obs[:-1], f_exp[:-1]
     assert chisquare(f_obs, f_exp * f_obs.sum() / f_exp.sum()).pvalue > 1e-3, (counts, exp)
+
+
+@pytest.mark.parametrize("mode", ["tfs", "typical", "bias", "all"])
+def test_sampler_tail_free_typical_bias_match_host_chain(torch, mode):
+    """Tail-free, locally-typical and logit bias on the device (stage 2 on the sorted <= 64
+    candidates; bias in stage 1 before the penalties) vs the host chain."""
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams, filtered_candidates, sample_token
+    rng = np.random.default_rng({"tfs": 31, "typical": 32, "bias": 33, "all": 34}[mode])
+    agree = outside = 0
+    n = 30
+    for i in range(n):
+        V = [32000, 128256, 1000][i % 3]
+        logits = (rng.standard_normal(V) * 3).astype(np.float32)
+        hist = list(rng.integers(0, V, 80))
+        kw = {}
+        if mode in ("tfs", "all"):
+            kw["tfs_z"] = 0.9
+        if mode in ("typical", "all"):
+            kw["typical_p"] = 0.8
+        if mode in ("bias", "all"):
+            top = np.argsort(-logits)[:3]
+            kw["logit_bias"] = {int(top[0]): -2.5, int(rng.integers(0, V)): 6.0, int(hist[-1]): 1.5}
+        p = SamplingParams(temperature=1.1, top_k=40, top_p=0.95, min_p=0.02, repeat_penalty=1.1,
+                           frequency_penalty=0.5, presence_penalty=0.3, seed=500 + i, **kw)
+        tok, _ = _run_sampler(torch, logits, hist, p, p.seed, step=i)
+        ids, _ = filtered_candidates(logits, hist[-64:], p)
+        outside += tok not in set(ids.tolist())
+        agree += tok == sample_token(logits, hist[-64:], p, i)
+    assert outside <= 2, outside
+    assert agree >= n - 3, agree
+
+
+def test_sampler_bias_greedy_forces_and_bans(torch):
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams
+    rng = np.random.default_rng(40)
+    logits = rng.standard_normal(128256).astype(np.float32)
+    top = int(np.argmax(logits))
+    p = SamplingParams(temperature=0.0, top_k=1, repeat_penalty=1.0, logit_bias={128255: 50.0})
+    assert _run_sampler(torch, logits, [], p, 0)[0] == 128255
+    p = SamplingParams(temperature=0.0, top_k=1, repeat_penalty=1.0, logit_bias={top: float("-inf")})
+    tok = _run_sampler(torch, logits, [], p, 0)[0]
+    assert tok != top and tok == int(np.argsort(-logits)[1])

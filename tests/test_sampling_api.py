@@ -1,0 +1,206 @@
+"""Sampler chain completeness (upstream ``llama_sample_*`` semantics) and the
+``Llama`` facade's generation options: tail-free, typical, logit bias, mirostat v1/v2,
+log-probabilities, echo, logits processors, stopping criteria, and stop strings that end
+generation early (with streamed text held back while it may still become a stop).
+
+Upstream values are hand-derived from llama.cpp's algorithm definitions (llama.cpp
+``llama_sample_tail_free`` / ``llama_sample_typical`` / ``llama_sample_token_mirostat*``)
+- the library itself is not importable here, so exact upstream draws are parity unpinned;
+the draw is checked in distribution.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+from llama_fastapi_k8s_gpu_amd.engine.sampling import (HostSampler, SamplingParams, _softmax, filtered_candidates,
+                                                       log_softmax, sample_token, tail_free, token_logprobs, typical)
+from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
+
+
+@pytest.fixture(scope="module")
+def tiny(tmp_path_factory):
+    d = tmp_path_factory.mktemp("sampling_models")
+    return write_synthetic_gguf("tiny-llama3-q4_k_m", str(d / "m.gguf"))
+
+
+def test_tail_free_hand_example():
+    # probabilities 0.5 0.3 0.1 0.05 0.05: d1 = .2 .2 .05 0, |d2| = 0 .15 .05 -> normalised 0 .75 .25
+    p = np.array([0.5, 0.3, 0.1, 0.05, 0.05])
+    vals = np.log(p).astype(np.float32)
+    ids = np.arange(5)
+    # cum = 0, .75, 1.0: first i >= 1 with cum > z=0.5 is i=1 -> keep 1
+    got, _ = tail_free(ids, vals, 0.5)
+    assert got.tolist() == [0]
+    # z=0.9: first i >= 1 with cum > 0.9 is i=2 -> keep 2
+    got, _ = tail_free(ids, vals, 0.9)
+    assert got.tolist() == [0, 1]
+    # z=1 is a no-op
+    assert tail_free(ids, vals, 1.0)[0].tolist() == ids.tolist()
+
+
+def test_typical_hand_example():
+    p = np.array([0.4, 0.3, 0.2, 0.1])
+    vals = np.log(p).astype(np.float32)
+    ent = -(p * np.log(p)).sum()
+    shifted = np.abs(-np.log(p) - ent)
+    order = np.argsort(shifted, kind="stable")
+    cum = np.cumsum(p[order])
+    last = int(np.nonzero(cum > 0.55)[0][0]) + 1
+    want = sorted(order[:last].tolist())
+    got, _ = typical(np.arange(4), vals, 0.55)
+    assert got.tolist() == want
+    # the most likely token is not necessarily kept (its surprise can be far from the entropy)
+    p2 = np.array([0.9, 0.025, 0.025, 0.025, 0.025])
+    got2, _ = typical(np.arange(5), np.log(p2).astype(np.float32), 0.05)
+    assert len(got2) >= 1
+
+
+def test_logit_bias_forces_and_bans():
+    rng = np.random.default_rng(0)
+    logits = rng.standard_normal(500).astype(np.float32)
+    top = int(np.argmax(logits))
+    p = SamplingParams(temperature=0.0, logit_bias={7: 100.0})
+    assert sample_token(logits, [], p, 0) == 7
+    p = SamplingParams(temperature=0.0, logit_bias={top: float("-inf")})
+    assert sample_token(logits, [], p, 0) != top
+    p = SamplingParams(temperature=1.0, top_k=40, logit_bias={top: -1e30})
+    assert all(sample_token(logits, [], p, s) != top for s in range(50))
+
+
+def test_mirostat_v1_v2_control_surprise():
+    """mu adapts from 2*tau, and a lower target surprise tau gives less surprising text."""
+    rng = np.random.default_rng(5)
+    logits = (rng.standard_normal(4000) * 3).astype(np.float32)
+    pr = _softmax(logits)
+    for mode in (1, 2):
+        means = []
+        for tau in (1.5, 6.0):
+            p = SamplingParams(temperature=1.0, mirostat_mode=mode, mirostat_tau=tau, mirostat_eta=0.1, seed=9)
+            hs = HostSampler(p)
+            assert hs.mu == pytest.approx(2 * tau)
+            surprises = [-np.log2(pr[hs.sample(logits, [], s)]) for s in range(300)]
+            assert hs.mu != pytest.approx(2 * tau)
+            means.append(np.mean(surprises[100:]))
+        assert means[0] + 1.0 < means[1], (mode, means)
+
+
+def test_mirostat_v2_never_exceeds_mu_plus_first():
+    rng = np.random.default_rng(6)
+    logits = (rng.standard_normal(1000) * 2).astype(np.float32)
+    p = SamplingParams(temperature=1.0, mirostat_mode=2, mirostat_tau=2.0, mirostat_eta=0.0, seed=1)
+    hs = HostSampler(p)
+    pr = _softmax(logits)
+    for s in range(100):
+        t = hs.sample(logits, [], s)
+        # eta = 0: mu stays 2*tau = 4 bits; every kept token has surprise <= mu (or is the argmax)
+        assert -np.log2(pr[t]) <= 4.0 + 1e-6 or t == int(np.argmax(logits))
+
+
+def test_unlimited_top_k_prefix_is_exact():
+    rng = np.random.default_rng(8)
+    for scale in (0.5, 3.0, 10.0):
+        logits = (rng.standard_normal(50000) * scale).astype(np.float32)
+        p = SamplingParams(temperature=1.0, top_k=0, top_p=0.9, min_p=0.0)
+        ids, _ = filtered_candidates(logits, [], p)
+        order = np.lexsort((np.arange(len(logits)), -logits))
+        cum = np.cumsum(_softmax(logits[order]))
+        last = int(np.searchsorted(cum, 0.9, side="left")) + 1
+        assert ids.tolist() == order[:last].tolist()
+
+
+def test_token_logprobs_match_log_softmax():
+    rng = np.random.default_rng(2)
+    logits = rng.standard_normal(300).astype(np.float32)
+    lp, top = token_logprobs(logits, 5, 4)
+    ref = log_softmax(logits)
+    assert lp == pytest.approx(float(ref[5]), abs=1e-5)
+    assert [t for t, _ in top] == np.argsort(-ref, kind="stable")[:4].tolist()
+    assert np.exp(ref.astype(np.float64)).sum() == pytest.approx(1.0, abs=1e-5)
+    np.testing.assert_allclose(Llama.logits_to_logprobs(logits), ref, atol=1e-5)
+
+
+@pytest.mark.parametrize("backend", ["cpu", "reference"])
+def test_stop_string_ends_generation_early(tiny, backend):
+    llm = Llama(tiny, n_ctx=128, backend=backend, seed=0, n_threads=2, verbose=False)
+    full = llm.create_completion("the quick brown fox", max_tokens=24, temperature=0.0)
+    text = full["choices"][0]["text"]
+    toks = llm.tokenize(text.encode(), add_bos=False)
+    if len(text) < 8 or len(toks) < 8:
+        pytest.skip("synthetic model produced too little text")
+    stop = text[len(text) // 2: len(text) // 2 + 3]
+    i = text.find(stop)
+    out = llm.create_completion("the quick brown fox", max_tokens=24, temperature=0.0, stop=[stop])
+    c = out["choices"][0]
+    assert c["text"] == text[:i]
+    assert c["finish_reason"] == "stop"
+    assert out["usage"]["completion_tokens"] < full["usage"]["completion_tokens"]
+    # streaming: the concatenated chunks are the same text, no chunk leaks the stop string
+    chunks = list(llm.create_completion("the quick brown fox", max_tokens=24, temperature=0.0, stop=[stop],
+                                        stream=True))
+    assert "".join(ch["choices"][0]["text"] for ch in chunks) == text[:i]
+    assert chunks[-1]["choices"][0]["finish_reason"] == "stop"
+
+
+def test_echo_logprobs_and_logit_bias_on_the_facade(tiny):
+    llm = Llama(tiny, n_ctx=128, backend="cpu", seed=0, n_threads=2, verbose=False)
+    out = llm.create_completion("hello world", max_tokens=5, temperature=0.0, logprobs=3, echo=True)
+    c = out["choices"][0]
+    assert c["text"].startswith("hello world")
+    lp = c["logprobs"]
+    n_gen = out["usage"]["completion_tokens"]
+    assert len(lp["token_logprobs"]) == len(lp["tokens"]) == len(lp["top_logprobs"]) == len(lp["text_offset"])
+    gen_lp = [x for x in lp["token_logprobs"] if x is not None]
+    assert len(gen_lp) == n_gen and all(x <= 1e-6 for x in gen_lp)
+    # greedy: the chosen token is the most likely one
+    for x, top in zip(lp["token_logprobs"], lp["top_logprobs"]):
+        if x is not None:
+            assert x == pytest.approx(max(top.values()), abs=1e-5)
+    # logit bias: force a token id
+    forced = 42
+    out = llm.create_completion("hello world", max_tokens=4, temperature=0.0, logit_bias={forced: 1e4})
+    want = llm.detokenize([forced] * out["usage"]["completion_tokens"]).decode("utf-8", errors="replace")
+    assert out["choices"][0]["text"] == want
+
+
+def test_chat_logprobs_processor_and_stopping_criteria(tiny):
+    llm = Llama(tiny, n_ctx=128, backend="cpu", seed=0, n_threads=2, verbose=False)
+    msgs = [{"role": "user", "content": "hi"}]
+    out = llm.create_chat_completion(msgs, max_tokens=4, temperature=0.0, logprobs=True, top_logprobs=2)
+    content = out["choices"][0]["logprobs"]["content"]
+    assert len(content) == out["usage"]["completion_tokens"] - (out["choices"][0]["finish_reason"] == "stop")
+    assert all(len(e["top_logprobs"]) == 2 and e["logprob"] <= 1e-6 for e in content)
+
+    def only(ids):
+        def proc(input_ids, scores):
+            s = np.full_like(scores, -np.inf)
+            s[ids] = scores[ids]
+            return s
+        return proc
+    out = llm.create_completion("x", max_tokens=6, temperature=0.9, seed=3, logits_processor=only([11, 12]))
+    toks = llm.tokenize(out["choices"][0]["text"].encode(), add_bos=False)
+    assert out["usage"]["completion_tokens"] == 6
+    seen = []
+
+    def crit(input_ids, logits):
+        seen.append(len(input_ids))
+        return len(seen) >= 3
+    out = llm.create_completion("x y z", max_tokens=20, temperature=0.0, stopping_criteria=crit)
+    assert out["usage"]["completion_tokens"] <= 4 and out["choices"][0]["finish_reason"] == "stop"
+    del toks
+
+
+def test_mirostat_and_typical_on_the_facade(tiny):
+    llm = Llama(tiny, n_ctx=128, backend="cpu", seed=0, n_threads=2, verbose=False)
+    for kw in ({"mirostat_mode": 1}, {"mirostat_mode": 2}, {"typical_p": 0.7}, {"tfs_z": 0.8}):
+        out = llm.create_completion("a b c", max_tokens=6, temperature=0.8, seed=4, **kw)
+        assert 1 <= out["usage"]["completion_tokens"] <= 6, kw
+
+
+def test_cancel_event_still_stops(tiny):
+    llm = Llama(tiny, n_ctx=128, backend="cpu", seed=0, n_threads=2, verbose=False)
+    ev = threading.Event()
+    ev.set()
+    out = llm.create_completion("hi", max_tokens=20, temperature=0.0, cancel_event=ev, stop=["zzz"])
+    assert out["usage"]["completion_tokens"] == 0
