@@ -74,6 +74,18 @@ PYBIND11_MODULE(_cpu, m) {
              std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
              return a;
            })
+      .def("kv_state_bytes", &CpuEngine::kv_state_bytes)
+      .def("kv_save",
+           [](CpuEngine& e, int n) {
+             py::array_t<uint8_t> a((py::ssize_t)e.kv_state_bytes(n));
+             e.kv_transfer(a.mutable_data(), n, false);
+             return a;
+           })
+      .def("kv_load",
+           [](CpuEngine& e, py::array_t<uint8_t, py::array::c_style> a, int n) {
+             if ((size_t)a.size() != e.kv_state_bytes(n)) throw std::runtime_error("kv_load: size mismatch");
+             e.kv_transfer(const_cast<uint8_t*>(a.data()), n, true);
+           })
       .def_property_readonly("layer_end", &CpuEngine::layer_end)
       .def_property_readonly("n_embd", &CpuEngine::n_embd)
       .def_property_readonly("tp_rank", &CpuEngine::tp_rank)

@@ -124,6 +124,29 @@ PYBIND11_MODULE(_hip, m) {
              }
              return py::array_t<float>(v.size(), v.data());
            })
+      .def("kv_state_bytes", &Engine::kv_state_bytes)
+      .def("kv_save",
+           [](Engine& e, int n) {
+             py::array_t<uint8_t> a((py::ssize_t)e.kv_state_bytes(n));
+             void* p = a.mutable_data();
+             {
+               py::gil_scoped_release nogil;
+               e.kv_transfer(p, n, false);
+             }
+             return a;
+           })
+      .def("kv_load",
+           [](Engine& e, py::array_t<uint8_t, py::array::c_style> a, int n) {
+             if ((size_t)a.size() != e.kv_state_bytes(n)) throw std::runtime_error("kv_load: size mismatch");
+             void* p = const_cast<uint8_t*>(a.data());
+             py::gil_scoped_release nogil;
+             e.kv_transfer(p, n, true);
+           })
+      .def("kv_transfer_ptr",  // device (or pinned host) buffer of kv_state_bytes(n) bytes
+           [](Engine& e, uintptr_t buf, int n, bool load) {
+             py::gil_scoped_release nogil;
+             e.kv_transfer(reinterpret_cast<void*>(buf), n, load);
+           })
       .def("bench_decode",
            [](Engine& e, int n, int pos0) {
              double ms = 0;

@@ -695,6 +695,22 @@ std::vector<float> CpuEngine::eval_logits(const std::vector<int>& tokens, int po
   return logits;
 }
 
+void CpuEngine::kv_transfer(void* buf, int n, bool load) {
+  if (n < 0 || n > n_ctx_) throw std::runtime_error("kv_transfer: n out of range");
+  const size_t hd = head_dim_, rows = kc_.size() / ((size_t)n_ctx_ * hd);
+  uint16_t* b = static_cast<uint16_t*>(buf);
+  for (int which = 0; which < 2; ++which) {
+    std::vector<uint16_t>& cache = which == 0 ? kc_ : vc_;
+    uint16_t* packed = b + (size_t)which * rows * n * hd;
+    for (size_t r = 0; r < rows; ++r) {
+      uint16_t* c = cache.data() + r * n_ctx_ * hd;
+      uint16_t* p = packed + r * n * hd;
+      if (load) std::memcpy(c, p, (size_t)n * hd * 2);
+      else std::memcpy(p, c, (size_t)n * hd * 2);
+    }
+  }
+}
+
 std::vector<float> CpuEngine::eval_hidden(const std::vector<int>& tokens, int pos0) {
   const int T = (int)tokens.size();
   if (T <= 0 || pos0 + T > n_ctx_) throw std::runtime_error("eval_hidden: bad range");

@@ -72,6 +72,9 @@ class CpuEngine {
   void head(const float* xrow, float* logits);
   // hybrid: hidden states after layers [0, layer_end) for tokens at pos0.. ([T][n_embd])
   std::vector<float> eval_hidden(const std::vector<int>& tokens, int pos0);
+  // KV state of positions [0, n): [K|V][n_layer][local kv heads][n][hd] f16 (save/load_state)
+  size_t kv_state_bytes(int n) const { return 2 * (kc_.size() / (size_t)n_ctx_) * (size_t)n * sizeof(uint16_t); }
+  void kv_transfer(void* buf, int n, bool load);
 
   int n_vocab() const { return n_vocab_; }
   int n_embd() const { return n_embd_; }

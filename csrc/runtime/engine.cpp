@@ -705,6 +705,23 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
   return out;
 }
 
+void Engine::kv_transfer(void* buf, int n, bool load) {
+  if (n < 0 || n > opt_.n_ctx) throw std::runtime_error("kv_transfer: n out of range");
+  if (n == 0) return;
+  const size_t row = (size_t)n * hp_.head_dim * 2, pitch = (size_t)opt_.n_ctx * hp_.head_dim * 2;
+  const size_t rows = (size_t)hp_.n_layer * nkv_l_;
+  char* b = static_cast<char*>(buf);
+  for (int which = 0; which < 2; ++which) {
+    char* cache = reinterpret_cast<char*>(which == 0 ? kc_ : vc_);
+    char* packed = b + which * rows * row;
+    if (load)
+      HIPCHK(hipMemcpy2DAsync(cache, pitch, packed, row, row, rows, hipMemcpyDefault, stream_));
+    else
+      HIPCHK(hipMemcpy2DAsync(packed, row, cache, pitch, row, rows, hipMemcpyDefault, stream_));
+  }
+  HIPCHK(hipStreamSynchronize(stream_));
+}
+
 std::vector<float> Engine::decode_logits(int token, int pos) {
   if (pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
   SamplerParamsDev p;

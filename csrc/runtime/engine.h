@@ -83,6 +83,11 @@ class Engine {
   // test hooks (numerics vs the reference model)
   std::vector<float> eval_logits(const std::vector<int>& tokens, int pos0);  // prefill path
   std::vector<float> decode_logits(int token, int pos);                      // decode path (eager)
+  // KV state of positions [0, n) for save/load_state and prompt caches: `buf` holds
+  // [K|V][n_layer][nkv_l][n][hd] f16, in host OR device memory (one strided copy each way;
+  // a device-resident snapshot is an HBM-to-HBM copy)
+  size_t kv_state_bytes(int n) const { return 2ull * hp_.n_layer * nkv_l_ * (size_t)n * hp_.head_dim * 2; }
+  void kv_transfer(void* buf, int n, bool load);
   // hybrid placement: hidden states [T][d] of layer `layer_begin` in, last-row logits out
   std::vector<float> eval_hidden(const float* x, int T, int pos0);
   void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing

@@ -97,6 +97,13 @@ class ReferenceBackend:
     def health(self):
         return {"ok": True, "backend": self.name}
 
+    def save_kv(self, n: int, on_device: bool = False):
+        return self.model.k_cache[:, :n].clone(), self.model.v_cache[:, :n].clone()
+
+    def load_kv(self, kv, n: int):
+        self.model.k_cache[:, :n] = kv[0]
+        self.model.v_cache[:, :n] = kv[1]
+
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
                  on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:

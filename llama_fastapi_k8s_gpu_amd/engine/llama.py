@@ -23,9 +23,12 @@ import time
 import uuid
 from typing import Any, Dict, Iterator, List, Optional, Sequence, Union
 
+import numpy as np
+
 from ..gguf.reader import GGUFReader
 from ..models.llama import LlamaHParams
 from .backends import GenerationResult, ReferenceBackend
+from .cache import BaseLlamaCache, LlamaState, longest_token_prefix
 from .chat_format import get_formatter
 from .sampling import SamplingParams
 from .tokenizer import tokenizer_from_metadata
@@ -101,6 +104,7 @@ class Llama:
             raise ValueError(f"unknown backend {kind!r}")
         del reader
         self._kv_tokens: List[int] = []   # tokens resident in the KV cache (prefix reuse)
+        self.cache: Optional[BaseLlamaCache] = None
         self.load_time_s = time.perf_counter() - t0
         if verbose:
             logger.info("loaded %s (%s backend, chat_format=%s) in %.2fs", model_path, kind,
@@ -135,6 +139,34 @@ class Llama:
     def reset(self):
         self._kv_tokens = []
 
+    # ------------------------------------------------------------ states / caches
+    def set_cache(self, cache: Optional[BaseLlamaCache]):
+        self.cache = cache
+
+    def _save_state(self, on_device: bool = False) -> LlamaState:
+        n = len(self._kv_tokens)
+        kv = self._backend.save_kv(n, on_device)
+        if hasattr(kv, "nbytes"):
+            size = int(kv.nbytes)
+        elif hasattr(kv, "numel"):
+            size = int(kv.numel() * kv.element_size())
+        else:
+            size = sum(int(getattr(x, "nbytes", 0) or x.numel() * x.element_size()) for x in kv)
+        return LlamaState(np.asarray(self._kv_tokens, np.int32), None, n, kv, size, self._seed)
+
+    def _load_state(self, state: LlamaState):
+        self._backend.load_kv(state.llama_state, state.n_tokens)
+        self._kv_tokens = [int(t) for t in state.input_ids[:state.n_tokens]]
+
+    def save_state(self, on_device: bool = False) -> LlamaState:
+        """Snapshot of the KV cache and its tokens (``on_device``: kept in GPU memory)."""
+        with self._lock:
+            return self._save_state(on_device)
+
+    def load_state(self, state: LlamaState):
+        with self._lock:
+            self._load_state(state)
+
     def close(self):
         c = getattr(self._backend, "close", None)
         if c:
@@ -164,13 +196,26 @@ class Llama:
         if max_tokens + n_prompt >= self._n_ctx:
             max_tokens = self._n_ctx - n_prompt
         stop_ids, text_stops = self._text_stops(stop)
+        self._lock.acquire()
+        try:
+            if self.cache is not None:   # restore a cached state that shares more of the prompt
+                try:
+                    item = self.cache[prompt_tokens]
+                    if longest_token_prefix(item.input_ids.tolist(), prompt_tokens) > \
+                            longest_token_prefix(self._kv_tokens, prompt_tokens):
+                        self._load_state(item)
+                except KeyError:
+                    pass
+            return self._generate_locked(prompt_tokens, max_tokens, params, stop_ids, text_stops, cancel_event,
+                                         on_token, stopping_criteria)
+        finally:
+            self._lock.release()
+
+    def _generate_locked(self, prompt_tokens, max_tokens, params, stop_ids, text_stops, cancel_event, on_token,
+                         stopping_criteria):
+        n_prompt = len(prompt_tokens)
         # KV prefix reuse (must re-evaluate at least one prompt token for logits)
-        n_keep = 0
-        for a, b in zip(self._kv_tokens, prompt_tokens):
-            if a != b:
-                break
-            n_keep += 1
-        n_keep = min(n_keep, n_prompt - 1)
+        n_keep = min(longest_token_prefix(self._kv_tokens, prompt_tokens), n_prompt - 1)
         # upstream stops as soon as a stop string appears in the generated text (or a
         # stopping criterion fires): watch the token stream and end the backend's loop
         # through its cancel poll
@@ -198,13 +243,14 @@ class Llama:
         def poll():
             return hit["stop"] or (cancel_event is not None and cancel_event.is_set())
         watched = bool(stops_b) or stopping_criteria is not None
-        with self._lock:
-            res: GenerationResult = self._backend.generate(
-                prompt_tokens, n_keep, max_tokens, params, sorted(stop_ids),
-                poll=poll if (watched or cancel_event is not None) else None,
-                on_token=watch if (watched or on_token) else None)
-            hist = list(prompt_tokens) + list(res.tokens)
-            self._kv_tokens = hist[:res.n_evaluated]
+        res: GenerationResult = self._backend.generate(
+            prompt_tokens, n_keep, max_tokens, params, sorted(stop_ids),
+            poll=poll if (watched or cancel_event is not None) else None,
+            on_token=watch if (watched or on_token) else None)
+        hist = list(prompt_tokens) + list(res.tokens)
+        self._kv_tokens = hist[:res.n_evaluated]
+        if self.cache is not None and self._kv_tokens:
+            self.cache[tuple(self._kv_tokens)] = self._save_state(self.cache.on_device)
         toks = list(res.tokens)
         reason = res.finish_reason
         if toks and toks[-1] in stop_ids:

@@ -57,6 +57,12 @@ class CpuBackend:
     def device_memory(self):
         return {}
 
+    def save_kv(self, n: int, on_device: bool = False):
+        return self.engine.kv_save(int(n))
+
+    def load_kv(self, kv, n: int):
+        self.engine.kv_load(kv, int(n))
+
     def eval_logits(self, tokens: Sequence[int], pos0: int = 0):
         return self.engine.eval_logits(list(tokens), int(pos0))
 

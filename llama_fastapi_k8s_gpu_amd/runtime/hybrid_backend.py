@@ -48,6 +48,13 @@ class HybridBackend:
     def device_memory(self):
         return {f"hip:{self.device}": int(self.gpu.device_bytes)}
 
+    def save_kv(self, n: int, on_device: bool = False):
+        return self.cpu.kv_save(int(n)), self.gpu.kv_save(int(n))
+
+    def load_kv(self, kv, n: int):
+        self.cpu.kv_load(kv[0], int(n))
+        self.gpu.kv_load(kv[1], int(n))
+
     def _forward(self, tokens: Sequence[int], pos0: int) -> np.ndarray:
         h = self.cpu.eval_hidden(list(tokens), int(pos0))
         logits = None

@@ -204,3 +204,29 @@ def test_facade_sampler_options_on_gpu(models):
         assert r["choices"][0]["text"] == text[:text.find(stop)]
         assert r["choices"][0]["finish_reason"] == "stop"
         assert r["usage"]["completion_tokens"] < full["usage"]["completion_tokens"]
+
+
+@pytest.mark.parametrize("on_device", [False, True])
+def test_save_load_state_and_device_cache(models, on_device):
+    """KV snapshots through host memory and through HBM (strided hipMemcpy2D both ways):
+    a restored state continues exactly like the original; the device prompt cache
+    restores the longest-prefix conversation."""
+    from llama_fastapi_k8s_gpu_amd.engine import LlamaDeviceCache
+    from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+    llm = Llama(models["tiny-llama3-q4_k_m"], n_gpu_layers=-1, n_ctx=256, seed=1, verbose=False)
+    llm.create_completion("one two three four five", max_tokens=6, temperature=0.0)
+    st = llm.save_state(on_device=on_device)
+    assert hasattr(st.llama_state, "data_ptr") == on_device
+    a = llm.create_completion(list(st.input_ids) + [5], max_tokens=6, temperature=0.0)
+    llm.create_completion("something else entirely", max_tokens=6, temperature=0.0)
+    llm.load_state(st)
+    b = llm.create_completion(list(st.input_ids) + [5], max_tokens=6, temperature=0.0)
+    assert a["choices"][0]["text"] == b["choices"][0]["text"] and b["timings"]["n_prefilled"] == 1
+    if on_device:
+        llm.set_cache(LlamaDeviceCache())
+        conv = "alpha beta gamma delta epsilon"
+        r1 = llm.create_completion(conv, max_tokens=3, temperature=0.0)
+        llm.create_completion("unrelated", max_tokens=3, temperature=0.0)
+        cont = conv + r1["choices"][0]["text"] + " zeta"
+        r2 = llm.create_completion(cont, max_tokens=2, temperature=0.0)
+        assert r2["timings"]["n_prefilled"] < len(llm.tokenize(cont.encode())) - 4

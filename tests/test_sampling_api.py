@@ -204,3 +204,41 @@ def test_cancel_event_still_stops(tiny):
     ev.set()
     out = llm.create_completion("hi", max_tokens=20, temperature=0.0, cancel_event=ev, stop=["zzz"])
     assert out["usage"]["completion_tokens"] == 0
+
+
+@pytest.mark.parametrize("backend", ["cpu", "reference"])
+def test_save_load_state_roundtrip(tiny, backend):
+    """save_state / load_state: restoring a snapshot continues exactly like the original
+    (greedy), even after the KV cache was overwritten by another prompt."""
+    llm = Llama(tiny, n_ctx=128, backend=backend, seed=0, n_threads=2, verbose=False)
+    llm.create_completion("one two three four", max_tokens=4, temperature=0.0)
+    st = llm.save_state()
+    assert st.n_tokens == len(st.input_ids) > 0 and st.llama_state_size > 0
+    a = llm.create_completion(list(st.input_ids) + [5], max_tokens=5, temperature=0.0)
+    llm.create_completion("completely different words here", max_tokens=4, temperature=0.0)
+    llm.load_state(st)
+    assert llm._kv_tokens == [int(t) for t in st.input_ids]
+    b = llm.create_completion(list(st.input_ids) + [5], max_tokens=5, temperature=0.0)
+    assert a["choices"][0]["text"] == b["choices"][0]["text"]
+    assert b["timings"]["n_prefilled"] == 1     # only the new token was evaluated
+
+
+def test_ram_cache_restores_longest_prefix(tiny):
+    from llama_fastapi_k8s_gpu_amd.engine import LlamaRAMCache
+    llm = Llama(tiny, n_ctx=128, backend="cpu", seed=0, n_threads=2, verbose=False)
+    cache = LlamaRAMCache(capacity_bytes=1 << 30)
+    llm.set_cache(cache)
+    conv_a = "alpha beta gamma delta epsilon zeta"
+    ra = llm.create_completion(conv_a, max_tokens=3, temperature=0.0)
+    llm.create_completion("unrelated prompt text", max_tokens=3, temperature=0.0)
+    assert len(cache.cache_state) == 2
+    # continuing conversation A restores its state: only the new tokens are prefilled
+    cont = conv_a + ra["choices"][0]["text"] + " eta"
+    n_prompt = len(llm.tokenize(cont.encode()))
+    r = llm.create_completion(cont, max_tokens=2, temperature=0.0)
+    assert r["timings"]["n_prefilled"] < n_prompt - 5
+    # LRU capacity bound
+    small = LlamaRAMCache(capacity_bytes=1)
+    small[(1, 2)] = cache[(9,)] if (9,) in cache else next(iter(cache.cache_state.values()))
+    small[(3, 4)] = next(iter(cache.cache_state.values()))
+    assert len(small.cache_state) == 1 and (3, 4) in small.cache_state
