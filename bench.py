@@ -84,9 +84,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal mode: LFK_BENCH_DEVICE=<d> puts every rank on GPU d (a one-GPU box running
+    # the N-rank DP flow); RCCL refuses two ranks on one device, so the bench's own barrier
+    # and reductions go over gloo then.
+    rehearse = os.environ.get("LFK_BENCH_DEVICE")
+    if rehearse is not None:
+        local = int(rehearse)
+        os.environ["LOCAL_RANK"] = str(local)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse is not None:
+            if args.parallel == "tp":
+                raise SystemExit("LFK_BENCH_DEVICE rehearses dp only (TP needs one GPU per rank)")
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    red_dev = "cpu" if rehearse is not None else "cuda"
 
     def barrier():
         if world > 1:
@@ -96,7 +109,7 @@ def main():
     from llama_fastapi_k8s_gpu_amd.gguf.synthetic import SPECS, write_synthetic_gguf
     os.makedirs(args.model_dir, exist_ok=True)
     path = os.path.join(args.model_dir, f"{args.model}-s0.gguf")
-    if local == 0 and not os.path.exists(path):
+    if (rank if rehearse is not None else local) == 0 and not os.path.exists(path):
         t0 = time.time()
         write_synthetic_gguf(args.model, path, seed=0)
         print(f"[bench] wrote synthetic {args.model} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
@@ -144,7 +157,7 @@ def main():
     ptoks = sum(eng.prompt_tokens[n0:])
     if world > 1:
         t = torch.tensor([elapsed, float(toks if (args.parallel == "dp" or rank == 0) else 0)],
-                         dtype=torch.float64, device="cuda")
+                         dtype=torch.float64, device=red_dev)
         tmax = t[0].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
