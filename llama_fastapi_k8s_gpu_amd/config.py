@@ -77,6 +77,7 @@ class Settings:
     parity_mode: bool = True            # keep the reference's prompt heuristics exactly
     exact_token_guard: bool = False     # tokenizer-exact trim behind a flag
     cooperative_cancel: bool = True     # stop timed-out generations
+    openai_api: bool = True             # /v1/models, /v1/completions, /v1/chat/completions
     sampling: SamplingDefaults = field(default_factory=SamplingDefaults)
 
     @property
@@ -110,6 +111,7 @@ class Settings:
         s.parity_mode = _env("PARITY_MODE", s.parity_mode, bool)
         s.exact_token_guard = _env("EXACT_TOKEN_GUARD", s.exact_token_guard, bool)
         s.cooperative_cancel = _env("COOPERATIVE_CANCEL", s.cooperative_cancel, bool)
+        s.openai_api = _env("OPENAI_API", s.openai_api, bool)
         sp = s.sampling
         for f in fields(SamplingDefaults):
             key = "SAMPLING_" + f.name.upper()

@@ -67,9 +67,14 @@ def follower_loop(llm, group=None) -> None:
             return
         try:
             if op == "chat":
-                llm.create_chat_completion(**kw)
+                r = llm.create_chat_completion(**kw)
             elif op == "completion":
-                llm.create_completion(kw.pop("prompt"), **kw)
+                r = llm.create_completion(kw.pop("prompt"), **kw)
+            else:
+                r = None
+            if r is not None and not isinstance(r, dict):   # a stream: drive it like the leader does
+                for _ in r:
+                    pass
         except Exception as e:  # the leader raises the same error and reports it
             logger.warning("follower: %s failed: %s", op, e)
 

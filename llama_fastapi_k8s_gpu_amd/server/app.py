@@ -15,7 +15,9 @@ Documented deviations:
   * lifespan instead of the deprecated ``on_event`` (C14), same ordering;
   * a timed-out in-flight generation is stopped cooperatively through a
     ``threading.Event`` the engine polls every decode step (C9) - the HTTP
-    result (408) is unchanged.
+    result (408) is unchanged;
+  * OpenAI-compatible ``/v1/*`` routes (``OPENAI_API``, server/openai_api.py) share
+    the admission queue and the one-at-a-time consumer.
 """
 from __future__ import annotations
 
@@ -135,7 +137,7 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
         while True:
             request_data = await queue.get()
             metrics.queue_depth.set(queue.qsize())
-            messages = request_data['messages']
+            messages = request_data.get('messages')
             future = request_data['future']
             if future.cancelled():
                 logger.info("Future was cancelled before processing; skipping.")
@@ -143,8 +145,17 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
                 continue
             metrics.queue_wait.observe(time.monotonic() - request_data['t_enqueue'])
             try:
-                response = await try_to_truncate_and_generate(messages, semaphore,
-                                                               request_data['cancel'])
+                job = request_data.get('job')
+                if job is not None:   # an OpenAI-route request: same queue, same one-at-a-time
+                    async with semaphore:
+                        metrics.in_flight.inc()
+                        try:
+                            response = await asyncio.to_thread(job, app_.state.engine, request_data['cancel'])
+                        finally:
+                            metrics.in_flight.dec()
+                else:
+                    response = await try_to_truncate_and_generate(messages, semaphore,
+                                                                  request_data['cancel'])
                 if not future.cancelled():
                     future.set_result(response)
                 else:
@@ -218,6 +229,23 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             logger.error(f"Internal server error: {str(e)}")
             metrics.requests.labels("error_500").inc()
             raise HTTPException(status_code=500, detail=f"Internal server error: {str(e)}")
+
+    def submit(job, cancel: threading.Event):
+        """Enqueue an engine job (OpenAI routes) behind the same FIFO as /response."""
+        fut = asyncio.get_running_loop().create_future()
+        try:
+            app.state.queue.put_nowait({'job': job, 'future': fut, 'cancel': cancel,
+                                        't_enqueue': time.monotonic()})
+        except asyncio.QueueFull:
+            metrics.requests.labels("rejected_503").inc()
+            raise HTTPException(status_code=503, detail="Server too busy. Please try again later.")
+        metrics.queue_depth.set(app.state.queue.qsize())
+        return fut
+
+    if settings.openai_api:
+        from .openai_api import add_openai_routes
+        add_openai_routes(app, settings, metrics, submit,
+                          lambda: getattr(app.state.engine, "model_path", None) or settings.model_file)
 
     @app.get("/items/{item_id}")
     async def read_item(item_id: int):
