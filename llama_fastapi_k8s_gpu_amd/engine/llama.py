@@ -267,7 +267,8 @@ class Llama:
 
     def _params(self, temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
                 frequency_penalty, presence_penalty, seed, logit_bias=None, mirostat_mode=0,
-                mirostat_tau=5.0, mirostat_eta=0.1, n_probs=0, logits_processor=None) -> SamplingParams:
+                mirostat_tau=5.0, mirostat_eta=0.1, n_probs=0, logits_processor=None,
+                grammar=None) -> SamplingParams:
         if seed is None:
             self._n_requests += 1
             seed = (self._seed * 1000003 + self._n_requests) & 0xFFFFFFFF
@@ -278,7 +279,39 @@ class Llama:
                               last_n=self.last_n_tokens_size, seed=int(seed), logit_bias=bias,
                               mirostat_mode=int(mirostat_mode or 0), mirostat_tau=float(mirostat_tau),
                               mirostat_eta=float(mirostat_eta), n_probs=int(n_probs or 0),
-                              logits_processor=logits_processor)
+                              logits_processor=logits_processor, grammar=self._grammar_state(grammar))
+
+    def _grammar_state(self, grammar):
+        """A per-request matcher for ``grammar`` (LlamaGrammar or GBNF text), or None."""
+        if grammar is None:
+            return None
+        from .grammar import GrammarState, GrammarVocab, LlamaGrammar
+        if isinstance(grammar, str):
+            grammar = LlamaGrammar.from_string(grammar)
+        if getattr(self, "_gvocab", None) is None:
+            n = self.n_vocab()
+            self._gvocab = GrammarVocab([self.tokenizer.detokenize_bytes([t], False) for t in range(n)],
+                                        self.tokenizer.eog_ids)
+        return GrammarState(grammar, self._gvocab)
+
+    @staticmethod
+    def _response_format_grammar(response_format):
+        """OpenAI ``response_format`` -> grammar: json_object (optionally with ``schema``,
+        llama-cpp-python's extension) or json_schema ({"json_schema": {"schema": ...}})."""
+        if not response_format:
+            return None
+        from .grammar import JSON_GBNF, LlamaGrammar
+        kind = response_format.get("type", "text")
+        if kind == "text":
+            return None
+        if kind == "json_object":
+            schema = response_format.get("schema")
+            return LlamaGrammar.from_json_schema(schema) if schema else LlamaGrammar.from_string(JSON_GBNF)
+        if kind == "json_schema":
+            js = response_format.get("json_schema") or {}
+            schema = js.get("schema", js) if isinstance(js, dict) else js
+            return LlamaGrammar.from_json_schema(schema)
+        raise ValueError(f"unsupported response_format type {kind!r}")
 
     @staticmethod
     def logits_to_logprobs(logits, axis: int = -1):
@@ -334,8 +367,6 @@ class Llama:
                           logit_bias: Optional[Dict[int, float]] = None,
                           cancel_event: Optional[threading.Event] = None, add_bos: bool = True,
                           **unused) -> Union[Dict[str, Any], Iterator[Dict[str, Any]]]:
-        if grammar is not None:
-            raise NotImplementedError("grammar-constrained sampling is not supported by this engine")
         if suffix:
             raise NotImplementedError("infill (suffix) is not supported by this engine")
         if isinstance(prompt, str):
@@ -347,7 +378,7 @@ class Llama:
         stops = [stop] if isinstance(stop, str) else list(stop or [])
         params = self._params(temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
                               frequency_penalty, presence_penalty, seed, logit_bias, mirostat_mode,
-                              mirostat_tau, mirostat_eta, logprobs, logits_processor)
+                              mirostat_tau, mirostat_eta, logprobs, logits_processor, grammar)
         cid = f"cmpl-{uuid.uuid4()}"
         mname = model or self.model_path
         if stream:
@@ -466,8 +497,8 @@ class Llama:
                                logits_processor=None, grammar=None, logit_bias: Optional[Dict[int, float]] = None,
                                logprobs: Optional[bool] = None, top_logprobs: Optional[int] = None,
                                cancel_event: Optional[threading.Event] = None, **unused):
-        if grammar is not None:
-            raise NotImplementedError("grammar-constrained sampling is not supported by this engine")
+        if grammar is None:
+            grammar = self._response_format_grammar(response_format)
         if functions or tools:
             raise NotImplementedError("function / tool calling needs a chat handler this engine does not ship")
         fr = self._formatter(messages)
@@ -480,7 +511,7 @@ class Llama:
             n_probs = 1   # the chosen token's log-probability is reported either way
         params = self._params(temperature, top_p, top_k, min_p, typical_p, tfs_z, repeat_penalty,
                               frequency_penalty, presence_penalty, seed, logit_bias, mirostat_mode,
-                              mirostat_tau, mirostat_eta, n_probs, logits_processor)
+                              mirostat_tau, mirostat_eta, n_probs, logits_processor, grammar)
         cid = f"chatcmpl-{uuid.uuid4()}"
         mname = model or self.model_path
         if stream:

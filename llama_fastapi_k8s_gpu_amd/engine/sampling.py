@@ -72,6 +72,8 @@ class SamplingParams:
     # LogitsProcessorList contract) and a sink for each token's (logprob, top) entry
     logits_processor: Optional[Callable] = field(default=None, compare=False, repr=False)
     logprob_cb: Optional[Callable] = field(default=None, compare=False, repr=False)
+    # engine.grammar.GrammarState of this request (grammar-constrained sampling, host only)
+    grammar: Optional[object] = field(default=None, compare=False, repr=False)
 
     def greedy(self) -> bool:
         return self.temperature <= 0.0
@@ -82,7 +84,8 @@ class SamplingParams:
         mirostat, no host-side log-probabilities."""
         if self.mirostat_mode and not self.greedy():
             return False
-        if self.n_probs > 0 or self.logits_processor is not None or len(self.logit_bias) > GPU_MAX_LOGIT_BIAS:
+        if self.n_probs > 0 or self.logits_processor is not None or self.grammar is not None \
+                or len(self.logit_bias) > GPU_MAX_LOGIT_BIAS:
             return False
         if self.greedy():
             return True
@@ -199,7 +202,10 @@ def prepare_logits(logits: np.ndarray, last_tokens: Sequence[int], p: SamplingPa
 def filtered_candidates(logits: np.ndarray, last_tokens: Sequence[int], p: SamplingParams):
     """Returns (token ids, final temperature-scaled logits) of the surviving candidates
     sorted by descending logit - the distribution the draw samples from."""
-    l = prepare_logits(logits, last_tokens, p)
+    return _filter_prepared(prepare_logits(logits, last_tokens, p), p)
+
+
+def _filter_prepared(l: np.ndarray, p: SamplingParams):
     n = l.shape[0]
     k = p.top_k if 0 < p.top_k < n else n
     order, zfull = None, None
@@ -245,10 +251,10 @@ def _draw(probs: np.ndarray, u: float) -> int:
 def sample_token(logits: np.ndarray, last_tokens: Sequence[int], p: SamplingParams, step: int) -> int:
     """Stateless host reference sampler (everything but mirostat, whose ``mu`` is
     per-request state: use :class:`HostSampler`)."""
+    if p.grammar is not None or p.mirostat_mode:
+        return HostSampler(p).sample(logits, last_tokens, step)
     if p.greedy():
         return int(np.argmax(prepare_logits(logits, last_tokens, p)))
-    if p.mirostat_mode:
-        return HostSampler(p).sample(logits, last_tokens, step)
     ids, vals = filtered_candidates(logits, last_tokens, p)
     return int(ids[_draw(_softmax(vals), philox_uniform(p.seed, step))])
 
@@ -299,11 +305,55 @@ class HostSampler:
 
     def sample(self, logits: np.ndarray, last_tokens: Sequence[int], step: int) -> int:
         p = self.p
+        l = prepare_logits(logits, last_tokens, p)
+        if p.grammar is not None:
+            tok = self._sample_grammar(l, step)
+            p.grammar.accept_token(tok)
+            return tok
         if p.greedy():
-            return int(np.argmax(prepare_logits(logits, last_tokens, p)))
+            return int(np.argmax(l))
         if p.mirostat_mode in (1, 2):
-            return self._mirostat(prepare_logits(logits, last_tokens, p), step)
-        ids, vals = filtered_candidates(logits, last_tokens, p)
+            return self._mirostat(l, step)
+        ids, vals = _filter_prepared(l, p)
+        return int(ids[_draw(_softmax(vals), philox_uniform(p.seed, step))])
+
+    def _sample_grammar(self, l: np.ndarray, step: int) -> int:
+        """Upstream masks every grammar-rejected token to -inf before the chain. The
+        chain's top-k only sees the k best ALLOWED tokens, so with top_k > 0 (or greedy)
+        candidates are checked in descending-logit order until k are found; otherwise
+        the allowed set is enumerated by the grammar's vocabulary-trie walk."""
+        p, gs = self.p, self.p.grammar
+        n = l.shape[0]
+        need = 1 if p.greedy() else (p.top_k if 0 < p.top_k < n and not p.mirostat_mode else 0)
+        allowed: Optional[List[int]] = None
+        if need:
+            found: List[int] = []
+            m = min(n, 256)
+            done = 0
+            while done < n and len(found) < need and done < 8192:
+                part = np.argpartition(-l, m - 1)[:m] if m < n else np.arange(n)
+                part = part[_sorted_desc(l[part], part)]
+                for t in part[done:]:
+                    if gs.allows(int(t)):
+                        found.append(int(t))
+                        if len(found) == need:
+                            break
+                done = m
+                m = min(n, m * 4)
+            if len(found) == need:
+                allowed = found
+        if allowed is None:
+            allowed = gs.allowed_tokens()
+        if not allowed:   # dead end (e.g. the token budget cut a structure): end the generation
+            return int(min(gs.v.eog)) if gs.v.eog else int(np.argmax(l))
+        masked = np.full(n, -np.inf, np.float32)
+        idx = np.asarray(allowed, np.int64)
+        masked[idx] = l[idx]
+        if p.greedy():
+            return int(np.argmax(masked))
+        if p.mirostat_mode in (1, 2):
+            return self._mirostat(masked, step)
+        ids, vals = _filter_prepared(masked, p)
         return int(ids[_draw(_softmax(vals), philox_uniform(p.seed, step))])
 
 

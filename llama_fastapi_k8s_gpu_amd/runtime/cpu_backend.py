@@ -21,7 +21,7 @@ def native_sampling(p: SamplingParams) -> bool:
     this chain: penalties, top-k, top-p, min-p, temperature - no tail-free, typical,
     logit bias, mirostat or log-probabilities (those take the host loop)."""
     return (p.tfs_z >= 1.0 and p.typical_p >= 1.0 and not p.logit_bias and p.n_probs <= 0
-            and p.logits_processor is None
+            and p.logits_processor is None and p.grammar is None
             and (p.mirostat_mode == 0 or p.greedy()))
 
 

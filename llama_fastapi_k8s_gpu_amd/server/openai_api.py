@@ -44,6 +44,7 @@ class _Base(BaseModel):
     mirostat_eta: float = 0.1
     n: int = 1
     user: Optional[str] = None
+    grammar: Optional[str] = None        # GBNF text (llama-cpp-python server extension)
 
 
 class CompletionRequest(_Base):
@@ -116,7 +117,7 @@ def add_openai_routes(app, settings, metrics, submit: Callable[[Callable, thread
                 cancel.set()
                 metrics.requests.labels("timeout_408").inc()
                 return _error(408, "Generation timed out", "timeout")
-            except ValueError as e:       # e.g. prompt longer than the context window
+            except ValueError as e:       # e.g. prompt longer than the context window, bad grammar
                 metrics.requests.labels("error_400").inc()
                 return _error(400, str(e))
             except NotImplementedError as e:
@@ -183,14 +184,13 @@ def add_openai_routes(app, settings, metrics, submit: Callable[[Callable, thread
             prompt = prompt[0]
 
         def call(eng, kw):
-            return eng.create_completion(prompt, logprobs=req.logprobs, echo=req.echo, suffix=req.suffix, **kw)
+            extra = {"grammar": req.grammar} if req.grammar else {}
+            return eng.create_completion(prompt, logprobs=req.logprobs, echo=req.echo, suffix=req.suffix, **extra,
+                                         **kw)
         return await _run(req, call)
 
     @app.post("/v1/chat/completions")
     async def chat_completions(req: ChatCompletionRequest):
-        if req.response_format and req.response_format.get("type", "text") != "text":
-            return _error(400, "response_format other than text needs grammar-constrained sampling, which this "
-                               "engine does not support")
         messages = [{"role": m.get("role", "user"), "content": _text_content(m.get("content"))}
                     for m in req.messages]
 
@@ -198,5 +198,9 @@ def add_openai_routes(app, settings, metrics, submit: Callable[[Callable, thread
             extra = {}
             if req.logprobs:
                 extra = {"logprobs": True, "top_logprobs": req.top_logprobs}
+            if req.response_format:
+                extra["response_format"] = req.response_format
+            if req.grammar:
+                extra["grammar"] = req.grammar
             return eng.create_chat_completion(messages=messages, **extra, **kw)
         return await _run(req, call)

@@ -192,6 +192,9 @@ def test_facade_sampler_options_on_gpu(models):
         if "logprobs" in kw:
             lp = r["choices"][0]["logprobs"]
             assert all(x <= 1e-6 for x in lp["token_logprobs"])
+    # grammar-constrained sampling runs on the host loop over the device logits
+    g = llm.create_completion("answer:", max_tokens=6, temperature=0.8, seed=2, grammar='root ::= "yes" | "no"')
+    assert g["choices"][0]["text"] in ("yes", "no") and g["choices"][0]["finish_reason"] == "stop"
     # host loop (greedy + logprobs) and device loop (greedy) produce the same tokens
     a = llm.create_completion("the quick", max_tokens=8, temperature=0.0, logprobs=1)
     b = llm.create_completion("the quick", max_tokens=8, temperature=0.0)

@@ -77,8 +77,10 @@ def test_chat_completion_stream_logprobs_and_bias(client, llm):
 def test_openai_errors(client):
     assert client.post("/v1/completions", json={"prompt": "x", "n": 2}).status_code == 400
     r = client.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "x"}],
-                                                  "response_format": {"type": "json_object"}})
+                                                  "response_format": {"type": "xml"}})
     assert r.status_code == 400 and "error" in r.json()
+    r = client.post("/v1/completions", json={"prompt": "x", "grammar": "root ::= missing"})
+    assert r.status_code == 400 and "undefined rule" in r.json()["error"]["message"]
     r = client.post("/v1/completions", json={"prompt": "word " * 400, "max_tokens": 4})
     assert r.status_code == 400 and "context window" in r.json()["error"]["message"]
     assert client.post("/v1/completions", json={"prompt": "hi", "max_tokens": 2, "stop": ["\n"]}).status_code == 200
@@ -117,3 +119,18 @@ def test_openai_api_can_be_disabled(llm):
     app = create_app(s, engine=llm)
     with TestClient(app) as c:
         assert c.get("/v1/models").status_code == 404
+
+
+def test_json_mode_and_grammar_routes(client):
+    r = client.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "give json"}], "max_tokens": 40, "temperature": 0.5, "seed": 3,
+        "response_format": {"type": "json_schema", "json_schema": {"name": "x", "schema": {
+            "type": "object", "properties": {"ok": {"type": "boolean"}}, "required": ["ok"]}}}})
+    assert r.status_code == 200, r.text
+    text = r.json()["choices"][0]["message"]["content"]
+    assert text.startswith("{")
+    if r.json()["choices"][0]["finish_reason"] == "stop":
+        assert isinstance(json.loads(text)["ok"], bool)
+    r = client.post("/v1/completions", json={"prompt": "n:", "max_tokens": 6, "temperature": 0.8,
+                                             "grammar": "root ::= [0-9]{1,3}"})
+    assert r.status_code == 200 and r.json()["choices"][0]["text"].isdigit()
