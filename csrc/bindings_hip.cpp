@@ -30,14 +30,35 @@ static void hip_ok(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+static SamplingOpts sampling_opts(py::dict sp) {
+  SamplingOpts o;
+  o.top_k = sp.contains("top_k") ? sp["top_k"].cast<int>() : 40;
+  o.top_p = sp.contains("top_p") ? sp["top_p"].cast<float>() : 0.95f;
+  o.min_p = sp.contains("min_p") ? sp["min_p"].cast<float>() : 0.05f;
+  o.temp = sp.contains("temperature") ? sp["temperature"].cast<float>() : 0.8f;
+  o.repeat_penalty = sp.contains("repeat_penalty") ? sp["repeat_penalty"].cast<float>() : 1.1f;
+  o.freq_penalty = sp.contains("frequency_penalty") ? sp["frequency_penalty"].cast<float>() : 0.f;
+  o.presence_penalty = sp.contains("presence_penalty") ? sp["presence_penalty"].cast<float>() : 0.f;
+  o.last_n = sp.contains("last_n") ? sp["last_n"].cast<int>() : 64;
+  o.seed = sp.contains("seed") ? sp["seed"].cast<unsigned long long>() : 0ull;
+  o.tfs_z = sp.contains("tfs_z") ? sp["tfs_z"].cast<float>() : 1.f;
+  o.typical_p = sp.contains("typical_p") ? sp["typical_p"].cast<float>() : 1.f;
+  if (sp.contains("logit_bias"))
+    for (auto kv : sp["logit_bias"].cast<py::dict>())
+      o.logit_bias.emplace_back(kv.first.cast<int>(), kv.second.cast<float>());
+  return o;
+}
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "MI355X (gfx950) runtime: GGUF engine + HIP kernels";
 
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
-                       int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split) {
+                       int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split,
+                       int n_slots) {
              EngineOptions o;
              o.layer_begin = layer_begin;
+             o.n_slots = n_slots;
              o.n_ctx = n_ctx;
              o.n_batch = n_batch;
              o.device = device;
@@ -52,26 +73,12 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
            py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0,
-           py::arg("tensor_split") = std::vector<float>{})
+           py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1)
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
              const std::vector<int>& stop_ids, py::object poll, py::object on_token) {
-            SamplingOpts o;
-            o.top_k = sp.contains("top_k") ? sp["top_k"].cast<int>() : 40;
-            o.top_p = sp.contains("top_p") ? sp["top_p"].cast<float>() : 0.95f;
-            o.min_p = sp.contains("min_p") ? sp["min_p"].cast<float>() : 0.05f;
-            o.temp = sp.contains("temperature") ? sp["temperature"].cast<float>() : 0.8f;
-            o.repeat_penalty = sp.contains("repeat_penalty") ? sp["repeat_penalty"].cast<float>() : 1.1f;
-            o.freq_penalty = sp.contains("frequency_penalty") ? sp["frequency_penalty"].cast<float>() : 0.f;
-            o.presence_penalty = sp.contains("presence_penalty") ? sp["presence_penalty"].cast<float>() : 0.f;
-            o.last_n = sp.contains("last_n") ? sp["last_n"].cast<int>() : 64;
-            o.seed = sp.contains("seed") ? sp["seed"].cast<unsigned long long>() : 0ull;
-            o.tfs_z = sp.contains("tfs_z") ? sp["tfs_z"].cast<float>() : 1.f;
-            o.typical_p = sp.contains("typical_p") ? sp["typical_p"].cast<float>() : 1.f;
-            if (sp.contains("logit_bias"))
-              for (auto kv : sp["logit_bias"].cast<py::dict>())
-                o.logit_bias.emplace_back(kv.first.cast<int>(), kv.second.cast<float>());
+            const SamplingOpts o = sampling_opts(sp);
             std::function<bool()> pf;
             std::function<void(int)> tf;
             if (!poll.is_none()) pf = [poll]() { py::gil_scoped_acquire g; return poll().cast<bool>(); };
@@ -123,6 +130,26 @@ PYBIND11_MODULE(_hip, m) {
                v = e.decode_logits(token, pos);
              }
              return py::array_t<float>(v.size(), v.data());
+           })
+      .def_property_readonly("n_slots", &Engine::n_slots)
+      .def_property_readonly("max_batch", &Engine::max_batch)
+      .def("slot_begin",
+           [](Engine& e, int slot, const std::vector<int>& prompt, int n_keep, py::dict sp) {
+             const SamplingOpts o = sampling_opts(sp);
+             py::gil_scoped_release nogil;
+             return e.slot_begin(slot, prompt, n_keep, o);
+           })
+      .def("batch_step",
+           [](Engine& e, const std::vector<int>& slots) {
+             py::gil_scoped_release nogil;
+             return e.batch_step(slots);
+           })
+      .def("batch_logits",
+           [](Engine& e, int B) {
+             std::vector<float> v = e.batch_logits(B);
+             py::array_t<float> a({(py::ssize_t)B, (py::ssize_t)(v.size() / B)});
+             std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+             return a;
            })
       .def("kv_state_bytes", &Engine::kv_state_bytes)
       .def("kv_save",

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   const long long t_entry = TL ? wall_clock64() : 0;
   const bool stamp = TL && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
 #define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) a.dbg_clk[i] = wall_clock64() - t_entry; } } while (0)
-  if (blockIdx.z == 1) {  // weight-touch plane (see AttnDecodeArgs::pf)
+  if (a.batch == 0 && blockIdx.z == 1) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;
     for (int r = 0; r < AttnDecodeArgs::kTouchRanges; ++r) {
@@ -103,6 +103,17 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     }
     if (acc == 0x9E3779B9u) *a.pf_sink = (int)acc;
     return;
+  }
+  if (a.batch > 0) {  // batched decode: this row's query, KV slot, position, workspaces and output
+    const int b = blockIdx.z;
+    const size_t so = (size_t)a.slots[b] * a.slot_stride;
+    a.q += (size_t)b * a.q_stride;
+    a.k_cache += so;
+    a.v_cache += so;
+    a.pos += b;
+    a.part += (size_t)b * a.part_stride;
+    a.counters += 64 * b;
+    a.out += (size_t)b * a.out_stride;
   }
   const int kvh = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -128,7 +139,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     const float2 qv = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
     qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv.x * a.scale), (_Float16)(qv.y * a.scale)};
   }
-  const int L = *a.pos + 1;
+  const int L = min(*a.pos + 1, a.n_ctx);
   LFK_STAMP(0);
   if (start >= L || a.debug_stop == 1) return;
 
@@ -340,7 +351,12 @@ void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
     if (!a.pf_sink || a.pf_bytes[r] < 4 || a.pf_nseg[r] < 1) throw std::runtime_error("attn_decode: weight touch needs pf_sink and >= 4 bytes");
     touch = true;
   }
-  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, touch ? 2 : 1);
+  if (a.batch > 0) {
+    if (touch) throw std::runtime_error("attn_decode: no weight touch in batched mode");
+    if (!a.slots || a.n_kv_head > 64 || a.part_stride < attn_decode_workspace_floats(a.n_ctx, a.n_head, a.head_dim))
+      throw std::runtime_error("attn_decode: bad batched arguments");
+  }
+  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, a.batch > 0 ? a.batch : (touch ? 2 : 1));
   if (a.head_dim == 128) launch_attn_decode<128>(a, G, grid, s);
   else if (a.head_dim == 64) launch_attn_decode<64>(a, G, grid, s);
   else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");

@@ -153,6 +153,13 @@ struct AttnDecodeArgs {
   // HBM idle). pf_sink: a 4-B device word the touch result is conditionally stored to.
   // Up to 6 ranges, each spread over all touch blocks. A range is pf_nseg segments of
   // pf_bytes bytes, pf_seg_stride apart (nseg 1: one contiguous span).
+  // batched decode (batch > 0): grid z = row b with query q + b*q_stride, KV slot
+  // slots[b] (caches slots[b]*slot_stride halves in), length pos[b] + 1, partials
+  // part + b*part_stride, split counters counters + 64*b, output out + b*out_stride.
+  // No weight touch in this mode.
+  int batch = 0;
+  const int* slots = nullptr;
+  size_t slot_stride = 0, q_stride = 0, out_stride = 0, part_stride = 0;
   static constexpr int kTouchRanges = 6;
   const uint8_t* pf[kTouchRanges] = {};
   size_t pf_bytes[kTouchRanges] = {};
@@ -212,9 +219,14 @@ void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip
                   float* zero = nullptr, int zero_ld = 0);
 // f32 activation [T][d] -> bf16 (for the next GEMM)
 void to_bf16(const float* x, int n, __hip_bfloat16* y, hipStream_t s);
-// prefill: rope q/k of QKV rows, write q (f32) and k/v to the caches at pos0+t
+// prefill: rope q/k of QKV rows, write q (f32) and k/v to the caches at pos0+t.
+// Batched decode (pos_arr != nullptr): row t is at position pos_arr[t] of KV slot
+// slot_arr[t], whose caches start slot_arr[t] * slot_stride halves after k_cache / v_cache.
 void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int head_dim, int n_ctx,
-                     const float2* rope, float* q_out, __half* k_cache, __half* v_cache, hipStream_t s);
+                     const float2* rope, float* q_out, __half* k_cache, __half* v_cache, hipStream_t s,
+                     const int* pos_arr = nullptr, const int* slot_arr = nullptr, size_t slot_stride = 0);
+// batched decode: tok[b] / pos[b] = the current token / position of KV slot slots[b]
+void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s);
 // out[i] = x[i] (+) ... small helpers
 void add_inplace(float* x, const float* y, int n, hipStream_t s);
 void set_i32(int* p, int v, hipStream_t s);
@@ -256,6 +268,13 @@ struct SamplerArgs {
   int* out_tokens = nullptr;       // optional device ring of sampled tokens [out_cap]
   int out_cap = 0;
   int advance_pos = 1;             // also bump state.pos (decode) after sampling
+  // batched (batch > 0): row b samples logits + b*logits_ld with the params / ring /
+  // state of slot slots[b] (p + slot, ring + 64*slot, state + S_NSTATE*slot), its own
+  // candidate workspace (cand_* + b * per-row size) and writes its token to batch_out[b]
+  int batch = 0;
+  const int* slots = nullptr;
+  size_t logits_ld = 0;
+  int* batch_out = nullptr;
 };
 int sampler_blocks(int V);
 void sample(const SamplerArgs& a, hipStream_t s);

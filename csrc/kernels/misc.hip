@@ -79,9 +79,14 @@ void to_bf16(const float* x, int n, __hip_bfloat16* y, hipStream_t s) {
 
 __global__ __launch_bounds__(256) void rope_kv_prefill_kernel(const float* qkv, int pos0, int n_q, int n_kv, int hd,
                                                               int n_ctx, const float2* rope, float* q_out,
-                                                              __half* kc, __half* vc) {
+                                                              __half* kc, __half* vc, const int* pos_arr,
+                                                              const int* slot_arr, size_t slot_stride) {
   const int t = blockIdx.x;
-  const int pos = pos0 + t;
+  const int pos = pos_arr ? min(max(pos_arr[t], 0), n_ctx - 1) : pos0 + t;
+  if (slot_arr) {
+    kc += (size_t)slot_arr[t] * slot_stride;
+    vc += (size_t)slot_arr[t] * slot_stride;
+  }
   const int ncol = n_q + 2 * n_kv;
   const float* row = qkv + (size_t)t * ncol;
   for (int p = threadIdx.x; p < ncol / 2; p += blockDim.x) {
@@ -109,10 +114,25 @@ __global__ __launch_bounds__(256) void rope_kv_prefill_kernel(const float* qkv, 
 }
 
 void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int head_dim, int n_ctx, const float2* rope,
-                     float* q_out, __half* k_cache, __half* v_cache, hipStream_t s) {
+                     float* q_out, __half* k_cache, __half* v_cache, hipStream_t s, const int* pos_arr,
+                     const int* slot_arr, size_t slot_stride) {
   if (T <= 0) return;
+  if ((pos_arr == nullptr) != (slot_arr == nullptr)) throw std::runtime_error("rope_kv_prefill: pos/slot arrays");
   hipLaunchKernelGGL(rope_kv_prefill_kernel, dim3(T), dim3(256), 0, s, qkv, pos0, n_q, n_kv, head_dim, n_ctx, rope,
-                     q_out, k_cache, v_cache);
+                     q_out, k_cache, v_cache, pos_arr, slot_arr, slot_stride);
+}
+
+__global__ void batch_gather_kernel(const int* slots, int B, const int* state, int* tok, int* pos) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) {
+    const int* st = state + (size_t)slots[b] * S_NSTATE;
+    tok[b] = st[S_TOKEN];
+    pos[b] = st[S_POS];
+  }
+}
+void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(batch_gather_kernel, dim3((B + 63) / 64), dim3(64), 0, s, slots, B, state, tok, pos);
 }
 
 __global__ void add_inplace_kernel(float* x, const float* y, int n) {

@@ -97,11 +97,28 @@ __device__ __forceinline__ int wave_collect(const float (&v)[NE], const int (&id
   return min(base, cap);
 }
 
+// Batched mode: row b of the launch (blockIdx.y in stage 1, blockIdx.x in stage 2)
+// works on its own logits row, the sampling state of its KV slot and its own
+// candidate workspace; every pointer is re-based here so the stage bodies are the
+// single-row code.
+__device__ __forceinline__ void batch_row(SamplerArgs& a, int b, int nb) {
+  if (a.batch <= 0) return;
+  const int slot = a.slots[b];
+  a.logits += (size_t)b * a.logits_ld;
+  a.p += slot;
+  a.ring += 64 * slot;
+  a.state += (size_t)S_NSTATE * slot;
+  a.cand_val += (size_t)b * nb * KMAX;
+  a.cand_idx += (size_t)b * nb * KMAX;
+  a.cand_tau += (size_t)b * 2 * nb;
+}
+
 // Stage 1: one wave per 1024-logit slice. The repetition/frequency/presence
 // penalties of ring tokens that fall in this slice are applied here (the wave
 // stages its slice in LDS, lanes owning a first occurrence patch their entry),
 // then the slice's top-K superset is selected without LDS or barriers.
 __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
+  batch_row(a, blockIdx.y, gridDim.x);
   __shared__ float sl[SLICE];
   const int lane = threadIdx.x;
   const int lo = blockIdx.x * SLICE;
@@ -257,6 +274,8 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
 static constexpr int CAP2 = 2048;  // survivors above the bounds (typically < 200)
 template <int NE2, bool TL = false>
 __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
+  const int brow = blockIdx.x;
+  batch_row(a, brow, nb);
   long long t0 = 0;
   if constexpr (TL) t0 = wall_clock64();
 #define LFK_ST(i) do { if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[i] = wall_clock64() - t0; } } while (0)
@@ -393,6 +412,7 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
     st[S_RING_HEAD] = (head + 1) & 63;
     st[S_RING_LEN] = min(st[S_RING_LEN] + 1, 64);
     if (a.out_tokens) a.out_tokens[st[S_NOUT] % a.out_cap] = tok;
+    if (a.batch_out) a.batch_out[brow] = tok;
     LFK_ST(3);
     st[S_NOUT] += 1;
     st[S_STEP] += 1;
@@ -404,11 +424,14 @@ int sampler_blocks(int V) { return (V + SLICE - 1) / SLICE; }
 
 void sample(const SamplerArgs& a, hipStream_t s) {
   const int nb = sampler_blocks(a.V);
-  hipLaunchKernelGGL(sample_stage1, dim3(nb), dim3(64), 0, s, a);
+  const int rows = a.batch > 0 ? a.batch : 1;
+  if (a.batch > 0 && (!a.slots || a.logits_ld < (size_t)a.V || a.out_tokens || a.dbg_clk))
+    throw std::runtime_error("sample: bad batched arguments");
+  hipLaunchKernelGGL(sample_stage1, dim3(nb, rows), dim3(64), 0, s, a);
   const int ncand = nb * KMAX;
   if (a.dbg_clk && ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, true>), dim3(1), dim3(256), 0, s, a, nb);
-  else if (ncand <= 256 * 8) hipLaunchKernelGGL((sample_stage2<8, false>), dim3(1), dim3(256), 0, s, a, nb);
-  else if (ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, false>), dim3(1), dim3(256), 0, s, a, nb);
+  else if (ncand <= 256 * 8) hipLaunchKernelGGL((sample_stage2<8, false>), dim3(rows), dim3(256), 0, s, a, nb);
+  else if (ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, false>), dim3(rows), dim3(256), 0, s, a, nb);
   else throw std::runtime_error("GPU sampler: vocabulary too large (max 131072)");
 }
 

@@ -90,6 +90,9 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   if (opt_.layer_begin < 0 || opt_.layer_begin > hp_.n_layer) throw std::runtime_error("bad layer_begin");
   if (opt_.layer_begin > 0 && tp > 1) throw std::runtime_error("partial offload cannot be combined with split_mode=row");
   if (opt_.n_ctx <= 0) opt_.n_ctx = hp_.n_ctx_train;
+  if (opt_.n_slots < 1) throw std::runtime_error("n_slots must be >= 1");
+  if (opt_.n_slots > 1 && (tp > 1 || opt_.layer_begin > 0))
+    throw std::runtime_error("KV slots (batched decode) need one rank holding every layer");
   if (tp > 1) {
     if (opt_.nccl_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad nccl id");
     ncclUniqueId id;
@@ -113,6 +116,8 @@ Engine::~Engine() {
   for (void* p : allocs_) hipFree(p);
   if (h_ring_) hipHostFree(h_ring_);
   if (h_tokens_) hipHostFree(h_tokens_);
+  if (h_bslots_) hipHostFree(h_bslots_);
+  if (h_btok_) hipHostFree(h_btok_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -219,10 +224,12 @@ void Engine::alloc_buffers() {
   logits_l_ = (float*)dalloc(sizeof(float) * V_l_);
   HIPCHK(hipMemset(logits_l_, 0, sizeof(float) * V_l_));
   const size_t kv = (size_t)hp_.n_layer * nkv_l_ * opt_.n_ctx * hd;
-  kc_ = (__half*)dalloc(kv * 2);
-  vc_ = (__half*)dalloc(kv * 2);
-  HIPCHK(hipMemset(kc_, 0, kv * 2));
-  HIPCHK(hipMemset(vc_, 0, kv * 2));
+  const int NS = opt_.n_slots;
+  slot_stride_ = kv;
+  kc_ = (__half*)dalloc(kv * 2 * NS);
+  vc_ = (__half*)dalloc(kv * 2 * NS);
+  HIPCHK(hipMemset(kc_, 0, kv * 2 * NS));
+  HIPCHK(hipMemset(vc_, 0, kv * 2 * NS));
   rope_ = (float2*)dalloc(sizeof(float2) * opt_.n_ctx * (hd / 2));
   attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
@@ -233,11 +240,11 @@ void Engine::alloc_buffers() {
   cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
   cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
   cand_tau_ = (unsigned*)dalloc(sizeof(unsigned) * 2 * nb);  // slice bounds + slice maxima
-  state_ = (int*)dalloc(sizeof(int) * S_NSTATE);
-  ring_ = (int*)dalloc(sizeof(int) * 64);
+  state_ = (int*)dalloc(sizeof(int) * S_NSTATE * NS);
+  ring_ = (int*)dalloc(sizeof(int) * 64 * NS);
   out_tokens_ = (int*)dalloc(sizeof(int) * 64);
   tokens_ = (int*)dalloc(sizeof(int) * B);
-  sparams_ = (SamplerParamsDev*)dalloc(sizeof(SamplerParamsDev));
+  sparams_ = (SamplerParamsDev*)dalloc(sizeof(SamplerParamsDev) * NS);
   router_logits_ = (float*)dalloc(sizeof(float) * B * E);
   moe_ids_ = (int*)dalloc(sizeof(int) * KU);
   moe_w_ = (float*)dalloc(sizeof(float) * KU);
@@ -253,8 +260,24 @@ void Engine::alloc_buffers() {
     moe_hg_ = (__hip_bfloat16*)dalloc(2 * R * F_l_);
     moe_yg_ = (float*)dalloc(sizeof(float) * R * d);
   }
-  HIPCHK(hipMemset(state_, 0, sizeof(int) * S_NSTATE));
-  HIPCHK(hipMemset(ring_, 0, sizeof(int) * 64));
+  HIPCHK(hipMemset(state_, 0, sizeof(int) * S_NSTATE * NS));
+  HIPCHK(hipMemset(ring_, 0, sizeof(int) * 64 * NS));
+  if (NS > 1) {
+    bmax_ = std::min(NS, B);
+    bslots_ = (int*)dalloc(sizeof(int) * bmax_);
+    bpos_ = (int*)dalloc(sizeof(int) * bmax_);
+    btok_ = (int*)dalloc(sizeof(int) * bmax_);
+    btok_out_ = (int*)dalloc(sizeof(int) * bmax_);
+    logits_b_ = (float*)dalloc(sizeof(float) * bmax_ * V_pad_);
+    cand_val_b_ = (float*)dalloc(sizeof(float) * bmax_ * nb * 64);
+    cand_idx_b_ = (int*)dalloc(sizeof(int) * bmax_ * nb * 64);
+    cand_tau_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * 2 * nb);
+    attn_part_b_ = (float*)dalloc(sizeof(float) * bmax_ * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
+    attn_cnt_b_ = (int*)dalloc(sizeof(int) * 64 * bmax_);
+    HIPCHK(hipMemset(attn_cnt_b_, 0, sizeof(int) * 64 * bmax_));
+    HIPCHK(hipHostMalloc((void**)&h_bslots_, sizeof(int) * bmax_, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
+  }
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
   ffn_cnt_ = (int*)dalloc(sizeof(int) * 32 * std::max(1, hp_.n_layer));
   HIPCHK(hipMemset(ffn_cnt_, 0, sizeof(int) * 32 * std::max(1, hp_.n_layer)));
@@ -451,7 +474,7 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   }
 }
 
-void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
+void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int slot) {
   GemvArgs h;
   h.w = output_; h.x = xrow; h.norm_w = out_norm_; h.eps = hp_.rms_eps;
   const int rows_real = std::max(0, std::min(V_l_, hp_.n_vocab - opt_.tp_rank * V_l_));
@@ -461,11 +484,15 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s) {
   if (opt_.tp_size > 1)
     ncclchk(ncclAllGather(logits_l_, logits_, V_l_, ncclFloat32, static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
   SamplerArgs sa;
-  sa.logits = logits_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
-  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.cand_tau = cand_tau_; sa.out_tokens = out_tokens_; sa.out_cap = 64;
+  sa.logits = logits_; sa.V = hp_.n_vocab; sa.p = sparams_ + slot; sa.ring = ring_ + 64 * slot;
+  sa.state = state_ + (size_t)S_NSTATE * slot;
+  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.cand_tau = cand_tau_;
   sa.advance_pos = advance_pos;
+  if (slot == 0) {
+    sa.out_tokens = out_tokens_; sa.out_cap = 64;
+  }
   sample(sa, s);
-  HIPCHK(hipMemcpyAsync(h_ring_, out_tokens_, sizeof(int) * 64, hipMemcpyDeviceToHost, s));
+  if (slot == 0) HIPCHK(hipMemcpyAsync(h_ring_, out_tokens_, sizeof(int) * 64, hipMemcpyDeviceToHost, s));
 }
 
 void Engine::enqueue_decode(hipStream_t s) {
@@ -479,12 +506,16 @@ void Engine::enqueue_decode(hipStream_t s) {
 }
 
 void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
+  if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_rows_layer(l, T, pos0, false, s);
+}
+
+void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim;
   const bool tp = opt_.tp_size > 1;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   const int ncol = nq_ + 2 * nkvd_;
-  if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
+  {
     const Layer& L = layers_[l];
     rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, qkv_, ncol);  // + zero the q|k|v rows
     GemmArgs g;
@@ -492,14 +523,30 @@ void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
     g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
-    __half* kcl = kc_ + kv_layer * l;
-    __half* vcl = vc_ + kv_layer * l;
-    rope_kv_prefill(qkv_, T, pos0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s);
-    AttnPrefillArgs pa;
-    pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
-    pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
-    pa.out_bf16 = attnb_; pa.out_stride = nq_;  // bf16 straight into the Wo GEMM's input
-    attn_prefill(pa, s);
+    if (!batched) {
+      __half* kcl = kc_ + slot_stride_ * kv_slot_ + kv_layer * l;
+      __half* vcl = vc_ + slot_stride_ * kv_slot_ + kv_layer * l;
+      rope_kv_prefill(qkv_, T, pos0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s);
+      AttnPrefillArgs pa;
+      pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
+      pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
+      pa.out_bf16 = attnb_; pa.out_stride = nq_;  // bf16 straight into the Wo GEMM's input
+      attn_prefill(pa, s);
+    } else {  // T decode rows, each of its own KV slot and position
+      __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
+      __half* vcl = vc_ + kv_layer * l;
+      rope_kv_prefill(qkv_, T, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
+      AttnDecodeArgs aa;
+      aa.q = q_; aa.k_cache = kcl; aa.v_cache = vcl; aa.pos = bpos_;
+      aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
+      aa.scale = 1.f / std::sqrt((float)hd);
+      aa.part = attn_part_b_; aa.counters = attn_cnt_b_; aa.out = attn_;
+      aa.batch = T; aa.slots = bslots_; aa.slot_stride = slot_stride_;
+      aa.q_stride = nq_; aa.out_stride = nq_;
+      aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
+      attn_decode(aa, s);
+      to_bf16(attn_, T * nq_, attnb_, s);
+    }
     GemmArgs o;
     o.w = L.wo; o.x = attnb_; o.T = T; o.ldo = d;
     if (!tp) {
@@ -575,18 +622,8 @@ void Engine::launch_step() {
 }
 
 // ------------------------------------------------------------------------ generation
-GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
-                        const std::vector<int>& stop_ids, const std::function<bool()>& poll,
-                        const std::function<void(int)>& on_token) {
-  GenOut out;
-  const int n_prompt = (int)prompt.size();
-  if (n_prompt == 0) throw std::runtime_error("empty prompt");
-  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
-  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+SamplerParamsDev Engine::make_sparams(const SamplingOpts& sp) const {
   if (sp.top_k < 0 || sp.top_k > 64) throw std::runtime_error("GPU sampler: top_k must be in [0, 64]");
-  const double t0 = now_s();
-
-  // per-request device state: sampling params, penalty ring (prompt tail), counters
   SamplerParamsDev p;
   p.greedy = sp.temp <= 0.f ? 1 : 0;
   p.top_k = p.greedy ? 1 : (sp.top_k == 0 ? 64 : sp.top_k);
@@ -603,6 +640,13 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
     p.bias_tok[p.n_bias] = t;
     p.bias_val[p.n_bias++] = b;
   }
+  return p;
+}
+
+// Sampling params, penalty ring (prompt tail) and counters of one slot's request.
+void Engine::begin_slot_state(int slot, const std::vector<int>& prompt, const SamplingOpts& sp) {
+  const SamplerParamsDev p = make_sparams(sp);
+  const int n_prompt = (int)prompt.size();
   int hstate[S_NSTATE] = {0};
   int hring[64] = {0};
   const int rl = std::min(n_prompt, 64);
@@ -611,9 +655,96 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   hstate[S_POS] = n_prompt;  // position the first generated token will occupy
   hstate[S_RING_LEN] = rl;
   hstate[S_RING_HEAD] = rl & 63;
-  HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
-  HIPCHK(hipMemcpyAsync(ring_, hring, sizeof(hring), hipMemcpyHostToDevice, stream_));
-  HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(sparams_ + slot, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(ring_ + 64 * slot, hring, sizeof(hring), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipMemcpyAsync(state_ + (size_t)S_NSTATE * slot, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));  // the host arrays are on this stack frame
+}
+
+int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {
+  if (!bmax_) throw std::runtime_error("slot_begin: the engine was built with one KV slot");
+  if (slot < 0 || slot >= opt_.n_slots) throw std::runtime_error("slot_begin: slot out of range");
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  begin_slot_state(slot, prompt, sp);
+  kv_slot_ = slot;
+  try {
+    int pos = n_keep;
+    while (pos < n_prompt) {
+      const int T = std::min(opt_.n_batch, n_prompt - pos);
+      std::memcpy(h_tokens_, prompt.data() + pos, sizeof(int) * T);
+      HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+      enqueue_prefill(T, pos, stream_);
+      pos += T;
+      if (pos == n_prompt) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_, slot);
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+  } catch (...) {
+    kv_slot_ = 0;
+    throw;
+  }
+  kv_slot_ = 0;
+  int tok = 0;
+  HIPCHK(hipMemcpy(&tok, state_ + (size_t)S_NSTATE * slot + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
+  check_device_err();
+  return tok;
+}
+
+std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
+  const int B = (int)slots.size();
+  if (!bmax_) throw std::runtime_error("batch_step: the engine was built with one KV slot");
+  if (B < 1 || B > bmax_) throw std::runtime_error("batch_step: 1 <= rows <= max_batch");
+  for (int b = 0; b < B; ++b) {
+    if (slots[b] < 0 || slots[b] >= opt_.n_slots) throw std::runtime_error("batch_step: slot out of range");
+    for (int c = 0; c < b; ++c)
+      if (slots[c] == slots[b]) throw std::runtime_error("batch_step: duplicate slot");
+  }
+  const int d = hp_.n_embd;
+  std::memcpy(h_bslots_, slots.data(), sizeof(int) * B);
+  HIPCHK(hipMemcpyAsync(bslots_, h_bslots_, sizeof(int) * B, hipMemcpyHostToDevice, stream_));
+  batch_gather(bslots_, B, state_, btok_, bpos_, stream_);
+  embed_rows(tok_embd_, btok_, B, x_, stream_);
+  for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, stream_);
+  rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, stream_);
+  GemmArgs h;
+  h.w = output_; h.x = xb_; h.T = B; h.out = logits_b_; h.ldo = V_pad_;
+  gemm_dq(h, GEMM_STORE, stream_);
+  SamplerArgs sa;
+  sa.logits = logits_b_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
+  sa.cand_val = cand_val_b_; sa.cand_idx = cand_idx_b_; sa.cand_tau = cand_tau_b_;
+  sa.advance_pos = 1;
+  sa.batch = B; sa.slots = bslots_; sa.logits_ld = V_pad_; sa.batch_out = btok_out_;
+  sample(sa, stream_);
+  HIPCHK(hipMemcpyAsync(h_btok_, btok_out_, sizeof(int) * B, hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(hipGetLastError());
+  check_device_err();
+  last_batch_ = B;
+  return std::vector<int>(h_btok_, h_btok_ + B);
+}
+
+std::vector<float> Engine::batch_logits(int B) {
+  if (!bmax_ || B < 1 || B > last_batch_) throw std::runtime_error("batch_logits: no such rows in the last batch_step");
+  std::vector<float> out((size_t)B * hp_.n_vocab);
+  HIPCHK(hipMemcpy2D(out.data(), sizeof(float) * hp_.n_vocab, logits_b_, sizeof(float) * V_pad_,
+                     sizeof(float) * hp_.n_vocab, B, hipMemcpyDeviceToHost));
+  return out;
+}
+
+GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
+                        const std::vector<int>& stop_ids, const std::function<bool()>& poll,
+                        const std::function<void(int)>& on_token) {
+  GenOut out;
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  const double t0 = now_s();
+
+  // per-request device state: sampling params, penalty ring (prompt tail), counters
+  begin_slot_state(0, prompt, sp);
 
   // prefill in n_batch chunks
   int pos = n_keep;

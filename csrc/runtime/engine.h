@@ -41,6 +41,9 @@ struct EngineOptions {
   std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1)
   std::vector<float> tensor_split;  // per-rank weights (empty = even); see shard.h
   int layer_begin = 0;  // hybrid placement: layers [0, layer_begin) run on the CPU backend
+  // KV slots (continuous batching): slot 0 serves generate() / the graph decode path, slots
+  // [0, n_slots) can decode together through batch_step()
+  int n_slots = 1;
   bool verbose = false;
 };
 
@@ -114,6 +117,19 @@ class Engine {
   int n_ctx() const { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
 
+  // ---- continuous batching over KV slots (EngineOptions::n_slots > 1, one rank, all layers)
+  int n_slots() const { return opt_.n_slots; }
+  int max_batch() const { return bmax_; }
+  // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
+  // set the slot's sampling state and sample its first token (synchronous).
+  int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp);
+  // One decode step of every listed slot, each at its own position: embeds each slot's
+  // current token, runs all layers over the B rows (MFMA GEMMs, per-row RoPE/KV append,
+  // batched split-L attention), the lm_head GEMM and the batched sampler; returns the
+  // next token of each slot (synchronous).
+  std::vector<int> batch_step(const std::vector<int>& slots);
+  std::vector<float> batch_logits(int B);  // test hook: logits [B][n_vocab] of the last batch_step
+
  private:
   void* dalloc(size_t bytes);
   QMat upload_matrix(const GGUFFile& f, const std::string& name, size_t r0, size_t R, size_t c0, size_t K,
@@ -129,7 +145,12 @@ class Engine {
   void enqueue_layer_decode(int l, hipStream_t s);
   void enqueue_decode(hipStream_t s);
   void enqueue_prefill(int T, int pos0, hipStream_t s, bool embed = true);
-  void enqueue_head(const float* xrow, int advance_pos, hipStream_t s);
+  // one layer over T activation rows: a prompt chunk at positions pos0.. of KV slot kv_slot_
+  // (batched == false) or T decode rows of slots bslots_ at positions bpos_ (batched == true)
+  void enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s);
+  void enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int slot = 0);
+  SamplerParamsDev make_sparams(const SamplingOpts& sp) const;
+  void begin_slot_state(int slot, const std::vector<int>& prompt, const SamplingOpts& sp);
   void launch_step();
   void check(hipError_t e, const char* what);
   void check_device_err();
@@ -204,6 +225,25 @@ class Engine {
   size_t pd_dump_n_ = 0, pd_tl_n_ = 0, pd_acct_n_ = 0;
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
+
+  // KV slots: kc_/vc_ hold n_slots caches of slot_stride_ halves each; state_/ring_/sparams_
+  // hold n_slots entries (slot 0 first)
+  size_t slot_stride_ = 0;
+  int kv_slot_ = 0;           // the slot enqueue_prefill writes
+  int bmax_ = 0;              // batch_step rows (min(n_slots, n_batch)); 0 = no batching
+  int* bslots_ = nullptr;     // [bmax] device: slot of each batch row
+  int* bpos_ = nullptr;       // [bmax] position of each row's current token
+  int* btok_ = nullptr;       // [bmax] current token of each row
+  int* btok_out_ = nullptr;   // [bmax] sampled tokens
+  float* logits_b_ = nullptr; // [bmax][V_pad]
+  float* cand_val_b_ = nullptr;
+  int* cand_idx_b_ = nullptr;
+  unsigned* cand_tau_b_ = nullptr;
+  float* attn_part_b_ = nullptr;   // [bmax][attn_decode_workspace_floats]
+  int* attn_cnt_b_ = nullptr;      // [bmax][64]
+  int* h_bslots_ = nullptr;   // pinned [bmax]
+  int* h_btok_ = nullptr;     // pinned [bmax]
+  int last_batch_ = 0;
 
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
