@@ -14,6 +14,12 @@ Parallelism (one process per GPU, launched by torch.distributed.run for N>1):
   * ``--parallel tp``: one model row-split over all GPUs (RCCL all-reduce over
     xGMI); every rank serves the same requests. Strong scaling; value = rank 0's.
 
+Load: ``--clients C`` concurrent clients (default 6 = the reference pod's admission
+capacity, 1 in flight + MAX_QUEUE_SIZE 5, reference api.py:19,113) post the K timed
+requests; the engine decodes up to ``--max-batch M`` (default = C) of them as rows of
+one continuous batch (csrc/runtime/scheduler.cpp). ``--clients 1 --max-batch 1`` is
+the reference's serial one-generation-at-a-time serving (recorded in profiles/).
+
 Weights are random-init of the exact Llama-3-8B Q4_K_M shapes and type mix
 (a synthetic GGUF written once per node), prompts are synthetic chat requests.
 """
@@ -74,6 +80,8 @@ def main():
     ap.add_argument("--model", default="llama3-8b-q4_k_m")
     ap.add_argument("--parallel", choices=["dp", "tp"], default="dp")
     ap.add_argument("--n-ctx", type=int, default=1024)
+    ap.add_argument("--clients", type=int, default=6, help="concurrent clients posting /response")
+    ap.add_argument("--max-batch", type=int, default=0, help="continuous-batch rows (0 = --clients)")
     ap.add_argument("--model-dir", default=os.environ.get("SYNTH_MODEL_DIR", os.path.join(
         os.environ.get("TMPDIR", "/tmp"), "llama_amd_models")))
     args = ap.parse_args()
@@ -121,13 +129,18 @@ def main():
 
     t0 = time.time()
     split = "row" if (args.parallel == "tp" and world > 1) else "none"
+    max_batch = args.max_batch or args.clients
+    if split == "row":
+        max_batch = 1   # continuous batching runs on one rank
     llm = Llama(path, n_gpu_layers=-1, n_ctx=args.n_ctx, seed=1234 + (0 if split == "row" else rank),
-                split_mode=split, verbose=False)
+                split_mode=split, verbose=False, **({"max_batch": max_batch} if max_batch > 1 else {}))
     print(f"[bench] rank {rank}: loaded in {time.time() - t0:.1f}s ({llm.backend_name})", file=sys.stderr,
           flush=True)
     eng = CountingEngine(llm)
     settings = Settings()
     settings.timeout_seconds = 600.0  # measure latency, do not 408 long generations in the bench
+    settings.max_batch = max_batch
+    settings.max_queue_size = max(settings.max_queue_size, args.clients)
     app = create_app(settings, engine=eng)
 
     import httpx
@@ -138,21 +151,28 @@ def main():
         async with app.router.lifespan_context(app):
             transport = httpx.ASGITransport(app=app)
             async with httpx.AsyncClient(transport=transport, base_url="http://bench", timeout=600) as c:
-                for i in range(args.warmup):
-                    r = await c.post("/response", json=make_request(1000 + i))
-                    assert r.status_code == 200, r.text
+                async def drive(ids, lat):
+                    todo = list(ids)
+
+                    async def client():
+                        while todo:
+                            i = todo.pop(0)
+                            t = time.perf_counter()
+                            r = await c.post("/response", json=make_request(i))
+                            assert r.status_code == 200, r.text
+                            if lat is not None:
+                                lat.append(time.perf_counter() - t)
+                    await asyncio.gather(*[client() for _ in range(max(1, args.clients))])
+                await drive(range(1000, 1000 + args.warmup), None)
                 barrier()
                 n0 = len(eng.completion_tokens)
                 t_start = time.perf_counter()
-                for i in range(args.steps):
-                    t = time.perf_counter()
-                    r = await c.post("/response", json=make_request(i))
-                    assert r.status_code == 200, r.text
-                    latencies.append(time.perf_counter() - t)
+                await drive(range(args.steps), latencies)
                 barrier()
                 return time.perf_counter() - t_start, n0
 
     elapsed, n0 = asyncio.run(run())
+    llm.close()
     toks = sum(eng.completion_tokens[n0:])
     ptoks = sum(eng.prompt_tokens[n0:])
     if world > 1:
@@ -174,10 +194,12 @@ def main():
             "higher_is_better": True, "scaling": "weak" if args.parallel == "dp" else "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None, "dtype": "q4_k_m weights, int8/bf16 activations, fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B Q4_K_M GGUF, synthetic chat requests)",
-            "config": {"model": "Llama-3-8B Q4_K_M", "global_batch": world if args.parallel == "dp" else 1,
+            "config": {"model": "Llama-3-8B Q4_K_M",
+                       "global_batch": (world if args.parallel == "dp" else 1) * min(args.clients, max_batch),
                        "seq_len": args.n_ctx, "parallelism": f"{args.parallel}{world}",
+                       "clients_per_gpu": args.clients, "max_batch": max_batch,
                        "p50_response_ms": round(p50, 1),
-                       "decode_tokens_per_s_per_gpu": round(toks / dec, 1) if dec > 0 else None,
+                       "decode_tokens_per_s_per_request": round(toks / dec, 1) if dec > 0 else None,
                        "avg_prompt_tokens": round(ptoks / max(1, args.steps), 1),
                        "avg_output_tokens": round(toks / max(1, args.steps), 1)},
         }

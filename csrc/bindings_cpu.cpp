@@ -4,10 +4,14 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "bind_scheduler.h"
 #include "cpu/cpu_backend.h"
 #include "runtime/repack.h"
 
+#include <chrono>
 #include <cstring>
+#include <mutex>
+#include <thread>
 
 namespace py = pybind11;
 using namespace lfk;
@@ -25,6 +29,66 @@ static CpuSampling parse_sampling(py::dict sp) {
   if (sp.contains("seed")) o.seed = sp["seed"].cast<unsigned long long>();
   return o;
 }
+
+// Deterministic stand-in for a multi-slot engine (scheduler tests on the CPU): each slot
+// keeps the token sequence its "KV" holds; the next token is a hash of the whole sequence,
+// so a request's output depends only on its own tokens (any batching must reproduce a
+// sequential run), and slot_begin checks that the reused prefix really is resident.
+class FakeSlotEngine : public SlotBackend {
+ public:
+  FakeSlotEngine(int n_slots, int max_batch, int n_ctx, int vocab, int step_us)
+      : n_slots_(n_slots), max_batch_(max_batch), n_ctx_(n_ctx), vocab_(vocab), step_us_(step_us),
+        kv_(n_slots), cur_(n_slots, 0) {}
+  int n_slots() const override { return n_slots_; }
+  int max_batch() const override { return max_batch_; }
+  int n_ctx() const override { return n_ctx_; }
+  static int next_token(const std::vector<int>& seq, int vocab) {
+    unsigned long long h = 1469598103934665603ull;
+    for (int t : seq) h = (h ^ (unsigned)t) * 1099511628211ull;
+    return (int)(h % (unsigned long long)vocab);
+  }
+  int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts&) override {
+    std::lock_guard<std::mutex> g(mu_);
+    if (slot < 0 || slot >= n_slots_) throw std::runtime_error("fake: slot out of range");
+    std::vector<int>& kv = kv_[slot];
+    if (n_keep > (int)kv.size()) throw std::runtime_error("fake: reused prefix is not resident");
+    for (int i = 0; i < n_keep; ++i)
+      if (kv[i] != prompt[i]) throw std::runtime_error("fake: reused prefix differs");
+    kv.assign(prompt.begin(), prompt.end());
+    prefilled_ += (long long)prompt.size() - n_keep;
+    cur_[slot] = next_token(kv, vocab_);
+    return cur_[slot];
+  }
+  std::vector<int> batch_step(const std::vector<int>& slots) override {
+    if (step_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(step_us_));
+    std::lock_guard<std::mutex> g(mu_);
+    if ((int)slots.size() > max_batch_) throw std::runtime_error("fake: too many rows");
+    std::vector<int> out;
+    for (int s : slots) {
+      std::vector<int>& kv = kv_[s];
+      if ((int)kv.size() >= n_ctx_) throw std::runtime_error("fake: KV write past n_ctx");
+      kv.push_back(cur_[s]);
+      cur_[s] = next_token(kv, vocab_);
+      out.push_back(cur_[s]);
+    }
+    ++steps_;
+    max_rows_ = std::max(max_rows_, (int)slots.size());
+    if (fail_at_ > 0 && steps_ == fail_at_) throw std::runtime_error("fake: injected device fault");
+    return out;
+  }
+  long long prefilled() { std::lock_guard<std::mutex> g(mu_); return prefilled_; }
+  long long steps() { std::lock_guard<std::mutex> g(mu_); return steps_; }
+  int max_rows() { std::lock_guard<std::mutex> g(mu_); return max_rows_; }
+  void fail_at(long long s) { std::lock_guard<std::mutex> g(mu_); fail_at_ = s; }
+
+ private:
+  int n_slots_, max_batch_, n_ctx_, vocab_, step_us_;
+  std::mutex mu_;
+  std::vector<std::vector<int>> kv_;
+  std::vector<int> cur_;
+  long long prefilled_ = 0, steps_ = 0, fail_at_ = 0;
+  int max_rows_ = 0;
+};
 
 PYBIND11_MODULE(_cpu, m) {
   m.doc() = "C++ CPU backend (OpenMP): GGUF engine for n_gpu_layers = 0";
@@ -133,4 +197,14 @@ PYBIND11_MODULE(_cpu, m) {
     return cpu_sample(l, window, parse_sampling(sp), step);
   });
   m.def("uniform", &splitmix_uniform);
+
+  py::class_<FakeSlotEngine>(m, "FakeSlotEngine")
+      .def(py::init<int, int, int, int, int>(), py::arg("n_slots"), py::arg("max_batch"), py::arg("n_ctx"),
+           py::arg("vocab") = 1000, py::arg("step_us") = 0)
+      .def_static("next_token", &FakeSlotEngine::next_token)
+      .def_property_readonly("prefilled", &FakeSlotEngine::prefilled)
+      .def_property_readonly("steps", &FakeSlotEngine::steps)
+      .def_property_readonly("max_rows", &FakeSlotEngine::max_rows)
+      .def("fail_at", &FakeSlotEngine::fail_at);
+  bind_scheduler<FakeSlotEngine>(m);
 }

@@ -13,6 +13,7 @@
 #include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
+#include "bind_scheduler.h"
 #include "kernels/kernels.h"
 #include "kernels/pdecode.h"
 #include "runtime/engine.h"
@@ -30,24 +31,7 @@ static void hip_ok(const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-static SamplingOpts sampling_opts(py::dict sp) {
-  SamplingOpts o;
-  o.top_k = sp.contains("top_k") ? sp["top_k"].cast<int>() : 40;
-  o.top_p = sp.contains("top_p") ? sp["top_p"].cast<float>() : 0.95f;
-  o.min_p = sp.contains("min_p") ? sp["min_p"].cast<float>() : 0.05f;
-  o.temp = sp.contains("temperature") ? sp["temperature"].cast<float>() : 0.8f;
-  o.repeat_penalty = sp.contains("repeat_penalty") ? sp["repeat_penalty"].cast<float>() : 1.1f;
-  o.freq_penalty = sp.contains("frequency_penalty") ? sp["frequency_penalty"].cast<float>() : 0.f;
-  o.presence_penalty = sp.contains("presence_penalty") ? sp["presence_penalty"].cast<float>() : 0.f;
-  o.last_n = sp.contains("last_n") ? sp["last_n"].cast<int>() : 64;
-  o.seed = sp.contains("seed") ? sp["seed"].cast<unsigned long long>() : 0ull;
-  o.tfs_z = sp.contains("tfs_z") ? sp["tfs_z"].cast<float>() : 1.f;
-  o.typical_p = sp.contains("typical_p") ? sp["typical_p"].cast<float>() : 1.f;
-  if (sp.contains("logit_bias"))
-    for (auto kv : sp["logit_bias"].cast<py::dict>())
-      o.logit_bias.emplace_back(kv.first.cast<int>(), kv.second.cast<float>());
-  return o;
-}
+static SamplingOpts sampling_opts(py::dict sp) { return sampling_opts_from(sp); }
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "MI355X (gfx950) runtime: GGUF engine + HIP kernels";
@@ -217,6 +201,8 @@ PYBIND11_MODULE(_hip, m) {
         d["rope_base"] = h.rope_base; d["rms_eps"] = h.rms_eps;
         return d;
       });
+
+  bind_scheduler<Engine>(m);
 
   m.def("pd_item_bench", [](int type, int rows, int K, int iters, int blocks, uintptr_t out, uintptr_t stream) {
     pd_item_bench(type, rows, K, iters, blocks, reinterpret_cast<long long*>(out), S(stream));

@@ -662,6 +662,7 @@ void Engine::begin_slot_state(int slot, const std::vector<int>& prompt, const Sa
 }
 
 int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {
+  ExecGuard guard(this);
   if (!bmax_) throw std::runtime_error("slot_begin: the engine was built with one KV slot");
   if (slot < 0 || slot >= opt_.n_slots) throw std::runtime_error("slot_begin: slot out of range");
   const int n_prompt = (int)prompt.size();
@@ -693,6 +694,7 @@ int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, con
 }
 
 std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
+  ExecGuard guard(this);
   const int B = (int)slots.size();
   if (!bmax_) throw std::runtime_error("batch_step: the engine was built with one KV slot");
   if (B < 1 || B > bmax_) throw std::runtime_error("batch_step: 1 <= rows <= max_batch");
@@ -726,6 +728,7 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
 }
 
 std::vector<float> Engine::batch_logits(int B) {
+  ExecGuard guard(this);
   if (!bmax_ || B < 1 || B > last_batch_) throw std::runtime_error("batch_logits: no such rows in the last batch_step");
   std::vector<float> out((size_t)B * hp_.n_vocab);
   HIPCHK(hipMemcpy2D(out.data(), sizeof(float) * hp_.n_vocab, logits_b_, sizeof(float) * V_pad_,
@@ -736,6 +739,7 @@ std::vector<float> Engine::batch_logits(int B) {
 GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
                         const std::vector<int>& stop_ids, const std::function<bool()>& poll,
                         const std::function<void(int)>& on_token) {
+  ExecGuard guard(this);
   GenOut out;
   const int n_prompt = (int)prompt.size();
   if (n_prompt == 0) throw std::runtime_error("empty prompt");
@@ -807,6 +811,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
 }
 
 std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0) {
+  ExecGuard guard(this);
   const int T = (int)tokens.size();
   if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_logits: bad size");
   SamplerParamsDev p;
@@ -826,6 +831,7 @@ std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0)
 }
 
 std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
+  ExecGuard guard(this);
   if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_hidden: bad size");
   HIPCHK(hipMemcpyAsync(x_, x, sizeof(float) * T * hp_.n_embd, hipMemcpyHostToDevice, stream_));
   enqueue_prefill(T, pos0, stream_, /*embed=*/false);
@@ -837,6 +843,7 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
 }
 
 void Engine::kv_transfer(void* buf, int n, bool load) {
+  ExecGuard guard(this);
   if (n < 0 || n > opt_.n_ctx) throw std::runtime_error("kv_transfer: n out of range");
   if (n == 0) return;
   const size_t row = (size_t)n * hp_.head_dim * 2, pitch = (size_t)opt_.n_ctx * hp_.head_dim * 2;
@@ -854,6 +861,7 @@ void Engine::kv_transfer(void* buf, int n, bool load) {
 }
 
 std::vector<float> Engine::decode_logits(int token, int pos) {
+  ExecGuard guard(this);
   if (pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
   SamplerParamsDev p;
   p.greedy = 1; p.top_k = 1; p.repeat_penalty = 1.f;
@@ -871,6 +879,7 @@ std::vector<float> Engine::decode_logits(int token, int pos) {
 }
 
 void Engine::bench_decode(int n_steps, int pos0, double* ms_per_step) {
+  ExecGuard guard(this);
   if (n_steps < 1 || pos0 + n_steps + 1 > opt_.n_ctx) throw std::runtime_error("bench_decode: exceeds n_ctx");
   SamplerParamsDev p;
   p.greedy = 1; p.top_k = 1;

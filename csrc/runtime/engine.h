@@ -14,6 +14,7 @@
 #include <atomic>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -21,6 +22,7 @@
 #include "../kernels/pdecode.h"
 #include "gguf.h"
 #include "p2p.h"
+#include "slots.h"
 
 namespace lfk {
 
@@ -47,15 +49,6 @@ struct EngineOptions {
   bool verbose = false;
 };
 
-struct SamplingOpts {
-  int top_k = 40;
-  float top_p = 0.95f, min_p = 0.05f, temp = 0.8f;
-  float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
-  int last_n = 64;
-  unsigned long long seed = 0;
-  float tfs_z = 1.f, typical_p = 1.f;
-  std::vector<std::pair<int, float>> logit_bias;  // distinct tokens, at most kMaxLogitBias
-};
 
 struct GenOut {
   std::vector<int> tokens;
@@ -73,7 +66,7 @@ struct Layer {
   QMat router, gu_exps, down_exps;   // MoE
 };
 
-class Engine {
+class Engine : public SlotBackend {
  public:
   Engine(const std::string& path, const EngineOptions& opts);
   ~Engine();
@@ -114,23 +107,35 @@ class Engine {
   std::vector<long long> pdecode_timeline();
   std::vector<long long> pdecode_acct();  // LFK_PDECODE_ACCT=1: cycle totals [CU][16]
   std::string last_error() const { return last_error_; }
-  int n_ctx() const { return opt_.n_ctx; }
+  int n_ctx() const override { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
+  int device() const { return opt_.device; }
 
   // ---- continuous batching over KV slots (EngineOptions::n_slots > 1, one rank, all layers)
-  int n_slots() const { return opt_.n_slots; }
-  int max_batch() const { return bmax_; }
+  int n_slots() const override { return opt_.n_slots; }
+  int max_batch() const override { return bmax_; }
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
-  int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp);
+  int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
   // One decode step of every listed slot, each at its own position: embeds each slot's
   // current token, runs all layers over the B rows (MFMA GEMMs, per-row RoPE/KV append,
   // batched split-L attention), the lm_head GEMM and the batched sampler; returns the
   // next token of each slot (synchronous).
-  std::vector<int> batch_step(const std::vector<int>& slots);
+  std::vector<int> batch_step(const std::vector<int>& slots) override;
   std::vector<float> batch_logits(int B);  // test hook: logits [B][n_vocab] of the last batch_step
 
  private:
+  // Every public entry point that runs device work takes this guard: it serialises the
+  // callers (the batch scheduler's thread and request threads of the legacy path) and makes
+  // the engine's device current on the calling thread - HIP's current device is per thread,
+  // and the threads that call in are not the one that built the engine (one process per GPU
+  // runs on device LOCAL_RANK, not 0).
+  struct ExecGuard {
+    std::lock_guard<std::mutex> lk;
+    explicit ExecGuard(Engine* e) : lk(e->exec_mu_) { (void)hipSetDevice(e->opt_.device); }
+  };
+  std::mutex exec_mu_;
+
   void* dalloc(size_t bytes);
   QMat upload_matrix(const GGUFFile& f, const std::string& name, size_t r0, size_t R, size_t c0, size_t K,
                      int n_expert = 0);

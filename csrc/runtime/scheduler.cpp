@@ -1,0 +1,247 @@
+// Continuous-batching scheduler: see scheduler.h.
+#include "scheduler.h"
+
+#include <algorithm>
+#include <chrono>
+#include <stdexcept>
+
+namespace lfk {
+
+static double sched_now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+BatchScheduler::BatchScheduler(SlotBackend& e) : eng_(e) {
+  n_slots_ = e.n_slots();
+  if (n_slots_ < 2 || e.max_batch() < 1)
+    throw std::runtime_error("BatchScheduler: the engine needs n_slots >= 2 (slot 0 stays with generate())");
+  // batch_step takes at most max_batch rows: never keep more slots active than that
+  n_slots_ = std::min(n_slots_, first_slot_ + e.max_batch());
+  slot_req_.resize(n_slots_);
+  slot_hist_.resize(n_slots_);
+  slot_used_.assign(n_slots_, 0);
+  st_.slots = n_slots_ - first_slot_;
+  th_ = std::thread([this] { loop(); });
+}
+
+BatchScheduler::~BatchScheduler() { shutdown(); }
+
+void BatchScheduler::shutdown() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_ && !th_.joinable()) return;
+    stop_ = true;
+  }
+  cv_work_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+int64_t BatchScheduler::submit(const std::vector<int>& prompt, int max_new, const SamplingOpts& sp,
+                               const std::vector<int>& stop_ids) {
+  if (prompt.empty()) throw std::runtime_error("empty prompt");
+  if ((int)prompt.size() >= eng_.n_ctx()) throw std::runtime_error("prompt exceeds context window");
+  auto r = std::make_shared<Req>();
+  r->prompt = prompt;
+  r->max_new = std::max(1, max_new);
+  r->sp = sp;
+  r->stop_ids = stop_ids;
+  r->t_submit = sched_now();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_) throw std::runtime_error("BatchScheduler: shut down");
+    r->id = next_id_++;
+    reqs_[r->id] = r;
+    pending_.push_back(r);
+  }
+  cv_work_.notify_one();
+  return r->id;
+}
+
+SchedPoll BatchScheduler::wait(int64_t id, size_t have, int timeout_ms) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = reqs_.find(id);
+  if (it == reqs_.end()) throw std::runtime_error("BatchScheduler: unknown request");
+  std::shared_ptr<Req> r = it->second;
+  cv_out_.wait_for(lk, std::chrono::milliseconds(std::max(0, timeout_ms)),
+                   [&] { return r->done || r->tokens.size() > have; });
+  SchedPoll p;
+  if (r->tokens.size() > have) p.tokens.assign(r->tokens.begin() + have, r->tokens.end());
+  p.done = r->done;
+  p.finish = r->finish;
+  p.error = r->error;
+  p.n_prompt = (int)r->prompt.size();
+  p.n_prefilled = r->n_prefilled;
+  if (r->t_start > 0) p.queue_s = r->t_start - r->t_submit;
+  if (r->t_first > 0) p.prefill_s = r->t_first - r->t_start;
+  if (r->t_first > 0) p.decode_s = (r->done ? r->t_done : sched_now()) - r->t_first;
+  return p;
+}
+
+void BatchScheduler::cancel(int64_t id) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = reqs_.find(id);
+    if (it == reqs_.end() || it->second->done) return;
+    it->second->cancel = true;
+  }
+  cv_work_.notify_one();
+}
+
+void BatchScheduler::release(int64_t id) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = reqs_.find(id);
+    if (it == reqs_.end()) return;
+    it->second->cancel = true;  // an abandoned active row leaves the batch at the next step
+    reqs_.erase(it);
+  }
+  cv_work_.notify_one();
+}
+
+SchedStats BatchScheduler::stats() {
+  std::lock_guard<std::mutex> g(mu_);
+  SchedStats s = st_;
+  s.pending = (int)pending_.size();
+  s.active = 0;
+  for (int i = first_slot_; i < n_slots_; ++i) s.active += slot_req_[i] != nullptr;
+  return s;
+}
+
+// caller holds mu_
+void BatchScheduler::finish(Req& r, const char* reason) {
+  if (r.done) return;
+  r.done = true;
+  r.finish = reason;
+  r.t_done = sched_now();
+  if (r.slot >= 0 && slot_req_[r.slot].get() == &r) slot_req_[r.slot] = nullptr;
+  cv_out_.notify_all();
+}
+
+// caller holds mu_. The KV of the row now holds every token but the newest one, which the
+// next batch_step feeds; a row ends on a stop id, max_new, a cancel, or when that next
+// step would write past the context.
+void BatchScheduler::push_token(Req& r, int tok) {
+  r.tokens.push_back(tok);
+  if (std::find(r.stop_ids.begin(), r.stop_ids.end(), tok) != r.stop_ids.end()) return finish(r, "stop");
+  if ((int)r.tokens.size() >= r.max_new) return finish(r, "length");
+  if ((int)(r.prompt.size() + r.tokens.size()) - 1 >= eng_.n_ctx()) return finish(r, "length");
+  if (r.cancel) return finish(r, "cancelled");
+}
+
+// caller holds mu_: the free slot whose resident tokens share the longest prefix with the
+// prompt (least recently admitted among equals, so other conversations' prefixes survive)
+int BatchScheduler::pick_slot(const std::vector<int>& prompt, int* lcp) {
+  int best = -1, best_lcp = -1;
+  for (int s = first_slot_; s < n_slots_; ++s) {
+    if (slot_req_[s]) continue;
+    const std::vector<int>& h = slot_hist_[s];
+    const size_t n = std::min(h.size(), prompt.size());
+    size_t k = 0;
+    while (k < n && h[k] == prompt[k]) ++k;
+    if ((int)k > best_lcp || ((int)k == best_lcp && slot_used_[s] < slot_used_[best])) {
+      best = s;
+      best_lcp = (int)k;
+    }
+  }
+  *lcp = std::max(0, best_lcp);
+  return best;
+}
+
+void BatchScheduler::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  std::vector<int> rows;
+  std::vector<std::shared_ptr<Req>> row_req;
+  while (true) {
+    cv_work_.wait(lk, [&] {
+      if (stop_ || !pending_.empty()) return true;
+      for (int s = first_slot_; s < n_slots_; ++s)
+        if (slot_req_[s]) return true;
+      return false;
+    });
+    if (stop_) break;
+    // 1. rows whose request was cancelled / abandoned leave before anything runs
+    for (int s = first_slot_; s < n_slots_; ++s)
+      if (slot_req_[s] && slot_req_[s]->cancel) finish(*slot_req_[s], "cancelled");
+    // 2. admission: queued requests into free slots (prefill + first token each)
+    while (!pending_.empty()) {
+      std::shared_ptr<Req> r = pending_.front();
+      if (r->cancel) {
+        pending_.pop_front();
+        finish(*r, "cancelled");
+        continue;
+      }
+      int lcp = 0;
+      const int slot = pick_slot(r->prompt, &lcp);
+      if (slot < 0) break;
+      pending_.pop_front();
+      const int n_prompt = (int)r->prompt.size();
+      const int n_keep = std::min(lcp, n_prompt - 1);
+      r->slot = slot;
+      slot_req_[slot] = r;
+      slot_used_[slot] = ++tick_;
+      r->t_start = sched_now();
+      std::string err;
+      int tok = 0;
+      lk.unlock();
+      try {
+        tok = eng_.slot_begin(slot, r->prompt, n_keep, r->sp);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+      lk.lock();
+      r->t_first = sched_now();
+      if (!err.empty()) {
+        slot_hist_[slot].clear();
+        r->error = err;
+        finish(*r, "error");
+        continue;
+      }
+      ++st_.admitted;
+      st_.reused_tokens += n_keep;
+      r->n_prefilled = n_prompt - n_keep;
+      slot_hist_[slot] = r->prompt;
+      push_token(*r, tok);
+    }
+    // 3. one decode step over every active row
+    rows.clear();
+    row_req.clear();
+    for (int s = first_slot_; s < n_slots_; ++s)
+      if (slot_req_[s]) {
+        rows.push_back(s);
+        row_req.push_back(slot_req_[s]);
+      }
+    if (rows.empty()) continue;
+    std::vector<int> out;
+    std::string err;
+    lk.unlock();
+    try {
+      out = eng_.batch_step(rows);
+    } catch (const std::exception& e) {
+      err = e.what();
+    }
+    lk.lock();
+    ++st_.steps;
+    st_.rows += (long long)rows.size();
+    for (size_t b = 0; b < rows.size(); ++b) {
+      Req& r = *row_req[b];
+      if (!err.empty()) {
+        slot_hist_[rows[b]].clear();
+        r.error = err;
+        finish(r, "error");
+        continue;
+      }
+      slot_hist_[rows[b]].push_back(r.tokens.back());  // the token this step fed is now in the KV
+      if (r.done) continue;
+      push_token(r, out[b]);
+    }
+    cv_out_.notify_all();
+  }
+  // shutdown: nothing runs any more
+  for (auto& r : pending_) finish(*r, "cancelled");
+  pending_.clear();
+  for (int s = first_slot_; s < n_slots_; ++s)
+    if (slot_req_[s]) finish(*slot_req_[s], "cancelled");
+  cv_out_.notify_all();
+}
+
+}  // namespace lfk

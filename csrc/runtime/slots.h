@@ -1,0 +1,34 @@
+// Host-only interface between the continuous-batching scheduler (scheduler.h) and an
+// engine that holds several KV slots. The MI355X Engine implements it; tests drive the
+// scheduler through a deterministic CPU stand-in (bindings_cpu.cpp) so its admission,
+// prefix-reuse and retirement logic is checked without a GPU.
+#pragma once
+#include <utility>
+#include <vector>
+
+namespace lfk {
+
+struct SamplingOpts {
+  int top_k = 40;
+  float top_p = 0.95f, min_p = 0.05f, temp = 0.8f;
+  float repeat_penalty = 1.1f, freq_penalty = 0.f, presence_penalty = 0.f;
+  int last_n = 64;
+  unsigned long long seed = 0;
+  float tfs_z = 1.f, typical_p = 1.f;
+  std::vector<std::pair<int, float>> logit_bias;  // distinct tokens, at most kMaxLogitBias
+};
+
+class SlotBackend {
+ public:
+  virtual ~SlotBackend() = default;
+  virtual int n_slots() const = 0;
+  virtual int max_batch() const = 0;   // rows one batch_step takes
+  virtual int n_ctx() const = 0;
+  // prefill prompt[n_keep:] into `slot` (its first n_keep positions are reused), set the
+  // slot's sampling state, return its first token
+  virtual int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) = 0;
+  // one decode step of every listed slot at its own position -> each slot's next token
+  virtual std::vector<int> batch_step(const std::vector<int>& slots) = 0;
+};
+
+}  // namespace lfk

@@ -69,6 +69,9 @@ class Settings:
     chat_format: Optional[str] = None
     engine: str = "native"  # native | fake
     verbose: bool = False
+    # continuous batching (MI355X engine, one rank): up to max_batch generations decode
+    # together as rows of one batched step. 1 = the reference's one-at-a-time serving.
+    max_batch: int = 1
     # --- service (reference api.py:17-19) ---
     max_context_tokens: int = 1024
     timeout_seconds: float = 25.0
@@ -104,6 +107,7 @@ class Settings:
         s.chat_format = _env("CHAT_FORMAT", None)
         s.engine = _env("ENGINE", s.engine).lower()
         s.verbose = _env("VERBOSE", s.verbose, bool)
+        s.max_batch = max(1, _env("MAX_BATCH", s.max_batch, int))
         s.max_context_tokens = _env("MAX_CONTEXT_TOKENS", s.max_context_tokens, int)
         s.timeout_seconds = _env("TIMEOUT_SECONDS", s.timeout_seconds, float)
         s.max_queue_size = _env("MAX_QUEUE_SIZE", s.max_queue_size, int)

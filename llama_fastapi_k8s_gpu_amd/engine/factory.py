@@ -13,4 +13,5 @@ def build_engine(settings: Settings):
                  n_ctx=settings.n_ctx, n_batch=settings.n_batch,
                  tensor_split=settings.tensor_split, split_mode=settings.split_mode,
                  main_gpu=settings.main_gpu, seed=settings.seed, chat_format=settings.chat_format,
-                 use_graphs=settings.use_graphs, verbose=settings.verbose)
+                 use_graphs=settings.use_graphs, verbose=settings.verbose,
+                 **({"max_batch": settings.max_batch} if settings.max_batch > 1 else {}))

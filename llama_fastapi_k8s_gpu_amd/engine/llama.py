@@ -196,6 +196,12 @@ class Llama:
         if max_tokens + n_prompt >= self._n_ctx:
             max_tokens = self._n_ctx - n_prompt
         stop_ids, text_stops = self._text_stops(stop)
+        batches = getattr(self._backend, "batches", None)
+        if batches is not None and batches(params):
+            # a row of the backend's continuous batch: no facade lock (requests run
+            # concurrently) and no facade KV bookkeeping (the scheduler reuses prefixes per slot)
+            return self._generate_locked(prompt_tokens, max_tokens, params, stop_ids, text_stops, cancel_event,
+                                         on_token, stopping_criteria, track_kv=False)
         self._lock.acquire()
         try:
             if self.cache is not None:   # restore a cached state that shares more of the prompt
@@ -212,10 +218,10 @@ class Llama:
             self._lock.release()
 
     def _generate_locked(self, prompt_tokens, max_tokens, params, stop_ids, text_stops, cancel_event, on_token,
-                         stopping_criteria):
+                         stopping_criteria, track_kv: bool = True):
         n_prompt = len(prompt_tokens)
         # KV prefix reuse (must re-evaluate at least one prompt token for logits)
-        n_keep = min(longest_token_prefix(self._kv_tokens, prompt_tokens), n_prompt - 1)
+        n_keep = min(longest_token_prefix(self._kv_tokens, prompt_tokens), n_prompt - 1) if track_kv else 0
         # upstream stops as soon as a stop string appears in the generated text (or a
         # stopping criterion fires): watch the token stream and end the backend's loop
         # through its cancel poll
@@ -247,10 +253,11 @@ class Llama:
             prompt_tokens, n_keep, max_tokens, params, sorted(stop_ids),
             poll=poll if (watched or cancel_event is not None) else None,
             on_token=watch if (watched or on_token) else None)
-        hist = list(prompt_tokens) + list(res.tokens)
-        self._kv_tokens = hist[:res.n_evaluated]
-        if self.cache is not None and self._kv_tokens:
-            self.cache[tuple(self._kv_tokens)] = self._save_state(self.cache.on_device)
+        if track_kv:
+            hist = list(prompt_tokens) + list(res.tokens)
+            self._kv_tokens = hist[:res.n_evaluated]
+            if self.cache is not None and self._kv_tokens:
+                self.cache[tuple(self._kv_tokens)] = self._save_state(self.cache.on_device)
         toks = list(res.tokens)
         reason = res.finish_reason
         if toks and toks[-1] in stop_ids:

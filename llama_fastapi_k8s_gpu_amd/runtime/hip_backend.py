@@ -14,6 +14,12 @@ api.py:24-28) mapped onto one process per GPU:
     split stays even (the logit all-gather moves equal counts).
   * ``split_mode="none"/"layer"`` in one process: the model runs on
     ``main_gpu`` (one GPU holds any BASELINE model: 288 GB HBM).
+  * ``max_batch=M > 1`` (one rank): continuous batching. The engine gets M + 1 KV
+    slots; a native scheduler thread (csrc/runtime/scheduler.cpp) decodes every
+    admitted request as one row of a batched step (one weight stream per step
+    instead of one per request) and admits new requests into free slots between
+    steps. Requests whose sampler settings the GPU chain does not cover take the
+    single-sequence path on slot 0 (serialised with the scheduler by the engine).
 """
 from __future__ import annotations
 
@@ -46,7 +52,7 @@ class HipBackend:
 
     def __init__(self, model_path: str, hparams, n_ctx: int = 1024, n_gpu_layers: int = -1,
                  tensor_split: Optional[Sequence[float]] = None, split_mode: str = "layer", main_gpu: int = 0,
-                 n_batch: int = 512, use_graphs: bool = True, **_):
+                 n_batch: int = 512, use_graphs: bool = True, max_batch: int = 1, **_):
         hip = load_hip()
         if 0 <= n_gpu_layers < hparams.n_layer:
             raise ValueError(f"n_gpu_layers={n_gpu_layers} < n_layer={hparams.n_layer}: partial offload runs on "
@@ -54,9 +60,15 @@ class HipBackend:
         rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split)
         device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)
         self.tp_rank, self.tp_size = rank, size
+        max_batch = max(1, int(max_batch or 1))
+        if max_batch > 1 and size > 1:
+            logger.warning("max_batch=%d ignored: continuous batching runs on one rank (tp=%d)", max_batch, size)
+            max_batch = 1
+        self.max_batch = max_batch
         self.engine = hip.Engine(model_path, n_ctx=n_ctx, n_batch=min(n_batch, n_ctx), device=device,
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
-                                 tensor_split=ts)
+                                 tensor_split=ts, n_slots=max_batch + 1 if max_batch > 1 else 1)
+        self.sched = hip.BatchScheduler(self.engine) if max_batch > 1 else None
         self.n_ctx = n_ctx
         self.n_vocab = int(hparams.n_vocab)
         self.n_batch = min(n_batch, n_ctx)  # the engine's prefill chunk bound (eval_logits rejects T > n_batch)
@@ -79,11 +91,55 @@ class HipBackend:
             logger.warning("P2P all-reduce unavailable, using RCCL only: %s", e)
 
     def health(self):
-        return {"ok": bool(self.engine.healthy), "backend": self.name, "tp": self.tp_size,
-                "error": self.engine.last_error or None}
+        h = {"ok": bool(self.engine.healthy), "backend": self.name, "tp": self.tp_size,
+             "error": self.engine.last_error or None}
+        if self.sched is not None:
+            h["batching"] = dict(self.sched.stats(), max_batch=self.max_batch)
+        return h
+
+    def batches(self, params: SamplingParams) -> bool:
+        """Whether this request runs as a row of the continuous batch (the facade then
+        skips its single-sequence lock and KV prefix bookkeeping: the scheduler reuses
+        prefixes per slot)."""
+        return self.sched is not None and params.gpu_compatible(self.n_vocab)
+
+    def close(self):
+        if self.sched is not None:
+            self.sched.shutdown()
 
     def device_memory(self):
         return {f"hip:{self.device}": int(self.engine.device_bytes)}
+
+    def _sp(self, params: SamplingParams) -> dict:
+        return {"top_k": params.top_k, "top_p": params.top_p, "min_p": params.min_p,
+                "temperature": params.temperature, "repeat_penalty": params.repeat_penalty,
+                "frequency_penalty": params.frequency_penalty, "presence_penalty": params.presence_penalty,
+                "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF, "tfs_z": params.tfs_z,
+                "typical_p": params.typical_p,
+                "logit_bias": {int(t): float(b) for t, b in params.logit_bias.items() if 0 <= int(t) < self.n_vocab}}
+
+    def _generate_batched(self, prompt: Sequence[int], max_new: int, params: SamplingParams,
+                          stop_ids: Sequence[int], poll: Optional[Callable[[], bool]],
+                          on_token: Optional[Callable[[int], None]]) -> GenerationResult:
+        rid = self.sched.submit(list(prompt), int(max_new), self._sp(params), list(stop_ids))
+        toks = []
+        try:
+            while True:
+                r = self.sched.wait(rid, len(toks), 20)
+                for t in r["tokens"]:
+                    toks.append(t)
+                    if on_token:
+                        on_token(t)
+                if r["done"]:
+                    break
+                if poll is not None and poll():
+                    self.sched.cancel(rid)
+        finally:
+            self.sched.release(rid)
+        if r["finish"] == "error":
+            raise RuntimeError(r["error"] or "batched generation failed")
+        return GenerationResult(toks, r["finish"], len(prompt) + max(0, len(toks) - 1), r["prefill_s"],
+                                r["decode_s"], int(r["n_prefilled"]))
 
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
@@ -91,12 +147,9 @@ class HipBackend:
         if not params.gpu_compatible(self.n_vocab):
             return host_generate(self._forward, prompt, n_keep, max_new, params, stop_ids, self.n_ctx, poll,
                                  on_token)
-        sp = {"top_k": params.top_k, "top_p": params.top_p, "min_p": params.min_p,
-              "temperature": params.temperature, "repeat_penalty": params.repeat_penalty,
-              "frequency_penalty": params.frequency_penalty, "presence_penalty": params.presence_penalty,
-              "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF, "tfs_z": params.tfs_z,
-              "typical_p": params.typical_p,
-              "logit_bias": {int(t): float(b) for t, b in params.logit_bias.items() if 0 <= int(t) < self.n_vocab}}
+        if self.sched is not None:
+            return self._generate_batched(prompt, max_new, params, stop_ids, poll, on_token)
+        sp = self._sp(params)
         r = self.engine.generate(list(prompt), int(n_keep), int(max_new), sp, list(stop_ids), poll, on_token)
         return GenerationResult(list(r["tokens"]), r["finish"], int(r["n_evaluated"]), r["prefill_s"],
                                 r["decode_s"], int(r["n_prefilled"]))

@@ -18,6 +18,10 @@ Documented deviations:
     result (408) is unchanged;
   * OpenAI-compatible ``/v1/*`` routes (``OPENAI_API``, server/openai_api.py) share
     the admission queue and the one-at-a-time consumer.
+  * ``MAX_BATCH=M`` (default 1 = the reference): M consumer tasks and a
+    Semaphore(M) feed the engine's continuous batch, so M generations run at once
+    (M in flight + ``MAX_QUEUE_SIZE`` waiting; the next request gets 503). FIFO
+    admission, timeouts and error strings are unchanged.
 """
 from __future__ import annotations
 
@@ -175,18 +179,22 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             # before the server accepts traffic, off the event loop.
             app_.state.engine = await asyncio.to_thread(factory, settings)
         app_.state.queue = asyncio.Queue(maxsize=settings.max_queue_size)
-        app_.state.semaphore = asyncio.Semaphore(1)
-        app_.state.consumer_task = asyncio.create_task(consumer(app_))
+        width = max(1, int(settings.max_batch))
+        app_.state.semaphore = asyncio.Semaphore(width)
+        app_.state.consumer_tasks = [asyncio.create_task(consumer(app_)) for _ in range(width)]
+        app_.state.consumer_task = app_.state.consumer_tasks[0]
         app_.state.ready = True
         try:
             yield
         finally:
             app_.state.ready = False
-            app_.state.consumer_task.cancel()
-            try:
-                await app_.state.consumer_task
-            except (asyncio.CancelledError, Exception):
-                pass
+            for t in app_.state.consumer_tasks:
+                t.cancel()
+            for t in app_.state.consumer_tasks:
+                try:
+                    await t
+                except (asyncio.CancelledError, Exception):
+                    pass
             close = getattr(app_.state.engine, "close", None)
             if close is not None and engine is None:
                 await asyncio.to_thread(close)
