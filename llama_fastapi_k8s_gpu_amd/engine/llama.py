@@ -45,9 +45,11 @@ def _select_backend(reader, hp: LlamaHParams, n_gpu_layers: int, backend: Option
     n_gpu = hp.n_layer + 1 if n_gpu_layers < 0 else n_gpu_layers
     if n_gpu == 0:
         return "cpu"
+    # ask the runtime that will run the model (the _hip extension's HIP runtime): torch may
+    # bundle a different HIP runtime that reports no device once ours initialised the GPU
     try:
-        import torch
-        if torch.cuda.is_available():
+        from ..runtime import load_hip
+        if load_hip().device_count() > 0:
             return "hip" if n_gpu >= hp.n_layer else "hybrid"
     except Exception:
         pass
