@@ -117,6 +117,7 @@ PYBIND11_MODULE(_hip, m) {
            })
       .def_property_readonly("n_slots", &Engine::n_slots)
       .def_property_readonly("max_batch", &Engine::max_batch)
+      .def_property_readonly("batch_gemv", &Engine::batch_gemv)
       .def("slot_begin",
            [](Engine& e, int slot, const std::vector<int>& prompt, int n_keep, py::dict sp) {
              const SamplingOpts o = sampling_opts(sp);
@@ -244,6 +245,26 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
      py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
      py::arg("debug") = 0, py::arg("dbg_clk") = 0);
+
+  m.def("bprep", [](uintptr_t x, int ldx, bool swiglu, uintptr_t norm, float eps, int K, int B, uintptr_t xh, int ldh,
+                    uintptr_t stream, uintptr_t zero, int zero_n) {
+    BPrepArgs a;
+    a.x = P<float>(x); a.ldx = ldx; a.swiglu = swiglu; a.norm_w = P<float>(norm); a.eps = eps; a.K = K; a.B = B;
+    a.xh = P<__half>(xh); a.ldh = ldh; a.zero = P<float>(zero); a.zero_n = zero_n;
+    bprep(a, S(stream));
+    hip_ok("bprep");
+  }, py::arg("x"), py::arg("ldx"), py::arg("swiglu"), py::arg("norm"), py::arg("eps"), py::arg("K"), py::arg("B"),
+     py::arg("xh"), py::arg("ldh"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0);
+  m.def("bmm", [](uintptr_t w, int type, int rows, int K, uintptr_t xh, int ldh, uintptr_t out, int ldo, int B,
+                  uintptr_t stream) {
+    BmmArgs a;
+    a.w = make_qmat(P<void>(w), type, rows, K);
+    a.xh = P<__half>(xh); a.ldh = ldh; a.out = P<float>(out); a.ldo = ldo; a.n_out = rows; a.B = B;
+    bmm(a, S(stream));
+    hip_ok("bmm");
+  }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("xh"), py::arg("ldh"), py::arg("out"),
+     py::arg("ldo"), py::arg("B"), py::arg("stream"));
+  m.def("bmm_supported", &bmm_supported);
 
   py::class_<P2PComm>(m, "P2PComm")
       .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_n"), py::arg("device"))

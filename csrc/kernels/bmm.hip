@@ -1,0 +1,317 @@
+// Batched decode projection on MFMA (continuous batching, 1-16 activation rows):
+//   out[b][row] += sum_k W[row][k] * xh[b][k]
+// W block-quantised (Q4_K / Q5_K / Q6_K / Q8_0, planar layout), xh f16 rows prepared once
+// per projection input by bprep (RMSNorm / SwiGLU / residual-free copy, f16, 4-group
+// swizzle - see below).
+//
+// Why MFMA: with 2-16 rows the integer-dot GEMV (bgemv.hip) does B dot products per decoded
+// weight on the VALU and ran VALU/epilogue-bound (6.2 ms per 8B step at B = 8,
+// profiles/README.md). Here a wave owns a 16-row weight tile and feeds it to
+// v_mfma_f32_16x16x32_f16 as the A operand, the activation rows as B: the matrix core does
+// all 16 columns in the same 16 cycles, so the per-weight work is the dequantisation only
+// (~2 VALU ops per weight, independent of B) and the weights stay ONE HBM stream.
+//
+// Dequantisation straight into MFMA fragments: lane l holds A[row l&15][k = 8(l>>4) + j];
+// here lane group kq = l>>4 takes chunk 4s + kq (32 weights) of its row at step s, and
+// MFMA i (0..3) of the step takes dword i of the chunk's 16 quant bytes: low nibbles
+// (4i, 4i+2), (4i+1, 4i+3) and high nibbles the same - two nibbles per v_and_or with the
+// f16 exponent of 1024 OR-ed in (1024 + q exactly), one v_pk_add (-1024, exact) and one
+// v_pk_fma (d*sc, -dmin*m) per pair. The k order inside each 4-group is therefore
+// (0, 2, 1, 3); bprep writes x in that order so B needs no shuffles: the B fragment of
+// MFMA i is 8 bytes at the chunk's low-run offset + 4i and 8 bytes at its high-run offset + 4i.
+//
+// Work items are (16-row tile, K part); partial tiles are added to `out` atomically (split-K
+// keeps >= 2 waves per SIMD busy on every projection shape, including the 256-tile Wo /
+// down); outputs that are not the residual stream are zeroed by the bprep launch before.
+#include <algorithm>
+#include <stdexcept>
+
+#include "gemv_dev.h"
+
+namespace lfk {
+
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ h2_t as_h2(unsigned v) { return __builtin_bit_cast(h2_t, v); }
+__device__ __forceinline__ unsigned as_u(h2_t v) { return __builtin_bit_cast(unsigned, v); }
+
+// two values (bits 0.. and 16..) -> (value * a + m) as f16 pair: magic 1024 exponent,
+// exact subtraction of `bias`, one fused multiply-add
+__device__ __forceinline__ unsigned deq_pair(unsigned two, h2_t bias, h2_t a, h2_t m) {
+  const h2_t v = as_h2(two | 0x64006400u) - bias;
+  return as_u(v * a + m);
+}
+
+struct HFrag {
+  unsigned w[16];  // MFMA i takes w[4i .. 4i+3]
+};
+
+// chunk c of one row (raw loads in WRaw) -> the four A fragments
+template <int T>
+__device__ __forceinline__ void dequant_frags(const WRaw<T>& w, int c, HFrag& F) {
+  const int j = c & 7;
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+    const int g = j >> 1;
+    const unsigned dd = (unsigned)w.m.x;
+    const float d = h2f(dd & 0xFFFF), dmin = h2f(dd >> 16);
+    const unsigned y = w.m.y, z = w.m.z, ww = w.m.w;
+    float sc[2], mn[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int s = 2 * g + h, sh = 8 * (s & 3);
+      const unsigned a_sc = (y >> sh) & 63, a_m = (z >> sh) & 63;
+      const unsigned b_sc = ((ww >> sh) & 0xF) | (((y >> (sh + 6)) & 3) << 4);
+      const unsigned b_m = ((ww >> (sh + 4)) & 0xF) | (((z >> (sh + 6)) & 3) << 4);
+      sc[h] = d * (float)(s >= 4 ? b_sc : a_sc);
+      mn[h] = -dmin * (float)(s >= 4 ? b_m : a_m);
+    }
+    const h2_t alo = {(_Float16)sc[0], (_Float16)sc[0]}, ahi = {(_Float16)sc[1], (_Float16)sc[1]};
+    const h2_t mlo = {(_Float16)mn[0], (_Float16)mn[0]}, mhi = {(_Float16)mn[1], (_Float16)mn[1]};
+    const h2_t bias = {(_Float16)1024.f, (_Float16)1024.f};
+    const int qv[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned lo, hi;  // the dword's 4 low-nibble and 4 high-nibble values as bytes
+      if constexpr (T == T_Q4_K) {
+        lo = (unsigned)qv[i] & 0x0F0F0F0Fu;
+        hi = ((unsigned)qv[i] >> 4) & 0x0F0F0F0Fu;
+      } else {
+        const unsigned hv = (unsigned)(i == 0 ? w.h.x : i == 1 ? w.h.y : i == 2 ? w.h.z : w.h.w);
+        lo = ((unsigned)qv[i] & 0x0F0F0F0Fu) | (((hv >> (2 * g)) & 0x01010101u) << 4);
+        hi = (((unsigned)qv[i] >> 4) & 0x0F0F0F0Fu) | (((hv >> (2 * g + 1)) & 0x01010101u) << 4);
+      }
+      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, alo, mlo);
+      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, alo, mlo);
+      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, ahi, mhi);
+      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, ahi, mhi);
+    }
+  } else if constexpr (T == T_Q6_K) {
+    const int o = 16 * (j & 3);
+    const int s = (o >= 32) ? 2 : 0;
+    const float d = h2f(w.d & 0xFFFF);
+    const float slo = d * (float)w.slo, shi = d * (float)w.shi;
+    const h2_t alo = {(_Float16)slo, (_Float16)slo}, ahi = {(_Float16)shi, (_Float16)shi};
+    const h2_t zero = {(_Float16)0.f, (_Float16)0.f};
+    const h2_t bias = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 + 32: (q - 32) exactly
+    const int lv[4] = {w.l.x, w.l.y, w.l.z, w.l.w};
+    const int hv[4] = {w.h.x, w.h.y, w.h.z, w.h.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned lo = ((unsigned)lv[i] & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> s) & 0x03030303u) << 4);
+      const unsigned hi = (((unsigned)lv[i] >> 4) & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> (s + 4)) & 0x03030303u) << 4);
+      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, alo, zero);
+      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, alo, zero);
+      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, ahi, zero);
+      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, ahi, zero);
+    }
+  } else {  // Q8_0: signed bytes, flipped to unsigned for the magic, one scale
+    const float d = h2f(w.d & 0xFFFF);
+    const h2_t a = {(_Float16)d, (_Float16)d};
+    const h2_t zero = {(_Float16)0.f, (_Float16)0.f};
+    const h2_t bias = {(_Float16)1152.f, (_Float16)1152.f};  // 1024 + 128
+    const int lo4[4] = {w.a.x, w.a.y, w.a.z, w.a.w};
+    const int hi4[4] = {w.b.x, w.b.y, w.b.z, w.b.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned lo = (unsigned)lo4[i] ^ 0x80808080u, hi = (unsigned)hi4[i] ^ 0x80808080u;
+      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, a, zero);
+      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, a, zero);
+      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, a, zero);
+      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, a, zero);
+    }
+  }
+}
+
+// element offsets (into an x row) of chunk c's low and high 16-runs
+template <int T>
+__device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
+  const int sb = c >> 3, j = c & 7;
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+    off_lo = sb * 256 + 64 * (j >> 1) + 16 * (j & 1);
+    off_hi = off_lo + 32;
+  } else if constexpr (T == T_Q6_K) {
+    off_lo = sb * 256 + 128 * (j >> 2) + 16 * (j & 3);
+    off_hi = off_lo + 64;
+  } else {
+    off_lo = 32 * c;
+    off_hi = off_lo + 16;
+  }
+}
+
+static constexpr int kBmmBlock = 256;
+
+template <int QT>
+__global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
+  const int lane = threadIdx.x & 63, wave = wave_id();
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int K = a.w.K, steps = K >> 7;  // 128 k (4 chunks) per step
+  const int tiles = (a.n_out + 15) >> 4;
+  const int kparts = a.kparts;
+  const int spp = (steps + kparts - 1) / kparts;
+  const int total = tiles * kparts;
+  // activation column of this lane's B fragment (columns past B re-read row 0: their
+  // outputs are never stored)
+  const bool col_ok = r16 < a.B;
+  const __half* xrow = a.xh + (size_t)(col_ok ? r16 : 0) * a.ldh;
+  for (int item = blockIdx.x * (kBmmBlock / 64) + wave; item < total; item += gridDim.x * (kBmmBlock / 64)) {
+    const int tile = item / kparts, kp = item - tile * kparts;
+    const int s0 = kp * spp, s1 = min(steps, s0 + spp);
+    const RowPtr R = row_ptr(a.w.base, a.w.P, (unsigned)min(tile * 16 + r16, a.n_out - 1));
+    f4_t acc = {0.f, 0.f, 0.f, 0.f};
+    // 2-deep register ring of raw weights (one chunk per lane per step)
+    WRaw<QT> w0, w1;
+    if (s0 < s1) wload<QT>(w0, R, 4 * s0 + kq);
+    if (s0 + 1 < s1) wload<QT>(w1, R, 4 * (s0 + 1) + kq);
+    for (int s = s0; s < s1; s += 2) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int st = s + h;
+        if (st < s1) {
+          const int c = 4 * st + kq;
+          int off_lo, off_hi;
+          chunk_runs<QT>(c, off_lo, off_hi);
+          const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+          const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+          uint4 bl0 = xl[0], bl1 = xl[1], bh0 = xh[0], bh1 = xh[1];
+          HFrag F;
+          dequant_frags<QT>(h == 0 ? w0 : w1, c, F);
+          if (st + 2 < s1) wload<QT>(h == 0 ? w0 : w1, R, 4 * (st + 2) + kq);
+          const unsigned bl[8] = {bl0.x, bl0.y, bl0.z, bl0.w, bl1.x, bl1.y, bl1.z, bl1.w};
+          const unsigned bh[8] = {bh0.x, bh0.y, bh0.z, bh0.w, bh1.x, bh1.y, bh1.z, bh1.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            // A: lo pairs (4i,4i+2),(4i+1,4i+3) then hi pairs; B: x[lo + 4i .. +3], x[hi + 4i .. +3]
+            const uint4 av = make_uint4(F.w[4 * i], F.w[4 * i + 1], F.w[4 * i + 2], F.w[4 * i + 3]);
+            const uint4 bv = make_uint4(bl[2 * i], bl[2 * i + 1], bh[2 * i], bh[2 * i + 1]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av), __builtin_bit_cast(h8_t, bv),
+                                                         acc, 0, 0, 0);
+          }
+        }
+      }
+    }
+    // C[row 4kq + i][col r16]
+    if (col_ok) {
+      float* o = a.out + (size_t)r16 * a.ldo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = tile * 16 + 4 * kq + i;
+        if (row < a.n_out) {
+          if (kparts > 1) atomicAdd(o + row, acc[i]);
+          else o[row] += acc[i];   // one owner per (row, column)
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- activation prep
+// One block per activation row: optional SwiGLU (gate/up pre-activations in 32-feature
+// interleaved groups), optional RMSNorm (* w), f16, k order (0,2,1,3) inside every 4-group.
+// Side job: zero [zero, zero + zero_n) (the split-K output of the projection this feeds).
+static constexpr int kPrepBlock = 1024;
+static constexpr int kPrepMaxVec = 8;  // float4 per thread: K <= 32768
+
+__global__ __launch_bounds__(kPrepBlock) void bprep_kernel(BPrepArgs a) {
+  __shared__ float red[kPrepBlock / 64];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (a.zero) {
+    float4* z = reinterpret_cast<float4*>(a.zero);
+    for (int i = b * kPrepBlock + tid; i < (a.zero_n >> 2); i += gridDim.x * kPrepBlock)
+      z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float* xr = a.x + (size_t)b * a.ldx;
+  float4 v[kPrepMaxVec];
+  float ss = 0.f;
+#pragma unroll
+  for (int u = 0; u < kPrepMaxVec; ++u) {
+    const int i = 4 * (tid + u * kPrepBlock);
+    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < a.K) {
+      if (a.swiglu) {
+        const int gi = (i >> 5) * 64 + (i & 31);
+        const float4 g = *reinterpret_cast<const float4*>(xr + gi);
+        const float4 up = *reinterpret_cast<const float4*>(xr + gi + 32);
+        v[u] = make_float4(silu(g.x) * up.x, silu(g.y) * up.y, silu(g.z) * up.z, silu(g.w) * up.w);
+      } else {
+        v[u] = *reinterpret_cast<const float4*>(xr + i);
+      }
+      ss += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+    }
+  }
+  float rs = 1.f;
+  if (a.norm_w) {
+    ss = wave_sum_fast(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kPrepBlock / 64; ++w) t += red[w];
+    rs = rsqrtf(t / (float)a.K + a.eps);
+  }
+  __half* out = a.xh + (size_t)b * a.ldh;
+#pragma unroll
+  for (int u = 0; u < kPrepMaxVec; ++u) {
+    const int i = 4 * (tid + u * kPrepBlock);
+    if (i < a.K) {
+      float4 t = v[u];
+      if (a.norm_w) {
+        const float4 nw = *reinterpret_cast<const float4*>(a.norm_w + i);
+        t = make_float4(t.x * rs * nw.x, t.y * rs * nw.y, t.z * rs * nw.z, t.w * rs * nw.w);
+      }
+      const h2_t p0 = {(_Float16)t.x, (_Float16)t.z}, p1 = {(_Float16)t.y, (_Float16)t.w};
+      *reinterpret_cast<uint2*>(out + i) = make_uint2(as_u(p0), as_u(p1));
+    }
+  }
+}
+
+void bprep(const BPrepArgs& a, hipStream_t s) {
+  if (a.B < 1 || a.K % 128 || a.K > 4 * kPrepBlock * kPrepMaxVec) throw std::runtime_error("bprep: bad shape");
+  if (a.zero_n % 4) throw std::runtime_error("bprep: zero_n must be a multiple of 4");
+  hipLaunchKernelGGL(bprep_kernel, dim3(a.B), dim3(kPrepBlock), 0, s, a);
+}
+
+// ---------------------------------------------------------------- launch
+bool bmm_supported(int type, int K) {
+  if (type != T_Q4_K && type != T_Q5_K && type != T_Q6_K && type != T_Q8_0) return false;
+  return K >= 128 && K % 256 == 0;
+}
+
+static int bmm_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return std::max(1, n);
+  }();
+  return cus;
+}
+
+template <int QT>
+static void launch_bmm(BmmArgs a, hipStream_t s) {
+  const int tiles = (a.n_out + 15) / 16, steps = a.w.K / 128;
+  // split K until ~8 waves per CU have an item, keeping >= 2 steps per part
+  const int want = 8 * bmm_cus();
+  int kp = 1;
+  while (tiles * kp < want && steps / (kp * 2) >= 2) kp *= 2;
+  a.kparts = kp;
+  const int items = tiles * kp, wpb = kBmmBlock / 64;
+  const int grid = std::max(1, std::min((items + wpb - 1) / wpb, 8 * bmm_cus()));
+  hipLaunchKernelGGL(bmm_kernel<QT>, dim3(grid), dim3(kBmmBlock), 0, s, a);
+}
+
+void bmm(const BmmArgs& a, hipStream_t s) {
+  if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
+  if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
+  if (a.n_out <= 0) return;
+  switch (a.w.type) {
+    case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;
+    case T_Q5_K: launch_bmm<T_Q5_K>(a, s); break;
+    case T_Q6_K: launch_bmm<T_Q6_K>(a, s); break;
+    case T_Q8_0: launch_bmm<T_Q8_0>(a, s); break;
+    default: throw std::runtime_error("bmm: unsupported weight type");
+  }
+}
+
+}  // namespace lfk

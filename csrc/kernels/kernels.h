@@ -60,6 +60,38 @@ struct GemvArgs {
 };
 void gemv(const GemvArgs& a, int epi, hipStream_t s);
 
+// Batched decode projection on MFMA (bmm.hip): out[b][row] += W xh[b] for B <= 16 rows
+// (split-K atomics: `out` holds the residual or zeros). xh rows come from bprep: f16, the
+// k order inside each 4-group swizzled (0, 2, 1, 3) to match the dequantised A fragments.
+static constexpr int kBmmMaxRows = 16;
+struct BmmArgs {
+  QMat w;
+  const __half* xh = nullptr;
+  int ldh = 0;                     // halves between rows of xh (multiple of 8)
+  float* out = nullptr;
+  int ldo = 0;
+  int n_out = 0;                   // rows of W
+  int B = 0;
+  int kparts = 1;                  // set by the launcher
+};
+bool bmm_supported(int type, int K);
+void bmm(const BmmArgs& a, hipStream_t s);
+// f32 rows -> bmm input: optional SwiGLU (x rows of 2K gate/up pre-activations, 32-feature
+// interleaved groups), optional RMSNorm (* norm_w), f16 swizzled; also zeroes zero[0, zero_n)
+struct BPrepArgs {
+  const float* x = nullptr;
+  int ldx = 0;
+  bool swiglu = false;
+  const float* norm_w = nullptr;
+  float eps = 1e-5f;
+  int K = 0, B = 0;
+  __half* xh = nullptr;
+  int ldh = 0;
+  float* zero = nullptr;
+  int zero_n = 0;
+};
+void bprep(const BPrepArgs& a, hipStream_t s);
+
 // Fused QKV projection + RoPE (adjacent pairs) + KV-cache append.
 struct QkvArgs {
   QMat wq, wk, wv;

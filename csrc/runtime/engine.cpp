@@ -105,12 +105,15 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   alloc_buffers();
   build_rope();
   setup_ffn_fused();
+  setup_batch_mfma();
   pdec_status_ = setup_pdecode();
   HIPCHK(hipStreamSynchronize(stream_));
 }
 
 Engine::~Engine() {
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  for (hipGraphExec_t g : bgraph_)
+    if (g) hipGraphExecDestroy(g);
   if (graph_) hipGraphDestroy(graph_);
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   for (void* p : allocs_) hipFree(p);
@@ -275,6 +278,7 @@ void Engine::alloc_buffers() {
     attn_part_b_ = (float*)dalloc(sizeof(float) * bmax_ * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
     attn_cnt_b_ = (int*)dalloc(sizeof(int) * 64 * bmax_);
     HIPCHK(hipMemset(attn_cnt_b_, 0, sizeof(int) * 64 * bmax_));
+    gu_b_ = (float*)dalloc(sizeof(float) * bmax_ * 2 * F_l_);
     HIPCHK(hipHostMalloc((void**)&h_bslots_, sizeof(int) * bmax_, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
   }
@@ -285,6 +289,25 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(dev_err_, 0, sizeof(int) * 4));
   HIPCHK(hipHostMalloc((void**)&h_ring_, sizeof(int) * 64, hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&h_tokens_, sizeof(int) * B, hipHostMallocDefault));
+}
+
+void Engine::setup_batch_mfma() {
+  bg_ = bg_ffn_ = false;
+  if (!bmax_ || opt_.layer_begin > 0) return;
+  const char* e = std::getenv("LFK_BATCH_MFMA");
+  if (e && e[0] == '0') return;
+  auto ok = [&](const QMat& m) { return m.base && bmm_supported(m.type, m.K); };
+  auto kfit = [](int K) { return K % 128 == 0 && K <= 32768; };  // bprep's row shapes
+  bool att = ok(output_) && kfit(hp_.n_embd) && kfit(nq_) && (V_pad_ % 4) == 0 && ((nq_ + 2 * nkvd_) % 4) == 0;
+  bool ffn = hp_.n_expert == 0 && kfit(F_l_);
+  for (int l = 0; l < hp_.n_layer; ++l) {
+    const Layer& L = layers_[l];
+    att = att && ok(L.wq) && ok(L.wk) && ok(L.wv) && ok(L.wo);
+    ffn = ffn && ok(L.w_gu) && ok(L.w_down);
+  }
+  bg_ = att;
+  bg_ffn_ = att && ffn;
+  if (bg_) xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
 }
 
 // The fused decode FFN needs: one rank (the TP path all-reduces the down
@@ -558,51 +581,60 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       gemm_dq(o, GEMM_STORE, s);
       allreduce_into(tmp_, x_, (size_t)T * d, s);
     }
-    rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s);
-    if (hp_.n_expert > 0) {
-      const int E = hp_.n_expert;
-      GemmArgs ra;
-      ra.w = L.router; ra.x = xb_; ra.T = T; ra.out = router_logits_; ra.ldo = E;
-      gemm_dq(ra, GEMM_STORE, s);
-      const int KU = hp_.n_expert_used;
-      // device-side routing -> per-expert row lists; gather the routed rows once
-      moe_route_group(router_logits_, T, E, KU, moe_sel_, moe_selw_, moe_off_, moe_tok_, moe_gw_, moe_pos_, s);
-      gather_rows_bf16(xb_, moe_tok_, T * KU, d, moe_xg_, s);
-      if (tp) {
-        if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * T * d, hipMemcpyDeviceToDevice, s));
-        else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * T * d, s));
-      }
-      float* acc = tp ? tmp_ : x_;
-      // split-K partials of the grouped down GEMMs meet by atomic add: zero the gathered output
-      HIPCHK(hipMemsetAsync(moe_yg_, 0, sizeof(float) * (size_t)T * KU * d, s));
-      const int hint = std::max(1, T * KU / E);
-      for (int e = 0; e < E; ++e) {  // each expert multiplies only its rows (count/offset read on the device)
-        GemmArgs gu;
-        gu.w = L.gu_exps; gu.w.base += L.gu_exps.expert_stride * e;
-        gu.x = moe_xg_; gu.T = T; gu.out_bf16 = moe_hg_; gu.seg_dev = moe_off_ + e; gu.rows_hint = hint;
-        gemm_dq(gu, GEMM_SWIGLU, s);
-        GemmArgs dn;
-        dn.w = L.down_exps; dn.w.base += L.down_exps.expert_stride * e;
-        dn.x = moe_hg_; dn.T = T; dn.ldo = d; dn.out = moe_yg_; dn.seg_dev = moe_off_ + e; dn.rows_hint = hint;
-        gemm_dq(dn, GEMM_STORE, s);
-      }
-      moe_scatter_add(acc, moe_yg_, moe_pos_, moe_gw_, T, KU, d, s);
-      if (tp) allreduce_into(tmp_, x_, (size_t)T * d, s);
-    } else {
+  }
+  enqueue_rows_ffn(l, T, s);
+}
+
+// The FFN half of a layer over T rows (prompt chunk or batched decode rows): RMSNorm ->
+// gate/up (or MoE routing + grouped experts) -> down, residual into x_.
+void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s) {
+  const Layer& L = layers_[l];
+  const int d = hp_.n_embd;
+  const bool tp = opt_.tp_size > 1;
+  rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s);
+  if (hp_.n_expert > 0) {
+    const int E = hp_.n_expert;
+    GemmArgs ra;
+    ra.w = L.router; ra.x = xb_; ra.T = T; ra.out = router_logits_; ra.ldo = E;
+    gemm_dq(ra, GEMM_STORE, s);
+    const int KU = hp_.n_expert_used;
+    // device-side routing -> per-expert row lists; gather the routed rows once
+    moe_route_group(router_logits_, T, E, KU, moe_sel_, moe_selw_, moe_off_, moe_tok_, moe_gw_, moe_pos_, s);
+    gather_rows_bf16(xb_, moe_tok_, T * KU, d, moe_xg_, s);
+    if (tp) {
+      if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * T * d, hipMemcpyDeviceToDevice, s));
+      else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * T * d, s));
+    }
+    float* acc = tp ? tmp_ : x_;
+    // split-K partials of the grouped down GEMMs meet by atomic add: zero the gathered output
+    HIPCHK(hipMemsetAsync(moe_yg_, 0, sizeof(float) * (size_t)T * KU * d, s));
+    const int hint = std::max(1, T * KU / E);
+    for (int e = 0; e < E; ++e) {  // each expert multiplies only its rows (count/offset read on the device)
       GemmArgs gu;
-      gu.w = L.w_gu; gu.x = xb_; gu.T = T; gu.out_bf16 = h_;
+      gu.w = L.gu_exps; gu.w.base += L.gu_exps.expert_stride * e;
+      gu.x = moe_xg_; gu.T = T; gu.out_bf16 = moe_hg_; gu.seg_dev = moe_off_ + e; gu.rows_hint = hint;
       gemm_dq(gu, GEMM_SWIGLU, s);
       GemmArgs dn;
-      dn.w = L.w_down; dn.x = h_; dn.T = T; dn.ldo = d;
-      if (!tp) {
-        dn.out = x_;
-        gemm_dq(dn, GEMM_ADD, s);
-      } else {
-        dn.out = tmp_;
-        dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;
-        gemm_dq(dn, GEMM_STORE, s);
-        allreduce_into(tmp_, x_, (size_t)T * d, s);
-      }
+      dn.w = L.down_exps; dn.w.base += L.down_exps.expert_stride * e;
+      dn.x = moe_hg_; dn.T = T; dn.ldo = d; dn.out = moe_yg_; dn.seg_dev = moe_off_ + e; dn.rows_hint = hint;
+      gemm_dq(dn, GEMM_STORE, s);
+    }
+    moe_scatter_add(acc, moe_yg_, moe_pos_, moe_gw_, T, KU, d, s);
+    if (tp) allreduce_into(tmp_, x_, (size_t)T * d, s);
+  } else {
+    GemmArgs gu;
+    gu.w = L.w_gu; gu.x = xb_; gu.T = T; gu.out_bf16 = h_;
+    gemm_dq(gu, GEMM_SWIGLU, s);
+    GemmArgs dn;
+    dn.w = L.w_down; dn.x = h_; dn.T = T; dn.ldo = d;
+    if (!tp) {
+      dn.out = x_;
+      gemm_dq(dn, GEMM_ADD, s);
+    } else {
+      dn.out = tmp_;
+      dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+      gemm_dq(dn, GEMM_STORE, s);
+      allreduce_into(tmp_, x_, (size_t)T * d, s);
     }
   }
 }
@@ -693,6 +725,87 @@ int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, con
   return tok;
 }
 
+// bmm over B rows: groups of kBmmMaxRows columns (one more weight stream per group)
+void Engine::bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B,
+                      hipStream_t s) {
+  for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
+    BmmArgs a;
+    a.w = w; a.xh = xh + (size_t)b0 * ldh; a.ldh = ldh;
+    a.out = out + (size_t)b0 * ldo; a.ldo = ldo; a.n_out = n_out;
+    a.B = std::min(kBmmMaxRows, B - b0);
+    bmm(a, s);
+  }
+}
+
+void Engine::bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero,
+                        int zero_n, hipStream_t s) {
+  BPrepArgs p;
+  p.x = x; p.ldx = ldx; p.swiglu = swiglu; p.norm_w = norm_w; p.eps = hp_.rms_eps;
+  p.K = K; p.B = B; p.xh = xh_b_; p.ldh = K; p.zero = zero; p.zero_n = zero_n;
+  bprep(p, s);
+}
+
+// One layer of batch_step on the MFMA batched projections (bmm.hip). Every projection input
+// is prepared once (bprep: norm / SwiGLU, f16) and that launch also zeroes the split-K output
+// of the projection it feeds (qkv_, gu_b_); Wo and down accumulate into the residual x_.
+void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
+  const Layer& L = layers_[l];
+  const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
+  const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
+  bprep_rows(x_, d, false, L.attn_norm, d, B, qkv_, B * ncol, s);
+  bmm_rows(L.wq, xh_b_, d, qkv_, ncol, nq_, B, s);
+  bmm_rows(L.wk, xh_b_, d, qkv_ + nq_, ncol, nkvd_, B, s);
+  bmm_rows(L.wv, xh_b_, d, qkv_ + nq_ + nkvd_, ncol, nkvd_, B, s);
+  __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
+  __half* vcl = vc_ + kv_layer * l;
+  rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
+  AttnDecodeArgs aa;
+  aa.q = q_; aa.k_cache = kcl; aa.v_cache = vcl; aa.pos = bpos_;
+  aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
+  aa.scale = 1.f / std::sqrt((float)hd);
+  aa.part = attn_part_b_; aa.counters = attn_cnt_b_; aa.out = attn_;
+  aa.batch = B; aa.slots = bslots_; aa.slot_stride = slot_stride_;
+  aa.q_stride = nq_; aa.out_stride = nq_;
+  aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
+  attn_decode(aa, s);
+  bprep_rows(attn_, nq_, false, nullptr, nq_, B, nullptr, 0, s);
+  bmm_rows(L.wo, xh_b_, nq_, x_, d, d, B, s);
+  if (bg_ffn_) {
+    bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
+    bmm_rows(L.w_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
+    bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s);
+    bmm_rows(L.w_down, xh_b_, F_l_, x_, d, d, B, s);
+    return;
+  }
+  // MoE (or unsupported FFN types): the grouped-GEMM FFN of the prompt path over the B rows
+  enqueue_rows_ffn(l, B, s);
+}
+
+// The device work of one batch step over B rows (slots / positions / tokens are read from
+// device memory, so one captured graph per B serves every step).
+void Engine::enqueue_batch_step(int B, hipStream_t s) {
+  const int d = hp_.n_embd;
+  batch_gather(bslots_, B, state_, btok_, bpos_, s);
+  embed_rows(tok_embd_, btok_, B, x_, s);
+  if (bg_) {
+    for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
+    bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
+    bmm_rows(output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
+  } else {
+    for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
+    rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, s);
+    GemmArgs h;
+    h.w = output_; h.x = xb_; h.T = B; h.out = logits_b_; h.ldo = V_pad_;
+    gemm_dq(h, GEMM_STORE, s);
+  }
+  SamplerArgs sa;
+  sa.logits = logits_b_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
+  sa.cand_val = cand_val_b_; sa.cand_idx = cand_idx_b_; sa.cand_tau = cand_tau_b_;
+  sa.advance_pos = 1;
+  sa.batch = B; sa.slots = bslots_; sa.logits_ld = V_pad_; sa.batch_out = btok_out_;
+  sample(sa, s);
+}
+
 std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
   ExecGuard guard(this);
   const int B = (int)slots.size();
@@ -703,22 +816,23 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
     for (int c = 0; c < b; ++c)
       if (slots[c] == slots[b]) throw std::runtime_error("batch_step: duplicate slot");
   }
-  const int d = hp_.n_embd;
   std::memcpy(h_bslots_, slots.data(), sizeof(int) * B);
   HIPCHK(hipMemcpyAsync(bslots_, h_bslots_, sizeof(int) * B, hipMemcpyHostToDevice, stream_));
-  batch_gather(bslots_, B, state_, btok_, bpos_, stream_);
-  embed_rows(tok_embd_, btok_, B, x_, stream_);
-  for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, stream_);
-  rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, stream_);
-  GemmArgs h;
-  h.w = output_; h.x = xb_; h.T = B; h.out = logits_b_; h.ldo = V_pad_;
-  gemm_dq(h, GEMM_STORE, stream_);
-  SamplerArgs sa;
-  sa.logits = logits_b_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
-  sa.cand_val = cand_val_b_; sa.cand_idx = cand_idx_b_; sa.cand_tau = cand_tau_b_;
-  sa.advance_pos = 1;
-  sa.batch = B; sa.slots = bslots_; sa.logits_ld = V_pad_; sa.batch_out = btok_out_;
-  sample(sa, stream_);
+  if (opt_.use_graph) {
+    if ((int)bgraph_.size() <= B) bgraph_.resize(B + 1, nullptr);
+    if (!bgraph_[B]) {
+      hipGraph_t g = nullptr;
+      HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      enqueue_batch_step(B, stream_);
+      HIPCHK(hipStreamEndCapture(stream_, &g));
+      const hipError_t e = hipGraphInstantiate(&bgraph_[B], g, nullptr, nullptr, 0);
+      hipGraphDestroy(g);
+      HIPCHK(e);
+    }
+    HIPCHK(hipGraphLaunch(bgraph_[B], stream_));
+  } else {
+    enqueue_batch_step(B, stream_);
+  }
   HIPCHK(hipMemcpyAsync(h_btok_, btok_out_, sizeof(int) * B, hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
   HIPCHK(hipGetLastError());

@@ -114,6 +114,8 @@ class Engine : public SlotBackend {
   // ---- continuous batching over KV slots (EngineOptions::n_slots > 1, one rank, all layers)
   int n_slots() const override { return opt_.n_slots; }
   int max_batch() const override { return bmax_; }
+  // 0: batch_step on the prefill GEMM; 1: attention/head on the batched GEMV; 2: every projection
+  int batch_gemv() const { return bg_ffn_ ? 2 : bg_ ? 1 : 0; }
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
   int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
@@ -153,7 +155,15 @@ class Engine : public SlotBackend {
   // one layer over T activation rows: a prompt chunk at positions pos0.. of KV slot kv_slot_
   // (batched == false) or T decode rows of slots bslots_ at positions bpos_ (batched == true)
   void enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s);
+  void enqueue_rows_ffn(int l, int T, hipStream_t s);
   void enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int slot = 0);
+  // batch_step on the MFMA batched projections (bmm.hip): one layer over the B decode rows
+  void enqueue_batch_layer(int l, int B, hipStream_t s);
+  void enqueue_batch_step(int B, hipStream_t s);
+  void bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B, hipStream_t s);
+  void bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero, int zero_n,
+                  hipStream_t s);
+  void setup_batch_mfma();
   SamplerParamsDev make_sparams(const SamplingOpts& sp) const;
   void begin_slot_state(int slot, const std::vector<int>& prompt, const SamplingOpts& sp);
   void launch_step();
@@ -249,7 +259,14 @@ class Engine : public SlotBackend {
   int* h_bslots_ = nullptr;   // pinned [bmax]
   int* h_btok_ = nullptr;     // pinned [bmax]
   int last_batch_ = 0;
+  // batch_step projections on the MFMA batched projection (bmm.hip: weights streamed once per
+  // step for all rows) instead of the prefill GEMM: attention/head (bg_) and the dense FFN
+  // (bg_ffn_); LFK_BATCH_MFMA=0 keeps the GEMM path (A/B)
+  bool bg_ = false, bg_ffn_ = false;
+  __half* xh_b_ = nullptr;    // [bmax][max(d, nq, F)] prepared f16 projection input
+  float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
 
+  std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   static constexpr int kDepth = 2;

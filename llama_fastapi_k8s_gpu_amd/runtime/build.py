@@ -29,7 +29,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = ["kernels/gemv.hip", "kernels/attention.hip", "kernels/sampler.hip", "kernels/gemm.hip",
-               "kernels/misc.hip",
+               "kernels/misc.hip", "kernels/bmm.hip",
                "kernels/ffn_fused.hip", "kernels/moe.hip", "kernels/p2p_allreduce.hip", "kernels/pdecode.hip"]
 HOST_HIP_SOURCES = ["runtime/engine.cpp", "runtime/engine_pdecode.cpp", "runtime/p2p.cpp", "runtime/scheduler.cpp",
                     "bindings_hip.cpp"]     # host code against the HIP runtime

@@ -433,3 +433,62 @@ def test_sampler_bias_greedy_forces_and_bans(torch):
     p = SamplingParams(temperature=0.0, top_k=1, repeat_penalty=1.0, logit_bias={top: float("-inf")})
     tok = _run_sampler(torch, logits, [], p, 0)[0]
     assert tok != top and tok == int(np.argsort(-logits)[1])
+
+
+
+BM_TYPES = [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.Q8_0]
+
+
+def _swizzle4(x):
+    """bprep's k order inside each 4-group: (0, 2, 1, 3)."""
+    return x.reshape(*x.shape[:-1], -1, 4)[..., [0, 2, 1, 3]].reshape(x.shape)
+
+
+@pytest.mark.parametrize("t", BM_TYPES)
+@pytest.mark.parametrize("B", [1, 3, 8, 16])
+@pytest.mark.parametrize("R,K", [(130, 4096), (48, 14336), (16, 256)])
+def test_bmm_rows_vs_fp32(torch, t, B, R, K):
+    """MFMA batched projection: out[b] += W x[b] for every row b, against the fp32 product
+    with the f16 activations; partials accumulate onto the existing output."""
+    rng = np.random.default_rng(B * 1000 + R + int(t))
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    X = rng.standard_normal((B, K)).astype(np.float32)
+    Xh = X.astype(np.float16)
+    y0 = rng.standard_normal((B, R)).astype(np.float32)
+    ldo = R + 6
+    out = torch.zeros(B, ldo, device="cuda")
+    out[:, :R] = torch.from_numpy(y0).cuda()
+    dxh = torch.from_numpy(_swizzle4(Xh)).cuda()   # keep device buffers referenced until the kernel ran
+    hip().bmm(dw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, out.data_ptr(), ldo, B, stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ref = Xh.astype(np.float64) @ W.astype(np.float64).T
+    for b in range(B):
+        assert rel_err(got[b, :R] - y0[b], ref[b]) < 2e-3, (b, rel_err(got[b, :R] - y0[b], ref[b]))
+        assert np.all(got[b, R:] == 0)
+
+
+def test_bprep_norm_swiglu_zero(torch):
+    """bprep: RMSNorm per row, SwiGLU on interleaved gate/up rows, f16 + (0,2,1,3) swizzle,
+    and the zero side job."""
+    rng = np.random.default_rng(5)
+    B, K = 5, 4096
+    X = (rng.standard_normal((B, K)) * 3).astype(np.float32)
+    nw = (1 + 0.1 * rng.standard_normal(K)).astype(np.float32)
+    dx, dn = torch.from_numpy(X).cuda(), torch.from_numpy(nw).cuda()
+    xh = torch.zeros(B, K, dtype=torch.float16, device="cuda")
+    z = torch.ones(1024, device="cuda")
+    hip().bprep(dx.data_ptr(), K, False, dn.data_ptr(), 1e-5, K, B, xh.data_ptr(), K, stream(), z.data_ptr(), 1024)
+    torch.cuda.synchronize()
+    want = np.stack([rmsnorm(X[b], nw) for b in range(B)]).astype(np.float16)
+    assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(want).astype(np.float32)) < 1e-3
+    assert float(z.abs().sum()) == 0.0
+    GU = rng.standard_normal((B, 2 * K)).astype(np.float32)
+    dgu = torch.from_numpy(GU).cuda()
+    hip().bprep(dgu.data_ptr(), 2 * K, True, 0, 1e-5, K, B, xh.data_ptr(), K, stream())
+    torch.cuda.synchronize()
+    g = GU.reshape(B, -1, 2, 32)[:, :, 0, :].reshape(B, K)
+    u = GU.reshape(B, -1, 2, 32)[:, :, 1, :].reshape(B, K)
+    h = (g / (1 + np.exp(-g)) * u).astype(np.float16)
+    assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(h).astype(np.float32)) < 2e-3
