@@ -142,67 +142,205 @@ __device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
 
 static constexpr int kBmmBlock = 256;
 
+// ---------------------------------------------------------------- tile16 weight layout
+// A second, batched-path copy of every projection matrix (288 GB of HBM holds it): per
+// 16-row tile and per 256-k step ONE contiguous block, ordered so that each of the kernel's
+// load instructions reads 1 KB contiguous (planar rows would give every instruction 16
+// scattered 64-B pieces - measured 1-2 TB/s). Lane l = 16 kq + r16 takes chunks 8s + kq
+// (h = 0) and 8s + 4 + kq (h = 1) of row 16t + r16:
+//   Q4_K: qs[h][l][16] | meta[r16][16]                                          2304 B
+//   Q5_K: qs[h][l][16] | qh[r16][32] | meta[r16][16]                            2816 B
+//   Q6_K: ql[h][l][16] | qh[h][r16][32] | scales[r16][16] | d[r16][2]           3360 B
+//   Q8_0: qs[h][a|b][l][16] | d[h][l][2]                                        4352 B
+// Rows past the matrix are zero.
+__host__ __device__ constexpr int t16_step_bytes(int t) {
+  return t == T_Q4_K ? 2304 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3360 : t == T_Q8_0 ? 4352 : 0;
+}
+
+size_t t16_bytes(int type, int rows, int K) {
+  return (size_t)((rows + 15) / 16) * (size_t)(K / 256) * (size_t)t16_step_bytes(type);
+}
+
+__device__ __forceinline__ void copy16(uint8_t* d, const uint8_t* s, bool ok) {
+  *reinterpret_cast<uint4*>(d) = ok ? *reinterpret_cast<const uint4*>(s) : make_uint4(0, 0, 0, 0);
+}
+
+template <int T>
+__global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
+  const int s = blockIdx.x, t = blockIdx.y, steps = gridDim.x;
+  const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
+  const int row = t * 16 + r16;
+  const bool ok = row < w.rows;
+  const size_t r = ok ? (size_t)row : 0;
+  uint8_t* blk = dst + ((size_t)t * steps + s) * t16_step_bytes(T);
+  const Planes& P = w.P;
+  const uint8_t* base = w.base;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 8 * s + 4 * h + kq;
+    if constexpr (T == T_Q8_0) {
+      copy16(blk + h * 2048 + l * 16, base + P.p0 + r * P.s0 + 32 * c, ok);
+      copy16(blk + h * 2048 + 1024 + l * 16, base + P.p0 + r * P.s0 + 32 * c + 16, ok);
+      *reinterpret_cast<unsigned short*>(blk + 4096 + h * 128 + l * 2) =
+          ok ? *reinterpret_cast<const unsigned short*>(base + P.p1 + r * P.s1 + 2 * c) : 0;
+    } else {
+      copy16(blk + h * 1024 + l * 16, base + P.p0 + r * P.s0 + 16 * c, ok);
+    }
+  }
+  if (kq != 0) return;
+  if constexpr (T == T_Q4_K) {
+    copy16(blk + 2048 + r16 * 16, base + P.p1 + r * P.s1 + 16 * s, ok);
+  } else if constexpr (T == T_Q5_K) {
+    copy16(blk + 2048 + r16 * 32, base + P.p1 + r * P.s1 + 32 * s, ok);
+    copy16(blk + 2048 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 32 * s + 16, ok);
+    copy16(blk + 2560 + r16 * 16, base + P.p2 + r * P.s2 + 16 * s, ok);
+  } else if constexpr (T == T_Q6_K) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      copy16(blk + 2048 + hh * 512 + r16 * 32, base + P.p1 + r * P.s1 + 64 * s + 32 * hh, ok);
+      copy16(blk + 2048 + hh * 512 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 64 * s + 32 * hh + 16, ok);
+    }
+    copy16(blk + 3072 + r16 * 16, base + P.p2 + r * P.s2 + 16 * s, ok);
+    *reinterpret_cast<unsigned short*>(blk + 3328 + r16 * 2) =
+        ok ? *reinterpret_cast<const unsigned short*>(base + P.p3 + r * P.s3 + 2 * s) : 0;
+  }
+}
+
+void t16_repack(const QMat& w, uint8_t* dst, hipStream_t st) {
+  if (!bmm_supported(w.type, w.K)) throw std::runtime_error("t16_repack: unsupported type / K");
+  const dim3 grid(w.K / 256, (w.rows + 15) / 16);
+  switch (w.type) {
+    case T_Q4_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q4_K>, grid, dim3(64), 0, st, w, dst); break;
+    case T_Q5_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q5_K>, grid, dim3(64), 0, st, w, dst); break;
+    case T_Q6_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q6_K>, grid, dim3(64), 0, st, w, dst); break;
+    default: hipLaunchKernelGGL(t16_repack_kernel<T_Q8_0>, grid, dim3(64), 0, st, w, dst); break;
+  }
+}
+
+// raw loads of lane l's chunk h (8s + 4h + kq) from a tile16 step block
+template <int T>
+__device__ __forceinline__ void tload(WRaw<T>& w, const uint8_t* blk, int h, int l, int r16, int kq) {
+  if constexpr (T == T_Q4_K) {
+    w.q = ld_nt16(blk + h * 1024 + l * 16);
+    w.m = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 16);
+  } else if constexpr (T == T_Q5_K) {
+    w.q = ld_nt16(blk + h * 1024 + l * 16);
+    w.h = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 32 + 16 * (kq & 1));
+    w.m = *reinterpret_cast<const int4*>(blk + 2560 + r16 * 16);
+  } else if constexpr (T == T_Q6_K) {
+    w.l = ld_nt16(blk + h * 1024 + l * 16);
+    w.h = *reinterpret_cast<const int4*>(blk + 2048 + h * 512 + r16 * 32 + 16 * (kq & 1));
+    const int si = 8 * h + kq;  // scale of the chunk's low 16; the high 16 use si + 4
+    w.slo = *reinterpret_cast<const signed char*>(blk + 3072 + r16 * 16 + si);
+    w.shi = *reinterpret_cast<const signed char*>(blk + 3072 + r16 * 16 + si + 4);
+    w.d = *reinterpret_cast<const unsigned short*>(blk + 3328 + r16 * 2);
+  } else {
+    w.a = ld_nt16(blk + h * 2048 + l * 16);
+    w.b = ld_nt16(blk + h * 2048 + 1024 + l * 16);
+    w.d = *reinterpret_cast<const unsigned short*>(blk + 4096 + h * 128 + l * 2);
+  }
+}
+
+template <int T>
+__device__ __forceinline__ int raw_word(const WRaw<T>& w) {
+  if constexpr (T == T_Q4_K || T == T_Q5_K) return w.q.x;
+  else if constexpr (T == T_Q6_K) return w.l.x;
+  else return w.a.x;
+}
+
+// Items are (16-row tile, K part). A block serves ONE K part (block b: part b % kparts):
+// it stages that part of the B activation rows in LDS once (f16, row stride padded 16 B), then
+// its 4 waves share every tile - wave w takes the part's steps w, w + 4, ... - and add their
+// partial tiles through LDS, so a tile leaves the block as one store (or one atomic add per
+// K part when the part count is > 1: few-way, not the 28-way contention of wave-level split-K).
 template <int QT>
 __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
-  const int lane = threadIdx.x & 63, wave = wave_id();
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = kBmmBlock / 64;
+  float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
+  __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16);
+  const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
-  const int K = a.w.K, steps = K >> 7;  // 128 k (4 chunks) per step
+  const int K = a.w.K, steps = K >> 8;
   const int tiles = (a.n_out + 15) >> 4;
-  const int kparts = a.kparts;
-  const int spp = (steps + kparts - 1) / kparts;
-  const int total = tiles * kparts;
-  // activation column of this lane's B fragment (columns past B re-read row 0: their
-  // outputs are never stored)
+  const int kparts = a.kparts, spp = a.spp;
+  const int kp = blockIdx.x % kparts;
+  const int s0 = kp * spp, s1 = min(steps, s0 + spp);
+  if (s0 >= s1) return;  // whole block, before any barrier
+  const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
+  // stage x[b][k0, k0 + kn) for the B rows
+  for (int i = tid; i < a.B * (kn >> 3); i += kBmmBlock) {
+    const int b = i / (kn >> 3), v = i - b * (kn >> 3);
+    *reinterpret_cast<uint4*>(xs + b * ldx + 8 * v) =
+        *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * v);
+  }
+  __syncthreads();
   const bool col_ok = r16 < a.B;
-  const __half* xrow = a.xh + (size_t)(col_ok ? r16 : 0) * a.ldh;
-  for (int item = blockIdx.x * (kBmmBlock / 64) + wave; item < total; item += gridDim.x * (kBmmBlock / 64)) {
-    const int tile = item / kparts, kp = item - tile * kparts;
-    const int s0 = kp * spp, s1 = min(steps, s0 + spp);
-    const RowPtr R = row_ptr(a.w.base, a.w.P, (unsigned)min(tile * 16 + r16, a.n_out - 1));
+  const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
+  const int SB = t16_step_bytes(QT);
+  const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
+  const int wlast = ws0 < s1 ? ws0 + ((s1 - 1 - ws0) / NW) * NW : ws0;
+  for (int tile = blockIdx.x / kparts; tile < tiles; tile += gridDim.x / kparts) {
+    const uint8_t* tb = a.w.base + (size_t)tile * steps * SB;
     f4_t acc = {0.f, 0.f, 0.f, 0.f};
-    // 2-deep register ring of raw weights (one chunk per lane per step)
-    WRaw<QT> w0, w1;
-    if (s0 < s1) wload<QT>(w0, R, 4 * s0 + kq);
-    if (s0 + 1 < s1) wload<QT>(w1, R, 4 * (s0 + 1) + kq);
-    for (int s = s0; s < s1; s += 2) {
+    if (ws0 < s1) {
+      // register ring: the wave's next step loads while this one is decoded; every load is
+      // unconditional (steps clamped to the wave's last), so no vmcnt drain at a branch join
+      WRaw<QT> wc[2], wn[2];
+      tload<QT>(wc[0], tb + (size_t)ws0 * SB, 0, lane, r16, kq);
+      tload<QT>(wc[1], tb + (size_t)ws0 * SB, 1, lane, r16, kq);
+      for (int s = ws0; s < s1; s += NW) {
+        const uint8_t* nb = tb + (size_t)min(s + NW, wlast) * SB;
+        tload<QT>(wn[0], nb, 0, lane, r16, kq);
+        tload<QT>(wn[1], nb, 1, lane, r16, kq);
+        if (a.debug == 1) {  // microbenchmark: weight stream only
+          acc[0] += (float)raw_word<QT>(wc[0]) + (float)raw_word<QT>(wc[1]);
+        } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int st = s + h;
-        if (st < s1) {
-          const int c = 4 * st + kq;
-          int off_lo, off_hi;
-          chunk_runs<QT>(c, off_lo, off_hi);
-          const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
-          const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
-          uint4 bl0 = xl[0], bl1 = xl[1], bh0 = xh[0], bh1 = xh[1];
-          HFrag F;
-          dequant_frags<QT>(h == 0 ? w0 : w1, c, F);
-          if (st + 2 < s1) wload<QT>(h == 0 ? w0 : w1, R, 4 * (st + 2) + kq);
-          const unsigned bl[8] = {bl0.x, bl0.y, bl0.z, bl0.w, bl1.x, bl1.y, bl1.z, bl1.w};
-          const unsigned bh[8] = {bh0.x, bh0.y, bh0.z, bh0.w, bh1.x, bh1.y, bh1.z, bh1.w};
+          for (int h = 0; h < 2; ++h) {
+            const int c = 8 * s + 4 * h + kq;
+            int off_lo, off_hi;
+            chunk_runs<QT>(c, off_lo, off_hi);
+            const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+            const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+            const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
+            HFrag F;
+            dequant_frags<QT>(wc[h], c, F);
+            const unsigned bl[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            const unsigned bh[8] = {x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            // A: lo pairs (4i,4i+2),(4i+1,4i+3) then hi pairs; B: x[lo + 4i .. +3], x[hi + 4i .. +3]
-            const uint4 av = make_uint4(F.w[4 * i], F.w[4 * i + 1], F.w[4 * i + 2], F.w[4 * i + 3]);
-            const uint4 bv = make_uint4(bl[2 * i], bl[2 * i + 1], bh[2 * i], bh[2 * i + 1]);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av), __builtin_bit_cast(h8_t, bv),
-                                                         acc, 0, 0, 0);
+            for (int i = 0; i < 4; ++i) {
+              // A: lo pairs (4i,4i+2),(4i+1,4i+3) then hi pairs; B: x[lo + 4i .. +3], x[hi + 4i .. +3]
+              const uint4 av = make_uint4(F.w[4 * i], F.w[4 * i + 1], F.w[4 * i + 2], F.w[4 * i + 3]);
+              const uint4 bv = make_uint4(bl[2 * i], bl[2 * i + 1], bh[2 * i], bh[2 * i + 1]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
+                                                           __builtin_bit_cast(h8_t, bv), acc, 0, 0, 0);
+            }
+          }
+        }
+        wc[0] = wn[0];
+        wc[1] = wn[1];
+      }
+    }
+    // the 4 waves' partial tiles meet in LDS; wave 0 writes C[row 4kq + i][col r16]
+    if (wave > 0) *reinterpret_cast<f4_t*>(red + ((wave - 1) * 64 + lane) * 4) = acc;
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
+      if (col_ok) {
+        float* o = a.out + (size_t)r16 * a.ldo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = tile * 16 + 4 * kq + i;
+          if (row < a.n_out) {
+            if (kparts > 1) atomicAdd(o + row, acc[i]);
+            else o[row] += acc[i];   // one owner per (row, column)
           }
         }
       }
     }
-    // C[row 4kq + i][col r16]
-    if (col_ok) {
-      float* o = a.out + (size_t)r16 * a.ldo;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = tile * 16 + 4 * kq + i;
-        if (row < a.n_out) {
-          if (kparts > 1) atomicAdd(o + row, acc[i]);
-          else o[row] += acc[i];   // one owner per (row, column)
-        }
-      }
-    }
+    __syncthreads();  // red is reused by the next tile
   }
 }
 
@@ -275,7 +413,7 @@ void bprep(const BPrepArgs& a, hipStream_t s) {
 // ---------------------------------------------------------------- launch
 bool bmm_supported(int type, int K) {
   if (type != T_Q4_K && type != T_Q5_K && type != T_Q6_K && type != T_Q8_0) return false;
-  return K >= 128 && K % 256 == 0;
+  return K % 256 == 0;  // 256 k per step
 }
 
 static int bmm_cus() {
@@ -290,15 +428,21 @@ static int bmm_cus() {
 
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
-  const int tiles = (a.n_out + 15) / 16, steps = a.w.K / 128;
-  // split K until ~8 waves per CU have an item, keeping >= 2 steps per part
-  const int want = 8 * bmm_cus();
-  int kp = 1;
-  while (tiles * kp < want && steps / (kp * 2) >= 2) kp *= 2;
-  a.kparts = kp;
-  const int items = tiles * kp, wpb = kBmmBlock / 64;
-  const int grid = std::max(1, std::min((items + wpb - 1) / wpb, 8 * bmm_cus()));
-  hipLaunchKernelGGL(bmm_kernel<QT>, dim3(grid), dim3(kBmmBlock), 0, s, a);
+  const int tiles = (a.n_out + 15) / 16, steps = a.w.K / 256;
+  // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
+  // (more blocks, more-way atomics) only while there are fewer than ~4 blocks per CU
+  const int bp = a.B <= 4 ? 4 : a.B <= 8 ? 8 : 16;
+  int spp = std::max(1, std::min(steps, 64 / bp));
+  static const int want_b = getenv("LFK_BMM_BLOCKS") ? atoi(getenv("LFK_BMM_BLOCKS")) : 4;  // per CU (tuning)
+  const int want = want_b * bmm_cus();
+  while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
+  const int kparts = (steps + spp - 1) / spp;
+  a.spp = spp;
+  a.kparts = kparts;
+  // blocks per part: one per tile, within ~16 resident blocks per CU overall
+  const int bpk = std::max(1, std::min(tiles, (16 * bmm_cus() + kparts - 1) / kparts));
+  const size_t lds = (kBmmBlock / 64 - 1) * 64 * 16 + (size_t)a.B * (spp * 256 + 8) * 2;
+  hipLaunchKernelGGL(bmm_kernel<QT>, dim3(bpk * kparts), dim3(kBmmBlock), lds, s, a);
 }
 
 void bmm(const BmmArgs& a, hipStream_t s) {

@@ -65,17 +65,21 @@ void gemv(const GemvArgs& a, int epi, hipStream_t s);
 // k order inside each 4-group swizzled (0, 2, 1, 3) to match the dequantised A fragments.
 static constexpr int kBmmMaxRows = 16;
 struct BmmArgs {
-  QMat w;
+  QMat w;                          // base = tile16 copy (t16_repack); type / rows / K as the matrix
   const __half* xh = nullptr;
   int ldh = 0;                     // halves between rows of xh (multiple of 8)
   float* out = nullptr;
   int ldo = 0;
   int n_out = 0;                   // rows of W
   int B = 0;
-  int kparts = 1;                  // set by the launcher
+  int kparts = 1, spp = 1;         // set by the launcher (K parts, 256-k steps per part)
+  int debug = 0;                   // microbenchmarks only: 1 = weight stream only
 };
 bool bmm_supported(int type, int K);
 void bmm(const BmmArgs& a, hipStream_t s);
+// the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
+size_t t16_bytes(int type, int rows, int K);
+void t16_repack(const QMat& planar, uint8_t* dst, hipStream_t s);
 // f32 rows -> bmm input: optional SwiGLU (x rows of 2K gate/up pre-activations, 32-feature
 // interleaved groups), optional RMSNorm (* norm_w), f16 swizzled; also zeroes zero[0, zero_n)
 struct BPrepArgs {

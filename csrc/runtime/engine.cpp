@@ -307,7 +307,23 @@ void Engine::setup_batch_mfma() {
   }
   bg_ = att;
   bg_ffn_ = att && ffn;
-  if (bg_) xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
+  if (!bg_) return;
+  xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
+  // the batched path reads its own copy of the weights, laid out per 16-row tile (bmm.hip)
+  auto tile = [&](const QMat& m) {
+    QMat t = m;
+    uint8_t* dst = (uint8_t*)dalloc(t16_bytes(m.type, m.rows, m.K));
+    t16_repack(m, dst, stream_);
+    t.base = dst;
+    return t;
+  };
+  t_output_ = tile(output_);
+  for (int l = 0; l < hp_.n_layer; ++l) {
+    Layer& L = layers_[l];
+    L.t_wq = tile(L.wq); L.t_wk = tile(L.wk); L.t_wv = tile(L.wv); L.t_wo = tile(L.wo);
+    if (bg_ffn_) { L.t_gu = tile(L.w_gu); L.t_down = tile(L.w_down); }
+  }
+  HIPCHK(hipStreamSynchronize(stream_));
 }
 
 // The fused decode FFN needs: one rank (the TP path all-reduces the down
@@ -753,9 +769,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   bprep_rows(x_, d, false, L.attn_norm, d, B, qkv_, B * ncol, s);
-  bmm_rows(L.wq, xh_b_, d, qkv_, ncol, nq_, B, s);
-  bmm_rows(L.wk, xh_b_, d, qkv_ + nq_, ncol, nkvd_, B, s);
-  bmm_rows(L.wv, xh_b_, d, qkv_ + nq_ + nkvd_, ncol, nkvd_, B, s);
+  bmm_rows(L.t_wq, xh_b_, d, qkv_, ncol, nq_, B, s);
+  bmm_rows(L.t_wk, xh_b_, d, qkv_ + nq_, ncol, nkvd_, B, s);
+  bmm_rows(L.t_wv, xh_b_, d, qkv_ + nq_ + nkvd_, ncol, nkvd_, B, s);
   __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
   __half* vcl = vc_ + kv_layer * l;
   rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
@@ -769,12 +785,12 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
   attn_decode(aa, s);
   bprep_rows(attn_, nq_, false, nullptr, nq_, B, nullptr, 0, s);
-  bmm_rows(L.wo, xh_b_, nq_, x_, d, d, B, s);
+  bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
   if (bg_ffn_) {
     bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
-    bmm_rows(L.w_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
+    bmm_rows(L.t_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
     bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s);
-    bmm_rows(L.w_down, xh_b_, F_l_, x_, d, d, B, s);
+    bmm_rows(L.t_down, xh_b_, F_l_, x_, d, d, B, s);
     return;
   }
   // MoE (or unsupported FFN types): the grouped-GEMM FFN of the prompt path over the B rows
@@ -790,7 +806,7 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
     bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
-    bmm_rows(output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
+    bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
   } else {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
     rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, s);

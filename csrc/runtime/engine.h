@@ -64,6 +64,8 @@ struct Layer {
   QMat wq, wk, wv, wo;
   QMat w_gu, w_down;                 // dense FFN (gate/up interleaved in 32-row groups)
   QMat router, gu_exps, down_exps;   // MoE
+  // batched decode (bmm.hip): tile16 copies of the projections (base = the copy)
+  QMat t_wq, t_wk, t_wv, t_wo, t_gu, t_down;
 };
 
 class Engine : public SlotBackend {
@@ -264,6 +266,7 @@ class Engine : public SlotBackend {
   // (bg_ffn_); LFK_BATCH_MFMA=0 keeps the GEMM path (A/B)
   bool bg_ = false, bg_ffn_ = false;
   __half* xh_b_ = nullptr;    // [bmax][max(d, nq, F)] prepared f16 projection input
+  QMat t_output_;             // tile16 copy of the output head
   float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count

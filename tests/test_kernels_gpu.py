@@ -460,7 +460,9 @@ def test_bmm_rows_vs_fp32(torch, t, B, R, K):
     out = torch.zeros(B, ldo, device="cuda")
     out[:, :R] = torch.from_numpy(y0).cuda()
     dxh = torch.from_numpy(_swizzle4(Xh)).cuda()   # keep device buffers referenced until the kernel ran
-    hip().bmm(dw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, out.data_ptr(), ldo, B, stream())
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    hip().bmm(tw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, out.data_ptr(), ldo, B, stream())
     torch.cuda.synchronize()
     got = out.cpu().numpy()
     ref = Xh.astype(np.float64) @ W.astype(np.float64).T
