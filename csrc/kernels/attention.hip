@@ -18,6 +18,10 @@
 
 namespace lfk {
 
+// bmm's k order inside each 4-group: (0, 2, 1, 3) (kernels/bmm.hip)
+__device__ __forceinline__ int swz4(int i) { return (i & ~3) | ((i & 1) << 1) | ((i >> 1) & 1); }
+
+
 static constexpr int CH = 64;  // keys per split
 
 // L2-coherent 4-B store / load (global_store/load ... sc1): the cross-block
@@ -114,6 +118,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     a.part += (size_t)b * a.part_stride;
     a.counters += 64 * b;
     a.out += (size_t)b * a.out_stride;
+    if (a.out_h) a.out_h += (size_t)b * a.out_h_stride;
   }
   const int kvh = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -248,7 +253,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
       acc += f * wo[w][g][d];
     }
     if (ns == 1) {
-      a.out[(size_t)(kvh * G + g) * HD + d] = acc / l;
+      const int o = (kvh * G + g) * HD + d;
+      a.out[o] = acc / l;
+      if (a.out_h) a.out_h[swz4(o)] = __float2half(acc / l);
     } else {
       float* dst = a.part + ((size_t)split * a.n_head + kvh * G + g) * (HD + 2);
       st_sc1(dst + d, acc);
@@ -315,7 +322,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
 #pragma unroll
   for (int j = 0; j < EPT; ++j) {
     const int e = tid + 256 * j;
-    if (e < G * HD) a.out[(size_t)(kvh * G + e / HD) * HD + e % HD] = num[j] / den[j];
+    if (e < G * HD) {
+      const int o = (kvh * G + e / HD) * HD + e % HD;
+      a.out[o] = num[j] / den[j];
+      if (a.out_h) a.out_h[swz4(o)] = __float2half(num[j] / den[j]);
+    }
   }
   if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[9] = wall_clock64() - t_entry; }
 #undef LFK_STAMP

@@ -262,7 +262,11 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
-  const int tiles = (a.n_out + 15) >> 4;
+  // segments (Q|K|V in one launch): tile index -> (matrix, local tile)
+  int tile0[4] = {0, 0, 0, 0};
+  tile0[1] = (a.n_out + 15) >> 4;
+  for (int i = 1; i < 3; ++i) tile0[i + 1] = tile0[i] + (i < a.nseg ? (a.seg_rows[i] + 15) >> 4 : 0);
+  const int tiles = tile0[a.nseg];
   const int kparts = a.kparts, spp = a.spp;
   const int kp = blockIdx.x % kparts;
   const int s0 = kp * spp, s1 = min(steps, s0 + spp);
@@ -280,8 +284,12 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   const int SB = t16_step_bytes(QT);
   const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
   const int wlast = ws0 < s1 ? ws0 + ((s1 - 1 - ws0) / NW) * NW : ws0;
-  for (int tile = blockIdx.x / kparts; tile < tiles; tile += gridDim.x / kparts) {
-    const uint8_t* tb = a.w.base + (size_t)tile * steps * SB;
+  for (int gt = blockIdx.x / kparts; gt < tiles; gt += gridDim.x / kparts) {
+    const int sg = gt >= tile0[1] ? (gt >= tile0[2] ? 2 : 1) : 0;   // wave-uniform
+    const int tile = gt - tile0[sg];
+    const int n_out = sg ? a.seg_rows[sg] : a.n_out;
+    float* out = sg ? a.seg_out[sg] : a.out;
+    const uint8_t* tb = (sg ? a.seg_base[sg] : a.w.base) + (size_t)tile * steps * SB;
     f4_t acc = {0.f, 0.f, 0.f, 0.f};
     if (ws0 < s1) {
       // register ring: the wave's next step loads while this one is decoded; every load is
@@ -329,11 +337,11 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
       if (col_ok) {
-        float* o = a.out + (size_t)r16 * a.ldo;
+        float* o = out + (size_t)r16 * a.ldo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = tile * 16 + 4 * kq + i;
-          if (row < a.n_out) {
+          if (row < n_out) {
             if (kparts > 1) atomicAdd(o + row, acc[i]);
             else o[row] += acc[i];   // one owner per (row, column)
           }
@@ -428,19 +436,24 @@ static int bmm_cus() {
 
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
-  const int tiles = (a.n_out + 15) / 16, steps = a.w.K / 256;
+  int tiles = (a.n_out + 15) / 16;
+  for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
+  const int steps = a.w.K / 256;
   // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
   // (more blocks, more-way atomics) only while there are fewer than ~4 blocks per CU
   const int bp = a.B <= 4 ? 4 : a.B <= 8 ? 8 : 16;
-  int spp = std::max(1, std::min(steps, 64 / bp));
+  static const int xkb = getenv("LFK_BMM_XKB") ? atoi(getenv("LFK_BMM_XKB")) : 32;  // staged-x budget (tuning)
+  int spp = std::max(1, std::min(steps, 2 * xkb / bp));
   static const int want_b = getenv("LFK_BMM_BLOCKS") ? atoi(getenv("LFK_BMM_BLOCKS")) : 4;  // per CU (tuning)
   const int want = want_b * bmm_cus();
   while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
   const int kparts = (steps + spp - 1) / spp;
   a.spp = spp;
   a.kparts = kparts;
-  // blocks per part: one per tile, within ~16 resident blocks per CU overall
-  const int bpk = std::max(1, std::min(tiles, (16 * bmm_cus() + kparts - 1) / kparts));
+  // blocks per part: ~4 blocks per CU overall (each block loops over tiles, so its staged x
+  // slice - as many bytes as a tile's weights at B = 8 - is amortised over several tiles)
+  static const int per_cu = getenv("LFK_BMM_GRID") ? atoi(getenv("LFK_BMM_GRID")) : 4;  // tuning
+  const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus() + kparts - 1) / kparts));
   const size_t lds = (kBmmBlock / 64 - 1) * 64 * 16 + (size_t)a.B * (spp * 256 + 8) * 2;
   hipLaunchKernelGGL(bmm_kernel<QT>, dim3(bpk * kparts), dim3(kBmmBlock), lds, s, a);
 }
@@ -448,6 +461,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
 void bmm(const BmmArgs& a, hipStream_t s) {
   if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
+  if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

@@ -73,6 +73,12 @@ struct BmmArgs {
   int n_out = 0;                   // rows of W
   int B = 0;
   int kparts = 1, spp = 1;         // set by the launcher (K parts, 256-k steps per part)
+  // optional further matrices of the same type and K over the same xh (one launch for Q|K|V):
+  // segment i > 0 uses seg_base[i], seg_rows[i], seg_out[i] (ldo shared)
+  int nseg = 1;
+  const uint8_t* seg_base[3] = {};
+  int seg_rows[3] = {};
+  float* seg_out[3] = {};
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only
 };
 bool bmm_supported(int type, int K);
@@ -196,6 +202,9 @@ struct AttnDecodeArgs {
   int batch = 0;
   const int* slots = nullptr;
   size_t slot_stride = 0, q_stride = 0, out_stride = 0, part_stride = 0;
+  // batched: also write the output as the next projection's bmm input (f16, bmm k swizzle)
+  __half* out_h = nullptr;
+  size_t out_h_stride = 0;
   static constexpr int kTouchRanges = 6;
   const uint8_t* pf[kTouchRanges] = {};
   size_t pf_bytes[kTouchRanges] = {};

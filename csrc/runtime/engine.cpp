@@ -769,9 +769,27 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   bprep_rows(x_, d, false, L.attn_norm, d, B, qkv_, B * ncol, s);
-  bmm_rows(L.t_wq, xh_b_, d, qkv_, ncol, nq_, B, s);
-  bmm_rows(L.t_wk, xh_b_, d, qkv_ + nq_, ncol, nkvd_, B, s);
-  bmm_rows(L.t_wv, xh_b_, d, qkv_ + nq_ + nkvd_, ncol, nkvd_, B, s);
+  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers)
+  {
+    const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
+    float* o[3] = {qkv_, qkv_ + nq_, qkv_ + nq_ + nkvd_};
+    for (int i = 0; i < 3;) {
+      int j = i + 1;
+      while (j < 3 && m[j]->type == m[i]->type) ++j;
+      for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
+        BmmArgs a;
+        a.w = *m[i]; a.xh = xh_b_ + (size_t)b0 * d; a.ldh = d;
+        a.out = o[i] + (size_t)b0 * ncol; a.ldo = ncol; a.n_out = m[i]->rows;
+        a.B = std::min(kBmmMaxRows, B - b0);
+        a.nseg = j - i;
+        for (int k = 1; k < a.nseg; ++k) {
+          a.seg_base[k] = m[i + k]->base; a.seg_rows[k] = m[i + k]->rows; a.seg_out[k] = o[i + k] + (size_t)b0 * ncol;
+        }
+        bmm(a, s);
+      }
+      i = j;
+    }
+  }
   __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
   __half* vcl = vc_ + kv_layer * l;
   rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
@@ -783,8 +801,8 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.batch = B; aa.slots = bslots_; aa.slot_stride = slot_stride_;
   aa.q_stride = nq_; aa.out_stride = nq_;
   aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
+  aa.out_h = xh_b_; aa.out_h_stride = nq_;   // the Wo input, already in bmm's f16 layout
   attn_decode(aa, s);
-  bprep_rows(attn_, nq_, false, nullptr, nq_, B, nullptr, 0, s);
   bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
   if (bg_ffn_) {
     bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
