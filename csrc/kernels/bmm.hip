@@ -272,6 +272,24 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   const int s0 = kp * spp, s1 = min(steps, s0 + spp);
   if (s0 >= s1) return;  // whole block, before any barrier
   const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
+  const int gstride = gridDim.x / kparts;
+  int gt = blockIdx.x / kparts;
+  if (gt >= tiles) return;  // whole block, before any barrier
+  const int SB = t16_step_bytes(QT);
+  auto tile_base = [&](int g) {  // first byte of global tile g's tile16 data
+    const int sg = g >= tile0[1] ? (g >= tile0[2] ? 2 : 1) : 0;
+    return (sg ? a.seg_base[sg] : a.w.base) + (size_t)(g - tile0[sg]) * steps * SB;
+  };
+  const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
+  const bool has = ws0 < s1;                      // (a part shorter than NW steps idles some waves)
+  const int wlast = has ? ws0 + ((s1 - 1 - ws0) / NW) * NW : ws0;
+  // the first tile's first weights load before the x staging round trip
+  const uint8_t* tb = tile_base(gt);
+  WRaw<QT> wc[2], wn[2];
+  if (has) {
+    tload<QT>(wc[0], tb + (size_t)ws0 * SB, 0, lane, r16, kq);
+    tload<QT>(wc[1], tb + (size_t)ws0 * SB, 1, lane, r16, kq);
+  }
   // stage x[b][k0, k0 + kn) for the B rows
   for (int i = tid; i < a.B * (kn >> 3); i += kBmmBlock) {
     const int b = i / (kn >> 3), v = i - b * (kn >> 3);
@@ -281,24 +299,18 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   __syncthreads();
   const bool col_ok = r16 < a.B;
   const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
-  const int SB = t16_step_bytes(QT);
-  const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
-  const int wlast = ws0 < s1 ? ws0 + ((s1 - 1 - ws0) / NW) * NW : ws0;
-  for (int gt = blockIdx.x / kparts; gt < tiles; gt += gridDim.x / kparts) {
+  for (; gt < tiles; gt += gstride) {
     const int sg = gt >= tile0[1] ? (gt >= tile0[2] ? 2 : 1) : 0;   // wave-uniform
     const int tile = gt - tile0[sg];
     const int n_out = sg ? a.seg_rows[sg] : a.n_out;
     float* out = sg ? a.seg_out[sg] : a.out;
-    const uint8_t* tb = (sg ? a.seg_base[sg] : a.w.base) + (size_t)tile * steps * SB;
+    // the ring runs across tiles: after this tile's last step the next tile's first one loads,
+    // so the reduction barrier below does not drain the weight stream
+    const uint8_t* tb_next = gt + gstride < tiles ? tile_base(gt + gstride) : tb;
     f4_t acc = {0.f, 0.f, 0.f, 0.f};
-    if (ws0 < s1) {
-      // register ring: the wave's next step loads while this one is decoded; every load is
-      // unconditional (steps clamped to the wave's last), so no vmcnt drain at a branch join
-      WRaw<QT> wc[2], wn[2];
-      tload<QT>(wc[0], tb + (size_t)ws0 * SB, 0, lane, r16, kq);
-      tload<QT>(wc[1], tb + (size_t)ws0 * SB, 1, lane, r16, kq);
+    if (has) {
       for (int s = ws0; s < s1; s += NW) {
-        const uint8_t* nb = tb + (size_t)min(s + NW, wlast) * SB;
+        const uint8_t* nb = s + NW <= wlast ? tb + (size_t)(s + NW) * SB : tb_next + (size_t)ws0 * SB;
         tload<QT>(wn[0], nb, 0, lane, r16, kq);
         tload<QT>(wn[1], nb, 1, lane, r16, kq);
         if (a.debug == 1) {  // microbenchmark: weight stream only
@@ -330,6 +342,7 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
         wc[1] = wn[1];
       }
     }
+    tb = tb_next;
     // the 4 waves' partial tiles meet in LDS; wave 0 writes C[row 4kq + i][col r16]
     if (wave > 0) *reinterpret_cast<f4_t*>(red + ((wave - 1) * 64 + lane) * 4) = acc;
     __syncthreads();
