@@ -349,7 +349,34 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
-      if (col_ok) {
+      if (col_ok && a.qkv_epi) {
+        // rows 4kq .. 4kq+3 of the tile: RoPE pairs (0,1), (2,3) are in this lane
+        const auto& q = a.qkv;
+        const int kind = q.kind[sg], b = r16, hd = q.head_dim;
+        const int pos = min(max(q.pos[b], 0), q.n_ctx - 1);
+        const size_t so = (size_t)q.slots[b] * q.slot_stride;
+#pragma unroll
+        for (int i = 0; i < 4; i += 2) {
+          const int row = tile * 16 + 4 * kq + i;
+          if (row < n_out) {  // rows come in (even, odd) pairs: n_out is even
+            float y0 = acc[i], y1 = acc[i + 1];
+            const int dd = row % hd;
+            if (kind < 2) {
+              const float2 cs = q.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
+              y0 = acc[i] * cs.x - acc[i + 1] * cs.y;
+              y1 = acc[i] * cs.y + acc[i + 1] * cs.x;
+            }
+            if (kind == 0) {
+              q.q_out[(size_t)b * q.q_ld + row] = y0;
+              q.q_out[(size_t)b * q.q_ld + row + 1] = y1;
+            } else {
+              __half* c = (kind == 1 ? q.k_cache : q.v_cache) + so + ((size_t)(row / hd) * q.n_ctx + pos) * hd + dd;
+              c[0] = __float2half(y0);
+              c[1] = __float2half(y1);
+            }
+          }
+        }
+      } else if (col_ok) {
         float* o = out + (size_t)r16 * a.ldo;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -432,6 +459,10 @@ void bprep(const BPrepArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- launch
+static size_t bmm_lds(int B, int spp) { return (kBmmBlock / 64 - 1) * 64 * 16 + (size_t)B * (spp * 256 + 8) * 2; }
+
+bool bmm_qkv_fits(int K, int B) { return K % 256 == 0 && B >= 1 && bmm_lds(B, K / 256) <= 80 * 1024; }
+
 bool bmm_supported(int type, int K) {
   if (type != T_Q4_K && type != T_Q5_K && type != T_Q6_K && type != T_Q8_0) return false;
   return K % 256 == 0;  // 256 k per step
@@ -460,6 +491,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   static const int want_b = getenv("LFK_BMM_BLOCKS") ? atoi(getenv("LFK_BMM_BLOCKS")) : 4;  // per CU (tuning)
   const int want = want_b * bmm_cus();
   while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
+  if (a.qkv_epi) spp = steps;  // the epilogue needs whole rows (caller checked bmm_qkv_fits)
   const int kparts = (steps + spp - 1) / spp;
   a.spp = spp;
   a.kparts = kparts;
@@ -467,7 +499,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   // slice - as many bytes as a tile's weights at B = 8 - is amortised over several tiles)
   static const int per_cu = getenv("LFK_BMM_GRID") ? atoi(getenv("LFK_BMM_GRID")) : 4;  // tuning
   const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus() + kparts - 1) / kparts));
-  const size_t lds = (kBmmBlock / 64 - 1) * 64 * 16 + (size_t)a.B * (spp * 256 + 8) * 2;
+  const size_t lds = bmm_lds(a.B, spp);
   hipLaunchKernelGGL(bmm_kernel<QT>, dim3(bpk * kparts), dim3(kBmmBlock), lds, s, a);
 }
 
@@ -475,6 +507,7 @@ void bmm(const BmmArgs& a, hipStream_t s) {
   if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
   if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
+  if (a.qkv_epi && (!bmm_qkv_fits(a.w.K, a.B) || a.qkv.head_dim % 2)) throw std::runtime_error("bmm: qkv epilogue");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

@@ -80,8 +80,26 @@ struct BmmArgs {
   int seg_rows[3] = {};
   float* seg_out[3] = {};
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only
+  // Q|K|V epilogue (one K part only, see bmm_qkv_fits): instead of accumulating into `out`,
+  // segment kinds seg_kind[i] (0 = Q, 1 = K, 2 = V) are finished in the epilogue - RoPE on
+  // adjacent pairs for Q and K, Q rows to q_out[b][row], K / V rows as f16 into the slot
+  // caches at the row's position (the batched rope_kv_prefill folded in)
+  struct Qkv {
+    int kind[3] = {0, 1, 2};
+    float* q_out = nullptr;
+    int q_ld = 0;
+    __half* k_cache = nullptr;     // layer base of slot 0; + slot * slot_stride
+    __half* v_cache = nullptr;
+    size_t slot_stride = 0;
+    int n_ctx = 0, head_dim = 0;
+    const int* pos = nullptr;      // [B] position of each row
+    const int* slots = nullptr;    // [B] KV slot of each row
+    const float2* rope = nullptr;  // [n_ctx][head_dim / 2]
+  } qkv;
+  bool qkv_epi = false;
 };
 bool bmm_supported(int type, int K);
+bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)
 void bmm(const BmmArgs& a, hipStream_t s);
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);

@@ -768,7 +768,11 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
-  bprep_rows(x_, d, false, L.attn_norm, d, B, qkv_, B * ncol, s);
+  __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
+  __half* vcl = vc_ + kv_layer * l;
+  // RoPE + KV append in the Q|K|V epilogue when the whole K fits one LDS-staged part
+  const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
+  bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
   // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers)
   {
     const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
@@ -785,14 +789,21 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
         for (int k = 1; k < a.nseg; ++k) {
           a.seg_base[k] = m[i + k]->base; a.seg_rows[k] = m[i + k]->rows; a.seg_out[k] = o[i + k] + (size_t)b0 * ncol;
         }
+        if (fused) {
+          a.qkv_epi = true;
+          for (int k = 0; k < a.nseg; ++k) a.qkv.kind[k] = i + k;
+          a.qkv.q_out = q_ + (size_t)b0 * nq_; a.qkv.q_ld = nq_;
+          a.qkv.k_cache = kcl; a.qkv.v_cache = vcl; a.qkv.slot_stride = slot_stride_;
+          a.qkv.n_ctx = opt_.n_ctx; a.qkv.head_dim = hd;
+          a.qkv.pos = bpos_ + b0; a.qkv.slots = bslots_ + b0; a.qkv.rope = rope_;
+        }
         bmm(a, s);
       }
       i = j;
     }
   }
-  __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
-  __half* vcl = vc_ + kv_layer * l;
-  rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
+  if (!fused)
+    rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
   AttnDecodeArgs aa;
   aa.q = q_; aa.k_cache = kcl; aa.v_cache = vcl; aa.pos = bpos_;
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
