@@ -192,7 +192,7 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "weak" if args.parallel == "dp" else "strong",
-            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None, "dtype": "q4_k_m weights, int8/bf16 activations, fp32 accumulate",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None, "dtype": "q4_k_m weights; f16 (batched MFMA) / int8 (single-row GEMV) / bf16 (prefill MFMA) activations; fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B Q4_K_M GGUF, synthetic chat requests)",
             "config": {"model": "Llama-3-8B Q4_K_M",
                        "global_batch": (world if args.parallel == "dp" else 1) * min(args.clients, max_batch),
