@@ -140,7 +140,6 @@ __device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
   }
 }
 
-static constexpr int kBmmBlock = 256;
 
 // ---------------------------------------------------------------- tile16 weight layout
 // A second, batched-path copy of every projection matrix (288 GB of HBM holds it): per
@@ -253,10 +252,14 @@ __device__ __forceinline__ int raw_word(const WRaw<T>& w) {
 // its 4 waves share every tile - wave w takes the part's steps w, w + 4, ... - and add their
 // partial tiles through LDS, so a tile leaves the block as one store (or one atomic add per
 // K part when the part count is > 1: few-way, not the 28-way contention of wave-level split-K).
-template <int QT>
-__global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
+//
+// NW waves per block: 4 for the split-K shapes (4 blocks per CU), 8 for the one-part shapes
+// (Q|K|V and SwiGLU epilogues: the whole-K x slice limits a CU to 2 blocks, so 8 waves keep
+// 16 waves per CU streaming).
+template <int QT, int NW>
+__global__ __launch_bounds__(NW * 64) void bmm_kernel(BmmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NW = kBmmBlock / 64;
+  constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
   __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16);
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
@@ -273,7 +276,10 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   if (s0 >= s1) return;  // whole block, before any barrier
   const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
   const int gstride = gridDim.x / kparts;
-  int gt = blockIdx.x / kparts;
+  // tile order: SwiGLU blocks take 4-tile units (4u .. 4u + 3, then unit u + gridDim.x)
+  const bool sw = a.swiglu_epi;
+  int gt = sw ? 4 * blockIdx.x : blockIdx.x / kparts;
+  auto next_tile = [&](int g) { return sw ? ((g & 3) != 3 ? g + 1 : g + 1 + 4 * (gridDim.x - 1)) : g + gstride; };
   if (gt >= tiles) return;  // whole block, before any barrier
   const int SB = t16_step_bytes(QT);
   auto tile_base = [&](int g) {  // first byte of global tile g's tile16 data
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
     tload<QT>(wc[1], tb + (size_t)ws0 * SB, 1, lane, r16, kq);
   }
   // stage x[b][k0, k0 + kn) for the B rows
-  for (int i = tid; i < a.B * (kn >> 3); i += kBmmBlock) {
+  for (int i = tid; i < a.B * (kn >> 3); i += kBlock) {
     const int b = i / (kn >> 3), v = i - b * (kn >> 3);
     *reinterpret_cast<uint4*>(xs + b * ldx + 8 * v) =
         *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * v);
@@ -299,14 +305,15 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
   __syncthreads();
   const bool col_ok = r16 < a.B;
   const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
-  for (; gt < tiles; gt += gstride) {
+  f4_t gate[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // SwiGLU: wave 0's gate tiles of the unit
+  for (; gt < tiles; gt = next_tile(gt)) {
     const int sg = gt >= tile0[1] ? (gt >= tile0[2] ? 2 : 1) : 0;   // wave-uniform
     const int tile = gt - tile0[sg];
     const int n_out = sg ? a.seg_rows[sg] : a.n_out;
     float* out = sg ? a.seg_out[sg] : a.out;
     // the ring runs across tiles: after this tile's last step the next tile's first one loads,
     // so the reduction barrier below does not drain the weight stream
-    const uint8_t* tb_next = gt + gstride < tiles ? tile_base(gt + gstride) : tb;
+    const uint8_t* tb_next = next_tile(gt) < tiles ? tile_base(next_tile(gt)) : tb;
     f4_t acc = {0.f, 0.f, 0.f, 0.f};
     if (has) {
       for (int s = ws0; s < s1; s += NW) {
@@ -349,7 +356,19 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
-      if (col_ok && a.qkv_epi) {
+      if (sw) {
+        // tiles 4u, 4u+1: gate rows; 4u+2, 4u+3: the up rows of the same features
+        const int qt = gt & 3;
+        if (qt == 0) gate[0] = acc;
+        else if (qt == 1) gate[1] = acc;
+        else if (col_ok) {
+          const f4_t g = qt == 2 ? gate[0] : gate[1];
+          const int f0 = (gt >> 2) * 32 + (qt - 2) * 16 + 4 * kq;  // 4 consecutive features
+          const h2_t p0 = {(_Float16)(silu(g[0]) * acc[0]), (_Float16)(silu(g[2]) * acc[2])};
+          const h2_t p1 = {(_Float16)(silu(g[1]) * acc[1]), (_Float16)(silu(g[3]) * acc[3])};
+          *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
+        }
+      } else if (col_ok && a.qkv_epi) {
         // rows 4kq .. 4kq+3 of the tile: RoPE pairs (0,1), (2,3) are in this lane
         const auto& q = a.qkv;
         const int kind = q.kind[sg], b = r16, hd = q.head_dim;
@@ -395,17 +414,21 @@ __global__ __launch_bounds__(kBmmBlock) void bmm_kernel(BmmArgs a) {
 // ---------------------------------------------------------------- activation prep
 // One block per activation row: optional SwiGLU (gate/up pre-activations in 32-feature
 // interleaved groups), optional RMSNorm (* w), f16, k order (0,2,1,3) inside every 4-group.
-// Side job: zero [zero, zero + zero_n) (the split-K output of the projection this feeds).
+// Side job: zero [zero, zero + zero_n) (the split-K output of the projection this feeds) -
+// done by extra blocks past the B row blocks (up to 4 MB for the lm_head logits: 8 row blocks
+// alone took tens of microseconds for it).
 static constexpr int kPrepBlock = 1024;
 static constexpr int kPrepMaxVec = 8;  // float4 per thread: K <= 32768
 
 __global__ __launch_bounds__(kPrepBlock) void bprep_kernel(BPrepArgs a) {
   __shared__ float red[kPrepBlock / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
-  if (a.zero) {
+  if (b >= a.B) {
     float4* z = reinterpret_cast<float4*>(a.zero);
-    for (int i = b * kPrepBlock + tid; i < (a.zero_n >> 2); i += gridDim.x * kPrepBlock)
+    const int nzb = gridDim.x - a.B;
+    for (int i = (b - a.B) * kPrepBlock + tid; i < (a.zero_n >> 2); i += nzb * kPrepBlock)
       z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
   }
   const float* xr = a.x + (size_t)b * a.ldx;
   float4 v[kPrepMaxVec];
@@ -455,13 +478,16 @@ __global__ __launch_bounds__(kPrepBlock) void bprep_kernel(BPrepArgs a) {
 void bprep(const BPrepArgs& a, hipStream_t s) {
   if (a.B < 1 || a.K % 128 || a.K > 4 * kPrepBlock * kPrepMaxVec) throw std::runtime_error("bprep: bad shape");
   if (a.zero_n % 4) throw std::runtime_error("bprep: zero_n must be a multiple of 4");
-  hipLaunchKernelGGL(bprep_kernel, dim3(a.B), dim3(kPrepBlock), 0, s, a);
+  // zero blocks: >= 4 float4 stores per thread, at most 512 blocks
+  const int nz = a.zero && a.zero_n ? std::min(512, std::max(1, (a.zero_n / 4 + 4 * kPrepBlock - 1) / (4 * kPrepBlock))) : 0;
+  hipLaunchKernelGGL(bprep_kernel, dim3(a.B + nz), dim3(kPrepBlock), 0, s, a);
 }
 
 // ---------------------------------------------------------------- launch
-static size_t bmm_lds(int B, int spp) { return (kBmmBlock / 64 - 1) * 64 * 16 + (size_t)B * (spp * 256 + 8) * 2; }
+static size_t bmm_lds(int B, int spp, int nw) { return (size_t)(nw - 1) * 64 * 16 + (size_t)B * (spp * 256 + 8) * 2; }
 
-bool bmm_qkv_fits(int K, int B) { return K % 256 == 0 && B >= 1 && bmm_lds(B, K / 256) <= 80 * 1024; }
+// one-part shapes run 8-wave blocks; two of them must fit a CU's 160 KB of LDS
+bool bmm_qkv_fits(int K, int B) { return K % 256 == 0 && B >= 1 && bmm_lds(B, K / 256, 8) <= 80 * 1024; }
 
 bool bmm_supported(int type, int K) {
   if (type != T_Q4_K && type != T_Q5_K && type != T_Q6_K && type != T_Q8_0) return false;
@@ -478,29 +504,46 @@ static int bmm_cus() {
   return cus;
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
   for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
   const int steps = a.w.K / 256;
+  if (a.qkv_epi || a.swiglu_epi) {
+    // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
+    static const int nw1 = env_int("LFK_BMM_NW1", 8);  // tuning: 4 or 8
+    a.spp = steps;
+    a.kparts = 1;
+    const size_t lds = bmm_lds(a.B, steps, nw1);
+    const int units = a.swiglu_epi ? tiles / 4 : tiles;
+    const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
+    const int nb = std::max(1, std::min(units, per_cu * bmm_cus()));
+    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4>), dim3(nb), dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((bmm_kernel<QT, 8>), dim3(nb), dim3(512), lds, s, a);
+    return;
+  }
   // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
   // (more blocks, more-way atomics) only while there are fewer than ~4 blocks per CU
   const int bp = a.B <= 4 ? 4 : a.B <= 8 ? 8 : 16;
-  static const int xkb = getenv("LFK_BMM_XKB") ? atoi(getenv("LFK_BMM_XKB")) : 32;  // staged-x budget (tuning)
+  static const int xkb = env_int("LFK_BMM_XKB", 32);  // staged-x budget (tuning)
   int spp = std::max(1, std::min(steps, 2 * xkb / bp));
-  static const int want_b = getenv("LFK_BMM_BLOCKS") ? atoi(getenv("LFK_BMM_BLOCKS")) : 4;  // per CU (tuning)
+  static const int want_b = env_int("LFK_BMM_BLOCKS", 4);  // per CU (tuning)
   const int want = want_b * bmm_cus();
   while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
-  if (a.qkv_epi) spp = steps;  // the epilogue needs whole rows (caller checked bmm_qkv_fits)
   const int kparts = (steps + spp - 1) / spp;
   a.spp = spp;
   a.kparts = kparts;
   // blocks per part: ~4 blocks per CU overall (each block loops over tiles, so its staged x
   // slice - as many bytes as a tile's weights at B = 8 - is amortised over several tiles)
-  static const int per_cu = getenv("LFK_BMM_GRID") ? atoi(getenv("LFK_BMM_GRID")) : 4;  // tuning
+  static const int per_cu = env_int("LFK_BMM_GRID", 4);  // tuning
   const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus() + kparts - 1) / kparts));
-  const size_t lds = bmm_lds(a.B, spp);
-  hipLaunchKernelGGL(bmm_kernel<QT>, dim3(bpk * kparts), dim3(kBmmBlock), lds, s, a);
+  const size_t lds = bmm_lds(a.B, spp, 4);
+  hipLaunchKernelGGL((bmm_kernel<QT, 4>), dim3(bpk * kparts), dim3(256), lds, s, a);
 }
 
 void bmm(const BmmArgs& a, hipStream_t s) {
@@ -508,6 +551,9 @@ void bmm(const BmmArgs& a, hipStream_t s) {
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
   if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
   if (a.qkv_epi && (!bmm_qkv_fits(a.w.K, a.B) || a.qkv.head_dim % 2)) throw std::runtime_error("bmm: qkv epilogue");
+  if (a.swiglu_epi && (a.qkv_epi || a.nseg != 1 || !bmm_qkv_fits(a.w.K, a.B) || a.n_out % 64 || !a.h_out ||
+                       a.ldh_out < a.n_out / 2 || a.ldh_out % 4))
+    throw std::runtime_error("bmm: swiglu epilogue");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

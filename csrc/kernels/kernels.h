@@ -97,6 +97,14 @@ struct BmmArgs {
     const float2* rope = nullptr;  // [n_ctx][head_dim / 2]
   } qkv;
   bool qkv_epi = false;
+  // SwiGLU epilogue (gate/up, one K part, see bmm_qkv_fits): W rows come in 32-row gate / up
+  // groups (rows 64g.. = gate features 32g.., rows 64g+32.. = up features 32g..); a block
+  // takes 4-tile units (gate, gate, up, up of one group) and writes silu(gate) * up as f16 in
+  // bmm's 4-group k order to h_out[b * ldh_out + feature] - the down projection's input -
+  // instead of accumulating into `out` (no zeroed pre-activation buffer, no SwiGLU prep)
+  __half* h_out = nullptr;
+  int ldh_out = 0;
+  bool swiglu_epi = false;
 };
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)

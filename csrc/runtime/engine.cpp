@@ -71,7 +71,9 @@ void* Engine::dalloc(size_t bytes) {
 Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) {
   HIPCHK(hipSetDevice(opt_.device));
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   for (auto& e : step_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (auto& e : fork_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GGUFFile f(path);
   hp_ = read_hparams(f);
   const int tp = opt_.tp_size, r = opt_.tp_rank;
@@ -122,6 +124,8 @@ Engine::~Engine() {
   if (h_bslots_) hipHostFree(h_bslots_);
   if (h_btok_) hipHostFree(h_btok_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
+  for (auto& e : fork_ev_) if (e) hipEventDestroy(e);
+  if (side_) hipStreamDestroy(side_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -307,8 +311,11 @@ void Engine::setup_batch_mfma() {
   }
   bg_ = att;
   bg_ffn_ = att && ffn;
+  const char* side = std::getenv("LFK_BMM_SIDE");
+  side_overlap_ = !(side && side[0] == '0');
   if (!bg_) return;
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
+  hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_));
   // the batched path reads its own copy of the weights, laid out per 16-row tile (bmm.hip)
   auto tile = [&](const QMat& m) {
     QMat t = m;
@@ -773,13 +780,24 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   // RoPE + KV append in the Q|K|V epilogue when the whole K fits one LDS-staged part
   const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
   bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
-  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers)
+  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers).
+  // A second run goes on the side stream (fork / join events, captured into the graph as a
+  // parallel branch): the V run alone is 64 tiles, a latency-bound launch that now overlaps
+  // the Q|K one instead of following it.
   {
     const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
     float* o[3] = {qkv_, qkv_ + nq_, qkv_ + nq_ + nkvd_};
+    bool forked = false;
     for (int i = 0; i < 3;) {
       int j = i + 1;
       while (j < 3 && m[j]->type == m[i]->type) ++j;
+      hipStream_t rs = s;
+      if (i > 0 && side_overlap_) {
+        HIPCHK(hipEventRecord(fork_ev_[0], s));
+        HIPCHK(hipStreamWaitEvent(side_, fork_ev_[0], 0));
+        rs = side_;
+        forked = true;
+      }
       for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
         BmmArgs a;
         a.w = *m[i]; a.xh = xh_b_ + (size_t)b0 * d; a.ldh = d;
@@ -797,9 +815,13 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
           a.qkv.n_ctx = opt_.n_ctx; a.qkv.head_dim = hd;
           a.qkv.pos = bpos_ + b0; a.qkv.slots = bslots_ + b0; a.qkv.rope = rope_;
         }
-        bmm(a, s);
+        bmm(a, rs);
       }
       i = j;
+    }
+    if (forked) {
+      HIPCHK(hipEventRecord(fork_ev_[1], side_));
+      HIPCHK(hipStreamWaitEvent(s, fork_ev_[1], 0));
     }
   }
   if (!fused)
@@ -815,6 +837,18 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.out_h = xh_b_; aa.out_h_stride = nq_;   // the Wo input, already in bmm's f16 layout
   attn_decode(aa, s);
   bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
+  if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {
+    // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
+    // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
+    bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
+    BmmArgs a;
+    a.w = L.t_gu; a.xh = xh_b_; a.ldh = d;
+    a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
+    a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
+    bmm(a, s);
+    bmm_rows(L.t_down, hh_b_, F_l_, x_, d, d, B, s);
+    return;
+  }
   if (bg_ffn_) {
     bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
     bmm_rows(L.t_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);

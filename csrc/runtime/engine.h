@@ -268,6 +268,12 @@ class Engine : public SlotBackend {
   __half* xh_b_ = nullptr;    // [bmax][max(d, nq, F)] prepared f16 projection input
   QMat t_output_;             // tile16 copy of the output head
   float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
+  __half* hh_b_ = nullptr;    // [bmax][F_l] down-projection input written by the SwiGLU epilogue
+  // side stream + fork/join events: the second Q|K|V run overlaps the first (graph branch);
+  // LFK_BMM_SIDE=0 serialises it (A/B)
+  hipStream_t side_ = nullptr;
+  hipEvent_t fork_ev_[2] = {};
+  bool side_overlap_ = true;
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   hipGraph_t graph_ = nullptr;

@@ -471,6 +471,38 @@ def test_bmm_rows_vs_fp32(torch, t, B, R, K):
         assert np.all(got[b, R:] == 0)
 
 
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B", [1, 5, 8])
+@pytest.mark.parametrize("F,K", [(256, 4096), (96, 2048)])
+def test_bmm_swiglu_epilogue_vs_fp32(torch, t, B, F, K):
+    """Gate/up projection with the SwiGLU epilogue: W rows in 32-row gate / up groups, the
+    kernel writes silu(gate) * up as f16 in bprep's (0, 2, 1, 3) 4-group order, against the
+    fp32 product of the same f16 activations."""
+    rng = np.random.default_rng(B * 100 + F + int(t))
+    R = 2 * F
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    X = rng.standard_normal((B, K)).astype(np.float32)
+    Xh = X.astype(np.float16)
+    dxh = torch.from_numpy(_swizzle4(Xh)).cuda()
+    ldh_out = F + 8
+    hout = torch.full((B, ldh_out), 7.0, dtype=torch.float16, device="cuda")
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    hip().bmm(tw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, 0, 0, B, stream(),
+              h_out=hout.data_ptr(), ldh_out=ldh_out)
+    torch.cuda.synchronize()
+    got = hout.cpu().numpy().astype(np.float64)
+    pre = Xh.astype(np.float64) @ W.astype(np.float64).T          # [B][2F]
+    g = pre.reshape(B, F // 32, 2, 32)[:, :, 0].reshape(B, F)
+    u = pre.reshape(B, F // 32, 2, 32)[:, :, 1].reshape(B, F)
+    ref = g / (1.0 + np.exp(-g)) * u
+    for b in range(B):
+        row = _swizzle4(got[b, :F][None])[0]   # the swizzle is its own inverse
+        assert rel_err(row, ref[b]) < 3e-3, (b, rel_err(row, ref[b]))
+        assert np.all(got[b, F:] == 7.0)
+
+
 def test_bprep_norm_swiglu_zero(torch):
     """bprep: RMSNorm per row, SwiGLU on interleaved gate/up rows, f16 + (0,2,1,3) swizzle,
     and the zero side job."""
