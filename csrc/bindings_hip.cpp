@@ -256,7 +256,8 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("x"), py::arg("ldx"), py::arg("swiglu"), py::arg("norm"), py::arg("eps"), py::arg("K"), py::arg("B"),
      py::arg("xh"), py::arg("ldh"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0);
   m.def("bmm", [](uintptr_t w, int type, int rows, int K, uintptr_t xh, int ldh, uintptr_t out, int ldo, int B,
-                  uintptr_t stream, int debug, uintptr_t h_out, int ldh_out) {
+                  uintptr_t stream, int debug, uintptr_t h_out, int ldh_out, uintptr_t xf, int ldxf,
+                  uintptr_t norm, float eps, bool store_out) {
     BmmArgs a;
     a.debug = debug;
     a.w = make_qmat(P<void>(w), type, rows, K);
@@ -264,11 +265,17 @@ PYBIND11_MODULE(_hip, m) {
     if (h_out) {  // SwiGLU epilogue (gate/up rows in 32-row groups)
       a.swiglu_epi = true; a.h_out = P<__half>(h_out); a.ldh_out = ldh_out;
     }
+    if (xf) {     // RMSNorm folded into the staging (fp32 rows xf, weights norm)
+      a.xf = P<float>(xf); a.ldxf = ldxf; a.norm_w = P<float>(norm); a.eps = eps;
+    }
+    a.store_out = store_out;
     bmm(a, S(stream));
     hip_ok("bmm");
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("xh"), py::arg("ldh"), py::arg("out"),
      py::arg("ldo"), py::arg("B"), py::arg("stream"), py::arg("debug") = 0, py::arg("h_out") = 0,
-     py::arg("ldh_out") = 0);
+     py::arg("ldh_out") = 0, py::arg("xf") = 0, py::arg("ldxf") = 0, py::arg("norm") = 0, py::arg("eps") = 1e-5f,
+     py::arg("store_out") = false);
+  m.def("bmm_norm_fits", &bmm_norm_fits);
   m.def("bmm_supported", &bmm_supported);
   m.def("t16_bytes", &t16_bytes);
   m.def("t16_repack", [](uintptr_t w, int type, int rows, int K, uintptr_t dst, uintptr_t stream) {

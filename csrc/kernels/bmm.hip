@@ -247,6 +247,18 @@ __device__ __forceinline__ int raw_word(const WRaw<T>& w) {
   else return w.a.x;
 }
 
+// Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads. __syncthreads() is a workgroup release/acquire, which makes every wave drain
+// its outstanding global loads (s_waitcnt vmcnt(0)) - at every tile boundary that emptied
+// the weight ring the loop keeps in flight across tiles. (`fence` = the plain barrier, A/B.)
+__device__ __forceinline__ void lds_barrier(bool fence) {
+  if (fence) {
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+}
+
 // Items are (16-row tile, K part). A block serves ONE K part (block b: part b % kparts):
 // it stages that part of the B activation rows in LDS once (f16, row stride padded 16 B), then
 // its 4 waves share every tile - wave w takes the part's steps w, w + 4, ... - and add their
@@ -256,12 +268,23 @@ __device__ __forceinline__ int raw_word(const WRaw<T>& w) {
 // NW waves per block: 4 for the split-K shapes (4 blocks per CU), 8 for the one-part shapes
 // (Q|K|V and SwiGLU epilogues: the whole-K x slice limits a CU to 2 blocks, so 8 waves keep
 // 16 waves per CU streaming).
-template <int QT, int NW>
-__global__ __launch_bounds__(NW * 64) void bmm_kernel(BmmArgs a) {
+//
+// Weights are double-buffered in registers with FIXED roles (ping-pong, the step loop
+// unrolled by two): step i computes from one buffer while step i + 1 loads into the other.
+// A rotating copy (wc = wn at the end of each step) made the compiler wait for the in-flight
+// loads before the copy - s_waitcnt vmcnt(0) every step, so no load ever overlapped the
+// next step's compute and the kernel ran on HBM latency. The buffers also run across tiles:
+// the last step of a tile loads the next tile's first one (the roles swap after a tile with
+// an odd number of steps per wave).
+// (second launch bound = minimum waves per SIMD: 4, except the 8-wave Q6_K kernel, which
+// would spill at 128 VGPRs)
+template <int QT, int NW, int PD>
+__global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 : 4) void bmm_kernel(BmmArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
-  __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16);
+  float* rowss = reinterpret_cast<float*>(smem + (NW - 1) * 64 * 16);  // [8 rows][8 waves] folded norm
+  __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16 + 256);
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
@@ -288,74 +311,129 @@ __global__ __launch_bounds__(NW * 64) void bmm_kernel(BmmArgs a) {
   };
   const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
   const bool has = ws0 < s1;                      // (a part shorter than NW steps idles some waves)
-  const int wlast = has ? ws0 + ((s1 - 1 - ws0) / NW) * NW : ws0;
+  const int n_ws = has ? (s1 - 1 - ws0) / NW + 1 : 1;  // this wave's steps per tile
   // the first tile's first weights load before the x staging round trip
   const uint8_t* tb = tile_base(gt);
-  WRaw<QT> wc[2], wn[2];
+  // tiles after the first (past the end: an earlier valid tile - loaded, never used)
+  const int g1 = next_tile(gt);
+  const uint8_t* tbn = g1 < tiles ? tile_base(g1) : tb;
+  const uint8_t* tbn2 = g1 < tiles && next_tile(g1) < tiles ? tile_base(next_tile(g1)) : tbn;
+  auto addr = [&](int j) {  // weights of the wave's step j counted from this tile's first
+    return j < n_ws ? tb + (size_t)(ws0 + j * NW) * SB
+         : j < 2 * n_ws ? tbn + (size_t)(ws0 + (j - n_ws) * NW) * SB : tbn2 + (size_t)ws0 * SB;
+  };
+  WRaw<QT> wa[2], wb[2], wc[2];
   if (has) {
-    tload<QT>(wc[0], tb + (size_t)ws0 * SB, 0, lane, r16, kq);
-    tload<QT>(wc[1], tb + (size_t)ws0 * SB, 1, lane, r16, kq);
+    const uint8_t* p0 = addr(0);
+    tload<QT>(wa[0], p0, 0, lane, r16, kq);
+    tload<QT>(wa[1], p0, 1, lane, r16, kq);
+    if constexpr (PD == 2) {
+      const uint8_t* p1 = addr(1);
+      tload<QT>(wb[0], p1, 0, lane, r16, kq);
+      tload<QT>(wb[1], p1, 1, lane, r16, kq);
+    }
   }
   // stage x[b][k0, k0 + kn) for the B rows
-  for (int i = tid; i < a.B * (kn >> 3); i += kBlock) {
-    const int b = i / (kn >> 3), v = i - b * (kn >> 3);
-    *reinterpret_cast<uint4*>(xs + b * ldx + 8 * v) =
-        *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * v);
+  if (NW == 8 && a.xf) {  // (8-wave kernels only: keeps the split-K kernels' registers)
+    // folded RMSNorm (K = 4096, B <= 8: each thread holds 2 float4 of every row): every load
+    // is issued first - one memory round trip, like the f16 staging - then f16(x * w) goes to
+    // LDS in bprep's 4-group order and each wave leaves its per-row partial sum of squares
+    // (rows past B load row B - 1 and are dropped: straight-line code, no predicated loads)
+    float4 xv[16];
+    const float4 w0 = *reinterpret_cast<const float4*>(a.norm_w + 4 * tid);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.norm_w + 4 * (tid + kBlock));
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
+      xv[2 * b] = *reinterpret_cast<const float4*>(xr + 4 * tid);
+      xv[2 * b + 1] = *reinterpret_cast<const float4*>(xr + 4 * (tid + kBlock));
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 x = xv[2 * b + j], w = j ? w1 : w0;
+        ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+        const h2_t p0 = {(_Float16)(x.x * w.x), (_Float16)(x.z * w.z)};
+        const h2_t p1 = {(_Float16)(x.y * w.y), (_Float16)(x.w * w.w)};
+        if (b < a.B) *reinterpret_cast<uint2*>(xs + b * ldx + 4 * (tid + j * kBlock)) = make_uint2(as_u(p0), as_u(p1));
+      }
+      ss = wave_sum_fast(ss);
+      if (lane == 0) rowss[b * 8 + wave] = ss;
+    }
+  } else {
+    for (int i = tid; i < a.B * (kn >> 3); i += kBlock) {
+      const int b = i / (kn >> 3), v = i - b * (kn >> 3);
+      *reinterpret_cast<uint4*>(xs + b * ldx + 8 * v) =
+          *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * v);
+    }
   }
   __syncthreads();
   const bool col_ok = r16 < a.B;
+  // folded norm: this lane's column scale (applied to the reduced tile before any epilogue)
+  float cs = 1.f;
+  if (NW == 8 && a.xf) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) t += rowss[(col_ok ? r16 : 0) * 8 + w];
+    cs = rsqrtf(t / (float)kn + a.eps);
+  }
   const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
   f4_t gate[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // SwiGLU: wave 0's gate tiles of the unit
-  for (; gt < tiles; gt = next_tile(gt)) {
+  // the wave's steps as one flattened sequence over its tiles, the buffers alternating
+  // (wa, wb, wa, ...) along it: no register copies, and a tile's end is just a point in it
+  // two accumulators (chunk h = 0 / 1): the 8 MFMAs of a step form two dependent chains of 4
+  // instead of one of 8 (SQ_WAIT_INST_ANY, the MFMA read-after-write stalls, was 24 % of the
+  // gate/up kernel's wave cycles)
+  f4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  int i = 0;  // step of the current tile
+  auto compute = [&](const WRaw<QT>* wc, int i) {
+    // one step per scheduling region: interleaving two steps' dequantisation raised the
+    // register count from ~110 to 150-180 (2-3 waves per SIMD)
+    __builtin_amdgcn_sched_barrier(0);
+    const int s = ws0 + i * NW;
+    if (a.debug == 1) {  // microbenchmark: weight stream only
+      acc[0] += (float)raw_word<QT>(wc[0]) + (float)raw_word<QT>(wc[1]);
+      return;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 8 * s + 4 * h + kq;
+      int off_lo, off_hi;
+      chunk_runs<QT>(c, off_lo, off_hi);
+      const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+      const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+      const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
+      HFrag F;
+      dequant_frags<QT>(wc[h], c, F);
+      const unsigned bl[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+      const unsigned bh[8] = {x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        // A: lo pairs (4m,4m+2),(4m+1,4m+3) then hi pairs; B: x[lo + 4m .. +3], x[hi + 4m .. +3]
+        const uint4 av = make_uint4(F.w[4 * m], F.w[4 * m + 1], F.w[4 * m + 2], F.w[4 * m + 3]);
+        const uint4 bv = make_uint4(bl[2 * m], bl[2 * m + 1], bh[2 * m], bh[2 * m + 1]);
+        f4_t& ac = h == 0 ? acc : acc2;
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
+                                                    __builtin_bit_cast(h8_t, bv), ac, 0, 0, 0);
+      }
+    }
+  };
+  // reduction + epilogue of tile gt (every wave of the block, once per tile)
+  auto finish_tile = [&]() {
+    acc += acc2;
     const int sg = gt >= tile0[1] ? (gt >= tile0[2] ? 2 : 1) : 0;   // wave-uniform
     const int tile = gt - tile0[sg];
     const int n_out = sg ? a.seg_rows[sg] : a.n_out;
     float* out = sg ? a.seg_out[sg] : a.out;
-    // the ring runs across tiles: after this tile's last step the next tile's first one loads,
-    // so the reduction barrier below does not drain the weight stream
-    const uint8_t* tb_next = next_tile(gt) < tiles ? tile_base(next_tile(gt)) : tb;
-    f4_t acc = {0.f, 0.f, 0.f, 0.f};
-    if (has) {
-      for (int s = ws0; s < s1; s += NW) {
-        const uint8_t* nb = s + NW <= wlast ? tb + (size_t)(s + NW) * SB : tb_next + (size_t)ws0 * SB;
-        tload<QT>(wn[0], nb, 0, lane, r16, kq);
-        tload<QT>(wn[1], nb, 1, lane, r16, kq);
-        if (a.debug == 1) {  // microbenchmark: weight stream only
-          acc[0] += (float)raw_word<QT>(wc[0]) + (float)raw_word<QT>(wc[1]);
-        } else {
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int c = 8 * s + 4 * h + kq;
-            int off_lo, off_hi;
-            chunk_runs<QT>(c, off_lo, off_hi);
-            const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
-            const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
-            const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
-            HFrag F;
-            dequant_frags<QT>(wc[h], c, F);
-            const unsigned bl[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-            const unsigned bh[8] = {x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              // A: lo pairs (4i,4i+2),(4i+1,4i+3) then hi pairs; B: x[lo + 4i .. +3], x[hi + 4i .. +3]
-              const uint4 av = make_uint4(F.w[4 * i], F.w[4 * i + 1], F.w[4 * i + 2], F.w[4 * i + 3]);
-              const uint4 bv = make_uint4(bl[2 * i], bl[2 * i + 1], bh[2 * i], bh[2 * i + 1]);
-              acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
-                                                           __builtin_bit_cast(h8_t, bv), acc, 0, 0, 0);
-            }
-          }
-        }
-        wc[0] = wn[0];
-        wc[1] = wn[1];
-      }
-    }
-    tb = tb_next;
     // the 4 waves' partial tiles meet in LDS; wave 0 writes C[row 4kq + i][col r16]
     if (wave > 0) *reinterpret_cast<f4_t*>(red + ((wave - 1) * 64 + lane) * 4) = acc;
-    __syncthreads();
+    lds_barrier(a.fence_sync);
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
+      if (NW == 8 && a.xf) acc *= cs;
       if (sw) {
         // tiles 4u, 4u+1: gate rows; 4u+2, 4u+3: the up rows of the same features
         const int qt = gt & 3;
@@ -402,12 +480,52 @@ __global__ __launch_bounds__(NW * 64) void bmm_kernel(BmmArgs a) {
           const int row = tile * 16 + 4 * kq + i;
           if (row < n_out) {
             if (kparts > 1) atomicAdd(o + row, acc[i]);
+            else if (a.store_out) o[row] = acc[i];
             else o[row] += acc[i];   // one owner per (row, column)
           }
         }
       }
     }
-    __syncthreads();  // red is reused by the next tile
+    lds_barrier(a.fence_sync);  // red is reused by the next tile
+    acc = f4_t{0.f, 0.f, 0.f, 0.f};
+    acc2 = acc;
+  };
+  // after step i: the tile's end finishes it and moves to the next tile (false: block done)
+  auto advance = [&]() {
+    if (++i < n_ws) return true;
+    finish_tile();
+    i = 0;
+    gt = next_tile(gt);
+    if (gt >= tiles) return false;
+    tb = tbn;
+    tbn = tbn2;
+    const int gn2 = next_tile(gt) < tiles ? next_tile(next_tile(gt)) : tiles;
+    tbn2 = gn2 < tiles ? tile_base(gn2) : tbn;
+    return true;
+  };
+  // one step: load step i + PD into `ld`, compute step i from `cur`
+  auto step = [&](WRaw<QT>* ld, const WRaw<QT>* cur) {
+    const uint8_t* p = addr(i + PD);
+    tload<QT>(ld[0], p, 0, lane, r16, kq);
+    tload<QT>(ld[1], p, 1, lane, r16, kq);
+    compute(cur, i);
+    return advance();
+  };
+  if (has) {
+    if constexpr (PD == 1) {
+      for (;;) {
+        if (!step(wb, wa)) break;
+        if (!step(wa, wb)) break;
+      }
+    } else {
+      for (;;) {
+        if (!step(wc, wa)) break;
+        if (!step(wa, wb)) break;
+        if (!step(wb, wc)) break;
+      }
+    }
+  } else {
+    for (; gt < tiles; gt = next_tile(gt)) finish_tile();  // idle waves still join every tile's barriers
   }
 }
 
@@ -484,10 +602,12 @@ void bprep(const BPrepArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- launch
-static size_t bmm_lds(int B, int spp, int nw) { return (size_t)(nw - 1) * 64 * 16 + (size_t)B * (spp * 256 + 8) * 2; }
+static size_t bmm_lds(int B, int spp, int nw) { return (size_t)(nw - 1) * 64 * 16 + 256 + (size_t)B * (spp * 256 + 8) * 2; }
 
 // one-part shapes run 8-wave blocks; two of them must fit a CU's 160 KB of LDS
 bool bmm_qkv_fits(int K, int B) { return K % 256 == 0 && B >= 1 && bmm_lds(B, K / 256, 8) <= 80 * 1024; }
+// folded norm: the 512-thread staging holds 2 float4 of each of <= 8 rows per thread
+bool bmm_norm_fits(int K, int B) { return bmm_qkv_fits(K, B) && K == 4096 && B <= 8; }
 
 bool bmm_supported(int type, int K) {
   if (type != T_Q4_K && type != T_Q5_K && type != T_Q6_K && type != T_Q8_0) return false;
@@ -509,22 +629,32 @@ static int env_int(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
+// weight steps in flight per wave (LFK_BMM_PD, tuning: 1 or 2; Q4_K only - the other types
+// need > 128 VGPRs for the third buffer)
+template <int QT>
+static int bmm_pd() {
+  static const int pd = env_int("LFK_BMM_PD", 1);
+  return QT == T_Q4_K ? pd : 1;
+}
+
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
   for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
   const int steps = a.w.K / 256;
-  if (a.qkv_epi || a.swiglu_epi) {
+  if (a.qkv_epi || a.swiglu_epi || a.xf) {
     // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
-    static const int nw1 = env_int("LFK_BMM_NW1", 8);  // tuning: 4 or 8
+    static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4 or 8
+    const int nw1 = a.xf ? 8 : nw1_env;                          // the folded norm is 8-wave only
     a.spp = steps;
     a.kparts = 1;
     const size_t lds = bmm_lds(a.B, steps, nw1);
     const int units = a.swiglu_epi ? tiles / 4 : tiles;
     const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
     const int nb = std::max(1, std::min(units, per_cu * bmm_cus()));
-    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4>), dim3(nb), dim3(256), lds, s, a);
-    else hipLaunchKernelGGL((bmm_kernel<QT, 8>), dim3(nb), dim3(512), lds, s, a);
+    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(nb), dim3(256), lds, s, a);
+    else if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 8, 2>), dim3(nb), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_kernel<QT, 8, 1>), dim3(nb), dim3(512), lds, s, a);
     return;
   }
   // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
@@ -543,10 +673,14 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   static const int per_cu = env_int("LFK_BMM_GRID", 4);  // tuning
   const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus() + kparts - 1) / kparts));
   const size_t lds = bmm_lds(a.B, spp, 4);
-  hipLaunchKernelGGL((bmm_kernel<QT, 4>), dim3(bpk * kparts), dim3(256), lds, s, a);
+  if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 4, 2>), dim3(bpk * kparts), dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a);
 }
 
-void bmm(const BmmArgs& a, hipStream_t s) {
+void bmm(const BmmArgs& a0, hipStream_t s) {
+  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
+  BmmArgs a = a0;
+  a.fence_sync = fence;
   if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
   if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
@@ -554,6 +688,9 @@ void bmm(const BmmArgs& a, hipStream_t s) {
   if (a.swiglu_epi && (a.qkv_epi || a.nseg != 1 || !bmm_qkv_fits(a.w.K, a.B) || a.n_out % 64 || !a.h_out ||
                        a.ldh_out < a.n_out / 2 || a.ldh_out % 4))
     throw std::runtime_error("bmm: swiglu epilogue");
+  if (a.xf && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))
+    throw std::runtime_error("bmm: folded norm");
+  if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi) throw std::runtime_error("bmm: store_out needs one K part");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

@@ -105,9 +105,19 @@ struct BmmArgs {
   __half* h_out = nullptr;
   int ldh_out = 0;
   bool swiglu_epi = false;
+  // RMSNorm folded into the x staging (one K part, K % 2048 == 0, see bmm_norm_fits): the
+  // block reads the fp32 rows xf[b * ldxf + k], stages f16(x * norm_w) and the row sums of
+  // squares; the epilogue scales each column by rsqrt(mean + eps) (xh is not read)
+  const float* xf = nullptr;
+  int ldxf = 0;
+  const float* norm_w = nullptr;
+  float eps = 1e-5f;
+  bool store_out = false;          // plain epilogue: out = result (default: out += result)
+  bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
 };
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)
+bool bmm_norm_fits(int K, int B);  // one K part + the folded RMSNorm's staging shape
 void bmm(const BmmArgs& a, hipStream_t s);
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);

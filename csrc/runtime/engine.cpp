@@ -313,6 +313,10 @@ void Engine::setup_batch_mfma() {
   bg_ffn_ = att && ffn;
   const char* side = std::getenv("LFK_BMM_SIDE");
   side_overlap_ = !(side && side[0] == '0');
+  const char* nf = std::getenv("LFK_BMM_NORM");
+  norm_fold_ = !(nf && nf[0] == '0');
+  const char* hf = std::getenv("LFK_BMM_HEAD1");
+  head_fold_ = hf && hf[0] == '1';
   if (!bg_) return;
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
   hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_));
@@ -779,7 +783,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   __half* vcl = vc_ + kv_layer * l;
   // RoPE + KV append in the Q|K|V epilogue when the whole K fits one LDS-staged part
   const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
-  bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
+  // attention / FFN RMSNorm folded into the one-part projections' x staging (no prep launch)
+  const bool fnorm = fused && norm_fold_ && bmm_norm_fits(d, B);
+  if (!fnorm) bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
   // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers).
   // A second run goes on the side stream (fork / join events, captured into the graph as a
   // parallel branch): the V run alone is 64 tiles, a latency-bound launch that now overlaps
@@ -806,6 +812,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
         a.nseg = j - i;
         for (int k = 1; k < a.nseg; ++k) {
           a.seg_base[k] = m[i + k]->base; a.seg_rows[k] = m[i + k]->rows; a.seg_out[k] = o[i + k] + (size_t)b0 * ncol;
+        }
+        if (fnorm) {
+          a.xf = x_ + (size_t)b0 * d; a.ldxf = d; a.norm_w = L.attn_norm; a.eps = hp_.rms_eps;
         }
         if (fused) {
           a.qkv_epi = true;
@@ -840,8 +849,12 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
-    bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
     BmmArgs a;
+    if (fnorm) {
+      a.xf = x_; a.ldxf = d; a.norm_w = L.ffn_norm; a.eps = hp_.rms_eps;
+    } else {
+      bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
+    }
     a.w = L.t_gu; a.xh = xh_b_; a.ldh = d;
     a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
     a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
@@ -868,8 +881,16 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
   embed_rows(tok_embd_, btok_, B, x_, s);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
-    bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
-    bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
+    if (head_fold_ && B <= kBmmMaxRows && bmm_norm_fits(d, B)) {
+      // final norm folded into a one-part head projection that stores the logits
+      BmmArgs a;
+      a.w = t_output_; a.xf = x_; a.ldxf = d; a.norm_w = out_norm_; a.eps = hp_.rms_eps;
+      a.out = logits_b_; a.ldo = V_pad_; a.n_out = hp_.n_vocab; a.B = B; a.store_out = true;
+      bmm(a, s);
+    } else {
+      bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
+      bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
+    }
   } else {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
     rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, s);

@@ -274,6 +274,10 @@ class Engine : public SlotBackend {
   hipStream_t side_ = nullptr;
   hipEvent_t fork_ev_[2] = {};
   bool side_overlap_ = true;
+  // RMSNorm folded into the one-part projections' staging (Q|K|V, gate/up: no prep launch;
+  // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
+  // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)
+  bool norm_fold_ = true, head_fold_ = false;
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   hipGraph_t graph_ = nullptr;

@@ -503,6 +503,56 @@ def test_bmm_swiglu_epilogue_vs_fp32(torch, t, B, F, K):
         assert np.all(got[b, F:] == 7.0)
 
 
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B", [1, 6, 16])
+@pytest.mark.parametrize("mode", ["store", "swiglu"])
+def test_bmm_folded_norm_vs_fp32(torch, t, B, mode):
+    """RMSNorm folded into the one-part staging: fp32 rows in, f16(x * w) staged, the column
+    scale rsqrt(mean(x^2) + eps) applied to the reduced tile; `store` writes the result over
+    the output, `swiglu` feeds the gate/up epilogue."""
+    K = 4096 if B <= 8 else 2048
+    if not hip().bmm_norm_fits(K, B):
+        pytest.skip("shape outside the folded-norm staging")
+    rng = np.random.default_rng(B * 7 + int(t) + (mode == "swiglu"))
+    R = 192 if mode == "swiglu" else 130
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    X = (rng.standard_normal((B, K)) * 3).astype(np.float32)
+    nw = (0.5 + rng.random(K)).astype(np.float32)
+    eps = 1e-5
+    ldxf = K + 4
+    dx = torch.zeros(B, ldxf, device="cuda")
+    dx[:, :K] = torch.from_numpy(X).cuda()
+    dn = torch.from_numpy(nw).cuda()
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    xn = X.astype(np.float64) / np.sqrt((X.astype(np.float64) ** 2).mean(1, keepdims=True) + eps) * nw
+    pre = xn @ W.astype(np.float64).T
+    if mode == "store":
+        ldo = R + 6
+        out = torch.full((B, ldo), 5.0, device="cuda")
+        hip().bmm(tw.data_ptr(), int(t), R, K, 0, 0, out.data_ptr(), ldo, B, stream(),
+                  xf=dx.data_ptr(), ldxf=ldxf, norm=dn.data_ptr(), eps=eps, store_out=True)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        for b in range(B):
+            assert rel_err(got[b, :R], pre[b]) < 3e-3, (b, rel_err(got[b, :R], pre[b]))
+            assert np.all(got[b, R:] == 5.0)
+    else:
+        F = R // 2
+        hout = torch.zeros((B, F), dtype=torch.float16, device="cuda")
+        hip().bmm(tw.data_ptr(), int(t), R, K, 0, 0, 0, 0, B, stream(), h_out=hout.data_ptr(), ldh_out=F,
+                  xf=dx.data_ptr(), ldxf=ldxf, norm=dn.data_ptr(), eps=eps)
+        torch.cuda.synchronize()
+        got = hout.cpu().numpy().astype(np.float64)
+        g = pre.reshape(B, F // 32, 2, 32)[:, :, 0].reshape(B, F)
+        u = pre.reshape(B, F // 32, 2, 32)[:, :, 1].reshape(B, F)
+        ref = g / (1.0 + np.exp(-g)) * u
+        for b in range(B):
+            row = _swizzle4(got[b][None])[0]
+            assert rel_err(row, ref[b]) < 3e-3, (b, rel_err(row, ref[b]))
+
+
 def test_bprep_norm_swiglu_zero(torch):
     """bprep: RMSNorm per row, SwiGLU on interleaved gate/up rows, f16 + (0,2,1,3) swizzle,
     and the zero side job."""

@@ -20,7 +20,8 @@ def main():
     from gpu_helpers import hip, stream
     from llama_fastapi_k8s_gpu_amd.gguf.constants import GGMLType
     h = hip()
-    shapes = [("gate_up", GGMLType.Q4_K, 28672, 4096), ("down", GGMLType.Q4_K, 4096, 14336),
+    shapes = [("gate_up", GGMLType.Q4_K, 28672, 4096), ("gate_up_sw", GGMLType.Q4_K, 28672, 4096),
+              ("down", GGMLType.Q4_K, 4096, 14336),
               ("down6", GGMLType.Q6_K, 4096, 14336), ("wq", GGMLType.Q4_K, 4096, 4096),
               ("wk", GGMLType.Q4_K, 1024, 4096), ("head", GGMLType.Q6_K, 128256, 4096)]
     res = {}
@@ -30,10 +31,12 @@ def main():
         ws = [torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda") for _ in range(nbuf)]
         xh = torch.randn(16, K, device="cuda").half()
         out = torch.zeros(16, R, device="cuda")
+        hout = torch.zeros(16, R // 2, dtype=torch.float16, device="cuda")
+        sw = name.endswith("_sw")  # SwiGLU epilogue (one K part, f16 output)
         for B in [int(b) for b in args.rows.split(",")]:
             def fn(i):
                 h.bmm(ws[i % nbuf].data_ptr(), int(t), R, K, xh.data_ptr(), K, out.data_ptr(), R, B, stream(),
-                      debug=args.debug)
+                      debug=args.debug, h_out=hout.data_ptr() if sw else 0, ldh_out=R // 2)
             fn(0)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
