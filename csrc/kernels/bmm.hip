@@ -280,6 +280,7 @@ __device__ __forceinline__ void lds_barrier(bool fence) {
 // would spill at 128 VGPRs)
 template <int QT, int NW, int PD>
 __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 : 4) void bmm_kernel(BmmArgs a) {
+  const int bid = blockIdx.x, nbk = gridDim.x;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
@@ -289,25 +290,28 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
   // segments (Q|K|V in one launch): tile index -> (matrix, local tile)
-  int tile0[4] = {0, 0, 0, 0};
-  tile0[1] = (a.n_out + 15) >> 4;
-  for (int i = 1; i < 3; ++i) tile0[i + 1] = tile0[i] + (i < a.nseg ? (a.seg_rows[i] + 15) >> 4 : 0);
-  const int tiles = tile0[a.nseg];
+  const int t1 = (a.n_out + 15) >> 4;
+  const int t2 = t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0);
+  const int t3 = t2 + (a.nseg > 2 ? (a.seg_rows[2] + 15) >> 4 : 0);
+  const int tiles = a.nseg == 1 ? t1 : a.nseg == 2 ? t2 : t3;
+  auto seg_of = [&](int g) { return g >= t1 ? (g >= t2 ? 2 : 1) : 0; };
+  auto seg_first = [&](int sg) { return sg == 0 ? 0 : sg == 1 ? t1 : t2; };
   const int kparts = a.kparts, spp = a.spp;
-  const int kp = blockIdx.x % kparts;
+  const int kp = bid % kparts;
   const int s0 = kp * spp, s1 = min(steps, s0 + spp);
   if (s0 >= s1) return;  // whole block, before any barrier
   const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
-  const int gstride = gridDim.x / kparts;
-  // tile order: SwiGLU blocks take 4-tile units (4u .. 4u + 3, then unit u + gridDim.x)
+  const int gstride = nbk / kparts;
+  // tile order: SwiGLU blocks take 4-tile units (4u .. 4u + 3, then unit u + nbk)
   const bool sw = a.swiglu_epi;
-  int gt = sw ? 4 * blockIdx.x : blockIdx.x / kparts;
-  auto next_tile = [&](int g) { return sw ? ((g & 3) != 3 ? g + 1 : g + 1 + 4 * (gridDim.x - 1)) : g + gstride; };
+  int gt = sw ? 4 * bid : bid / kparts;
+  auto next_tile = [&](int g) { return sw ? ((g & 3) != 3 ? g + 1 : g + 1 + 4 * (nbk - 1)) : g + gstride; };
   if (gt >= tiles) return;  // whole block, before any barrier
   const int SB = t16_step_bytes(QT);
   auto tile_base = [&](int g) {  // first byte of global tile g's tile16 data
-    const int sg = g >= tile0[1] ? (g >= tile0[2] ? 2 : 1) : 0;
-    return (sg ? a.seg_base[sg] : a.w.base) + (size_t)(g - tile0[sg]) * steps * SB;
+    const int sg = seg_of(g);
+    const uint8_t* base = sg == 0 ? a.w.base : sg == 1 ? a.seg_base[1] : a.seg_base[2];
+    return base + (size_t)(g - seg_first(sg)) * steps * SB;
   };
   const int ws0 = s0 + wave;                     // this wave's steps: ws0, ws0 + NW, ...
   const bool has = ws0 < s1;                      // (a part shorter than NW steps idles some waves)
@@ -423,10 +427,10 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   // reduction + epilogue of tile gt (every wave of the block, once per tile)
   auto finish_tile = [&]() {
     acc += acc2;
-    const int sg = gt >= tile0[1] ? (gt >= tile0[2] ? 2 : 1) : 0;   // wave-uniform
-    const int tile = gt - tile0[sg];
-    const int n_out = sg ? a.seg_rows[sg] : a.n_out;
-    float* out = sg ? a.seg_out[sg] : a.out;
+    const int sg = seg_of(gt);   // wave-uniform
+    const int tile = gt - seg_first(sg);
+    const int n_out = sg == 0 ? a.n_out : sg == 1 ? a.seg_rows[1] : a.seg_rows[2];
+    float* out = sg == 0 ? a.out : sg == 1 ? a.seg_out[1] : a.seg_out[2];
     // the 4 waves' partial tiles meet in LDS; wave 0 writes C[row 4kq + i][col r16]
     if (wave > 0) *reinterpret_cast<f4_t*>(red + ((wave - 1) * 64 + lane) * 4) = acc;
     lds_barrier(a.fence_sync);
@@ -449,7 +453,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       } else if (col_ok && a.qkv_epi) {
         // rows 4kq .. 4kq+3 of the tile: RoPE pairs (0,1), (2,3) are in this lane
         const auto& q = a.qkv;
-        const int kind = q.kind[sg], b = r16, hd = q.head_dim;
+        const int kind = sg == 0 ? q.kind[0] : sg == 1 ? q.kind[1] : q.kind[2], b = r16, hd = q.head_dim;
         const int pos = min(max(q.pos[b], 0), q.n_ctx - 1);
         const size_t so = (size_t)q.slots[b] * q.slot_stride;
 #pragma unroll

@@ -71,9 +71,7 @@ void* Engine::dalloc(size_t bytes) {
 Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) {
   HIPCHK(hipSetDevice(opt_.device));
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   for (auto& e : step_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  for (auto& e : fork_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   GGUFFile f(path);
   hp_ = read_hparams(f);
   const int tp = opt_.tp_size, r = opt_.tp_rank;
@@ -124,8 +122,6 @@ Engine::~Engine() {
   if (h_bslots_) hipHostFree(h_bslots_);
   if (h_btok_) hipHostFree(h_btok_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
-  for (auto& e : fork_ev_) if (e) hipEventDestroy(e);
-  if (side_) hipStreamDestroy(side_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -311,8 +307,6 @@ void Engine::setup_batch_mfma() {
   }
   bg_ = att;
   bg_ffn_ = att && ffn;
-  const char* side = std::getenv("LFK_BMM_SIDE");
-  side_overlap_ = !(side && side[0] == '0');
   const char* nf = std::getenv("LFK_BMM_NORM");
   norm_fold_ = !(nf && nf[0] == '0');
   const char* hf = std::getenv("LFK_BMM_HEAD1");
@@ -786,24 +780,15 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   // attention / FFN RMSNorm folded into the one-part projections' x staging (no prep launch)
   const bool fnorm = fused && norm_fold_ && bmm_norm_fits(d, B);
   if (!fnorm) bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
-  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers).
-  // A second run goes on the side stream (fork / join events, captured into the graph as a
-  // parallel branch): the V run alone is 64 tiles, a latency-bound launch that now overlaps
-  // the Q|K one instead of following it.
+  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers;
+  // a side-stream graph branch for the V run measured no gain)
   {
     const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
     float* o[3] = {qkv_, qkv_ + nq_, qkv_ + nq_ + nkvd_};
-    bool forked = false;
+    std::vector<BmmArgs> rl;
     for (int i = 0; i < 3;) {
       int j = i + 1;
       while (j < 3 && m[j]->type == m[i]->type) ++j;
-      hipStream_t rs = s;
-      if (i > 0 && side_overlap_) {
-        HIPCHK(hipEventRecord(fork_ev_[0], s));
-        HIPCHK(hipStreamWaitEvent(side_, fork_ev_[0], 0));
-        rs = side_;
-        forked = true;
-      }
       for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
         BmmArgs a;
         a.w = *m[i]; a.xh = xh_b_ + (size_t)b0 * d; a.ldh = d;
@@ -824,14 +809,11 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
           a.qkv.n_ctx = opt_.n_ctx; a.qkv.head_dim = hd;
           a.qkv.pos = bpos_ + b0; a.qkv.slots = bslots_ + b0; a.qkv.rope = rope_;
         }
-        bmm(a, rs);
+        rl.push_back(a);
       }
       i = j;
     }
-    if (forked) {
-      HIPCHK(hipEventRecord(fork_ev_[1], side_));
-      HIPCHK(hipStreamWaitEvent(s, fork_ev_[1], 0));
-    }
+    for (const BmmArgs& a : rl) bmm(a, s);
   }
   if (!fused)
     rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);

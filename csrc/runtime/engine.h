@@ -269,11 +269,6 @@ class Engine : public SlotBackend {
   QMat t_output_;             // tile16 copy of the output head
   float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
   __half* hh_b_ = nullptr;    // [bmax][F_l] down-projection input written by the SwiGLU epilogue
-  // side stream + fork/join events: the second Q|K|V run overlaps the first (graph branch);
-  // LFK_BMM_SIDE=0 serialises it (A/B)
-  hipStream_t side_ = nullptr;
-  hipEvent_t fork_ev_[2] = {};
-  bool side_overlap_ = true;
   // RMSNorm folded into the one-part projections' staging (Q|K|V, gate/up: no prep launch;
   // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
   // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)

@@ -52,6 +52,34 @@ def test_batch_step_rows_match_reference(models, spec):
     assert eng.healthy, eng.last_error
 
 
+def test_batch_step_d4096_fused_paths(tmp_path):
+    """d = 4096 (the 8B width, 4 layers): the batched step runs the folded RMSNorm (Q|K|V and
+    gate/up stage fp32 rows), the SwiGLU epilogue and, on the bumped layers (Q6_K Wv), the
+    Q|K + V two-type launch - rows against the fp32 reference."""
+    from llama_fastapi_k8s_gpu_amd.gguf.reader import GGUFReader
+    from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = write_synthetic_gguf("pd-llama-g4", str(tmp_path / "g4.gguf"))
+    eng = load_hip().Engine(path, n_ctx=128, n_batch=64, device=0, use_graph=True, n_slots=4)
+    ref = ReferenceLlama(GGUFReader(path), n_ctx=128)
+    rng = np.random.default_rng(5)
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    seqs = {}
+    for s, n in zip((2, 0, 3), (6, 11, 9)):
+        prompt = [int(t) for t in rng.integers(3, 300, n)]
+        seqs[s] = prompt + [eng.slot_begin(s, prompt, 0, greedy)]
+    for rows in ([2, 0, 3], [0, 3]):
+        toks = eng.batch_step(rows)
+        logits = eng.batch_logits(len(rows))
+        for b, s in enumerate(rows):
+            want = ref.forward(seqs[s], 0).numpy()
+            assert rel_err(logits[b], want) < 5e-2, (s, rel_err(logits[b], want))
+            assert toks[b] == int(np.argmax(logits[b]))
+            seqs[s].append(toks[b])
+    assert eng.healthy, eng.last_error
+
+
 def test_batch_sampling_params_are_per_slot(models):
     """Each slot samples with its own parameters, penalty ring and seed."""
     from llama_fastapi_k8s_gpu_amd.runtime import load_hip
