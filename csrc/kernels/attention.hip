@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   const long long t_entry = TL ? wall_clock64() : 0;
   const bool stamp = TL && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
 #define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) a.dbg_clk[i] = wall_clock64() - t_entry; } } while (0)
-  if (a.batch == 0 && blockIdx.z == 1) {  // weight-touch plane (see AttnDecodeArgs::pf)
+  if ((int)blockIdx.z == (a.batch > 0 ? a.batch : 1)) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;
     for (int r = 0; r < AttnDecodeArgs::kTouchRanges; ++r) {
@@ -363,11 +363,11 @@ void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
     touch = true;
   }
   if (a.batch > 0) {
-    if (touch) throw std::runtime_error("attn_decode: no weight touch in batched mode");
     if (!a.slots || a.n_kv_head > 64 || a.part_stride < attn_decode_workspace_floats(a.n_ctx, a.n_head, a.head_dim))
       throw std::runtime_error("attn_decode: bad batched arguments");
   }
-  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, a.batch > 0 ? a.batch : (touch ? 2 : 1));
+  // z: the rows (batched) or one; the weight-touch plane, if any, is the next z index
+  dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, (a.batch > 0 ? a.batch : 1) + (touch ? 1 : 0));
   if (a.head_dim == 128) launch_attn_decode<128>(a, G, grid, s);
   else if (a.head_dim == 64) launch_attn_decode<64>(a, G, grid, s);
   else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");

@@ -307,6 +307,9 @@ void Engine::setup_batch_mfma() {
   }
   bg_ = att;
   bg_ffn_ = att && ffn;
+  const char* bt = std::getenv("LFK_BATT_TOUCH");
+  batt_touch_ = bt ? std::atoi(bt) : 0;
+  if (nkv_l_ >= 63) batt_touch_ = 0;
   const char* nf = std::getenv("LFK_BMM_NORM");
   norm_fold_ = !(nf && nf[0] == '0');
   const char* hf = std::getenv("LFK_BMM_HEAD1");
@@ -826,6 +829,19 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.q_stride = nq_; aa.out_stride = nq_;
   aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
   aa.out_h = xh_b_; aa.out_h_stride = nq_;   // the Wo input, already in bmm's f16 layout
+  // weight touch (LFK_BATT_TOUCH bit mask: 1 this layer's Wo, 2 the next layer's Q|K|V - tile16
+  // copies): the latency-bound attention pulls them into the memory-side cache
+  if (batt_touch_ & 1) {
+    aa.pf[0] = L.t_wo.base; aa.pf_bytes[0] = t16_bytes(L.t_wo.type, L.t_wo.rows, L.t_wo.K);
+  }
+  if ((batt_touch_ & 2) && l + 1 < hp_.n_layer) {
+    const Layer& N = layers_[l + 1];
+    const QMat* nm[3] = {&N.t_wq, &N.t_wk, &N.t_wv};
+    for (int k = 0; k < 3; ++k) {
+      aa.pf[1 + k] = nm[k]->base; aa.pf_bytes[1 + k] = t16_bytes(nm[k]->type, nm[k]->rows, nm[k]->K);
+    }
+  }
+  if (batt_touch_ & 3) aa.pf_sink = attn_cnt_b_ + 63;   // row 0's word 63: kv heads < 63
   attn_decode(aa, s);
   bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
   if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {

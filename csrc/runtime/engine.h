@@ -273,6 +273,7 @@ class Engine : public SlotBackend {
   // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
   // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)
   bool norm_fold_ = true, head_fold_ = false;
+  int batt_touch_ = 0;        // batched attention weight touch (LFK_BATT_TOUCH bit mask)
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   hipGraph_t graph_ = nullptr;
