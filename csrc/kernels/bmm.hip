@@ -284,8 +284,8 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
-  float* rowss = reinterpret_cast<float*>(smem + (NW - 1) * 64 * 16);  // [8 rows][8 waves] folded norm
-  __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16 + 256);
+  float* rowss = reinterpret_cast<float*>(smem + (NW - 1) * 64 * 16);  // [8 rows][NW waves] folded norm
+  __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16 + 512);
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
@@ -338,33 +338,34 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     }
   }
   // stage x[b][k0, k0 + kn) for the B rows
-  if (NW == 8 && a.xf) {  // (8-wave kernels only: keeps the split-K kernels' registers)
+  if (NW >= 8 && a.xf) {  // (8/16-wave kernels only: keeps the split-K kernels' registers)
     // folded RMSNorm (K = 4096, B <= 8: each thread holds 2 float4 of every row): every load
     // is issued first - one memory round trip, like the f16 staging - then f16(x * w) goes to
     // LDS in bprep's 4-group order and each wave leaves its per-row partial sum of squares
     // (rows past B load row B - 1 and are dropped: straight-line code, no predicated loads)
-    float4 xv[16];
-    const float4 w0 = *reinterpret_cast<const float4*>(a.norm_w + 4 * tid);
-    const float4 w1 = *reinterpret_cast<const float4*>(a.norm_w + 4 * (tid + kBlock));
+    constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
+    float4 xv[8 * J], w[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) w[j] = *reinterpret_cast<const float4*>(a.norm_w + 4 * (tid + j * kBlock));
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
-      xv[2 * b] = *reinterpret_cast<const float4*>(xr + 4 * tid);
-      xv[2 * b + 1] = *reinterpret_cast<const float4*>(xr + 4 * (tid + kBlock));
+#pragma unroll
+      for (int j = 0; j < J; ++j) xv[J * b + j] = *reinterpret_cast<const float4*>(xr + 4 * (tid + j * kBlock));
     }
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float4 x = xv[2 * b + j], w = j ? w1 : w0;
+      for (int j = 0; j < J; ++j) {
+        const float4 x = xv[J * b + j], ww = w[j];
         ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-        const h2_t p0 = {(_Float16)(x.x * w.x), (_Float16)(x.z * w.z)};
-        const h2_t p1 = {(_Float16)(x.y * w.y), (_Float16)(x.w * w.w)};
+        const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
+        const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
         if (b < a.B) *reinterpret_cast<uint2*>(xs + b * ldx + 4 * (tid + j * kBlock)) = make_uint2(as_u(p0), as_u(p1));
       }
       ss = wave_sum_fast(ss);
-      if (lane == 0) rowss[b * 8 + wave] = ss;
+      if (lane == 0) rowss[b * NW + wave] = ss;
     }
   } else {
     for (int i = tid; i < a.B * (kn >> 3); i += kBlock) {
@@ -377,10 +378,10 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   const bool col_ok = r16 < a.B;
   // folded norm: this lane's column scale (applied to the reduced tile before any epilogue)
   float cs = 1.f;
-  if (NW == 8 && a.xf) {
+  if (NW >= 8 && a.xf) {
     float t = 0.f;
 #pragma unroll
-    for (int w = 0; w < 8; ++w) t += rowss[(col_ok ? r16 : 0) * 8 + w];
+    for (int w = 0; w < NW; ++w) t += rowss[(col_ok ? r16 : 0) * NW + w];
     cs = rsqrtf(t / (float)kn + a.eps);
   }
   const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
-      if (NW == 8 && a.xf) acc *= cs;
+      if (NW >= 8 && a.xf) acc *= cs;
       if (sw) {
         // tiles 4u, 4u+1: gate rows; 4u+2, 4u+3: the up rows of the same features
         const int qt = gt & 3;
@@ -606,7 +607,7 @@ void bprep(const BPrepArgs& a, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- launch
-static size_t bmm_lds(int B, int spp, int nw) { return (size_t)(nw - 1) * 64 * 16 + 256 + (size_t)B * (spp * 256 + 8) * 2; }
+static size_t bmm_lds(int B, int spp, int nw) { return (size_t)(nw - 1) * 64 * 16 + 512 + (size_t)B * (spp * 256 + 8) * 2; }
 
 // one-part shapes run 8-wave blocks; two of them must fit a CU's 160 KB of LDS
 bool bmm_qkv_fits(int K, int B) { return K % 256 == 0 && B >= 1 && bmm_lds(B, K / 256, 8) <= 80 * 1024; }
@@ -648,14 +649,24 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   const int steps = a.w.K / 256;
   if (a.qkv_epi || a.swiglu_epi || a.xf) {
     // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
-    static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4 or 8
-    const int nw1 = a.xf ? 8 : nw1_env;                          // the folded norm is 8-wave only
+    static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4, 8 or 16
+    // the folded norm needs 8 or 16 waves; 16-wave blocks only for Q4_K (the other types need
+    // more than 128 VGPRs, and a 1024-thread block must hold 4 waves per SIMD)
+    int nw1 = a.xf ? std::max(8, nw1_env) : nw1_env;
+    if (nw1 == 16 && QT != T_Q4_K) nw1 = 8;
     a.spp = steps;
     a.kparts = 1;
     const size_t lds = bmm_lds(a.B, steps, nw1);
     const int units = a.swiglu_epi ? tiles / 4 : tiles;
-    const int per_cu = (int)std::max<size_t>(1, (160 * 1024) / lds);
+    // blocks per CU: LDS and the 16 waves a CU holds at this kernel's register count
+    const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 16 / nw1));
     const int nb = std::max(1, std::min(units, per_cu * bmm_cus()));
+    if constexpr (QT == T_Q4_K) {
+      if (nw1 == 16) {
+        hipLaunchKernelGGL((bmm_kernel<QT, 16, 1>), dim3(nb), dim3(1024), lds, s, a);
+        return;
+      }
+    }
     if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(nb), dim3(256), lds, s, a);
     else if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 8, 2>), dim3(nb), dim3(512), lds, s, a);
     else hipLaunchKernelGGL((bmm_kernel<QT, 8, 1>), dim3(nb), dim3(512), lds, s, a);
