@@ -647,7 +647,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
   for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
   const int steps = a.w.K / 256;
-  if (a.qkv_epi || a.swiglu_epi || a.xf) {
+  if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
     // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
     static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4, 8 or 16
     // the folded norm needs 8 or 16 waves; 16-wave blocks only for Q4_K (the other types need
@@ -705,7 +705,9 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
     throw std::runtime_error("bmm: swiglu epilogue");
   if (a.xf && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))
     throw std::runtime_error("bmm: folded norm");
-  if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi) throw std::runtime_error("bmm: store_out needs one K part");
+  if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi && !a.one_part)
+    throw std::runtime_error("bmm: store_out needs one K part");
+  if (a.one_part && !bmm_qkv_fits(a.w.K, a.B)) throw std::runtime_error("bmm: one_part x slice exceeds LDS");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

@@ -114,6 +114,7 @@ struct BmmArgs {
   float eps = 1e-5f;
   bool store_out = false;          // plain epilogue: out = result (default: out += result)
   bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
+  bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
 };
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)

@@ -307,6 +307,8 @@ void Engine::setup_batch_mfma() {
   }
   bg_ = att;
   bg_ffn_ = att && ffn;
+  const char* wo1 = std::getenv("LFK_BMM_WO1");
+  wo_one_part_ = wo1 && wo1[0] == '1';
   const char* bt = std::getenv("LFK_BATT_TOUCH");
   batt_touch_ = bt ? std::atoi(bt) : 0;
   if (nkv_l_ >= 63) batt_touch_ = 0;
@@ -843,7 +845,13 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   }
   if (batt_touch_ & 3) aa.pf_sink = attn_cnt_b_ + 63;   // row 0's word 63: kv heads < 63
   attn_decode(aa, s);
-  bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
+  if (wo_one_part_ && B <= kBmmMaxRows && bmm_qkv_fits(nq_, B)) {
+    BmmArgs a;
+    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = x_; a.ldo = d; a.n_out = d; a.B = B; a.one_part = true;
+    bmm(a, s);
+  } else {
+    bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
+  }
   if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)

@@ -274,6 +274,7 @@ class Engine : public SlotBackend {
   // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)
   bool norm_fold_ = true, head_fold_ = false;
   int batt_touch_ = 0;        // batched attention weight touch (LFK_BATT_TOUCH bit mask)
+  bool wo_one_part_ = false;  // Wo as one K part (LFK_BMM_WO1=1, A/B)
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   hipGraph_t graph_ = nullptr;
