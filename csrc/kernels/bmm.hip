@@ -37,10 +37,15 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ h2_t as_h2(unsigned v) { return __builtin_bit_cast(h2_t, v); }
 __device__ __forceinline__ unsigned as_u(h2_t v) { return __builtin_bit_cast(unsigned, v); }
 
-// two values (bits 0.. and 16..) -> (value * a + m) as f16 pair: magic 1024 exponent,
-// exact subtraction of `bias`, one fused multiply-add
-__device__ __forceinline__ unsigned deq_pair(unsigned two, h2_t bias, h2_t a, h2_t m) {
-  const h2_t v = as_h2(two | 0x64006400u) - bias;
+// bytes 0 and 2 (or 1 and 3) of x under the f16 exponent of 1024: one v_perm_b32 builds the
+// pair (1024 + b0, 1024 + b2) - the and / shift / or it replaces were 2-3 VALU ops per pair
+// (the compiler did not form v_and_or_b32: CDNA VOP3 takes no literal constant)
+__device__ __forceinline__ unsigned bytes02(unsigned x) { return __builtin_amdgcn_perm(0x64646464u, x, 0x04020400u); }
+__device__ __forceinline__ unsigned bytes13(unsigned x) { return __builtin_amdgcn_perm(0x64646464u, x, 0x04030401u); }
+
+// a (1024 + v0, 1024 + v1) f16 pair -> (v * a + m): exact subtraction of `bias`, one fma
+__device__ __forceinline__ unsigned deq_pair(unsigned magic_pair, h2_t bias, h2_t a, h2_t m) {
+  const h2_t v = as_h2(magic_pair) - bias;
   return as_u(v * a + m);
 }
 
@@ -48,11 +53,38 @@ struct HFrag {
   unsigned w[16];  // MFMA i takes w[4i .. 4i+3]
 };
 
+// bmm's raw weights of one chunk: the WRaw layouts, except Q4_K, whose tile16 copy carries
+// the sub-block scales pre-decoded - per row and sub-block one f16 pair (d * sc, -dmin * m) -
+// instead of the packed 12-byte scales: the 6-bit unpacking was ~40 VALU ops per chunk, about
+// a third of the dequantisation (the kernel ran with its SIMDs ~75 % busy issuing)
+struct Q4Raw {
+  int4 q;
+  uint2 m;  // (d*sc, -dmin*m) as f16 pairs of sub-blocks 2g (low nibbles) and 2g + 1 (high)
+};
+template <int T> struct BRaw { using type = WRaw<T>; };
+template <> struct BRaw<T_Q4_K> { using type = Q4Raw; };
+template <int T> using BRawT = typename BRaw<T>::type;
+
 // chunk c of one row (raw loads in WRaw) -> the four A fragments
 template <int T>
-__device__ __forceinline__ void dequant_frags(const WRaw<T>& w, int c, HFrag& F) {
+__device__ __forceinline__ void dequant_frags(const BRawT<T>& w, int c, HFrag& F) {
   const int j = c & 7;
-  if constexpr (T == T_Q4_K || T == T_Q5_K) {
+  if constexpr (T == T_Q4_K) {
+    const h2_t pa = as_h2(w.m.x), pb = as_h2(w.m.y);
+    const h2_t alo = {pa[0], pa[0]}, mlo = {pa[1], pa[1]};
+    const h2_t ahi = {pb[0], pb[0]}, mhi = {pb[1], pb[1]};
+    const h2_t bias = {(_Float16)1024.f, (_Float16)1024.f};
+    const int qv[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const unsigned lo = (unsigned)qv[i] & 0x0F0F0F0Fu, hi = ((unsigned)qv[i] >> 4) & 0x0F0F0F0Fu;
+      F.w[4 * i + 0] = deq_pair(bytes02(lo), bias, alo, mlo);
+      F.w[4 * i + 1] = deq_pair(bytes13(lo), bias, alo, mlo);
+      F.w[4 * i + 2] = deq_pair(bytes02(hi), bias, ahi, mhi);
+      F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, ahi, mhi);
+    }
+    (void)j;
+  } else if constexpr (T == T_Q5_K) {
     const int g = j >> 1;
     const unsigned dd = (unsigned)w.m.x;
     const float d = h2f(dd & 0xFFFF), dmin = h2f(dd >> 16);
@@ -82,10 +114,10 @@ __device__ __forceinline__ void dequant_frags(const WRaw<T>& w, int c, HFrag& F)
         lo = ((unsigned)qv[i] & 0x0F0F0F0Fu) | (((hv >> (2 * g)) & 0x01010101u) << 4);
         hi = (((unsigned)qv[i] >> 4) & 0x0F0F0F0Fu) | (((hv >> (2 * g + 1)) & 0x01010101u) << 4);
       }
-      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, alo, mlo);
-      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, alo, mlo);
-      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, ahi, mhi);
-      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, ahi, mhi);
+      F.w[4 * i + 0] = deq_pair(bytes02(lo), bias, alo, mlo);
+      F.w[4 * i + 1] = deq_pair(bytes13(lo), bias, alo, mlo);
+      F.w[4 * i + 2] = deq_pair(bytes02(hi), bias, ahi, mhi);
+      F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, ahi, mhi);
     }
   } else if constexpr (T == T_Q6_K) {
     const int o = 16 * (j & 3);
@@ -101,10 +133,10 @@ __device__ __forceinline__ void dequant_frags(const WRaw<T>& w, int c, HFrag& F)
     for (int i = 0; i < 4; ++i) {
       const unsigned lo = ((unsigned)lv[i] & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> s) & 0x03030303u) << 4);
       const unsigned hi = (((unsigned)lv[i] >> 4) & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> (s + 4)) & 0x03030303u) << 4);
-      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, alo, zero);
-      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, alo, zero);
-      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, ahi, zero);
-      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, ahi, zero);
+      F.w[4 * i + 0] = deq_pair(bytes02(lo), bias, alo, zero);
+      F.w[4 * i + 1] = deq_pair(bytes13(lo), bias, alo, zero);
+      F.w[4 * i + 2] = deq_pair(bytes02(hi), bias, ahi, zero);
+      F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, ahi, zero);
     }
   } else {  // Q8_0: signed bytes, flipped to unsigned for the magic, one scale
     const float d = h2f(w.d & 0xFFFF);
@@ -116,10 +148,10 @@ __device__ __forceinline__ void dequant_frags(const WRaw<T>& w, int c, HFrag& F)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const unsigned lo = (unsigned)lo4[i] ^ 0x80808080u, hi = (unsigned)hi4[i] ^ 0x80808080u;
-      F.w[4 * i + 0] = deq_pair(lo & 0x00FF00FFu, bias, a, zero);
-      F.w[4 * i + 1] = deq_pair((lo >> 8) & 0x00FF00FFu, bias, a, zero);
-      F.w[4 * i + 2] = deq_pair(hi & 0x00FF00FFu, bias, a, zero);
-      F.w[4 * i + 3] = deq_pair((hi >> 8) & 0x00FF00FFu, bias, a, zero);
+      F.w[4 * i + 0] = deq_pair(bytes02(lo), bias, a, zero);
+      F.w[4 * i + 1] = deq_pair(bytes13(lo), bias, a, zero);
+      F.w[4 * i + 2] = deq_pair(bytes02(hi), bias, a, zero);
+      F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, a, zero);
     }
   }
 }
@@ -147,13 +179,13 @@ __device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
 // load instructions reads 1 KB contiguous (planar rows would give every instruction 16
 // scattered 64-B pieces - measured 1-2 TB/s). Lane l = 16 kq + r16 takes chunks 8s + kq
 // (h = 0) and 8s + 4 + kq (h = 1) of row 16t + r16:
-//   Q4_K: qs[h][l][16] | meta[r16][16]                                          2304 B
+//   Q4_K: qs[h][l][16] | sb[r16][8][(d*sc, -dmin*m) f16]                         2560 B
 //   Q5_K: qs[h][l][16] | qh[r16][32] | meta[r16][16]                            2816 B
 //   Q6_K: ql[h][l][16] | qh[h][r16][32] | scales[r16][16] | d[r16][2]           3360 B
 //   Q8_0: qs[h][a|b][l][16] | d[h][l][2]                                        4352 B
 // Rows past the matrix are zero.
 __host__ __device__ constexpr int t16_step_bytes(int t) {
-  return t == T_Q4_K ? 2304 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3360 : t == T_Q8_0 ? 4352 : 0;
+  return t == T_Q4_K ? 2560 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3360 : t == T_Q8_0 ? 4352 : 0;
 }
 
 size_t t16_bytes(int type, int rows, int K) {
@@ -188,7 +220,29 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
   }
   if (kq != 0) return;
   if constexpr (T == T_Q4_K) {
-    copy16(blk + 2048 + r16 * 16, base + P.p1 + r * P.s1 + 16 * s, ok);
+    // decode the 8 sub-block scale / min pairs once, here (as the old in-kernel decode did:
+    // f32 products, one rounding to f16)
+    const uint8_t* m = base + P.p1 + r * P.s1 + 16 * s;
+    const float d = ok ? h2f(*reinterpret_cast<const unsigned short*>(m)) : 0.f;
+    const float dmin = ok ? h2f(*reinterpret_cast<const unsigned short*>(m + 2)) : 0.f;
+    const uint8_t* q = m + 4;
+    unsigned outw[8];
+#pragma unroll
+    for (int sb = 0; sb < 8; ++sb) {
+      unsigned sc, mn;
+      if (sb < 4) {
+        sc = q[sb] & 63;
+        mn = q[sb + 4] & 63;
+      } else {
+        sc = (q[sb + 4] & 0xF) | ((q[sb - 4] >> 6) << 4);
+        mn = (q[sb + 4] >> 4) | ((q[sb] >> 6) << 4);
+      }
+      const h2_t p = {(_Float16)(d * (float)sc), (_Float16)(-dmin * (float)mn)};
+      outw[sb] = ok ? as_u(p) : 0u;
+    }
+    uint4* dst16 = reinterpret_cast<uint4*>(blk + 2048 + r16 * 32);
+    dst16[0] = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+    dst16[1] = make_uint4(outw[4], outw[5], outw[6], outw[7]);
   } else if constexpr (T == T_Q5_K) {
     copy16(blk + 2048 + r16 * 32, base + P.p1 + r * P.s1 + 32 * s, ok);
     copy16(blk + 2048 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 32 * s + 16, ok);
@@ -218,10 +272,11 @@ void t16_repack(const QMat& w, uint8_t* dst, hipStream_t st) {
 
 // raw loads of lane l's chunk h (8s + 4h + kq) from a tile16 step block
 template <int T>
-__device__ __forceinline__ void tload(WRaw<T>& w, const uint8_t* blk, int h, int l, int r16, int kq) {
+__device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, int l, int r16, int kq) {
   if constexpr (T == T_Q4_K) {
     w.q = ld_nt16(blk + h * 1024 + l * 16);
-    w.m = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 16);
+    // chunk 4h + kq covers sub-blocks 2g, 2g + 1 with g = 2h + kq / 2
+    w.m = *reinterpret_cast<const uint2*>(blk + 2048 + r16 * 32 + 8 * (2 * h + (kq >> 1)));
   } else if constexpr (T == T_Q5_K) {
     w.q = ld_nt16(blk + h * 1024 + l * 16);
     w.h = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 32 + 16 * (kq & 1));
@@ -241,7 +296,7 @@ __device__ __forceinline__ void tload(WRaw<T>& w, const uint8_t* blk, int h, int
 }
 
 template <int T>
-__device__ __forceinline__ int raw_word(const WRaw<T>& w) {
+__device__ __forceinline__ int raw_word(const BRawT<T>& w) {
   if constexpr (T == T_Q4_K || T == T_Q5_K) return w.q.x;
   else if constexpr (T == T_Q6_K) return w.l.x;
   else return w.a.x;
@@ -326,7 +381,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     return j < n_ws ? tb + (size_t)(ws0 + j * NW) * SB
          : j < 2 * n_ws ? tbn + (size_t)(ws0 + (j - n_ws) * NW) * SB : tbn2 + (size_t)ws0 * SB;
   };
-  WRaw<QT> wa[2], wb[2], wc[2];
+  BRawT<QT> wa[2], wb[2], wc[2];
   if (has) {
     const uint8_t* p0 = addr(0);
     tload<QT>(wa[0], p0, 0, lane, r16, kq);
@@ -393,7 +448,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   // gate/up kernel's wave cycles)
   f4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
   int i = 0;  // step of the current tile
-  auto compute = [&](const WRaw<QT>* wc, int i) {
+  auto compute = [&](const BRawT<QT>* wc, int i) {
     // one step per scheduling region: interleaving two steps' dequantisation raised the
     // register count from ~110 to 150-180 (2-3 waves per SIMD)
     __builtin_amdgcn_sched_barrier(0);
@@ -509,7 +564,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     return true;
   };
   // one step: load step i + PD into `ld`, compute step i from `cur`
-  auto step = [&](WRaw<QT>* ld, const WRaw<QT>* cur) {
+  auto step = [&](BRawT<QT>* ld, const BRawT<QT>* cur) {
     const uint8_t* p = addr(i + PD);
     tload<QT>(ld[0], p, 0, lane, r16, kq);
     tload<QT>(ld[1], p, 1, lane, r16, kq);
