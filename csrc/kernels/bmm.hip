@@ -1,28 +1,31 @@
 // Batched decode projection on MFMA (continuous batching, 1-16 activation rows):
-//   out[b][row] += sum_k W[row][k] * xh[b][k]
-// W block-quantised (Q4_K / Q5_K / Q6_K / Q8_0, planar layout), xh f16 rows prepared once
-// per projection input by bprep (RMSNorm / SwiGLU / residual-free copy, f16, 4-group
-// swizzle - see below).
+//   out[b][row] += sum_k W[row][k] * x[b][k]
+// W block-quantised (Q4_K / Q5_K / Q6_K / Q8_0) read from a tile-ordered copy (tile16, below);
+// x f16 rows in a 4-group swizzled k order, staged per block in LDS - from xh (written by
+// bprep or by the attention kernel) or, for Q|K|V and gate/up, straight from the fp32
+// residual with the RMSNorm folded in.
 //
 // Why MFMA: with 2-16 rows the integer-dot GEMV (bgemv.hip) does B dot products per decoded
 // weight on the VALU and ran VALU/epilogue-bound (6.2 ms per 8B step at B = 8,
 // profiles/README.md). Here a wave owns a 16-row weight tile and feeds it to
 // v_mfma_f32_16x16x32_f16 as the A operand, the activation rows as B: the matrix core does
 // all 16 columns in the same 16 cycles, so the per-weight work is the dequantisation only
-// (~2 VALU ops per weight, independent of B) and the weights stay ONE HBM stream.
+// (independent of B) and the weights stay ONE HBM stream. The kernel is bound by instruction
+// issue (profiles/README.md, r2g/r2i), so the dequantisation is counted per instruction.
 //
 // Dequantisation straight into MFMA fragments: lane l holds A[row l&15][k = 8(l>>4) + j];
-// here lane group kq = l>>4 takes chunk 4s + kq (32 weights) of its row at step s, and
-// MFMA i (0..3) of the step takes dword i of the chunk's 16 quant bytes: low nibbles
-// (4i, 4i+2), (4i+1, 4i+3) and high nibbles the same - two nibbles per v_and_or with the
-// f16 exponent of 1024 OR-ed in (1024 + q exactly), one v_pk_add (-1024, exact) and one
-// v_pk_fma (d*sc, -dmin*m) per pair. The k order inside each 4-group is therefore
-// (0, 2, 1, 3); bprep writes x in that order so B needs no shuffles: the B fragment of
-// MFMA i is 8 bytes at the chunk's low-run offset + 4i and 8 bytes at its high-run offset + 4i.
+// lane group kq = l>>4 takes chunk 8s + 4h + kq (32 weights: a low and a high 16-run) of its
+// row at step s. Quant bytes are masked to one value per byte (low / high nibbles, plus the
+// Q5_K / Q6_K high bits), one v_perm_b32 per pair puts two bytes under the f16 exponent of
+// 1024 (1024 + q exactly), one v_pk_add removes the 1024 (exact) and one v_pk_fma applies
+// (d*sc, -dmin*m) - pre-decoded per sub-block in the Q4_K tile16 copy. A pair holds bytes
+// (0, 2) or (1, 3) of a dword, so the k order inside each 4-group is (0, 2, 1, 3); x is
+// written in that order. MFMA m of a chunk takes 8 weights of ONE run (low run 0-7 / 8-15,
+// then high run 0-7 / 8-15): its B operand is one 16-byte LDS read as it stands.
 //
 // Work items are (16-row tile, K part); partial tiles are added to `out` atomically (split-K
 // keeps >= 2 waves per SIMD busy on every projection shape, including the 256-tile Wo /
-// down); outputs that are not the residual stream are zeroed by the bprep launch before.
+// down); one-part launches own their outputs (epilogues: RoPE + KV append, SwiGLU).
 #include <algorithm>
 #include <stdexcept>
 
@@ -467,13 +470,15 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
       HFrag F;
       dequant_frags<QT>(wc[h], c, F);
-      const unsigned bl[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      const unsigned bh[8] = {x2.x, x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w};
+      const uint4 xr[4] = {x0, x1, x2, x3};
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        // A: lo pairs (4m,4m+2),(4m+1,4m+3) then hi pairs; B: x[lo + 4m .. +3], x[hi + 4m .. +3]
-        const uint4 av = make_uint4(F.w[4 * m], F.w[4 * m + 1], F.w[4 * m + 2], F.w[4 * m + 3]);
-        const uint4 bv = make_uint4(bl[2 * m], bl[2 * m + 1], bh[2 * m], bh[2 * m + 1]);
+        // MFMA m takes 8 weights of ONE run: the low run's 0-7 / 8-15 (m = 0 / 1), then the high
+        // run's (m = 2 / 3) - pairs of quant dwords 2(m % 2), 2(m % 2) + 1 - so its B operand is
+        // the 16-byte LDS read as it stands (taking 4 halves from each run cost 3 v_mov per MFMA)
+        const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
+        const uint4 av = make_uint4(F.w[4 * dw + sh], F.w[4 * dw + sh + 1], F.w[4 * dw + 4 + sh], F.w[4 * dw + 5 + sh]);
+        const uint4 bv = xr[m];
         f4_t& ac = h == 0 ? acc : acc2;
         ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
                                                     __builtin_bit_cast(h8_t, bv), ac, 0, 0, 0);
