@@ -64,8 +64,17 @@ struct Q4Raw {
   int4 q;
   uint2 m;  // (d*sc, -dmin*m) as f16 pairs of sub-blocks 2g (low nibbles) and 2g + 1 (high)
 };
+// Q6_K likewise: the chunk's two scales arrive as one f16 pair (d * sc_lo, d * sc_hi), and its
+// 2-bit high fields as two dwords already in place for the bit assembly (tile16 layout below):
+// 6.5 VALU per quant dword instead of 9, no per-chunk scale conversion, one scale load not three
+struct Q6Raw {
+  int4 l;
+  uint2 x;     // high fields of quant dwords (0, 1) and (2, 3)
+  unsigned s;  // (d * sc_lo, d * sc_hi) f16 pair
+};
 template <int T> struct BRaw { using type = WRaw<T>; };
 template <> struct BRaw<T_Q4_K> { using type = Q4Raw; };
+template <> struct BRaw<T_Q6_K> { using type = Q6Raw; };
 template <int T> using BRawT = typename BRaw<T>::type;
 
 // chunk c of one row (raw loads in WRaw) -> the four A fragments
@@ -123,24 +132,32 @@ __device__ __forceinline__ void dequant_frags(const BRawT<T>& w, int c, HFrag& F
       F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, ahi, mhi);
     }
   } else if constexpr (T == T_Q6_K) {
-    const int o = 16 * (j & 3);
-    const int s = (o >= 32) ? 2 : 0;
-    const float d = h2f(w.d & 0xFFFF);
-    const float slo = d * (float)w.slo, shi = d * (float)w.shi;
-    const h2_t alo = {(_Float16)slo, (_Float16)slo}, ahi = {(_Float16)shi, (_Float16)shi};
+    const h2_t p = as_h2(w.s);
+    const h2_t alo = {p[0], p[0]}, ahi = {p[1], p[1]};
     const h2_t zero = {(_Float16)0.f, (_Float16)0.f};
     const h2_t bias = {(_Float16)1056.f, (_Float16)1056.f};  // 1024 + 32: (q - 32) exactly
-    const int lv[4] = {w.l.x, w.l.y, w.l.z, w.l.w};
-    const int hv[4] = {w.h.x, w.h.y, w.h.z, w.h.w};
+    const unsigned lv[4] = {(unsigned)w.l.x, (unsigned)w.l.y, (unsigned)w.l.z, (unsigned)w.l.w};
+    // per byte of x dword e: bits 5:4 / 7:6 = the low / high 16-run fields of quant dword 2e,
+    // bits 1:0 / 3:2 = those of dword 2e + 1; each lands on bits 5:4 with one shift and a mask
+    const unsigned xv[2] = {w.x.x, w.x.y};
+    unsigned fl[4], fh[4];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      fl[2 * e] = xv[e] & 0x30303030u;
+      fh[2 * e] = (xv[e] >> 2) & 0x30303030u;
+      fl[2 * e + 1] = (xv[e] << 4) & 0x30303030u;
+      fh[2 * e + 1] = (xv[e] << 2) & 0x30303030u;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const unsigned lo = ((unsigned)lv[i] & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> s) & 0x03030303u) << 4);
-      const unsigned hi = (((unsigned)lv[i] >> 4) & 0x0F0F0F0Fu) | ((((unsigned)hv[i] >> (s + 4)) & 0x03030303u) << 4);
+      const unsigned lo = (lv[i] & 0x0F0F0F0Fu) | fl[i];
+      const unsigned hi = ((lv[i] >> 4) & 0x0F0F0F0Fu) | fh[i];
       F.w[4 * i + 0] = deq_pair(bytes02(lo), bias, alo, zero);
       F.w[4 * i + 1] = deq_pair(bytes13(lo), bias, alo, zero);
       F.w[4 * i + 2] = deq_pair(bytes02(hi), bias, ahi, zero);
       F.w[4 * i + 3] = deq_pair(bytes13(hi), bias, ahi, zero);
     }
+    (void)j;
   } else {  // Q8_0: signed bytes, flipped to unsigned for the magic, one scale
     const float d = h2f(w.d & 0xFFFF);
     const h2_t a = {(_Float16)d, (_Float16)d};
@@ -184,11 +201,12 @@ __device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
 // (h = 0) and 8s + 4 + kq (h = 1) of row 16t + r16:
 //   Q4_K: qs[h][l][16] | sb[r16][8][(d*sc, -dmin*m) f16]                         2560 B
 //   Q5_K: qs[h][l][16] | qh[r16][32] | meta[r16][16]                            2816 B
-//   Q6_K: ql[h][l][16] | qh[h][r16][32] | scales[r16][16] | d[r16][2]           3360 B
+//   Q6_K: ql[h][l][16] | qx[h][l][8] | sc[r16][h][kq][(d*sc_lo, d*sc_hi) f16]   3584 B
+//         (qx: the chunk's 2-bit high fields regrouped per lane - see dequant_frags)
 //   Q8_0: qs[h][a|b][l][16] | d[h][l][2]                                        4352 B
 // Rows past the matrix are zero.
 __host__ __device__ constexpr int t16_step_bytes(int t) {
-  return t == T_Q4_K ? 2560 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3360 : t == T_Q8_0 ? 4352 : 0;
+  return t == T_Q4_K ? 2560 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3584 : t == T_Q8_0 ? 4352 : 0;
 }
 
 size_t t16_bytes(int type, int rows, int K) {
@@ -221,7 +239,7 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
       copy16(blk + h * 1024 + l * 16, base + P.p0 + r * P.s0 + 16 * c, ok);
     }
   }
-  if (kq != 0) return;
+  if (T != T_Q6_K && kq != 0) return;  // Q6_K: every lane writes its own chunks' fields
   if constexpr (T == T_Q4_K) {
     // decode the 8 sub-block scale / min pairs once, here (as the old in-kernel decode did:
     // f32 products, one rounding to f16)
@@ -250,15 +268,36 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
     copy16(blk + 2048 + r16 * 32, base + P.p1 + r * P.s1 + 32 * s, ok);
     copy16(blk + 2048 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 32 * s + 16, ok);
     copy16(blk + 2560 + r16 * 16, base + P.p2 + r * P.s2 + 16 * s, ok);
-  } else if constexpr (T == T_Q6_K) {
+  }
+  if constexpr (T == T_Q6_K) {
+    // every lane: its chunks 4h + kq. Chunk j of a 256-block reads ql bytes 16 (j & 3) of half
+    // j >> 2, whose high fields sit in qh[32 (j >> 2) + 16 (kq & 1) + byte] at bit 2 (kq >> 1)
+    // (low 16-run) and 4 + 2 (kq >> 1) (high 16-run); x dword e packs the fields of quant
+    // dwords 2e (bits 5:4 low run, 7:6 high run) and 2e + 1 (bits 1:0, 3:2) of each byte
+    const int sh = 2 * (kq >> 1);
+    const uint8_t* scp = base + P.p2 + r * P.s2 + 16 * s;
+    const float d = ok ? h2f(*reinterpret_cast<const unsigned short*>(base + P.p3 + r * P.s3 + 2 * s)) : 0.f;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      copy16(blk + 2048 + hh * 512 + r16 * 32, base + P.p1 + r * P.s1 + 64 * s + 32 * hh, ok);
-      copy16(blk + 2048 + hh * 512 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 64 * s + 32 * hh + 16, ok);
+    for (int h = 0; h < 2; ++h) {
+      const uint8_t* qh = base + P.p1 + r * P.s1 + 64 * s + 32 * h + 16 * (kq & 1);
+      unsigned xw[2] = {0u, 0u};
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const unsigned q0 = ok ? qh[8 * e + b] : 0u, q1 = ok ? qh[8 * e + 4 + b] : 0u;
+          const unsigned byte = (((q0 >> sh) & 3u) << 4) | (((q0 >> (sh + 4)) & 3u) << 6) |
+                                ((q1 >> sh) & 3u) | (((q1 >> (sh + 4)) & 3u) << 2);
+          xw[e] |= byte << (8 * b);
+        }
+      *reinterpret_cast<uint2*>(blk + 2048 + h * 512 + l * 8) = make_uint2(xw[0], xw[1]);
+      // scales as in the old in-kernel decode: f32 product, one rounding to f16
+      const int si = 8 * h + kq;  // the chunk's low 16-run; the high run uses si + 4
+      const float slo = ok ? d * (float)(signed char)scp[si] : 0.f;
+      const float shi = ok ? d * (float)(signed char)scp[si + 4] : 0.f;
+      const h2_t pr = {(_Float16)slo, (_Float16)shi};
+      *reinterpret_cast<unsigned*>(blk + 3072 + r16 * 32 + (4 * h + kq) * 4) = as_u(pr);
     }
-    copy16(blk + 3072 + r16 * 16, base + P.p2 + r * P.s2 + 16 * s, ok);
-    *reinterpret_cast<unsigned short*>(blk + 3328 + r16 * 2) =
-        ok ? *reinterpret_cast<const unsigned short*>(base + P.p3 + r * P.s3 + 2 * s) : 0;
   }
 }
 
@@ -286,11 +325,8 @@ __device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, in
     w.m = *reinterpret_cast<const int4*>(blk + 2560 + r16 * 16);
   } else if constexpr (T == T_Q6_K) {
     w.l = ld_nt16(blk + h * 1024 + l * 16);
-    w.h = *reinterpret_cast<const int4*>(blk + 2048 + h * 512 + r16 * 32 + 16 * (kq & 1));
-    const int si = 8 * h + kq;  // scale of the chunk's low 16; the high 16 use si + 4
-    w.slo = *reinterpret_cast<const signed char*>(blk + 3072 + r16 * 16 + si);
-    w.shi = *reinterpret_cast<const signed char*>(blk + 3072 + r16 * 16 + si + 4);
-    w.d = *reinterpret_cast<const unsigned short*>(blk + 3328 + r16 * 2);
+    w.x = *reinterpret_cast<const uint2*>(blk + 2048 + h * 512 + l * 8);
+    w.s = *reinterpret_cast<const unsigned*>(blk + 3072 + r16 * 32 + (4 * h + kq) * 4);
   } else {
     w.a = ld_nt16(blk + h * 2048 + l * 16);
     w.b = ld_nt16(blk + h * 2048 + 1024 + l * 16);
