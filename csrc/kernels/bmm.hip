@@ -75,6 +75,12 @@ struct Q6Raw {
 template <int T> struct BRaw { using type = WRaw<T>; };
 template <> struct BRaw<T_Q4_K> { using type = Q4Raw; };
 template <> struct BRaw<T_Q6_K> { using type = Q6Raw; };
+// Q5_K: as Q4_K plus the chunk's high bits
+struct Q5Raw {
+  int4 q, h;
+  uint2 m;
+};
+template <> struct BRaw<T_Q5_K> { using type = Q5Raw; };
 template <int T> using BRawT = typename BRaw<T>::type;
 
 // chunk c of one row (raw loads in WRaw) -> the four A fragments
@@ -98,21 +104,9 @@ __device__ __forceinline__ void dequant_frags(const BRawT<T>& w, int c, HFrag& F
     (void)j;
   } else if constexpr (T == T_Q5_K) {
     const int g = j >> 1;
-    const unsigned dd = (unsigned)w.m.x;
-    const float d = h2f(dd & 0xFFFF), dmin = h2f(dd >> 16);
-    const unsigned y = w.m.y, z = w.m.z, ww = w.m.w;
-    float sc[2], mn[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int s = 2 * g + h, sh = 8 * (s & 3);
-      const unsigned a_sc = (y >> sh) & 63, a_m = (z >> sh) & 63;
-      const unsigned b_sc = ((ww >> sh) & 0xF) | (((y >> (sh + 6)) & 3) << 4);
-      const unsigned b_m = ((ww >> (sh + 4)) & 0xF) | (((z >> (sh + 6)) & 3) << 4);
-      sc[h] = d * (float)(s >= 4 ? b_sc : a_sc);
-      mn[h] = -dmin * (float)(s >= 4 ? b_m : a_m);
-    }
-    const h2_t alo = {(_Float16)sc[0], (_Float16)sc[0]}, ahi = {(_Float16)sc[1], (_Float16)sc[1]};
-    const h2_t mlo = {(_Float16)mn[0], (_Float16)mn[0]}, mhi = {(_Float16)mn[1], (_Float16)mn[1]};
+    const h2_t pa = as_h2(w.m.x), pb = as_h2(w.m.y);  // pre-decoded, as for Q4_K
+    const h2_t alo = {pa[0], pa[0]}, mlo = {pa[1], pa[1]};
+    const h2_t ahi = {pb[0], pb[0]}, mhi = {pb[1], pb[1]};
     const h2_t bias = {(_Float16)1024.f, (_Float16)1024.f};
     const int qv[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
 #pragma unroll
@@ -200,13 +194,13 @@ __device__ __forceinline__ void chunk_runs(int c, int& off_lo, int& off_hi) {
 // scattered 64-B pieces - measured 1-2 TB/s). Lane l = 16 kq + r16 takes chunks 8s + kq
 // (h = 0) and 8s + 4 + kq (h = 1) of row 16t + r16:
 //   Q4_K: qs[h][l][16] | sb[r16][8][(d*sc, -dmin*m) f16]                         2560 B
-//   Q5_K: qs[h][l][16] | qh[r16][32] | meta[r16][16]                            2816 B
+//   Q5_K: qs[h][l][16] | qh[r16][32] | sb[r16][8][(d*sc, -dmin*m) f16]             3072 B
 //   Q6_K: ql[h][l][16] | qx[h][l][8] | sc[r16][h][kq][(d*sc_lo, d*sc_hi) f16]   3584 B
 //         (qx: the chunk's 2-bit high fields regrouped per lane - see dequant_frags)
 //   Q8_0: qs[h][a|b][l][16] | d[h][l][2]                                        4352 B
 // Rows past the matrix are zero.
 __host__ __device__ constexpr int t16_step_bytes(int t) {
-  return t == T_Q4_K ? 2560 : t == T_Q5_K ? 2816 : t == T_Q6_K ? 3584 : t == T_Q8_0 ? 4352 : 0;
+  return t == T_Q4_K ? 2560 : t == T_Q5_K ? 3072 : t == T_Q6_K ? 3584 : t == T_Q8_0 ? 4352 : 0;
 }
 
 size_t t16_bytes(int type, int rows, int K) {
@@ -240,10 +234,10 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
     }
   }
   if (T != T_Q6_K && kq != 0) return;  // Q6_K: every lane writes its own chunks' fields
-  if constexpr (T == T_Q4_K) {
+  if constexpr (T == T_Q4_K || T == T_Q5_K) {
     // decode the 8 sub-block scale / min pairs once, here (as the old in-kernel decode did:
-    // f32 products, one rounding to f16)
-    const uint8_t* m = base + P.p1 + r * P.s1 + 16 * s;
+    // f32 products, one rounding to f16); Q5_K's metadata plane is p2, Q4_K's p1
+    const uint8_t* m = T == T_Q4_K ? base + P.p1 + r * P.s1 + 16 * s : base + P.p2 + r * P.s2 + 16 * s;
     const float d = ok ? h2f(*reinterpret_cast<const unsigned short*>(m)) : 0.f;
     const float dmin = ok ? h2f(*reinterpret_cast<const unsigned short*>(m + 2)) : 0.f;
     const uint8_t* q = m + 4;
@@ -261,13 +255,13 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
       const h2_t p = {(_Float16)(d * (float)sc), (_Float16)(-dmin * (float)mn)};
       outw[sb] = ok ? as_u(p) : 0u;
     }
-    uint4* dst16 = reinterpret_cast<uint4*>(blk + 2048 + r16 * 32);
+    uint4* dst16 = reinterpret_cast<uint4*>(blk + (T == T_Q4_K ? 2048 : 2560) + r16 * 32);
     dst16[0] = make_uint4(outw[0], outw[1], outw[2], outw[3]);
     dst16[1] = make_uint4(outw[4], outw[5], outw[6], outw[7]);
-  } else if constexpr (T == T_Q5_K) {
+  }
+  if constexpr (T == T_Q5_K) {
     copy16(blk + 2048 + r16 * 32, base + P.p1 + r * P.s1 + 32 * s, ok);
     copy16(blk + 2048 + r16 * 32 + 16, base + P.p1 + r * P.s1 + 32 * s + 16, ok);
-    copy16(blk + 2560 + r16 * 16, base + P.p2 + r * P.s2 + 16 * s, ok);
   }
   if constexpr (T == T_Q6_K) {
     // every lane: its chunks 4h + kq. Chunk j of a 256-block reads ql bytes 16 (j & 3) of half
@@ -322,7 +316,7 @@ __device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, in
   } else if constexpr (T == T_Q5_K) {
     w.q = ld_nt16(blk + h * 1024 + l * 16);
     w.h = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 32 + 16 * (kq & 1));
-    w.m = *reinterpret_cast<const int4*>(blk + 2560 + r16 * 16);
+    w.m = *reinterpret_cast<const uint2*>(blk + 2560 + r16 * 32 + 8 * (2 * h + (kq >> 1)));
   } else if constexpr (T == T_Q6_K) {
     w.l = ld_nt16(blk + h * 1024 + l * 16);
     w.x = *reinterpret_cast<const uint2*>(blk + 2048 + h * 512 + l * 8);
