@@ -43,6 +43,12 @@ class CpuBackend:
             from ..parallel.comm import check_tensor_split, tp_group_info
             rank, size = tp_group_info(tensor_split)
             ts = check_tensor_split(tensor_split, size) if size > 1 else []
+        if size > 1 and threads == 0:
+            # TP ranks on one host share its cores: an OpenMP team per rank as wide as the
+            # machine oversubscribes it, and the per-layer all-reduces then wait on
+            # descheduled threads (a 2-rank tiny-model request ran past the 25 s timeout)
+            local = int(os.environ.get("LOCAL_WORLD_SIZE", size) or size)
+            threads = max(1, len(os.sched_getaffinity(0)) // max(1, local))
         self.engine = cpu.CpuEngine(model_path, n_ctx=n_ctx, n_threads=threads, n_batch=min(n_batch, 128),
                                     tp_rank=rank, tp_size=size, tensor_split=ts)
         if size > 1:
