@@ -15,7 +15,6 @@
 
 #include "bind_scheduler.h"
 #include "kernels/kernels.h"
-#include "kernels/pdecode.h"
 #include "runtime/engine.h"
 #include "runtime/repack.h"
 
@@ -168,20 +167,6 @@ PYBIND11_MODULE(_hip, m) {
            })
       .def_property_readonly("device_bytes", &Engine::device_bytes)
       .def_property_readonly("healthy", &Engine::healthy)
-      .def_property_readonly("ffn_fused", &Engine::ffn_fused)
-      .def_property_readonly("pdecode", &Engine::pdecode_status)
-      .def("pdecode_acct", [](Engine& e) {
-        std::vector<long long> v = e.pdecode_acct();
-        return py::array_t<long long>(v.size(), v.data());
-      })
-      .def("pdecode_timeline", [](Engine& e) {
-        std::vector<long long> v = e.pdecode_timeline();
-        return py::array_t<long long>(v.size(), v.data());
-      })
-      .def("pdecode_dump", [](Engine& e) {
-        std::vector<float> v = e.pdecode_dump();
-        return py::array_t<float>(v.size(), v.data());
-      })
       .def("p2p_handle", [](Engine& e) { return py::bytes(e.p2p_handle()); })
       .def("p2p_open", [](Engine& e, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
@@ -205,10 +190,6 @@ PYBIND11_MODULE(_hip, m) {
 
   bind_scheduler<Engine>(m);
 
-  m.def("pd_item_bench", [](int type, int rows, int K, int iters, int blocks, uintptr_t out, uintptr_t stream) {
-    pd_item_bench(type, rows, K, iters, blocks, reinterpret_cast<long long*>(out), S(stream));
-    hip_ok("pd_item_bench");
-  });
   m.def("nccl_unique_id", []() {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
@@ -297,22 +278,6 @@ PYBIND11_MODULE(_hip, m) {
       })
       .def("error", &P2PComm::error)
       .def("reset_error", &P2PComm::reset_error);
-
-  m.def("ffn_fused", [](uintptr_t wgu, int tgu, uintptr_t wdn, int tdn, int d, int F, uintptr_t x, uintptr_t norm,
-                        float eps, uintptr_t h, uintptr_t ctr, uintptr_t ctr_clear, uintptr_t err, uintptr_t stream,
-                        uintptr_t dbg_clk) {
-    FfnFusedArgs a;
-    a.w_gu = make_qmat(P<void>(wgu), tgu, 2 * F, d);
-    a.w_down = make_qmat(P<void>(wdn), tdn, d, F);
-    a.x = P<float>(x); a.norm_w = P<float>(norm); a.eps = eps; a.h = P<float>(h); a.F = F;
-    a.counters = P<int>(ctr); a.counters_clear = P<int>(ctr_clear); a.err = P<int>(err);
-    a.dbg_clk = P<long long>(dbg_clk);
-    if (!ffn_fused_supported(a)) throw std::runtime_error("ffn_fused: unsupported shape/types");
-    ffn_fused(a, S(stream));
-    hip_ok("ffn_fused");
-  }, py::arg("wgu"), py::arg("tgu"), py::arg("wdn"), py::arg("tdn"), py::arg("d"), py::arg("F"), py::arg("x"),
-     py::arg("norm"), py::arg("eps"), py::arg("h"), py::arg("ctr"), py::arg("ctr_clear"), py::arg("err"),
-     py::arg("stream"), py::arg("dbg_clk") = 0);
 
   m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,
                        uintptr_t x, uintptr_t norm, float eps, uintptr_t q_out, uintptr_t kc, uintptr_t vc, int n_ctx,

@@ -1,5 +1,5 @@
-// Device building blocks shared by the decode GEMV kernels (gemv.hip) and the
-// fused FFN kernel (ffn_fused.hip): the x prologue (RMSNorm + q8 into LDS), the
+// Device building blocks shared by the decode GEMV kernels (gemv.hip, moe.hip,
+// bmm.hip): the x prologue (RMSNorm + q8 into LDS), the
 // per-wave weight stream, the cross-lane row reduction and item -> row mapping.
 #pragma once
 #include "kernels.h"

@@ -155,24 +155,6 @@ struct QkvArgs {
 };
 void gemv_qkv(const QkvArgs& a, hipStream_t s);
 
-// Fused dense FFN (decode): x += W_down * (silu(W_gate n) * (W_up n)), n = RMSNorm(x) * norm_w.
-// One launch, one workgroup per CU; see ffn_fused.hip for the in-launch hand-off.
-struct FfnFusedArgs {
-  QMat w_gu;                       // [2F][d], gate/up interleaved in 32-row groups
-  QMat w_down;                     // [d][F]
-  float* x = nullptr;              // [d] residual: input, and output (accumulated)
-  const float* norm_w = nullptr;
-  float eps = 1e-5f;
-  float* h = nullptr;              // [F] scratch (SwiGLU output)
-  int F = 0;
-  int* counters = nullptr;         // this layer's 32 hand-off words (zero on entry)
-  int* counters_clear = nullptr;   // 32 words the launch zeroes (the previous layer's), or null
-  int* err = nullptr;              // set non-zero if a bounded wait timed out
-  long long* dbg_clk = nullptr;    // microbenchmarks only: per-workgroup wall-clock stamps [grid][8]
-};
-bool ffn_fused_supported(const FfnFusedArgs& a);  // shape/type/residency check (host)
-void ffn_fused(const FfnFusedArgs& a, hipStream_t s);
-
 // MoE down projection: out[r] += sum_s w[s] * dot(W_{ids[s]}[r], h_s)
 struct MoeDownArgs {
   QMat w;

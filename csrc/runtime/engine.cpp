@@ -104,9 +104,7 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   load(f);
   alloc_buffers();
   build_rope();
-  setup_ffn_fused();
   setup_batch_mfma();
-  pdec_status_ = setup_pdecode();
   HIPCHK(hipStreamSynchronize(stream_));
 }
 
@@ -283,8 +281,6 @@ void Engine::alloc_buffers() {
     HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
   }
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
-  ffn_cnt_ = (int*)dalloc(sizeof(int) * 32 * std::max(1, hp_.n_layer));
-  HIPCHK(hipMemset(ffn_cnt_, 0, sizeof(int) * 32 * std::max(1, hp_.n_layer)));
   dev_err_ = (int*)dalloc(sizeof(int) * 4);
   HIPCHK(hipMemset(dev_err_, 0, sizeof(int) * 4));
   HIPCHK(hipHostMalloc((void**)&h_ring_, sizeof(int) * 64, hipHostMallocDefault));
@@ -334,20 +330,6 @@ void Engine::setup_batch_mfma() {
     if (bg_ffn_) { L.t_gu = tile(L.w_gu); L.t_down = tile(L.w_down); }
   }
   HIPCHK(hipStreamSynchronize(stream_));
-}
-
-// The fused decode FFN needs: one rank (the TP path all-reduces the down
-// projection), a dense FFN, >= 2 GPU layers (each launch zeroes the previous
-// layer's counters), and every layer's gate/up + down type pair supported.
-void Engine::setup_ffn_fused() {
-  ffn_fused_ = false;
-  if (opt_.tp_size > 1 || hp_.n_expert > 0 || hp_.n_layer - opt_.layer_begin < 2) return;
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
-    FfnFusedArgs f;
-    f.w_gu = layers_[l].w_gu; f.w_down = layers_[l].w_down; f.F = F_l_;
-    if (!ffn_fused_supported(f)) return;
-  }
-  ffn_fused_ = true;
 }
 
 void Engine::check_device_err() {
@@ -495,16 +477,6 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
       allreduce_into(tmp_, x_, d, s);
     }
   } else {
-    if (ffn_fused_) {
-      FfnFusedArgs f;
-      f.w_gu = L.w_gu; f.w_down = L.w_down; f.x = x_; f.norm_w = L.ffn_norm; f.eps = hp_.rms_eps;
-      f.h = hf_; f.F = F_l_;
-      f.counters = ffn_cnt_ + 32 * l;
-      f.counters_clear = ffn_cnt_ + 32 * (l == opt_.layer_begin ? hp_.n_layer - 1 : l - 1);
-      f.err = dev_err_;
-      ::lfk::ffn_fused(f, s);
-      return;
-    }
     GemvArgs g;
     g.w = L.w_gu; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
     g.out = hf_; g.n_out = F_l_;
@@ -546,11 +518,7 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int
 
 void Engine::enqueue_decode(hipStream_t s) {
   embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
-  if (pdec_) {
-    pdecode(pda_, pda_dev_, s);  // every layer in one launch
-  } else {
-    for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
-  }
+  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
   enqueue_head(x_, 1, s);
 }
 

@@ -19,7 +19,6 @@
 #include <vector>
 
 #include "../kernels/kernels.h"
-#include "../kernels/pdecode.h"
 #include "gguf.h"
 #include "p2p.h"
 #include "slots.h"
@@ -100,14 +99,6 @@ class Engine : public SlotBackend {
   void p2p_open(const std::vector<std::string>& handles);
   bool p2p_ready() const { return p2p_ && p2p_->ready(); }
   bool healthy() const { return healthy_; }
-  bool ffn_fused() const { return ffn_fused_; }
-  // persistent decode step (kernels/pdecode.h): "on", or why it is off
-  const std::string& pdecode_status() const { return pdec_status_; }
-  // LFK_PDECODE_DUMP=1: every layer's intermediates of the last persistent decode step
-  std::vector<float> pdecode_dump();
-  // LFK_PDECODE_TIMELINE=1: wall-clock stamps [CU][layer][kPdStamps] of the last step
-  std::vector<long long> pdecode_timeline();
-  std::vector<long long> pdecode_acct();  // LFK_PDECODE_ACCT=1: cycle totals [CU][16]
   std::string last_error() const { return last_error_; }
   int n_ctx() const override { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
@@ -171,8 +162,6 @@ class Engine : public SlotBackend {
   void launch_step();
   void check(hipError_t e, const char* what);
   void check_device_err();
-  void setup_ffn_fused();
-  std::string setup_pdecode();  // returns the status string
 
   HParams hp_;
   EngineOptions opt_;
@@ -232,14 +221,7 @@ class Engine : public SlotBackend {
   __hip_bfloat16* moe_xg_ = nullptr; __hip_bfloat16* moe_hg_ = nullptr; float* moe_yg_ = nullptr;
   int* moe_ids_ = nullptr;
   float* moe_w_ = nullptr;
-  int* ffn_cnt_ = nullptr;    // [n_layer][32] fused-FFN hand-off counters (zero between launches)
   int* dev_err_ = nullptr;    // device error word (bounded in-kernel waits that timed out)
-  bool ffn_fused_ = false;    // dense decode FFN as one fused launch (ffn_fused.hip)
-  bool pdec_ = false;         // decode layers as ONE persistent launch (pdecode.hip)
-  PDecodeArgs pda_;
-  PDecodeArgs* pda_dev_ = nullptr;
-  std::string pdec_status_;
-  size_t pd_dump_n_ = 0, pd_tl_n_ = 0, pd_acct_n_ = 0;
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 

@@ -30,8 +30,8 @@ EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 HIP_SOURCES = ["kernels/gemv.hip", "kernels/attention.hip", "kernels/sampler.hip", "kernels/gemm.hip",
                "kernels/misc.hip", "kernels/bmm.hip",
-               "kernels/ffn_fused.hip", "kernels/moe.hip", "kernels/p2p_allreduce.hip", "kernels/pdecode.hip"]
-HOST_HIP_SOURCES = ["runtime/engine.cpp", "runtime/engine_pdecode.cpp", "runtime/p2p.cpp", "runtime/scheduler.cpp",
+               "kernels/moe.hip", "kernels/p2p_allreduce.hip"]
+HOST_HIP_SOURCES = ["runtime/engine.cpp", "runtime/p2p.cpp", "runtime/scheduler.cpp",
                     "bindings_hip.cpp"]     # host code against the HIP runtime
 HOST_SOURCES = ["runtime/gguf.cpp", "runtime/repack.cpp"]          # plain C++ (+OpenMP)
 CPU_SOURCES = ["cpu/cpu_backend.cpp", "runtime/gguf.cpp", "runtime/repack.cpp", "runtime/scheduler.cpp",
