@@ -7,21 +7,31 @@ truncation, admission queue, ``create_chat_completion(temperature=1.2,
 top_p=0.9, frequency_penalty=0.7, presence_penalty=0.8)`` with no max_tokens -
 so each request decodes until EOS or the 1024-token context is full.
 
-Parallelism (one process per GPU, launched by torch.distributed.run for N>1):
-  * ``--parallel dp`` (default): every GPU is an independent replica serving its
-    own request stream - the reference's deployment model (4 replicas behind one
-    Service, reference helm/values.yaml:17). Weak scaling; value = sum over ranks.
-  * ``--parallel tp``: one model row-split over all GPUs (RCCL all-reduce over
-    xGMI); every rank serves the same requests. Strong scaling; value = rank 0's.
+GPUs: ``--gpus N`` runs N ranks, one process per GPU. Without ``WORLD_SIZE`` in the
+environment and N > 1, bench.py starts ``torch.distributed.run`` itself (before anything
+touches a GPU) and exits with its status; under a launcher, ``WORLD_SIZE`` must equal N.
+
+Parallelism (``--parallel``, default ``auto`` = ``tp`` for N > 1):
+  * ``tp``: ONE model row-split over the N GPUs (BASELINE configs "8B tensor_split across
+    2 MI355X", "70B across 8"): heads / FFN / vocabulary sharded, two all-reduces per
+    layer (one-shot P2P kernel over xGMI for decode messages, RCCL for prefill), rank 0
+    serves HTTP and drives the continuous batch, ranks 1..N-1 replay its engine commands
+    natively. Strong scaling: value = the job's output tokens/s.
+  * ``dp``: every GPU an independent replica with its own request stream (the reference's
+    deployment model: replicas behind one Service, reference helm/values.yaml:17). Weak
+    scaling; value = sum over ranks.
 
 Load: ``--clients C`` concurrent clients (default 6 = the reference pod's admission
 capacity, 1 in flight + MAX_QUEUE_SIZE 5, reference api.py:19,113) post the K timed
-requests; the engine decodes up to ``--max-batch M`` (default = C) of them as rows of
-one continuous batch (csrc/runtime/scheduler.cpp). ``--clients 1 --max-batch 1`` is
-the reference's serial one-generation-at-a-time serving (recorded in profiles/).
+requests; the engine decodes up to ``--max-batch M`` (default = C) of them as rows of one
+continuous batch. After the timed run, ``--serial-steps`` requests from ONE client (the
+reference's one-generation-at-a-time serving) are timed as well and reported in
+``config.serial`` (rank 0's GPU group, same engine).
 
-Weights are random-init of the exact Llama-3-8B Q4_K_M shapes and type mix
-(a synthetic GGUF written once per node), prompts are synthetic chat requests.
+The bench raises the server timeout to 600 s and the queue to >= C so no request of the
+measurement is rejected (production: 25 s / 5, reference api.py:17-19); both overrides
+are recorded in the JSON. Weights are random-init of the exact Llama-3-8B Q4_K_M shapes
+and type mix (a synthetic GGUF written once per node), prompts are synthetic chat requests.
 """
 from __future__ import annotations
 
@@ -29,7 +39,9 @@ import argparse
 import asyncio
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -38,6 +50,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "output tokens/sec + p50 /response latency, Llama-3-8B Q4_K_M at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # BASELINE.json "published": {} - no reference number exists
+BENCH_TIMEOUT_S = 600.0
 
 
 class CountingEngine:
@@ -49,6 +62,13 @@ class CountingEngine:
         self.completion_tokens = []
         self.prompt_tokens = []
         self.decode_s = []
+
+    @property
+    def batch_width(self):
+        return self.llm.batch_width
+
+    def n_ctx(self):
+        return self.llm.n_ctx()
 
     def create_chat_completion(self, **kw):
         out = self.llm.create_chat_completion(**kw)
@@ -72,86 +92,111 @@ def make_request(i: int) -> dict:
             "user_profile": {"name": "bench"}, "context": ctx}
 
 
-def main():
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """Start n ranks of this script under torch.distributed.run (no GPU touched here)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b-q4_k_m")
-    ap.add_argument("--parallel", choices=["dp", "tp"], default="dp")
+    ap.add_argument("--parallel", choices=["auto", "dp", "tp"], default="auto")
     ap.add_argument("--n-ctx", type=int, default=1024)
     ap.add_argument("--clients", type=int, default=6, help="concurrent clients posting /response")
     ap.add_argument("--max-batch", type=int, default=0, help="continuous-batch rows (0 = --clients)")
+    ap.add_argument("--serial-steps", type=int, default=-1,
+                    help="requests of the one-client serial run after the timed run (-1: max(2, steps // 4))")
     ap.add_argument("--model-dir", default=os.environ.get("SYNTH_MODEL_DIR", os.path.join(
         os.environ.get("TMPDIR", "/tmp"), "llama_amd_models")))
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _launch_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # Rehearsal mode: LFK_BENCH_DEVICE=<d> puts every rank on GPU d (a one-GPU box running
-    # the N-rank DP flow); RCCL refuses two ranks on one device, so the bench's own barrier
-    # and reductions go over gloo then.
+    parallel = args.parallel if args.parallel != "auto" else ("tp" if world > 1 else "dp")
+    # Rehearsal mode: LFK_BENCH_DEVICE=<d> puts every rank on GPU d (a one-GPU box running the
+    # N-rank flow); RCCL refuses two ranks on one device, so TP collectives take the P2P kernel
+    # for every message (comm=ipc) and the bench's own reductions go over gloo.
     rehearse = os.environ.get("LFK_BENCH_DEVICE")
-    if rehearse is not None:
-        local = int(rehearse)
-        os.environ["LOCAL_RANK"] = str(local)
-    torch.cuda.set_device(local)
+    device = int(rehearse) if rehearse is not None else local
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
-        if rehearse is not None:
-            if args.parallel == "tp":
-                raise SystemExit("LFK_BENCH_DEVICE rehearses dp only (TP needs one GPU per rank)")
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    red_dev = "cpu" if rehearse is not None else "cuda"
+        # control plane only (barriers, object broadcasts): the engine runs its own collectives
+        dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(device)
 
-    from llama_fastapi_k8s_gpu_amd.gguf.synthetic import SPECS, write_synthetic_gguf
+    from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
     os.makedirs(args.model_dir, exist_ok=True)
     path = os.path.join(args.model_dir, f"{args.model}-s0.gguf")
     if (rank if rehearse is not None else local) == 0 and not os.path.exists(path):
         t0 = time.time()
         write_synthetic_gguf(args.model, path, seed=0)
         print(f"[bench] wrote synthetic {args.model} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
-    barrier()
+    if world > 1:
+        dist.barrier()
 
     from llama_fastapi_k8s_gpu_amd.config import Settings
     from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
     from llama_fastapi_k8s_gpu_amd.server.app import create_app
 
     t0 = time.time()
-    split = "row" if (args.parallel == "tp" and world > 1) else "none"
+    tp = parallel == "tp" and world > 1
     max_batch = args.max_batch or args.clients
-    if split == "row":
-        max_batch = 1   # continuous batching runs on one rank
-    llm = Llama(path, n_gpu_layers=-1, n_ctx=args.n_ctx, seed=1234 + (0 if split == "row" else rank),
-                split_mode=split, verbose=False, **({"max_batch": max_batch} if max_batch > 1 else {}))
-    print(f"[bench] rank {rank}: loaded in {time.time() - t0:.1f}s ({llm.backend_name})", file=sys.stderr,
-          flush=True)
+    extra = {"max_batch": max_batch} if max_batch > 1 else {}
+    if tp:
+        extra.update(tp_comm="ipc" if rehearse is not None else "auto", device=device)
+    elif rehearse is not None:
+        extra.update(device=device)
+    llm = Llama(path, n_gpu_layers=-1, n_ctx=args.n_ctx, seed=1234 + (0 if tp else rank),
+                split_mode="row" if tp else "none", verbose=False, **extra)
+    print(f"[bench] rank {rank}: loaded in {time.time() - t0:.1f}s ({llm.backend_name}, parallel={parallel})",
+          file=sys.stderr, flush=True)
+    if tp and rank > 0:
+        # follower: replay rank 0's engine commands until it closes the group
+        llm.follow()
+        llm.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return 0
+
     eng = CountingEngine(llm)
     settings = Settings()
-    settings.timeout_seconds = 600.0  # measure latency, do not 408 long generations in the bench
+    settings.timeout_seconds = BENCH_TIMEOUT_S  # measure latency, do not 408 long generations in the bench
     settings.max_batch = max_batch
     settings.max_queue_size = max(settings.max_queue_size, args.clients)
     app = create_app(settings, engine=eng)
+    serial_steps = args.serial_steps if args.serial_steps >= 0 else max(2, args.steps // 4)
 
     import httpx
 
-    latencies = []
+    latencies, serial_lat = [], []
 
     async def run():
         async with app.router.lifespan_context(app):
             transport = httpx.ASGITransport(app=app)
-            async with httpx.AsyncClient(transport=transport, base_url="http://bench", timeout=600) as c:
-                async def drive(ids, lat):
+            async with httpx.AsyncClient(transport=transport, base_url="http://bench", timeout=BENCH_TIMEOUT_S) as c:
+                async def drive(ids, lat, clients):
                     todo = list(ids)
 
                     async def client():
@@ -162,22 +207,35 @@ def main():
                             assert r.status_code == 200, r.text
                             if lat is not None:
                                 lat.append(time.perf_counter() - t)
-                    await asyncio.gather(*[client() for _ in range(max(1, args.clients))])
-                await drive(range(1000, 1000 + args.warmup), None)
-                barrier()
+                    await asyncio.gather(*[client() for _ in range(max(1, clients))])
+                await drive(range(1000, 1000 + args.warmup), None, args.clients)
+                if not tp:
+                    barrier()
+                else:
+                    torch.cuda.synchronize(device)
                 n0 = len(eng.completion_tokens)
                 t_start = time.perf_counter()
-                await drive(range(args.steps), latencies)
-                barrier()
-                return time.perf_counter() - t_start, n0
+                await drive(range(args.steps), latencies, args.clients)
+                # TP: rank 0's last step completed its all-reduces, so every rank is done with it
+                if not tp:
+                    barrier()
+                else:
+                    torch.cuda.synchronize(device)
+                elapsed = time.perf_counter() - t_start
+                n1 = len(eng.completion_tokens)
+                ts = time.perf_counter()
+                if serial_steps > 0:
+                    await drive(range(2000, 2000 + serial_steps), serial_lat, 1)
+                return elapsed, n0, n1, time.perf_counter() - ts
 
-    elapsed, n0 = asyncio.run(run())
-    llm.close()
-    toks = sum(eng.completion_tokens[n0:])
-    ptoks = sum(eng.prompt_tokens[n0:])
-    if world > 1:
-        t = torch.tensor([elapsed, float(toks if (args.parallel == "dp" or rank == 0) else 0)],
-                         dtype=torch.float64, device=red_dev)
+    elapsed, n0, n1, serial_s = asyncio.run(run())
+    llm.close()   # TP: publishes STOP, the followers' follow() returns
+    toks = sum(eng.completion_tokens[n0:n1])
+    ptoks = sum(eng.prompt_tokens[n0:n1])
+    s_toks = sum(eng.completion_tokens[n1:])
+    if world > 1 and not tp:
+        dev = "cpu"
+        t = torch.tensor([elapsed, float(toks)], dtype=torch.float64, device=dev)
         tmax = t[0].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -186,28 +244,39 @@ def main():
         total = float(toks)
     value = total / elapsed
     p50 = statistics.median(latencies) * 1e3
-    dec = sum(eng.decode_s[n0:])
+    dec = sum(eng.decode_s[n0:n1])
     if rank == 0:
         res = {
             "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-            "higher_is_better": True, "scaling": "weak" if args.parallel == "dp" else "strong",
-            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None, "dtype": "q4_k_m weights; f16 (batched MFMA) / int8 (single-row GEMV) / bf16 (prefill MFMA) activations; fp32 accumulate",
+            "higher_is_better": True, "scaling": "strong" if tp else "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "q4_k_m weights; f16 (batched MFMA) / int8 (single-row GEMV) / bf16 (prefill MFMA) "
+                     "activations; fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B Q4_K_M GGUF, synthetic chat requests)",
             "config": {"model": "Llama-3-8B Q4_K_M",
-                       "global_batch": (world if args.parallel == "dp" else 1) * min(args.clients, max_batch),
-                       "seq_len": args.n_ctx, "parallelism": f"{args.parallel}{world}",
-                       "clients_per_gpu": args.clients, "max_batch": max_batch,
+                       "global_batch": (1 if tp else world) * min(args.clients, max_batch),
+                       "seq_len": args.n_ctx, "parallelism": f"{'tp' if tp else 'dp'}{world}",
+                       "clients_per_group": args.clients, "max_batch": max_batch,
                        "p50_response_ms": round(p50, 1),
                        "decode_tokens_per_s_per_request": round(toks / dec, 1) if dec > 0 else None,
                        "avg_prompt_tokens": round(ptoks / max(1, args.steps), 1),
-                       "avg_output_tokens": round(toks / max(1, args.steps), 1)},
+                       "avg_output_tokens": round(toks / max(1, args.steps), 1),
+                       "serial": {"requests": serial_steps, "clients": 1,
+                                  "tokens_per_s": round(s_toks / serial_s, 2) if serial_steps else None,
+                                  "p50_response_ms": round(statistics.median(serial_lat) * 1e3, 1)
+                                  if serial_lat else None,
+                                  "scope": "rank 0's GPU group" if world > 1 else "whole job"},
+                       "bench_overrides": {"timeout_seconds": BENCH_TIMEOUT_S,
+                                           "max_queue_size": settings.max_queue_size,
+                                           "production": {"timeout_seconds": 25.0, "max_queue_size": 5}}},
         }
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

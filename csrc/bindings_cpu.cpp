@@ -7,6 +7,7 @@
 #include "bind_scheduler.h"
 #include "cpu/cpu_backend.h"
 #include "runtime/repack.h"
+#include "runtime/tp_channel.h"
 
 #include <chrono>
 #include <cstring>
@@ -207,4 +208,31 @@ PYBIND11_MODULE(_cpu, m) {
       .def_property_readonly("max_rows", &FakeSlotEngine::max_rows)
       .def("fail_at", &FakeSlotEngine::fail_at);
   bind_scheduler<FakeSlotEngine>(m);
+
+  // the tensor-parallel control channel (runtime/tp_channel.h), for host-side tests of its
+  // ordering / acknowledgement / leader-liveness semantics across processes
+  py::class_<TPChannel>(m, "TPChannel")
+      .def_static("create", [](const std::string& name, int world, size_t cap) {
+        return TPChannel::create(name, world, cap);
+      })
+      .def_static("attach", [](const std::string& name, int rank) { return TPChannel::attach(name, rank); })
+      .def("publish", [](TPChannel& c, py::bytes b) {
+        TPMsg m;
+        const std::string v(b);
+        m.buf.assign(v.begin(), v.end());
+        py::gil_scoped_release nogil;
+        c.publish(m);
+      })
+      .def("receive", [](TPChannel& c, int timeout_ms) -> py::object {
+        TPMsg m;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = c.receive(m, timeout_ms);
+        }
+        if (!ok) return py::none();
+        return py::bytes(reinterpret_cast<const char*>(m.buf.data()), m.buf.size());
+      })
+      .def("leader_alive", &TPChannel::leader_alive)
+      .def_property_readonly("world", &TPChannel::world);
 }

@@ -38,7 +38,7 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
                        int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split,
-                       int n_slots) {
+                       int n_slots, const std::string& comm) {
              EngineOptions o;
              o.layer_begin = layer_begin;
              o.n_slots = n_slots;
@@ -50,13 +50,14 @@ PYBIND11_MODULE(_hip, m) {
              o.tp_size = tp_size;
              o.nccl_id = std::string(nccl_id);
              o.tensor_split = tensor_split;
+             o.comm = comm;
              py::gil_scoped_release nogil;
              return std::make_unique<Engine>(path, o);
            }),
            py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
            py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0,
-           py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1)
+           py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1, py::arg("comm") = "auto")
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
@@ -174,6 +175,17 @@ PYBIND11_MODULE(_hip, m) {
         e.p2p_open(v);
       })
       .def_property_readonly("p2p_ready", &Engine::p2p_ready)
+      .def("tp_ctl_create", &Engine::tp_ctl_create)
+      .def("tp_ctl_attach", &Engine::tp_ctl_attach)
+      .def_property_readonly("tp_ctl_open", &Engine::tp_ctl_open)
+      .def("follow", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.follow();
+      })
+      .def("tp_stop", [](Engine& e) {
+        py::gil_scoped_release nogil;
+        e.tp_stop();
+      })
       .def_property_readonly("last_error", &Engine::last_error)
       .def_property_readonly("n_ctx", &Engine::n_ctx)
       .def_property_readonly("tp_rank", &Engine::tp_rank)
@@ -276,6 +288,10 @@ PYBIND11_MODULE(_hip, m) {
         c.allreduce(P<float>(src), P<float>(dst), n, S(stream));
         hip_ok("p2p_allreduce");
       })
+      .def("allgather", [](P2PComm& c, uintptr_t src, uintptr_t dst, int n, uintptr_t stream) {
+        c.allgather(P<float>(src), P<float>(dst), n, S(stream));
+        hip_ok("p2p_allgather");
+      })
       .def("error", &P2PComm::error)
       .def("reset_error", &P2PComm::reset_error);
 
@@ -362,20 +378,26 @@ PYBIND11_MODULE(_hip, m) {
     hip_ok("clock_probe");
   });
   m.def("sampler_blocks", &sampler_blocks);
-  m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cv,
-                     uintptr_t ci, uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream, uintptr_t ct,
-                     uintptr_t dbg_clk) {
+  m.def("sampler_cand_words", &sampler_cand_words);
+  // stage 1 over logits[0, V) whose global ids start at vocab_off (slices over [0, V_span)),
+  // then - if cand_all is given - stage 2 over `world` gathered blocks, else over this one
+  m.def("sample", [](uintptr_t logits, int V, uintptr_t params, uintptr_t ring, uintptr_t state, uintptr_t cand,
+                     uintptr_t out_tokens, int out_cap, int advance, uintptr_t stream, uintptr_t dbg_clk,
+                     int vocab_off, int V_glob, int V_span, uintptr_t cand_all, int world, int stage) {
     SamplerArgs a;
     a.dbg_clk = P<long long>(dbg_clk);
-    a.cand_tau = P<unsigned>(ct);
     a.logits = P<float>(logits); a.V = V; a.p = P<SamplerParamsDev>(params); a.ring = P<int>(ring);
-    a.state = P<int>(state); a.cand_val = P<float>(cv); a.cand_idx = P<int>(ci); a.out_tokens = P<int>(out_tokens);
+    a.state = P<int>(state); a.cand = P<unsigned>(cand); a.out_tokens = P<int>(out_tokens);
     a.out_cap = out_cap; a.advance_pos = advance;
-    sample(a, S(stream));
+    a.vocab_off = vocab_off; a.V_glob = V_glob; a.V_span = V_span;
+    a.cand_all = P<const unsigned>(cand_all); a.world = world;
+    if (stage & 1) sample_stage1(a, S(stream));
+    if (stage & 2) sample_stage2(a, S(stream));
     hip_ok("sample");
-  }, py::arg("logits"), py::arg("V"), py::arg("params"), py::arg("ring"), py::arg("state"), py::arg("cv"),
-     py::arg("ci"), py::arg("out_tokens"), py::arg("out_cap"), py::arg("advance"), py::arg("stream"), py::arg("ct"),
-     py::arg("dbg_clk") = 0);
+  }, py::arg("logits"), py::arg("V"), py::arg("params"), py::arg("ring"), py::arg("state"), py::arg("cand"),
+     py::arg("out_tokens"), py::arg("out_cap"), py::arg("advance"), py::arg("stream"), py::arg("dbg_clk") = 0,
+     py::arg("vocab_off") = 0, py::arg("V_glob") = 0, py::arg("V_span") = 0, py::arg("cand_all") = 0,
+     py::arg("world") = 1, py::arg("stage") = 3);
   m.def("sampler_params_bytes", [](int top_k, float top_p, float min_p, float temp, float rp, float fp, float pp,
                                    int last_n, unsigned long long seed, int greedy, float tfs_z, float typical_p,
                                    py::dict logit_bias) {

@@ -175,24 +175,26 @@ void moe_router_fused(const float* x, const float* nw, float eps, const float* W
 // Router: softmax over n_expert logits, top-k, renormalise -> ids / weights (device).
 void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hipStream_t s);
 
-// ---------------------------------------------------------------- tensor-parallel all-reduce
-// One-shot push all-reduce over peer memory (p2p_allreduce.hip). Rank p's receive
-// region: data [2 slots][world][max_n] f32, then flags [2][world][kP2PMaxBlocks] i32.
+// ---------------------------------------------------------------- tensor-parallel collectives
+// One-shot push all-reduce / all-gather over peer memory (p2p_allreduce.hip). Rank p's
+// receive region: data [2 slots][world][max_n] f32, then flags [2][world][kP2PMaxBlocks] i32.
+// Every launch runs exactly kP2PMaxBlocks blocks (the slot-reuse argument needs it).
 static constexpr int kP2PMaxRanks = 8;
 static constexpr int kP2PMaxBlocks = 64;
 struct P2PPeers {
   float* data[kP2PMaxRanks] = {};
   int* flags[kP2PMaxRanks] = {};
 };
-struct P2PAllreduceArgs {
+struct P2PArgs {
   P2PPeers peers;                  // every rank's region as mapped in THIS process (own one included)
-  const float* src = nullptr;      // [n] this rank's partial
-  float* dst = nullptr;            // [n] the sum (may alias nothing in the regions)
-  int n = 0, max_n = 0, rank = 0, world = 1, blocks = 16;
+  const float* src = nullptr;      // [n] this rank's buffer
+  float* dst = nullptr;            // all-reduce: [n] the sum; all-gather: [world][n]
+  int n = 0, max_n = 0, rank = 0, world = 1;
+  int gather = 0;                  // 0: all-reduce (sum), 1: all-gather
   int* epochs = nullptr;           // [kP2PMaxBlocks] local, zero-initialised, advanced per launch
   int* err = nullptr;              // set on a timed-out wait
 };
-void p2p_allreduce(const P2PAllreduceArgs& a, hipStream_t s);
+void p2p_collective(const P2PArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- attention
 // Decode: split-L flash decoding over chunks of 64 keys, GQA-packed.
@@ -318,30 +320,41 @@ struct SamplerParamsDev {
 // Device state block (ints) shared by the decode kernels.
 enum StateIdx : int { S_TOKEN = 0, S_POS = 1, S_STEP = 2, S_RING_LEN = 3, S_RING_HEAD = 4, S_NOUT = 5, S_NSTATE = 8 };
 
+// Stage 1 writes, per row, one packed candidate block of sampler_cand_words(V_span) 4-byte
+// words: [values nb*64 f32][global ids nb*64 i32][slice bounds nb][slice maxima nb]
+// (nb = sampler_blocks(V_span)). Stage 2 reads `world` such blocks per row, laid out
+// [world][rows][words] - under tensor parallelism each rank runs stage 1 on its vocabulary
+// shard, the blocks are all-gathered (a few KB instead of the shard's logits) and every rank
+// runs the identical stage 2 (same candidates, same RNG step -> the same token).
 struct SamplerArgs {
-  float* logits = nullptr;         // [V]; the penalty kernel patches it in place
-  int V = 0;
+  float* logits = nullptr;         // [V] this rank's logits; the penalty pass patches a copy in LDS
+  int V = 0;                       // real logits in `logits` (this rank's shard)
+  int vocab_off = 0;               // global id of logits[0] (tensor-parallel vocabulary shard)
+  int V_glob = 0;                  // full vocabulary (0: V); sampled ids are clamped below it
+  int V_span = 0;                  // stage-1 slices cover [0, V_span) (0: V); the same on every rank
   const SamplerParamsDev* p = nullptr;
   int* ring = nullptr;             // [64] penalty window ring (prompt + generated tokens)
   int* state = nullptr;            // [S_NSTATE]
-  float* logits_rw = nullptr;      // unused (penalties patch `logits` in place)
-  float* cand_val = nullptr;       // workspace [sampler_blocks(V) * 64]
-  int* cand_idx = nullptr;
-  unsigned* cand_tau = nullptr;    // workspace [2 * sampler_blocks(V)]: slice bounds, slice maxima
+  unsigned* cand = nullptr;        // stage-1 output [rows][sampler_cand_words(V)]
+  const unsigned* cand_all = nullptr;  // stage-2 input [world][rows][words] (null: `cand`, world 1)
+  int world = 1;
   long long* dbg_clk = nullptr;    // microbenchmarks only: stage-2 timeline stamps (instrumented build)
   int* out_tokens = nullptr;       // optional device ring of sampled tokens [out_cap]
   int out_cap = 0;
   int advance_pos = 1;             // also bump state.pos (decode) after sampling
   // batched (batch > 0): row b samples logits + b*logits_ld with the params / ring /
   // state of slot slots[b] (p + slot, ring + 64*slot, state + S_NSTATE*slot), its own
-  // candidate workspace (cand_* + b * per-row size) and writes its token to batch_out[b]
+  // candidate block and writes its token to batch_out[b]
   int batch = 0;
   const int* slots = nullptr;
   size_t logits_ld = 0;
   int* batch_out = nullptr;
 };
 int sampler_blocks(int V);
-void sample(const SamplerArgs& a, hipStream_t s);
+size_t sampler_cand_words(int V);
+void sample_stage1(const SamplerArgs& a, hipStream_t s);
+void sample_stage2(const SamplerArgs& a, hipStream_t s);
+void sample(const SamplerArgs& a, hipStream_t s);  // both stages (world 1)
 
 // ---------------------------------------------------------------- synthetic fill
 // Random valid quant blocks generated on device (for synthetic models without a file).

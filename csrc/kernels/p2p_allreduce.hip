@@ -1,46 +1,48 @@
-// One-shot push all-reduce for decode-sized tensor-parallel messages (SURVEY
-// §2.4 X7, §2.6 N0c, §5.8): the two per-layer all-reduces of a row-parallel
-// decode step carry 16-32 KiB, where a ring all-reduce is latency-bound
-// (2(N-1) dependent steps over a ring). Here every rank WRITES its partial
-// straight into every peer's receive slot over its point-to-point xGMI link
-// (7 links used at once on an 8-GPU node), raises one flag per (rank, block)
-// in each peer, then waits for the N flags in its OWN memory and sums the N
-// slots locally in fixed rank order - so every rank computes bit-identical
-// results (the TP ranks must stay in lock-step).
+// One-shot push collectives for tensor-parallel messages (SURVEY §2.4 X7, §2.6 N0c,
+// §5.8): the two per-layer all-reduces of a row-parallel decode step carry 16-32 KiB
+// per row, where a ring all-reduce is latency-bound (2(N-1) dependent steps). Here
+// every rank WRITES its buffer straight into every peer's receive slot over its
+// point-to-point xGMI link (7 links used at once on an 8-GPU node), raises one flag
+// per (rank, block) in each peer, then waits for the N flags in its OWN memory and
+//   * all-reduce: sums the N slots locally in fixed rank order - every rank computes
+//     bit-identical results (the TP ranks must stay in lock-step), or
+//   * all-gather: copies slot p to dst[p * n ...] (the sampler's candidate blocks,
+//     logit shards for the test hooks).
 //
-// Receive regions are exported/imported once with hipIpc* handles (one process
-// per GPU); the kernel is graph-capturable: the epoch (per block) lives in
-// device memory and advances on every launch, and slots alternate with the
-// epoch's parity. Slot reuse is safe without a second barrier: a rank writes
-// slot s again at epoch e+2 only after it saw every peer's flag for e+1, which
-// each peer raised after finishing its reads of epoch e (stream order).
+// Receive regions are exported/imported once with hipIpc* handles (one process per
+// GPU, or several processes on one GPU in the IPC-only test mode); the kernel is
+// graph-capturable: the epoch lives in device memory and advances on every launch.
 //
-// Memory model: data and flags are stored with system-scope atomics (write-
-// through, visible to the peer agent), a system-scope release fence orders
-// each thread's data stores before the block barrier and the flag stores;
-// the reader polls its local flags with system-scope acquire loads and reads
-// the slots with system-scope loads (bypassing an L2 that may hold the slot's
-// previous epoch). Every wait is bounded: a timeout sets *err and the launch
-// completes (the engine then reports itself unhealthy) instead of hanging.
+// Slot reuse needs no second barrier because EVERY launch uses the same fixed grid
+// (kP2PMaxBlocks blocks, whatever n is): all blocks share one epoch sequence, slot
+// parity alternates per launch, and a rank writes parity e&1 again at epoch e+2 only
+// after it saw every peer's flags of epoch e+1 - raised by a peer's launch e+1, which
+// started after that peer's launch e (and its reads of the slot) completed (stream
+// order). A per-launch block count would break this: blocks of different launches
+// would advance different epochs and alias slot ranges.
+//
+// Memory model: payload stores are plain (vectorised) stores into the peer's memory,
+// ordered before the flag stores by a system-scope release fence + block barrier; the
+// reader polls its local flags with system-scope acquire loads and reads the slots
+// with system-scope loads (bypassing an L2 that may hold the slot's previous epoch).
+// Every wait is bounded: a timeout sets *err and the launch completes (the engine
+// then reports itself unhealthy) instead of hanging.
 #include "kernels.h"
 
 namespace lfk {
 
 static constexpr int kP2PSpin = 1 << 22;
 
-__device__ __forceinline__ void st_sys(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 __device__ __forceinline__ float ld_sys(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(256) void p2p_allreduce_kernel(P2PAllreduceArgs a) {
+__global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
   __shared__ int s_ep, s_ok;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int W = a.world, R = a.rank;
-  const int chunk = ((a.n + gridDim.x - 1) / gridDim.x + 3) & ~3;
-  const int i0 = b * chunk, i1 = min(a.n, i0 + chunk);
+  const int chunk = ((a.n + kP2PMaxBlocks - 1) / kP2PMaxBlocks + 3) & ~3;
+  const int i0 = min(a.n, b * chunk), i1 = min(a.n, i0 + chunk);
   if (tid == 0) {
     const int e = a.epochs[b] + 1;  // block-private word: plain access
     a.epochs[b] = e;
@@ -51,9 +53,13 @@ __global__ __launch_bounds__(256) void p2p_allreduce_kernel(P2PAllreduceArgs a) 
   const int ep = s_ep, slot = ep & 1;
   const size_t FB = kP2PMaxBlocks;
   // 1. push this rank's chunk into slot [slot][R] of every rank (self included)
+  const bool vec = ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0) && (a.max_n % 4 == 0);
+  const int v0 = i0, v1 = vec ? i0 + ((i1 - i0) & ~3) : i0;
   for (int p = 0; p < W; ++p) {
     float* dst = a.peers.data[p] + ((size_t)slot * W + R) * a.max_n;
-    for (int i = i0 + tid; i < i1; i += blockDim.x) st_sys(dst + i, a.src[i]);
+    for (int i = v0 + 4 * tid; i < v1; i += 4 * blockDim.x)
+      *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(a.src + i);
+    for (int i = v1 + tid; i < i1; i += blockDim.x) dst[i] = a.src[i];
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this thread's stores before the barrier
   __syncthreads();
@@ -76,8 +82,14 @@ __global__ __launch_bounds__(256) void p2p_allreduce_kernel(P2PAllreduceArgs a) 
   }
   __syncthreads();
   if (!s_ok) return;
-  // 4. sum the W slots in rank order (bit-identical on every rank)
   const float* mine = a.peers.data[R] + (size_t)slot * W * a.max_n;
+  if (a.gather) {
+    // 4a. rank p's chunk -> dst[p * n + i]
+    for (int p = 0; p < W; ++p)
+      for (int i = i0 + tid; i < i1; i += blockDim.x) a.dst[(size_t)p * a.n + i] = ld_sys(mine + (size_t)p * a.max_n + i);
+    return;
+  }
+  // 4b. sum the W slots in rank order (bit-identical on every rank)
   for (int i = i0 + tid; i < i1; i += blockDim.x) {
     float v = 0.f;
     for (int p = 0; p < W; ++p) v += ld_sys(mine + (size_t)p * a.max_n + i);
@@ -85,13 +97,11 @@ __global__ __launch_bounds__(256) void p2p_allreduce_kernel(P2PAllreduceArgs a) 
   }
 }
 
-void p2p_allreduce(const P2PAllreduceArgs& a, hipStream_t s) {
-  if (a.world < 1 || a.world > kP2PMaxRanks) throw std::runtime_error("p2p_allreduce: world must be 1..8");
+void p2p_collective(const P2PArgs& a, hipStream_t s) {
+  if (a.world < 1 || a.world > kP2PMaxRanks) throw std::runtime_error("p2p: world must be 1..8");
   if (a.n <= 0) return;
-  if (a.n > a.max_n) throw std::runtime_error("p2p_allreduce: message larger than the slot");
-  const int blocks = a.blocks > 0 ? a.blocks : 1;
-  if (blocks > kP2PMaxBlocks) throw std::runtime_error("p2p_allreduce: too many blocks");
-  hipLaunchKernelGGL(p2p_allreduce_kernel, dim3(blocks), dim3(256), 0, s, a);
+  if (a.n > a.max_n) throw std::runtime_error("p2p: message larger than the slot");
+  hipLaunchKernelGGL(p2p_collective_kernel, dim3(kP2PMaxBlocks), dim3(256), 0, s, a);
 }
 
 }  // namespace lfk

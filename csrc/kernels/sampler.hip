@@ -98,27 +98,30 @@ __device__ __forceinline__ int wave_collect(const float (&v)[NE], const int (&id
 }
 
 // Batched mode: row b of the launch (blockIdx.y in stage 1, blockIdx.x in stage 2)
-// works on its own logits row, the sampling state of its KV slot and its own
-// candidate workspace; every pointer is re-based here so the stage bodies are the
-// single-row code.
-__device__ __forceinline__ void batch_row(SamplerArgs& a, int b, int nb) {
+// works on its own logits row and the sampling state of its KV slot; every pointer is
+// re-based here so the stage bodies are the single-row code.
+__device__ __forceinline__ void batch_row(SamplerArgs& a, int b) {
   if (a.batch <= 0) return;
   const int slot = a.slots[b];
   a.logits += (size_t)b * a.logits_ld;
   a.p += slot;
   a.ring += 64 * slot;
   a.state += (size_t)S_NSTATE * slot;
-  a.cand_val += (size_t)b * nb * KMAX;
-  a.cand_idx += (size_t)b * nb * KMAX;
-  a.cand_tau += (size_t)b * 2 * nb;
 }
+
+__host__ __device__ __forceinline__ size_t cand_words(int nb) { return (size_t)nb * (2 * KMAX + 2); }
 
 // Stage 1: one wave per 1024-logit slice. The repetition/frequency/presence
 // penalties of ring tokens that fall in this slice are applied here (the wave
 // stages its slice in LDS, lanes owning a first occurrence patch their entry),
 // then the slice's top-K superset is selected without LDS or barriers.
-__global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
-  batch_row(a, blockIdx.y, gridDim.x);
+__global__ __launch_bounds__(64) void sample_stage1_kernel(SamplerArgs a) {
+  batch_row(a, blockIdx.y);
+  const int nb = gridDim.x;
+  unsigned* blk = a.cand + (size_t)blockIdx.y * cand_words(nb);
+  float* cand_val = reinterpret_cast<float*>(blk);
+  int* cand_idx = reinterpret_cast<int*>(blk) + nb * KMAX;
+  unsigned* cand_tau = blk + 2 * nb * KMAX;
   __shared__ float sl[SLICE];
   const int lane = threadIdx.x;
   const int lo = blockIdx.x * SLICE;
@@ -130,24 +133,26 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
   for (int e = 0; e < NE1; ++e) {
     const int i = lo + 64 * e + lane;
     v[e] = i < a.V ? a.logits[i] : -FLT_MAX;
-    idx[e] = i;
+    idx[e] = a.vocab_off + i;
   }
+  // window / bias tokens are global ids; this slice holds [g0, g0 + SLICE) of them
+  const int g0 = a.vocab_off + lo, gend = a.vocab_off + a.V;
   // ---- logit bias (lane j holds entry j; distinct tokens), then the penalties
   // (window = last min(ring_len, last_n) tokens) on the biased values
   const int nbias = P.n_bias;
   const int bt = lane < nbias ? P.bias_tok[lane] : -1;
-  const bool bmine = bt >= lo && bt < lo + SLICE && bt < a.V;
+  const bool bmine = bt >= g0 && bt < g0 + SLICE && bt < gend;
   const int rlen = a.state[S_RING_LEN], rhead = a.state[S_RING_HEAD];
   const int wn = min(rlen, P.last_n);
   const int t = lane < wn ? a.ring[(rhead - wn + lane + 64) & 63] : -1;
-  const bool mine = t >= lo && t < lo + SLICE && t < a.V;
+  const bool mine = t >= g0 && t < g0 + SLICE && t < gend;
   if (__ballot(mine) | __ballot(bmine)) {  // wave-uniform: a window or bias token lies in this slice
 #pragma unroll
     for (int e = 0; e < NE1; ++e) sl[64 * e + lane] = v[e];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (bmine) sl[bt - lo] += P.bias_val[lane];
+    if (bmine) sl[bt - g0] += P.bias_val[lane];
     int cnt = 0;
     bool first = true;
     for (int j = 0; j < wn; ++j) {
@@ -161,10 +166,10 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (mine && first) {
-      float l = sl[t - lo];
+      float l = sl[t - g0];
       l = l <= 0.f ? l * P.repeat_penalty : l / P.repeat_penalty;
       l -= (float)cnt * P.freq_penalty + P.presence_penalty;
-      sl[t - lo] = l;
+      sl[t - g0] = l;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -174,8 +179,8 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
   }
   // ---- top-K superset of the slice
   const float T = wave_superset_threshold<NE1>(v, K);
-  float* ov = a.cand_val + blockIdx.x * KMAX;
-  int* oi = a.cand_idx + blockIdx.x * KMAX;
+  float* ov = cand_val + blockIdx.x * KMAX;
+  int* oi = cand_idx + blockIdx.x * KMAX;
   const int m = wave_collect<NE1>(v, idx, T, KMAX, ov, oi);
   if (lane >= m) {
     ov[lane] = -FLT_MAX;
@@ -189,8 +194,8 @@ __global__ __launch_bounds__(64) void sample_stage1(SamplerArgs a) {
   vmax = wave_max_fast(vmax);
   if (lane == 0) {
     const int nvalid = min(SLICE, a.V - lo);
-    a.cand_tau[blockIdx.x] = __float_as_uint(m >= K && nvalid >= K ? T : -FLT_MAX);
-    a.cand_tau[gridDim.x + blockIdx.x] = __float_as_uint(vmax);
+    cand_tau[blockIdx.x] = __float_as_uint(m >= K && nvalid >= K ? T : -FLT_MAX);
+    cand_tau[nb + blockIdx.x] = __float_as_uint(vmax);
   }
 }
 
@@ -272,10 +277,39 @@ __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
 // sorts (value desc, index asc), keeps K, applies top-p / min-p / temperature,
 // draws and updates the device state.
 static constexpr int CAP2 = 2048;  // survivors above the bounds (typically < 200)
+// The candidate blocks of one row: `world` of them (one per vocabulary shard), nb_l slices
+// each; slice g of the row is slice g % nb_l of block g / nb_l.
+struct CandRow {
+  const unsigned* base;
+  size_t rank_stride;   // words between two ranks' blocks of this row
+  int nb_l;
+  __device__ __forceinline__ const unsigned* blk(int r) const { return base + (size_t)r * rank_stride; }
+  __device__ __forceinline__ void cand(int i, float& v, int& id) const {
+    const int per = nb_l * KMAX, r = i / per, j = i - r * per;
+    const unsigned* b = blk(r);
+    v = __uint_as_float(b[j]);
+    id = (int)b[per + j];
+  }
+  __device__ __forceinline__ float bound(int g) const {
+    const int r = g / nb_l;
+    return __uint_as_float(blk(r)[2 * nb_l * KMAX + (g - r * nb_l)]);
+  }
+  __device__ __forceinline__ float smax(int g) const {
+    const int r = g / nb_l;
+    return __uint_as_float(blk(r)[2 * nb_l * KMAX + nb_l + (g - r * nb_l)]);
+  }
+};
+
 template <int NE2, bool TL = false>
-__global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
+__global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int nb_l) {
   const int brow = blockIdx.x;
-  batch_row(a, brow, nb);
+  batch_row(a, brow);
+  const int rows = a.batch > 0 ? a.batch : 1;
+  const int nb = nb_l * a.world;   // slices of the whole vocabulary
+  CandRow cr;
+  cr.nb_l = nb_l;
+  cr.rank_stride = (size_t)rows * cand_words(nb_l);
+  cr.base = (a.cand_all ? a.cand_all : a.cand) + (size_t)brow * cand_words(nb_l);
   long long t0 = 0;
   if constexpr (TL) t0 = wall_clock64();
 #define LFK_ST(i) do { if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[i] = wall_clock64() - t0; } } while (0)
@@ -294,20 +328,19 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
 #pragma unroll
   for (int e = 0; e < NE2; ++e) {  // independent loads (no value-dependent second load)
     const int i = min(256 * e + tid, nb * KMAX - 1);
-    idx[e] = a.cand_idx[i];
-    v[e] = a.cand_val[i];
+    cr.cand(i, v[e], idx[e]);
   }
   // Two lower bounds of the global K-th largest value: (a) each slice bound
   // (that slice alone holds >= K values above it); (b) a superset threshold of
   // the slice MAXIMA (>= K distinct slices have their maximum above it).
   // (b) keeps the survivor count small even for flat (high-entropy) logits.
   float lb = -FLT_MAX;
-  for (int b = tid; b < nb; b += 256) lb = fmaxf(lb, __uint_as_float(a.cand_tau[b]));
+  for (int b = tid; b < nb; b += 256) lb = fmaxf(lb, cr.bound(b));
   lb = wave_max_fast(lb);
   if (tid < 64) {
     float mx[2];
-    mx[0] = tid < nb ? __uint_as_float(a.cand_tau[nb + tid]) : -FLT_MAX;
-    mx[1] = tid + 64 < nb ? __uint_as_float(a.cand_tau[nb + 64 + tid]) : -FLT_MAX;
+    mx[0] = tid < nb ? cr.smax(tid) : -FLT_MAX;
+    mx[1] = tid + 64 < nb ? cr.smax(tid + 64) : -FLT_MAX;
     int valid = (mx[0] > -FLT_MAX) + (mx[1] > -FLT_MAX);
     valid = (int)wave_sum_fast((float)valid);
     if (valid >= K) lb = fmaxf(lb, wave_superset_threshold<2>(mx, K));
@@ -405,7 +438,7 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
   }
   if (lane == 0) {
     int* st = a.state;
-    tok = min(max(tok, 0), a.V - 1);  // non-finite logits must not leave an out-of-range id behind
+    tok = min(max(tok, 0), (a.V_glob > 0 ? a.V_glob : a.V) - 1);  // non-finite logits must not leave an out-of-range id behind
     st[S_TOKEN] = tok;
     const int head = st[S_RING_HEAD];
     a.ring[head & 63] = tok;
@@ -421,18 +454,32 @@ __global__ __launch_bounds__(256) void sample_stage2(SamplerArgs a, int nb) {
 }
 
 int sampler_blocks(int V) { return (V + SLICE - 1) / SLICE; }
+size_t sampler_cand_words(int V) { return cand_words(sampler_blocks(V)); }
 
-void sample(const SamplerArgs& a, hipStream_t s) {
-  const int nb = sampler_blocks(a.V);
+void sample_stage1(const SamplerArgs& a, hipStream_t s) {
   const int rows = a.batch > 0 ? a.batch : 1;
   if (a.batch > 0 && (!a.slots || a.logits_ld < (size_t)a.V || a.out_tokens || a.dbg_clk))
     throw std::runtime_error("sample: bad batched arguments");
-  hipLaunchKernelGGL(sample_stage1, dim3(nb, rows), dim3(64), 0, s, a);
-  const int ncand = nb * KMAX;
-  if (a.dbg_clk && ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, true>), dim3(1), dim3(256), 0, s, a, nb);
-  else if (ncand <= 256 * 8) hipLaunchKernelGGL((sample_stage2<8, false>), dim3(rows), dim3(256), 0, s, a, nb);
-  else if (ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2<32, false>), dim3(rows), dim3(256), 0, s, a, nb);
-  else throw std::runtime_error("GPU sampler: vocabulary too large (max 131072)");
+  if (!a.cand || a.V < 0 || (a.V == 0 && a.V_span <= 0)) throw std::runtime_error("sample: no candidate buffer / empty vocabulary");
+  if (a.V_span && a.V_span < a.V) throw std::runtime_error("sample: V_span < V");
+  hipLaunchKernelGGL(sample_stage1_kernel, dim3(sampler_blocks(a.V_span ? a.V_span : a.V), rows), dim3(64), 0, s, a);
+}
+
+void sample_stage2(const SamplerArgs& a, hipStream_t s) {
+  const int nb_l = sampler_blocks(a.V_span ? a.V_span : a.V);
+  const int rows = a.batch > 0 ? a.batch : 1;
+  if (a.world < 1 || (a.world > 1 && !a.cand_all)) throw std::runtime_error("sample: bad world / gathered blocks");
+  const int ncand = nb_l * a.world * KMAX;
+  if (a.dbg_clk && ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2_kernel<32, true>), dim3(1), dim3(256), 0, s, a, nb_l);
+  else if (ncand <= 256 * 8) hipLaunchKernelGGL((sample_stage2_kernel<8, false>), dim3(rows), dim3(256), 0, s, a, nb_l);
+  else if (ncand <= 256 * 32) hipLaunchKernelGGL((sample_stage2_kernel<32, false>), dim3(rows), dim3(256), 0, s, a, nb_l);
+  else throw std::runtime_error("GPU sampler: vocabulary too large (max 8192 candidate slots)");
+}
+
+void sample(const SamplerArgs& a, hipStream_t s) {
+  if (a.world != 1) throw std::runtime_error("sample: world > 1 needs the gathered two-stage form");
+  sample_stage1(a, s);
+  sample_stage2(a, s);
 }
 
 }  // namespace lfk

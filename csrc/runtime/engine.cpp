@@ -5,6 +5,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -87,13 +88,16 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   F_l_ = sp.F_l;
   V_l_ = sp.V_l;
   V_pad_ = sp.V_pad;
+  V_real_l_ = std::max(0, std::min(V_l_, hp_.n_vocab - r * V_l_));
+  if (opt_.comm != "auto" && opt_.comm != "ipc" && opt_.comm != "rccl")
+    throw std::runtime_error("comm must be auto, ipc or rccl");
   if (opt_.layer_begin < 0 || opt_.layer_begin > hp_.n_layer) throw std::runtime_error("bad layer_begin");
   if (opt_.layer_begin > 0 && tp > 1) throw std::runtime_error("partial offload cannot be combined with split_mode=row");
   if (opt_.n_ctx <= 0) opt_.n_ctx = hp_.n_ctx_train;
   if (opt_.n_slots < 1) throw std::runtime_error("n_slots must be >= 1");
-  if (opt_.n_slots > 1 && (tp > 1 || opt_.layer_begin > 0))
-    throw std::runtime_error("KV slots (batched decode) need one rank holding every layer");
-  if (tp > 1) {
+  if (opt_.n_slots > 1 && opt_.layer_begin > 0)
+    throw std::runtime_error("KV slots (batched decode) need the GPU to hold every layer");
+  if (tp > 1 && opt_.comm != "ipc") {
     if (opt_.nccl_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad nccl id");
     ncclUniqueId id;
     std::memcpy(&id, opt_.nccl_id.data(), sizeof(id));
@@ -109,7 +113,13 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
 }
 
 Engine::~Engine() {
+  try {
+    if (leader() && tp_ctl_ && !tp_stopped_) tp_stop();
+  } catch (...) {
+  }
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  for (size_t i = 1; i < sgraph_.size(); ++i)
+    if (sgraph_[i]) hipGraphExecDestroy(sgraph_[i]);
   for (hipGraphExec_t g : bgraph_)
     if (g) hipGraphExecDestroy(g);
   if (graph_) hipGraphDestroy(graph_);
@@ -237,10 +247,10 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = std::atoi(e);
   if (const char* e = std::getenv("LFK_ATTN_TOUCH_GU_FRAC")) attn_touch_gu_frac_ = std::atof(e);
-  const int nb = sampler_blocks(hp_.n_vocab);
-  cand_val_ = (float*)dalloc(sizeof(float) * nb * 64);
-  cand_idx_ = (int*)dalloc(sizeof(int) * nb * 64);
-  cand_tau_ = (unsigned*)dalloc(sizeof(unsigned) * 2 * nb);  // slice bounds + slice maxima
+  const int tp = opt_.tp_size;
+  cand_words_ = sampler_cand_words(V_l_);
+  cand_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_);
+  if (tp > 1) cand_all_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_ * tp);
   state_ = (int*)dalloc(sizeof(int) * S_NSTATE * NS);
   ring_ = (int*)dalloc(sizeof(int) * 64 * NS);
   out_tokens_ = (int*)dalloc(sizeof(int) * 64);
@@ -270,9 +280,8 @@ void Engine::alloc_buffers() {
     btok_ = (int*)dalloc(sizeof(int) * bmax_);
     btok_out_ = (int*)dalloc(sizeof(int) * bmax_);
     logits_b_ = (float*)dalloc(sizeof(float) * bmax_ * V_pad_);
-    cand_val_b_ = (float*)dalloc(sizeof(float) * bmax_ * nb * 64);
-    cand_idx_b_ = (int*)dalloc(sizeof(int) * bmax_ * nb * 64);
-    cand_tau_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * 2 * nb);
+    cand_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * cand_words_);
+    if (tp > 1) cand_all_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * cand_words_ * tp);
     attn_part_b_ = (float*)dalloc(sizeof(float) * bmax_ * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
     attn_cnt_b_ = (int*)dalloc(sizeof(int) * 64 * bmax_);
     HIPCHK(hipMemset(attn_cnt_b_, 0, sizeof(int) * 64 * bmax_));
@@ -283,6 +292,15 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
   dev_err_ = (int*)dalloc(sizeof(int) * 4);
   HIPCHK(hipMemset(dev_err_, 0, sizeof(int) * 4));
+  // P2P messages: a decode step's hidden rows and the sampler's candidate blocks; in "ipc"
+  // mode (no RCCL) also prefill chunks and the test hooks' logit gathers
+  {
+    size_t m = (size_t)std::max(bmax_, 1) * std::max<size_t>((size_t)d, cand_words_);
+    if (opt_.comm == "ipc")
+      m = std::max({m, (size_t)B * d, (size_t)std::max(bmax_, 1) * V_pad_});
+    if (m > (size_t)INT32_MAX / 4) throw std::runtime_error("p2p message bound too large");
+    p2p_max_n_ = (int)m;
+  }
   HIPCHK(hipHostMalloc((void**)&h_ring_, sizeof(int) * 64, hipHostMallocDefault));
   HIPCHK(hipHostMalloc((void**)&h_tokens_, sizeof(int) * B, hipHostMallocDefault));
 }
@@ -290,6 +308,8 @@ void Engine::alloc_buffers() {
 void Engine::setup_batch_mfma() {
   bg_ = bg_ffn_ = false;
   if (!bmax_ || opt_.layer_begin > 0) return;
+  const char* b1 = std::getenv("LFK_B1_GEMV");
+  b1_gemv_ = !(b1 && b1[0] == '0');
   const char* e = std::getenv("LFK_BATCH_MFMA");
   if (e && e[0] == '0') return;
   auto ok = [&](const QMat& m) { return m.base && bmm_supported(m.type, m.K); };
@@ -358,7 +378,8 @@ void Engine::build_rope() {
 // ------------------------------------------------------------------------ schedule
 std::string Engine::p2p_handle() {
   if (opt_.tp_size < 2) throw std::runtime_error("p2p: tensor parallelism is off");
-  if (!p2p_) p2p_ = std::make_unique<P2PComm>(opt_.tp_rank, opt_.tp_size, hp_.n_embd, opt_.device);
+  if (opt_.comm == "rccl") throw std::runtime_error("p2p: comm=rccl has no P2P path");
+  if (!p2p_) p2p_ = std::make_unique<P2PComm>(opt_.tp_rank, opt_.tp_size, p2p_max_n_, opt_.device);
   return p2p_->handle();
 }
 
@@ -368,14 +389,58 @@ void Engine::p2p_open(const std::vector<std::string>& handles) {
   p2p_->open(handles);
 }
 
-// Decode-sized messages (one token's hidden state) take the one-shot P2P path when
-// the peers are open; prefill-sized ones (T x d) go to RCCL's ring/tree algorithms.
+// Decode-sized messages (a step's hidden rows, the sampler's candidate blocks) take the
+// one-shot P2P path when the peers are open; prefill-sized ones (T x d) go to RCCL's
+// ring/tree algorithms - or, with comm=ipc (no RCCL), to the P2P kernel as well.
 void Engine::allreduce_into(const float* send, float* recv, size_t n, hipStream_t s) {
   if (p2p_ && p2p_->ready() && n <= (size_t)p2p_->max_n()) {
     p2p_->allreduce(send, recv, (int)n, s);
     return;
   }
+  if (!comm_) throw std::runtime_error("all-reduce of " + std::to_string(n) + " floats: no RCCL communicator and " +
+                                       (p2p_ready() ? "the message exceeds the P2P slot" : "P2P peers not open"));
   ncclchk(ncclAllReduce(send, recv, n, ncclFloat32, ncclSum, static_cast<ncclComm_t>(comm_), s), "ncclAllReduce");
+}
+
+void Engine::allgather_into(const float* send, float* recv, size_t n, hipStream_t s) {
+  if (p2p_ && p2p_->ready() && n <= (size_t)p2p_->max_n()) {
+    p2p_->allgather(send, recv, (int)n, s);
+    return;
+  }
+  if (!comm_) throw std::runtime_error("all-gather of " + std::to_string(n) + " floats: no RCCL communicator and " +
+                                       (p2p_ready() ? "the message exceeds the P2P slot" : "P2P peers not open"));
+  ncclchk(ncclAllGather(send, recv, n, ncclFloat32, static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
+}
+
+void Engine::enqueue_sample(const float* logits, int rows, size_t ld, int slot, int advance_pos, hipStream_t s) {
+  const bool batched = rows > 0;
+  SamplerArgs sa;
+  sa.logits = const_cast<float*>(logits);
+  sa.V = V_real_l_;
+  sa.vocab_off = opt_.tp_rank * V_l_;
+  sa.V_glob = hp_.n_vocab;
+  sa.V_span = V_l_;
+  sa.advance_pos = advance_pos;
+  if (batched) {
+    sa.p = sparams_; sa.ring = ring_; sa.state = state_;
+    sa.batch = rows; sa.slots = bslots_; sa.logits_ld = ld; sa.batch_out = btok_out_;
+    sa.cand = cand_b_;
+  } else {
+    sa.p = sparams_ + slot; sa.ring = ring_ + 64 * slot; sa.state = state_ + (size_t)S_NSTATE * slot;
+    sa.cand = cand_;
+    if (slot == 0) {
+      sa.out_tokens = out_tokens_; sa.out_cap = 64;
+    }
+  }
+  sample_stage1(sa, s);
+  if (opt_.tp_size > 1) {
+    const size_t words = cand_words_ * (batched ? rows : 1);
+    unsigned* all = batched ? cand_all_b_ : cand_all_;
+    allgather_into(reinterpret_cast<const float*>(sa.cand), reinterpret_cast<float*>(all), words, s);
+    sa.cand_all = all;
+    sa.world = opt_.tp_size;
+  }
+  sample_stage2(sa, s);
 }
 
 void Engine::enqueue_layer_decode(int l, hipStream_t s) {
@@ -383,19 +448,20 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim;
   const bool tp = opt_.tp_size > 1;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
+  int* st = state_ + (size_t)S_NSTATE * dslot_;
   QkvArgs qa;
   qa.wq = L.wq; qa.wk = L.wk; qa.wv = L.wv;
   qa.x = x_; qa.norm_w = L.attn_norm; qa.eps = hp_.rms_eps;
   qa.q_out = q_;
-  qa.k_cache = kc_ + kv_layer * l;
-  qa.v_cache = vc_ + kv_layer * l;
+  qa.k_cache = kc_ + slot_stride_ * dslot_ + kv_layer * l;
+  qa.v_cache = vc_ + slot_stride_ * dslot_ + kv_layer * l;
   qa.n_ctx = opt_.n_ctx; qa.head_dim = hd;
-  qa.pos = state_ + S_POS;
+  qa.pos = st + S_POS;
   qa.rope = rope_;
   gemv_qkv(qa, s);
 
   AttnDecodeArgs aa;
-  aa.q = q_; aa.k_cache = qa.k_cache; aa.v_cache = qa.v_cache; aa.pos = state_ + S_POS;
+  aa.q = q_; aa.k_cache = qa.k_cache; aa.v_cache = qa.v_cache; aa.pos = st + S_POS;
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
@@ -498,28 +564,19 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
 void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int slot) {
   GemvArgs h;
   h.w = output_; h.x = xrow; h.norm_w = out_norm_; h.eps = hp_.rms_eps;
-  const int rows_real = std::max(0, std::min(V_l_, hp_.n_vocab - opt_.tp_rank * V_l_));
-  h.n_out = rows_real;
+  h.n_out = V_real_l_;
   h.out = opt_.tp_size > 1 ? logits_l_ : logits_;
   if (h.n_out > 0) gemv(h, EPI_STORE, s);
-  if (opt_.tp_size > 1)
-    ncclchk(ncclAllGather(logits_l_, logits_, V_l_, ncclFloat32, static_cast<ncclComm_t>(comm_), s), "ncclAllGather");
-  SamplerArgs sa;
-  sa.logits = logits_; sa.V = hp_.n_vocab; sa.p = sparams_ + slot; sa.ring = ring_ + 64 * slot;
-  sa.state = state_ + (size_t)S_NSTATE * slot;
-  sa.cand_val = cand_val_; sa.cand_idx = cand_idx_; sa.cand_tau = cand_tau_;
-  sa.advance_pos = advance_pos;
-  if (slot == 0) {
-    sa.out_tokens = out_tokens_; sa.out_cap = 64;
-  }
-  sample(sa, s);
+  // vocabulary-parallel sampling: stage 1 on this rank's shard, all-gather of the candidate
+  // blocks (a few KB), identical stage 2 on every rank (no logit all-gather)
+  enqueue_sample(h.out, 0, 0, slot, advance_pos, s);
   if (slot == 0) HIPCHK(hipMemcpyAsync(h_ring_, out_tokens_, sizeof(int) * 64, hipMemcpyDeviceToHost, s));
 }
 
 void Engine::enqueue_decode(hipStream_t s) {
-  embed_rows(tok_embd_, state_ + S_TOKEN, 1, x_, s);
+  embed_rows(tok_embd_, state_ + (size_t)S_NSTATE * dslot_ + S_TOKEN, 1, x_, s);
   for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
-  enqueue_head(x_, 1, s);
+  enqueue_head(x_, 1, s, dslot_);
 }
 
 void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
@@ -633,18 +690,34 @@ void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s) {
   }
 }
 
-void Engine::launch_step() {
+void Engine::launch_step(int slot) {
+  dslot_ = slot;
   if (opt_.use_graph) {
-    if (!graph_exec_) {
-      HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      enqueue_decode(stream_);
-      HIPCHK(hipStreamEndCapture(stream_, &graph_));
-      HIPCHK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+    if (slot == 0) {
+      if (!graph_exec_) {
+        HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+        enqueue_decode(stream_);
+        HIPCHK(hipStreamEndCapture(stream_, &graph_));
+        HIPCHK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+      }
+      HIPCHK(hipGraphLaunch(graph_exec_, stream_));
+    } else {
+      if ((int)sgraph_.size() <= slot) sgraph_.resize(slot + 1, nullptr);
+      if (!sgraph_[slot]) {
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+        enqueue_decode(stream_);
+        HIPCHK(hipStreamEndCapture(stream_, &g));
+        const hipError_t e = hipGraphInstantiate(&sgraph_[slot], g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        HIPCHK(e);
+      }
+      HIPCHK(hipGraphLaunch(sgraph_[slot], stream_));
     }
-    HIPCHK(hipGraphLaunch(graph_exec_, stream_));
   } else {
     enqueue_decode(stream_);
   }
+  dslot_ = 0;
 }
 
 // ------------------------------------------------------------------------ generation
@@ -687,38 +760,6 @@ void Engine::begin_slot_state(int slot, const std::vector<int>& prompt, const Sa
   HIPCHK(hipStreamSynchronize(stream_));  // the host arrays are on this stack frame
 }
 
-int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {
-  ExecGuard guard(this);
-  if (!bmax_) throw std::runtime_error("slot_begin: the engine was built with one KV slot");
-  if (slot < 0 || slot >= opt_.n_slots) throw std::runtime_error("slot_begin: slot out of range");
-  const int n_prompt = (int)prompt.size();
-  if (n_prompt == 0) throw std::runtime_error("empty prompt");
-  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
-  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
-  begin_slot_state(slot, prompt, sp);
-  kv_slot_ = slot;
-  try {
-    int pos = n_keep;
-    while (pos < n_prompt) {
-      const int T = std::min(opt_.n_batch, n_prompt - pos);
-      std::memcpy(h_tokens_, prompt.data() + pos, sizeof(int) * T);
-      HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-      enqueue_prefill(T, pos, stream_);
-      pos += T;
-      if (pos == n_prompt) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_, slot);
-      HIPCHK(hipStreamSynchronize(stream_));
-    }
-  } catch (...) {
-    kv_slot_ = 0;
-    throw;
-  }
-  kv_slot_ = 0;
-  int tok = 0;
-  HIPCHK(hipMemcpy(&tok, state_ + (size_t)S_NSTATE * slot + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
-  check_device_err();
-  return tok;
-}
-
 // bmm over B rows: groups of kBmmMaxRows columns (one more weight stream per group)
 void Engine::bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B,
                       hipStream_t s) {
@@ -745,6 +786,18 @@ void Engine::bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_
 void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
+  // row-parallel Wo / down under TP: accumulate this rank's partial into tmp_ (holding the
+  // residual on rank 0, zeros elsewhere), then all-reduce into x_
+  const bool tp = opt_.tp_size > 1;
+  float* acc = tp ? tmp_ : x_;
+  auto tp_begin = [&]() {
+    if (!tp) return;
+    if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * B * d, hipMemcpyDeviceToDevice, s));
+    else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * B * d, s));
+  };
+  auto tp_end = [&]() {
+    if (tp) allreduce_into(tmp_, x_, (size_t)B * d, s);
+  };
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
   __half* vcl = vc_ + kv_layer * l;
@@ -813,13 +866,15 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   }
   if (batt_touch_ & 3) aa.pf_sink = attn_cnt_b_ + 63;   // row 0's word 63: kv heads < 63
   attn_decode(aa, s);
+  tp_begin();
   if (wo_one_part_ && B <= kBmmMaxRows && bmm_qkv_fits(nq_, B)) {
     BmmArgs a;
-    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = x_; a.ldo = d; a.n_out = d; a.B = B; a.one_part = true;
+    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = acc; a.ldo = d; a.n_out = d; a.B = B; a.one_part = true;
     bmm(a, s);
   } else {
-    bmm_rows(L.t_wo, xh_b_, nq_, x_, d, d, B, s);
+    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s);
   }
+  tp_end();
   if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
@@ -833,14 +888,18 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
     a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
     bmm(a, s);
-    bmm_rows(L.t_down, hh_b_, F_l_, x_, d, d, B, s);
+    tp_begin();
+    bmm_rows(L.t_down, hh_b_, F_l_, acc, d, d, B, s);
+    tp_end();
     return;
   }
   if (bg_ffn_) {
     bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
     bmm_rows(L.t_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
     bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s);
-    bmm_rows(L.t_down, xh_b_, F_l_, x_, d, d, B, s);
+    tp_begin();
+    bmm_rows(L.t_down, xh_b_, F_l_, acc, d, d, B, s);
+    tp_end();
     return;
   }
   // MoE (or unsupported FFN types): the grouped-GEMM FFN of the prompt path over the B rows
@@ -859,11 +918,11 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
       // final norm folded into a one-part head projection that stores the logits
       BmmArgs a;
       a.w = t_output_; a.xf = x_; a.ldxf = d; a.norm_w = out_norm_; a.eps = hp_.rms_eps;
-      a.out = logits_b_; a.ldo = V_pad_; a.n_out = hp_.n_vocab; a.B = B; a.store_out = true;
+      a.out = logits_b_; a.ldo = V_pad_; a.n_out = V_l_; a.B = B; a.store_out = true;
       bmm(a, s);
     } else {
       bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
-      bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, hp_.n_vocab, B, s);
+      bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, V_l_, B, s);
     }
   } else {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
@@ -872,12 +931,191 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
     h.w = output_; h.x = xb_; h.T = B; h.out = logits_b_; h.ldo = V_pad_;
     gemm_dq(h, GEMM_STORE, s);
   }
-  SamplerArgs sa;
-  sa.logits = logits_b_; sa.V = hp_.n_vocab; sa.p = sparams_; sa.ring = ring_; sa.state = state_;
-  sa.cand_val = cand_val_b_; sa.cand_idx = cand_idx_b_; sa.cand_tau = cand_tau_b_;
-  sa.advance_pos = 1;
-  sa.batch = B; sa.slots = bslots_; sa.logits_ld = V_pad_; sa.batch_out = btok_out_;
-  sample(sa, s);
+  enqueue_sample(logits_b_, B, V_pad_, 0, 1, s);
+}
+
+
+
+// ------------------------------------------------------------------------ tensor-parallel control
+// Commands rank 0 publishes before enqueueing the matching device work (tp_channel.h).
+enum TPOp : int32_t {
+  TPO_STOP = 1,
+  TPO_SLOT_STATE,   // generate(): slot, prompt, sampling
+  TPO_PREFILL,      // generate(): slot, pos, head?, tokens of one chunk
+  TPO_DECODE_STEP,  // generate(): one graph-replayed decode step
+  TPO_SYNC,         // generate(): end of the request
+  TPO_SLOT_BEGIN,   // slot_begin()
+  TPO_BATCH_STEP,   // batch_step()
+  TPO_EVAL_LOGITS,  // eval_logits()
+  TPO_DECODE_LOGITS,
+  TPO_BATCH_LOGITS,
+  TPO_BENCH_DECODE,
+};
+
+static void put_sp(TPMsg& m, const SamplingOpts& sp) {
+  m.put(sp.top_k); m.put(sp.top_p); m.put(sp.min_p); m.put(sp.temp);
+  m.put(sp.repeat_penalty); m.put(sp.freq_penalty); m.put(sp.presence_penalty);
+  m.put(sp.last_n); m.put(sp.seed); m.put(sp.tfs_z); m.put(sp.typical_p);
+  m.put_vec(sp.logit_bias);
+}
+
+static SamplingOpts get_sp(TPMsg& m) {
+  SamplingOpts sp;
+  sp.top_k = m.get<int>(); sp.top_p = m.get<float>(); sp.min_p = m.get<float>(); sp.temp = m.get<float>();
+  sp.repeat_penalty = m.get<float>(); sp.freq_penalty = m.get<float>(); sp.presence_penalty = m.get<float>();
+  sp.last_n = m.get<int>(); sp.seed = m.get<unsigned long long>(); sp.tfs_z = m.get<float>();
+  sp.typical_p = m.get<float>();
+  sp.logit_bias = m.get_vec<std::pair<int, float>>();
+  return sp;
+}
+
+void Engine::mirror(const TPMsg& m) {
+  if (opt_.tp_size < 2) return;
+  if (opt_.tp_rank != 0) throw std::runtime_error("tensor parallelism: follower ranks only run follow()");
+  if (!tp_ctl_) throw std::runtime_error("tensor parallelism: the control channel is not open (tp_ctl_create)");
+  if (tp_stopped_) throw std::runtime_error("tensor parallelism: the group was stopped");
+  tp_ctl_->publish(m);
+}
+
+void Engine::tp_ctl_create(const std::string& name) {
+  if (opt_.tp_size < 2 || opt_.tp_rank != 0) throw std::runtime_error("tp_ctl_create: rank 0 of a TP group only");
+  // largest command: a prefill chunk / a whole prompt plus sampling options
+  const size_t cap = 4096 + sizeof(int) * (size_t)std::max(opt_.n_ctx, opt_.n_batch) + 16 * kMaxLogitBias;
+  tp_ctl_ = TPChannel::create(name, opt_.tp_size, cap);
+}
+
+void Engine::tp_ctl_attach(const std::string& name) {
+  if (opt_.tp_size < 2 || opt_.tp_rank == 0) throw std::runtime_error("tp_ctl_attach: follower ranks only");
+  tp_ctl_ = TPChannel::attach(name, opt_.tp_rank);
+}
+
+void Engine::tp_stop() {
+  if (!leader() || !tp_ctl_ || tp_stopped_) return;
+  ExecGuard guard(this);
+  TPMsg m;
+  m.put<int32_t>(TPO_STOP);
+  tp_ctl_->publish(m);
+  tp_stopped_ = true;
+}
+
+// Follower ranks: replay rank 0's commands until TPO_STOP. A failing command marks this
+// rank unhealthy (rank 0's next collective then times out and reports it) and the loop
+// goes on, so a later STOP still ends it.
+void Engine::follow() {
+  if (!tp_ctl_ || opt_.tp_rank == 0) throw std::runtime_error("follow: attach a follower rank first");
+  TPMsg m;
+  while (true) {
+    if (!tp_ctl_->receive(m, 1000)) {
+      if (!tp_ctl_->leader_alive()) throw std::runtime_error("follow: rank 0 exited without stopping the group");
+      continue;
+    }
+    const int32_t op = m.get<int32_t>();
+    ExecGuard guard(this);
+    if (op == TPO_STOP) {
+      HIPCHK(hipStreamSynchronize(stream_));
+      return;
+    }
+    try {
+      switch (op) {
+        case TPO_SLOT_STATE: {
+          const int slot = m.get<int>();
+          const std::vector<int> prompt = m.get_vec<int>();
+          begin_slot_state(slot, prompt, get_sp(m));
+          break;
+        }
+        case TPO_PREFILL: {
+          const int slot = m.get<int>(), pos = m.get<int>(), head = m.get<int>();
+          const std::vector<int> toks = m.get_vec<int>();
+          prefill_chunk(slot, toks.data(), (int)toks.size(), pos, head != 0);
+          break;
+        }
+        case TPO_DECODE_STEP: launch_step(); break;
+        case TPO_SYNC:
+          HIPCHK(hipStreamSynchronize(stream_));
+          check_device_err();
+          break;
+        case TPO_SLOT_BEGIN: {
+          const int slot = m.get<int>(), n_keep = m.get<int>();
+          const std::vector<int> prompt = m.get_vec<int>();
+          slot_begin_impl(slot, prompt, n_keep, get_sp(m));
+          break;
+        }
+        case TPO_BATCH_STEP: batch_step_impl(m.get_vec<int>()); break;
+        case TPO_EVAL_LOGITS: {
+          const int pos0 = m.get<int>();
+          eval_logits_impl(m.get_vec<int>(), pos0);
+          break;
+        }
+        case TPO_DECODE_LOGITS: {
+          const int tok = m.get<int>(), pos = m.get<int>();
+          decode_logits_impl(tok, pos);
+          break;
+        }
+        case TPO_BATCH_LOGITS: batch_logits_impl(m.get<int>()); break;
+        case TPO_BENCH_DECODE: {
+          const int n = m.get<int>(), pos0 = m.get<int>();
+          bench_decode_impl(n, pos0);
+          break;
+        }
+        default: throw std::runtime_error("follow: unknown command " + std::to_string(op));
+      }
+    } catch (const std::exception& e) {
+      healthy_ = false;
+      last_error_ = std::string("follower rank ") + std::to_string(opt_.tp_rank) + ": " + e.what();
+      fprintf(stderr, "[lfk] %s\n", last_error_.c_str());
+    }
+  }
+}
+
+// ------------------------------------------------------------------------ serving entry points
+// Each takes the execution guard, validates its arguments (so a follower never receives a
+// command that fails validation), publishes the command under TP, then runs the *_impl.
+
+void Engine::prefill_chunk(int slot, const int* toks, int T, int pos, bool head) {
+  kv_slot_ = slot;
+  try {
+    std::memcpy(h_tokens_, toks, sizeof(int) * T);
+    HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+    enqueue_prefill(T, pos, stream_);
+    if (head) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_, slot);
+    HIPCHK(hipStreamSynchronize(stream_));  // h_tokens_ is reused by the next chunk
+  } catch (...) {
+    kv_slot_ = 0;
+    throw;
+  }
+  kv_slot_ = 0;
+}
+
+int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {
+  ExecGuard guard(this);
+  if (!bmax_) throw std::runtime_error("slot_begin: the engine was built with one KV slot");
+  if (slot < 0 || slot >= opt_.n_slots) throw std::runtime_error("slot_begin: slot out of range");
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  (void)make_sparams(sp);  // validates top_k / logit_bias before any rank starts
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_SLOT_BEGIN); m.put(slot); m.put(n_keep); m.put_vec(prompt); put_sp(m, sp);
+    mirror(m);
+  }
+  return slot_begin_impl(slot, prompt, n_keep, sp);
+}
+
+int Engine::slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {
+  const int n_prompt = (int)prompt.size();
+  begin_slot_state(slot, prompt, sp);
+  int pos = n_keep;
+  while (pos < n_prompt) {
+    const int T = std::min(opt_.n_batch, n_prompt - pos);
+    prefill_chunk(slot, prompt.data() + pos, T, pos, pos + T == n_prompt);
+    pos += T;
+  }
+  int tok = 0;
+  HIPCHK(hipMemcpy(&tok, state_ + (size_t)S_NSTATE * slot + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
+  check_device_err();
+  return tok;
 }
 
 std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
@@ -890,6 +1128,29 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
     for (int c = 0; c < b; ++c)
       if (slots[c] == slots[b]) throw std::runtime_error("batch_step: duplicate slot");
   }
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_BATCH_STEP); m.put_vec(slots);
+    mirror(m);
+  }
+  return batch_step_impl(slots);
+}
+
+std::vector<int> Engine::batch_step_impl(const std::vector<int>& slots) {
+  const int B = (int)slots.size();
+  if (B == 1 && b1_gemv_) {
+    // one active row: the single-row GEMV decode of that slot beats the batched projections
+    launch_step(slots[0]);
+    HIPCHK(hipMemcpyAsync(h_btok_, state_ + (size_t)S_NSTATE * slots[0] + S_TOKEN, sizeof(int),
+                          hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipGetLastError());
+    check_device_err();
+    last_batch_ = 1;
+    last_b1_ = true;
+    return std::vector<int>(h_btok_, h_btok_ + 1);
+  }
+  last_b1_ = false;
   std::memcpy(h_bslots_, slots.data(), sizeof(int) * B);
   HIPCHK(hipMemcpyAsync(bslots_, h_bslots_, sizeof(int) * B, hipMemcpyHostToDevice, stream_));
   if (opt_.use_graph) {
@@ -915,12 +1176,53 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
   return std::vector<int>(h_btok_, h_btok_ + B);
 }
 
+// Rows [0, B) of a logits buffer with row pitch ld_src holding this rank's vocabulary shard
+// -> full rows [B][n_vocab] on the host (under TP: one all-gather of the shards).
+void Engine::gather_logits_rows(int B, size_t ld_src, const float* src, std::vector<float>& out) {
+  const int V = hp_.n_vocab, tp = opt_.tp_size;
+  out.assign((size_t)B * V, 0.f);
+  if (tp == 1) {
+    HIPCHK(hipMemcpy2DAsync(out.data(), sizeof(float) * V, src, sizeof(float) * ld_src, sizeof(float) * V, B,
+                            hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    return;
+  }
+  // pack the shard rows [B][V_l] contiguously, all-gather -> [tp][B][V_l]
+  float* packed = nullptr;
+  float* all = nullptr;
+  HIPCHK(hipMalloc((void**)&packed, sizeof(float) * B * V_l_));
+  HIPCHK(hipMalloc((void**)&all, sizeof(float) * B * V_l_ * tp));
+  HIPCHK(hipMemcpy2DAsync(packed, sizeof(float) * V_l_, src, sizeof(float) * ld_src, sizeof(float) * V_l_, B,
+                          hipMemcpyDeviceToDevice, stream_));
+  allgather_into(packed, all, (size_t)B * V_l_, stream_);
+  std::vector<float> h((size_t)B * V_l_ * tp);
+  HIPCHK(hipMemcpyAsync(h.data(), all, sizeof(float) * h.size(), hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(hipFree(packed));
+  HIPCHK(hipFree(all));
+  for (int r = 0; r < tp; ++r) {
+    const int n = std::max(0, std::min(V_l_, V - r * V_l_));
+    for (int b = 0; b < B; ++b)
+      std::memcpy(out.data() + (size_t)b * V + (size_t)r * V_l_, h.data() + ((size_t)r * B + b) * V_l_,
+                  sizeof(float) * n);
+  }
+}
+
 std::vector<float> Engine::batch_logits(int B) {
   ExecGuard guard(this);
   if (!bmax_ || B < 1 || B > last_batch_) throw std::runtime_error("batch_logits: no such rows in the last batch_step");
-  std::vector<float> out((size_t)B * hp_.n_vocab);
-  HIPCHK(hipMemcpy2D(out.data(), sizeof(float) * hp_.n_vocab, logits_b_, sizeof(float) * V_pad_,
-                     sizeof(float) * hp_.n_vocab, B, hipMemcpyDeviceToHost));
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_BATCH_LOGITS); m.put(B);
+    mirror(m);
+  }
+  return batch_logits_impl(B);
+}
+
+std::vector<float> Engine::batch_logits_impl(int B) {
+  std::vector<float> out;
+  if (last_b1_) gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
+  else gather_logits_rows(B, V_pad_, logits_b_, out);
   return out;
 }
 
@@ -932,25 +1234,34 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   const int n_prompt = (int)prompt.size();
   if (n_prompt == 0) throw std::runtime_error("empty prompt");
   if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  (void)make_sparams(sp);
   if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
   const double t0 = now_s();
 
   // per-request device state: sampling params, penalty ring (prompt tail), counters
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_SLOT_STATE); m.put<int>(0); m.put_vec(prompt); put_sp(m, sp);
+    mirror(m);
+  }
   begin_slot_state(0, prompt, sp);
 
   // prefill in n_batch chunks
   int pos = n_keep;
   {
-  RoctxRange prefill_range("lfk.prefill");
-  while (pos < n_prompt) {
-    const int T = std::min(opt_.n_batch, n_prompt - pos);
-    std::memcpy(h_tokens_, prompt.data() + pos, sizeof(int) * T);
-    HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
-    enqueue_prefill(T, pos, stream_);
-    pos += T;
-    if (pos == n_prompt) enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
-    HIPCHK(hipStreamSynchronize(stream_));  // h_tokens_ is reused by the next chunk
-  }
+    RoctxRange prefill_range("lfk.prefill");
+    while (pos < n_prompt) {
+      const int T = std::min(opt_.n_batch, n_prompt - pos);
+      const bool head = pos + T == n_prompt;
+      if (leader()) {
+        TPMsg m;
+        m.put<int32_t>(TPO_PREFILL); m.put<int>(0); m.put(pos); m.put<int>(head ? 1 : 0);
+        m.put_vec(std::vector<int>(prompt.begin() + pos, prompt.begin() + pos + T));
+        mirror(m);
+      }
+      prefill_chunk(0, prompt.data() + pos, T, pos, head);
+      pos += T;
+    }
   }
   HIPCHK(hipGetLastError());
   const double t1 = now_s();
@@ -960,6 +1271,17 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   auto is_stop = [&](int t) {
     for (int s : stop_ids) if (s == t) return true;
     return false;
+  };
+  // one decode step: the followers replay exactly the steps rank 0 launches, so a stop
+  // token, a cancel or max_new on rank 0 ends every rank at the same step
+  auto step = [&](int k) {
+    if (leader()) {
+      TPMsg m;
+      m.put<int32_t>(TPO_DECODE_STEP);
+      mirror(m);
+    }
+    launch_step();
+    HIPCHK(hipEventRecord(step_ev_[k % kDepth], stream_));
   };
   RoctxRange decode_range("lfk.decode");
   int tok = h_ring_[0];
@@ -971,11 +1293,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
     out.finish = "stop";
   } else if (max_steps > 0) {
     int launched = 0;
-    while (launched < std::min(kDepth, max_steps)) {
-      launch_step();
-      HIPCHK(hipEventRecord(step_ev_[launched % kDepth], stream_));
-      ++launched;
-    }
+    while (launched < std::min(kDepth, max_steps)) step(launched++);
     for (int i = 1; i <= max_steps; ++i) {
       HIPCHK(hipEventSynchronize(step_ev_[(i - 1) % kDepth]));
       tok = h_ring_[i & 63];
@@ -983,13 +1301,14 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
       if (on_token) on_token(tok);
       if (is_stop(tok)) { out.finish = "stop"; break; }
       if (poll && (i & 3) == 0 && poll()) { out.finish = "cancelled"; break; }
-      if (launched < max_steps) {
-        launch_step();
-        HIPCHK(hipEventRecord(step_ev_[launched % kDepth], stream_));
-        ++launched;
-      }
+      if (launched < max_steps) step(launched++);
     }
     HIPCHK(hipStreamSynchronize(stream_));
+  }
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_SYNC);
+    mirror(m);
   }
   HIPCHK(hipGetLastError());
   out.decode_s = now_s() - t1;
@@ -1001,7 +1320,17 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
 std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0) {
   ExecGuard guard(this);
   const int T = (int)tokens.size();
-  if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_logits: bad size");
+  if (T <= 0 || T > opt_.n_batch || pos0 < 0 || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_logits: bad size");
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_EVAL_LOGITS); m.put(pos0); m.put_vec(tokens);
+    mirror(m);
+  }
+  return eval_logits_impl(tokens, pos0);
+}
+
+std::vector<float> Engine::eval_logits_impl(const std::vector<int>& tokens, int pos0) {
+  const int T = (int)tokens.size();
   SamplerParamsDev p;
   p.greedy = 1; p.top_k = 1; p.repeat_penalty = 1.f;
   int hstate[S_NSTATE] = {0};
@@ -1012,14 +1341,14 @@ std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0)
   HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
   enqueue_prefill(T, pos0, stream_);
   enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
-  std::vector<float> out(hp_.n_vocab);
-  HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  std::vector<float> out;
+  gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
   return out;
 }
 
 std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
   ExecGuard guard(this);
+  if (opt_.tp_size > 1) throw std::runtime_error("eval_hidden: not available with tensor parallelism");
   if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_hidden: bad size");
   HIPCHK(hipMemcpyAsync(x_, x, sizeof(float) * T * hp_.n_embd, hipMemcpyHostToDevice, stream_));
   enqueue_prefill(T, pos0, stream_, /*embed=*/false);
@@ -1032,6 +1361,8 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
 
 void Engine::kv_transfer(void* buf, int n, bool load) {
   ExecGuard guard(this);
+  if (opt_.tp_size > 1)
+    throw std::runtime_error("KV snapshots hold one rank's heads: not available with tensor parallelism");
   if (n < 0 || n > opt_.n_ctx) throw std::runtime_error("kv_transfer: n out of range");
   if (n == 0) return;
   const size_t row = (size_t)n * hp_.head_dim * 2, pitch = (size_t)opt_.n_ctx * hp_.head_dim * 2;
@@ -1050,7 +1381,16 @@ void Engine::kv_transfer(void* buf, int n, bool load) {
 
 std::vector<float> Engine::decode_logits(int token, int pos) {
   ExecGuard guard(this);
-  if (pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
+  if (pos < 0 || pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_DECODE_LOGITS); m.put(token); m.put(pos);
+    mirror(m);
+  }
+  return decode_logits_impl(token, pos);
+}
+
+std::vector<float> Engine::decode_logits_impl(int token, int pos) {
   SamplerParamsDev p;
   p.greedy = 1; p.top_k = 1; p.repeat_penalty = 1.f;
   int hstate[S_NSTATE] = {0};
@@ -1059,16 +1399,24 @@ std::vector<float> Engine::decode_logits(int token, int pos) {
   HIPCHK(hipMemcpyAsync(sparams_, &p, sizeof(p), hipMemcpyHostToDevice, stream_));
   HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
   launch_step();
-  std::vector<float> out(hp_.n_vocab);
-  HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
+  std::vector<float> out;
+  gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
   check_device_err();
   return out;
 }
 
 void Engine::bench_decode(int n_steps, int pos0, double* ms_per_step) {
   ExecGuard guard(this);
-  if (n_steps < 1 || pos0 + n_steps + 1 > opt_.n_ctx) throw std::runtime_error("bench_decode: exceeds n_ctx");
+  if (n_steps < 1 || pos0 < 0 || pos0 + n_steps + 1 > opt_.n_ctx) throw std::runtime_error("bench_decode: exceeds n_ctx");
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_BENCH_DECODE); m.put(n_steps); m.put(pos0);
+    mirror(m);
+  }
+  *ms_per_step = bench_decode_impl(n_steps, pos0);
+}
+
+double Engine::bench_decode_impl(int n_steps, int pos0) {
   SamplerParamsDev p;
   p.greedy = 1; p.top_k = 1;
   int hstate[S_NSTATE] = {0};
@@ -1081,8 +1429,9 @@ void Engine::bench_decode(int n_steps, int pos0, double* ms_per_step) {
   const double t0 = now_s();
   for (int i = 0; i < n_steps; ++i) launch_step();
   HIPCHK(hipStreamSynchronize(stream_));
-  *ms_per_step = (now_s() - t0) * 1e3 / n_steps;
+  const double ms = (now_s() - t0) * 1e3 / n_steps;
   check_device_err();
+  return ms;
 }
 
 }  // namespace lfk

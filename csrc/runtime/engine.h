@@ -22,6 +22,7 @@
 #include "gguf.h"
 #include "p2p.h"
 #include "slots.h"
+#include "tp_channel.h"
 
 namespace lfk {
 
@@ -39,11 +40,15 @@ struct EngineOptions {
   bool use_graph = true;
   int tp_rank = 0;
   int tp_size = 1;
-  std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1)
+  std::string nccl_id;  // ncclUniqueId bytes (tp_size > 1, comm != "ipc")
+  // tensor-parallel collectives: "auto" = one-shot P2P kernel for decode-sized messages +
+  // RCCL for the rest; "ipc" = P2P for every message, no RCCL (ranks may share a GPU - the
+  // one-GPU test box); "rccl" = RCCL only
+  std::string comm = "auto";
   std::vector<float> tensor_split;  // per-rank weights (empty = even); see shard.h
   int layer_begin = 0;  // hybrid placement: layers [0, layer_begin) run on the CPU backend
   // KV slots (continuous batching): slot 0 serves generate() / the graph decode path, slots
-  // [0, n_slots) can decode together through batch_step()
+  // [0, n_slots) can decode together through batch_step() (also under tensor parallelism)
   int n_slots = 1;
   bool verbose = false;
 };
@@ -98,6 +103,13 @@ class Engine : public SlotBackend {
   std::string p2p_handle();
   void p2p_open(const std::vector<std::string>& handles);
   bool p2p_ready() const { return p2p_ && p2p_->ready(); }
+  // tensor parallelism: the host control channel (tp_channel.h). Rank 0 creates it, the
+  // followers attach and then sit in follow() replaying rank 0's commands until tp_stop().
+  void tp_ctl_create(const std::string& name);
+  void tp_ctl_attach(const std::string& name);
+  void follow();
+  void tp_stop();
+  bool tp_ctl_open() const { return tp_ctl_ != nullptr; }
   bool healthy() const { return healthy_; }
   std::string last_error() const { return last_error_; }
   int n_ctx() const override { return opt_.n_ctx; }
@@ -142,6 +154,21 @@ class Engine : public SlotBackend {
   void build_rope();
 
   void allreduce_into(const float* send, float* recv, size_t n, hipStream_t s);
+  void allgather_into(const float* send, float* recv, size_t n, hipStream_t s);  // recv [tp][n]
+  // the sampler over this rank's logits rows (vocabulary shard under TP): stage 1, the
+  // candidate all-gather, stage 2 (single row: slot; batched: the bslots_ rows)
+  void enqueue_sample(const float* logits, int rows, size_t ld, int slot, int advance_pos, hipStream_t s);
+  void gather_logits_rows(int B, size_t ld_src, const float* src, std::vector<float>& out);
+  // tensor parallelism: publish a command to the followers (rank 0); no-op on one rank
+  bool leader() const { return opt_.tp_size > 1 && opt_.tp_rank == 0; }
+  void mirror(const TPMsg& m);
+  void prefill_chunk(int slot, const int* toks, int T, int pos, bool head);
+  int slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp);
+  std::vector<int> batch_step_impl(const std::vector<int>& slots);
+  std::vector<float> eval_logits_impl(const std::vector<int>& tokens, int pos0);
+  std::vector<float> decode_logits_impl(int token, int pos);
+  std::vector<float> batch_logits_impl(int B);
+  double bench_decode_impl(int n_steps, int pos0);
   void enqueue_layer_decode(int l, hipStream_t s);
   void enqueue_decode(hipStream_t s);
   void enqueue_prefill(int T, int pos0, hipStream_t s, bool embed = true);
@@ -159,7 +186,7 @@ class Engine : public SlotBackend {
   void setup_batch_mfma();
   SamplerParamsDev make_sparams(const SamplingOpts& sp) const;
   void begin_slot_state(int slot, const std::vector<int>& prompt, const SamplingOpts& sp);
-  void launch_step();
+  void launch_step(int slot = 0);  // one decode step of `slot` on the single-row GEMV path
   void check(hipError_t e, const char* what);
   void check_device_err();
 
@@ -168,6 +195,9 @@ class Engine : public SlotBackend {
   hipStream_t stream_ = nullptr;
   void* comm_ = nullptr;  // ncclComm_t
   std::unique_ptr<P2PComm> p2p_;
+  int p2p_max_n_ = 0;       // floats per P2P message (decode-sized, or everything in "ipc" mode)
+  std::unique_ptr<TPChannel> tp_ctl_;
+  bool tp_stopped_ = false;
   std::vector<void*> allocs_;
   size_t dev_bytes_ = 0;
   bool healthy_ = true;
@@ -175,6 +205,7 @@ class Engine : public SlotBackend {
 
   // local (per-rank) sizes
   int nh_l_ = 0, nkv_l_ = 0, nq_ = 0, nkvd_ = 0, F_l_ = 0, V_l_ = 0, V_pad_ = 0;
+  int V_real_l_ = 0;          // real vocabulary rows of this rank's shard (<= V_l_)
   size_t q0_ = 0, kv0_ = 0, f0_ = 0;   // this rank's first q row / kv row / FFN feature
 
   // weights
@@ -206,9 +237,9 @@ class Engine : public SlotBackend {
   // gate/up range (LFK_ATTN_TOUCH_GU_FRAC of it, clamped to (0, 1])
   int attn_touch_ = 1;
   double attn_touch_gu_frac_ = 0.3;
-  float* cand_val_ = nullptr;
-  int* cand_idx_ = nullptr;
-  unsigned* cand_tau_ = nullptr;
+  size_t cand_words_ = 0;     // sampler candidate block of one row (sampler_cand_words(V_l))
+  unsigned* cand_ = nullptr;  // [cand_words_] this rank's stage-1 block (single row)
+  unsigned* cand_all_ = nullptr;   // [tp][cand_words_] gathered blocks (tp > 1)
   int* state_ = nullptr;
   int* ring_ = nullptr;
   int* out_tokens_ = nullptr;
@@ -235,9 +266,8 @@ class Engine : public SlotBackend {
   int* btok_ = nullptr;       // [bmax] current token of each row
   int* btok_out_ = nullptr;   // [bmax] sampled tokens
   float* logits_b_ = nullptr; // [bmax][V_pad]
-  float* cand_val_b_ = nullptr;
-  int* cand_idx_b_ = nullptr;
-  unsigned* cand_tau_b_ = nullptr;
+  unsigned* cand_b_ = nullptr;      // [bmax][cand_words_]
+  unsigned* cand_all_b_ = nullptr;  // [tp][bmax][cand_words_]
   float* attn_part_b_ = nullptr;   // [bmax][attn_decode_workspace_floats]
   int* attn_cnt_b_ = nullptr;      // [bmax][64]
   int* h_bslots_ = nullptr;   // pinned [bmax]
@@ -259,6 +289,13 @@ class Engine : public SlotBackend {
   bool wo_one_part_ = false;  // Wo as one K part (LFK_BMM_WO1=1, A/B)
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
+  // single-row decode (GEMV path) of KV slot dslot_: enqueue_decode reads it while capturing;
+  // one graph per slot (slot 0's is graph_exec_). batch_step over ONE row takes this path
+  // (LFK_B1_GEMV=0: the batched projections), the faster one at B = 1
+  int dslot_ = 0;
+  std::vector<hipGraphExec_t> sgraph_;
+  bool b1_gemv_ = true;
+  bool last_b1_ = false;      // the last batch_step ran its one row on the single-row path
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;
   static constexpr int kDepth = 2;

@@ -10,11 +10,11 @@ static void p2pchk(hipError_t e, const char* what) {
 }
 
 P2PComm::P2PComm(int rank, int world, int max_n, int device)
-    : rank_(rank), world_(world), max_n_(max_n), device_(device) {
+    : rank_(rank), world_(world), max_n_((max_n + 3) & ~3), device_(device) {
   if (world < 1 || world > kP2PMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("p2p: bad rank/world");
   if (max_n <= 0) throw std::runtime_error("p2p: bad max_n");
   p2pchk(hipSetDevice(device_), "hipSetDevice");
-  data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n;
+  data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n_;
   data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
   region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
   p2pchk(hipMalloc(&region_, region_bytes_), "hipMalloc region");
@@ -62,15 +62,18 @@ void P2PComm::open(const std::vector<std::string>& handles) {
   ready_ = true;
 }
 
-void P2PComm::allreduce(const float* src, float* dst, int n, hipStream_t s) {
+void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_t s) {
   if (!ready_) throw std::runtime_error("p2p: open() the peer handles first");
-  P2PAllreduceArgs a;
+  P2PArgs a;
   a.peers = peers_;
-  a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_;
-  a.blocks = std::min(kP2PMaxBlocks, std::max(1, (n + 255) / 256));
+  a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_; a.gather = gather;
   a.epochs = epochs_; a.err = err_;
-  p2p_allreduce(a, s);
+  p2p_collective(a, s);
 }
+
+void P2PComm::allreduce(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 0, s); }
+
+void P2PComm::allgather(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 1, s); }
 
 int P2PComm::error() const {
   int e = 0;

@@ -1,7 +1,8 @@
-// Host side of the one-shot P2P all-reduce: owns this rank's
+// Host side of the one-shot P2P collectives: owns this rank's
 // receive region (exported with a hipIpc handle) and the peers' imported
-// regions; dispatches decode-sized all-reduces to kernels/p2p_allreduce.hip.
-// One process per GPU: handles are exchanged by the caller (torch.distributed).
+// regions; dispatches all-reduces and all-gathers of up to max_n floats to
+// kernels/p2p_allreduce.hip. One process per GPU (or, in the IPC-only test mode,
+// several per GPU): handles are exchanged by the caller (torch.distributed).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -24,6 +25,7 @@ class P2PComm {
   bool ready() const { return ready_; }
   int max_n() const { return max_n_; }
   void allreduce(const float* src, float* dst, int n, hipStream_t s);
+  void allgather(const float* src, float* dst, int n, hipStream_t s);  // dst [world][n]
   int error() const;                                   // device error word (0 = ok)
   void reset_error();
 
@@ -36,6 +38,7 @@ class P2PComm {
   int* err_ = nullptr;
   P2PPeers peers_;
   bool ready_ = false;
+  void launch(const float* src, float* dst, int n, int gather, hipStream_t s);
 };
 
 }  // namespace lfk

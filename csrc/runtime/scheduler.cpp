@@ -201,6 +201,7 @@ void BatchScheduler::loop() {
       r->n_prefilled = n_prompt - n_keep;
       slot_hist_[slot] = r->prompt;
       push_token(*r, tok);
+      cv_out_.notify_all();  // the first token reaches its waiter now, not after the next step
     }
     // 3. one decode step over every active row
     rows.clear();

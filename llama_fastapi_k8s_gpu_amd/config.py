@@ -77,8 +77,13 @@ class Settings:
     timeout_seconds: float = 25.0
     max_queue_size: int = 5
     message_char_cap: int = 400        # reference api.py:36-39
-    parity_mode: bool = True            # keep the reference's prompt heuristics exactly
-    exact_token_guard: bool = False     # tokenizer-exact trim behind a flag
+    # True: the reference's prompt heuristics exactly (the 400-char cap applies to the system
+    # message too, C6). False: system messages keep their full text.
+    parity_mode: bool = True
+    # after the char/4 trim, drop oldest messages by REAL token count so the
+    # prompt stays below n_ctx - exact_token_reserve (no 500 on token-dense text)
+    exact_token_guard: bool = False
+    exact_token_reserve: int = 32       # tokens kept free for the answer under the guard
     cooperative_cancel: bool = True     # stop timed-out generations
     openai_api: bool = True             # /v1/models, /v1/completions, /v1/chat/completions
     sampling: SamplingDefaults = field(default_factory=SamplingDefaults)
@@ -114,6 +119,7 @@ class Settings:
         s.message_char_cap = _env("MESSAGE_CHAR_CAP", s.message_char_cap, int)
         s.parity_mode = _env("PARITY_MODE", s.parity_mode, bool)
         s.exact_token_guard = _env("EXACT_TOKEN_GUARD", s.exact_token_guard, bool)
+        s.exact_token_reserve = max(1, _env("EXACT_TOKEN_RESERVE", s.exact_token_reserve, int))
         s.cooperative_cancel = _env("COOPERATIVE_CANCEL", s.cooperative_cancel, bool)
         s.openai_api = _env("OPENAI_API", s.openai_api, bool)
         sp = s.sampling

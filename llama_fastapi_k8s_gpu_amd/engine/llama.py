@@ -16,6 +16,7 @@ the default sampler chain and values.
 """
 from __future__ import annotations
 
+import itertools
 import logging
 import os
 import threading
@@ -80,8 +81,9 @@ class Llama:
         self.last_n_tokens_size = last_n_tokens_size
         self.verbose = verbose
         self._seed = seed if seed is not None else int.from_bytes(os.urandom(4), "little")
-        self._n_requests = 0
+        self._request_ids = itertools.count(1)   # per-request seed derivation (thread-safe)
         self._lock = threading.Lock()
+        self._gvocab_lock = threading.Lock()
         bos = self.tokenizer.tokens[self.tokenizer.bos_id] if self.tokenizer.bos_id >= 0 else ""
         eos = self.tokenizer.tokens[self.tokenizer.eos_id] if self.tokenizer.eos_id >= 0 else ""
         self.chat_format, self._formatter = get_formatter(self.metadata, chat_format, bos, eos)
@@ -124,6 +126,11 @@ class Llama:
             text = text.decode("utf-8", errors="replace")
         return self.tokenizer.encode(text, add_bos=add_bos, special=special)
 
+    def count_chat_tokens(self, messages: List[Dict[str, str]]) -> int:
+        """Prompt tokens create_chat_completion would evaluate for these messages."""
+        fr = self._formatter(messages)
+        return len(self.tokenize(fr.prompt, add_bos=not fr.added_special, special=True))
+
     def detokenize(self, tokens: Sequence[int], special: bool = False) -> bytes:
         return self.tokenizer.detokenize_bytes(tokens, special)
 
@@ -133,6 +140,22 @@ class Llama:
         if bh:
             h.update(bh())
         return h
+
+    @property
+    def batch_width(self) -> int:
+        """Generations the backend runs at once (its continuous batch; 1 without a scheduler)."""
+        if getattr(self._backend, "sched", None) is not None:
+            return max(1, int(getattr(self._backend, "max_batch", 1)))
+        return 1
+
+    @property
+    def follows(self) -> bool:
+        """This process is a follower rank of a tensor-parallel group (see follow())."""
+        return bool(getattr(self._backend, "follows", False))
+
+    def follow(self):
+        """Follower ranks: replay rank 0's engine commands until rank 0 closes the group."""
+        self._backend.follow()
 
     def device_memory(self) -> Dict[str, int]:
         f = getattr(self._backend, "device_memory", None)
@@ -279,8 +302,7 @@ class Llama:
                 mirostat_tau=5.0, mirostat_eta=0.1, n_probs=0, logits_processor=None,
                 grammar=None) -> SamplingParams:
         if seed is None:
-            self._n_requests += 1
-            seed = (self._seed * 1000003 + self._n_requests) & 0xFFFFFFFF
+            seed = (self._seed * 1000003 + next(self._request_ids)) & 0xFFFFFFFF
         bias = {int(k): float(v) for k, v in (logit_bias or {}).items()}
         return SamplingParams(temperature=temperature, top_k=top_k, top_p=top_p, min_p=min_p,
                               typical_p=typical_p, tfs_z=tfs_z, repeat_penalty=repeat_penalty,
@@ -297,10 +319,11 @@ class Llama:
         from .grammar import GrammarState, GrammarVocab, LlamaGrammar
         if isinstance(grammar, str):
             grammar = LlamaGrammar.from_string(grammar)
-        if getattr(self, "_gvocab", None) is None:
-            n = self.n_vocab()
-            self._gvocab = GrammarVocab([self.tokenizer.detokenize_bytes([t], False) for t in range(n)],
-                                        self.tokenizer.eog_ids)
+        with self._gvocab_lock:   # concurrent batched requests may build it at once
+            if getattr(self, "_gvocab", None) is None:
+                n = self.n_vocab()
+                self._gvocab = GrammarVocab([self.tokenizer.detokenize_bytes([t], False) for t in range(n)],
+                                            self.tokenizer.eog_ids)
         return GrammarState(grammar, self._gvocab)
 
     @staticmethod

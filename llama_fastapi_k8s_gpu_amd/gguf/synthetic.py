@@ -107,15 +107,9 @@ SPECS: Dict[str, ModelSpec] = {
     # weight touch's per-CU gate/up segments must clamp to the plane end)
     "tiny-q8-oddff": ModelSpec("tiny-q8-oddff", 256, 2, 4, 2, 576, 0, 10000.0, "spm", "q8_0",
                                n_ctx_train=1024),
-    # smallest shapes the persistent decode kernel takes on a 256-CU MI355X (d = 4096 rows split
-    # 16 per CU, kv heads onto CU groups): 4 layers (Q4_K_M mix: layers 0 and 3 bump V/down to
-    # Q6_K), GQA groups of 4 and of 8
+    # d = 4096 with the Llama-3 GQA grouping (32 q heads on 8 kv heads), 4 layers (Q4_K_M mix:
+    # layers 0 and 3 bump V/down to Q6_K): full-width kernels at test cost
     "pd-llama-g4": ModelSpec("pd-llama-g4", 4096, 4, 32, 8, 2048, 0, 500000.0, "bpe", "q4_k_m",
-                             n_ctx_train=1024),
-    # two layers of the exact Llama-3-8B layer shape (F = 14336: multi-item ring stages)
-    "pd-llama-8b2": ModelSpec("pd-llama-8b2", 4096, 2, 32, 8, 14336, 0, 500000.0, "bpe", "q4_k_m",
-                              n_ctx_train=1024),
-    "pd-llama-g8": ModelSpec("pd-llama-g8", 4096, 4, 32, 4, 2048, 0, 500000.0, "bpe", "q4_k_m",
                              n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),

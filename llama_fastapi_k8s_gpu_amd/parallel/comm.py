@@ -62,6 +62,14 @@ def broadcast_nccl_id(make_id: Callable[[], bytes]) -> bytes:
     return obj[0]
 
 
+def broadcast_object(obj, src: int = 0, group=None):
+    """Rank `src`'s object on every rank."""
+    import torch.distributed as dist
+    box = [obj]
+    dist.broadcast_object_list(box, src=src, group=group)
+    return box[0]
+
+
 def allgather_bytes(b: bytes, group=None) -> list:
     """Every rank's bytes object, in rank order (IPC handle exchange)."""
     import torch.distributed as dist

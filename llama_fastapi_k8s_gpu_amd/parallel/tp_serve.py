@@ -2,15 +2,20 @@
 
 The reference serves one model per pod from one process (gunicorn -w 1,
 reference docker/Dockerfile.app:12). With ``split_mode=row`` over N GPUs every
-rank holds a shard and must run every generation in lock-step (its RCCL
-all-reduces pair with the other ranks'). Rank 0 owns the HTTP server and the
-admission queue unchanged; before each engine call it broadcasts the call's
-arguments over a CPU (gloo) control group and the follower ranks replay it.
+rank holds a shard and must run every generation in lock-step (its all-reduces
+pair with the other ranks'). Rank 0 owns the HTTP server and the admission
+queue unchanged.
 
-Generation is deterministic across ranks (identical all-reduced activations,
-identical gathered logits, shared seed), so every rank stops at the same token
-without further coordination. Cooperative cancel is disabled in this mode: a
-leader that stopped early would leave followers blocked in a collective.
+  * MI355X engine: the engine itself mirrors every command rank 0 runs to the
+    followers over a native shared-memory channel (csrc/runtime/tp_channel.h);
+    followers call ``Llama.follow()``. Continuous batching and cooperative
+    cancel work as on one GPU (a cancelled row simply gets no further steps).
+  * CPU backend (shard-plan validation): ``TPLeader`` broadcasts each
+    facade call over a gloo control group and ``follower_loop`` replays it.
+    Generation is deterministic across ranks, so every rank stops at the same
+    token; cooperative cancel is off there (a leader that stopped early would
+    leave followers blocked in a collective), and one lock keeps the broadcast
+    order equal to the execution order.
 """
 from __future__ import annotations
 
@@ -25,12 +30,17 @@ _LONG = datetime.timedelta(days=365)   # followers may idle between requests
 
 
 class TPLeader:
-    """Engine wrapper for rank 0: mirrors each call to the follower ranks."""
+    """Engine wrapper for rank 0 (CPU backend): mirrors each call to the follower ranks."""
     supports_cancel = False
+    batch_width = 1
 
     def __init__(self, llm, group=None):
+        import threading
         self.llm = llm
         self.group = group
+        # broadcast + generate as one critical section: the followers replay calls in
+        # broadcast order, which must be the order rank 0 runs them
+        self._lock = threading.Lock()
 
     def _send(self, op: str, kw: Optional[Dict[str, Any]]):
         import torch.distributed as dist
@@ -38,13 +48,15 @@ class TPLeader:
 
     def create_chat_completion(self, **kw):
         kw.pop("cancel_event", None)
-        self._send("chat", kw)
-        return self.llm.create_chat_completion(**kw)
+        with self._lock:
+            self._send("chat", kw)
+            return self.llm.create_chat_completion(**kw)
 
     def create_completion(self, prompt, **kw):
         kw.pop("cancel_event", None)
-        self._send("completion", dict(kw, prompt=prompt))
-        return self.llm.create_completion(prompt, **kw)
+        with self._lock:
+            self._send("completion", dict(kw, prompt=prompt))
+            return self.llm.create_completion(prompt, **kw)
 
     def health(self):
         return self.llm.health()
@@ -53,7 +65,8 @@ class TPLeader:
         return self.llm.device_memory()
 
     def close(self):
-        self._send("stop", None)
+        with self._lock:
+            self._send("stop", None)
         self.llm.close()
 
 

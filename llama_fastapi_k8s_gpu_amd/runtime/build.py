@@ -33,9 +33,9 @@ HIP_SOURCES = ["kernels/gemv.hip", "kernels/attention.hip", "kernels/sampler.hip
                "kernels/moe.hip", "kernels/p2p_allreduce.hip"]
 HOST_HIP_SOURCES = ["runtime/engine.cpp", "runtime/p2p.cpp", "runtime/scheduler.cpp",
                     "bindings_hip.cpp"]     # host code against the HIP runtime
-HOST_SOURCES = ["runtime/gguf.cpp", "runtime/repack.cpp"]          # plain C++ (+OpenMP)
+HOST_SOURCES = ["runtime/gguf.cpp", "runtime/repack.cpp", "runtime/tp_channel.cpp"]          # plain C++ (+OpenMP)
 CPU_SOURCES = ["cpu/cpu_backend.cpp", "runtime/gguf.cpp", "runtime/repack.cpp", "runtime/scheduler.cpp",
-               "bindings_cpu.cpp"]
+               "runtime/tp_channel.cpp", "bindings_cpu.cpp"]
 
 
 def _includes() -> List[str]:

@@ -9,12 +9,17 @@ api.py:24-28) mapped onto one process per GPU:
   * ``split_mode="row"`` + ``torch.distributed`` initialised with world size N:
     tensor parallelism over N ranks (one per GPU) - heads and FFN features are
     sharded, two all-reduces per layer over xGMI (decode: one-shot P2P kernel;
-    prefill: RCCL). ``tensor_split`` weights apportion kv heads / FFN superblocks
-    per rank (llama.cpp proportions; csrc/runtime/shard.h), the vocabulary
-    split stays even (the logit all-gather moves equal counts).
+    prefill: RCCL; ``comm="ipc"``: the P2P kernel for everything, no RCCL - ranks
+    may then share a GPU, which is how the one-GPU test box runs TP). The
+    vocabulary is split evenly and sampled vocabulary-parallel (each rank's
+    top-k candidates are all-gathered, csrc/kernels/sampler.hip). ``tensor_split``
+    weights apportion kv heads / FFN superblocks per rank (llama.cpp proportions;
+    csrc/runtime/shard.h). Rank 0 drives; ranks 1..N-1 run ``follow()``, which
+    replays rank 0's engine commands natively (csrc/runtime/tp_channel.h), so
+    continuous batching and cooperative cancel work unchanged under TP.
   * ``split_mode="none"/"layer"`` in one process: the model runs on
     ``main_gpu`` (one GPU holds any BASELINE model: 288 GB HBM).
-  * ``max_batch=M > 1`` (one rank): continuous batching. The engine gets M + 1 KV
+  * ``max_batch=M > 1``: continuous batching (under TP the scheduler runs on rank 0). The engine gets M + 1 KV
     slots; a native scheduler thread (csrc/runtime/scheduler.cpp) decodes every
     admitted request as one row of a batched step (one weight stream per step
     instead of one per request) and admits new requests into free slots between
@@ -34,7 +39,7 @@ from . import load_hip
 logger = logging.getLogger(__name__)
 
 
-def _tp_setup(split_mode: str, tensor_split):
+def _tp_setup(split_mode: str, tensor_split, comm: str):
     """(tp_rank, tp_size, device, nccl_id, shard weights) from torch.distributed (if initialised)."""
     from ..parallel.comm import broadcast_nccl_id, check_tensor_split, local_rank, tp_group_info
     local = local_rank()
@@ -43,8 +48,8 @@ def _tp_setup(split_mode: str, tensor_split):
     rank, ws = tp_group_info(tensor_split)
     if ws == 1:
         return 0, 1, local, b"", []
-    return (rank, ws, local, broadcast_nccl_id(lambda: load_hip().nccl_unique_id()),
-            check_tensor_split(tensor_split, ws))
+    nccl_id = b"" if comm == "ipc" else broadcast_nccl_id(lambda: load_hip().nccl_unique_id())
+    return rank, ws, local, nccl_id, check_tensor_split(tensor_split, ws)
 
 
 class HipBackend:
@@ -52,43 +57,67 @@ class HipBackend:
 
     def __init__(self, model_path: str, hparams, n_ctx: int = 1024, n_gpu_layers: int = -1,
                  tensor_split: Optional[Sequence[float]] = None, split_mode: str = "layer", main_gpu: int = 0,
-                 n_batch: int = 512, use_graphs: bool = True, max_batch: int = 1, **_):
+                 n_batch: int = 512, use_graphs: bool = True, max_batch: int = 1, tp_comm: Optional[str] = None,
+                 device: Optional[int] = None, **_):
         hip = load_hip()
         if 0 <= n_gpu_layers < hparams.n_layer:
             raise ValueError(f"n_gpu_layers={n_gpu_layers} < n_layer={hparams.n_layer}: partial offload runs on "
                              "the hybrid backend (backend='hybrid')")
-        rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split)
-        device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)
+        if split_mode == "layer" and tensor_split and sum(1 for v in tensor_split if float(v) > 0) > 1:
+            # upstream's layer split places contiguous layer ranges by tensor_split; one MI355X
+            # holds any supported model (288 GB), so layers are not split across GPUs here -
+            # a tensor_split given for a layer split would be silently ignored
+            raise ValueError("tensor_split needs split_mode='row' (tensor parallelism); split_mode='layer' runs the "
+                             "whole model on main_gpu")
+        comm = tp_comm or os.environ.get("LFK_TP_COMM", "auto")
+        rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split, comm)
+        if device is None:
+            device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)
         self.tp_rank, self.tp_size = rank, size
         max_batch = max(1, int(max_batch or 1))
-        if max_batch > 1 and size > 1:
-            logger.warning("max_batch=%d ignored: continuous batching runs on one rank (tp=%d)", max_batch, size)
-            max_batch = 1
         self.max_batch = max_batch
         self.engine = hip.Engine(model_path, n_ctx=n_ctx, n_batch=min(n_batch, n_ctx), device=device,
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
-                                 tensor_split=ts, n_slots=max_batch + 1 if max_batch > 1 else 1)
-        self.sched = hip.BatchScheduler(self.engine) if max_batch > 1 else None
+                                 tensor_split=ts, n_slots=max_batch + 1 if max_batch > 1 else 1, comm=comm)
         self.n_ctx = n_ctx
         self.n_vocab = int(hparams.n_vocab)
         self.n_batch = min(n_batch, n_ctx)  # the engine's prefill chunk bound (eval_logits rejects T > n_batch)
         self.device = device
         if size > 1:
-            self._open_p2p()
+            self._tp_connect(comm)
+        # the continuous-batching scheduler drives the engine from rank 0 only
+        self.sched = hip.BatchScheduler(self.engine) if max_batch > 1 and rank == 0 else None
 
-    def _open_p2p(self):
-        """Exchange the ranks' IPC handles so decode all-reduces take the one-shot
-        P2P kernel over xGMI (prefill-sized ones stay on RCCL). Any failure leaves
-        the engine on RCCL for everything."""
-        import os
-        if os.environ.get("LFK_P2P_ALLREDUCE", "1") == "0":
-            return
-        from ..parallel.comm import allgather_bytes
-        try:
-            handles = allgather_bytes(self.engine.p2p_handle())
-            self.engine.p2p_open(handles)
-        except Exception as e:  # pragma: no cover - depends on the node's IPC support
-            logger.warning("P2P all-reduce unavailable, using RCCL only: %s", e)
+    def _tp_connect(self, comm: str):
+        """Join the TP group: exchange the ranks' IPC handles (one-shot P2P collectives over
+        xGMI) and open the native control channel rank 0 publishes its commands on."""
+        import torch.distributed as dist
+
+        from ..parallel.comm import allgather_bytes, broadcast_object
+        if comm != "rccl":
+            try:
+                handles = allgather_bytes(self.engine.p2p_handle())
+                self.engine.p2p_open(handles)
+            except Exception as e:  # pragma: no cover - depends on the node's IPC support
+                if comm == "ipc":
+                    raise
+                logger.warning("P2P collectives unavailable, using RCCL only: %s", e)
+        name = broadcast_object(f"lfk_tp_{os.getpid()}_{os.urandom(6).hex()}" if self.tp_rank == 0 else None)
+        if self.tp_rank == 0:
+            self.engine.tp_ctl_create(name)
+        dist.barrier()
+        if self.tp_rank > 0:
+            self.engine.tp_ctl_attach(name)
+        dist.barrier()
+
+    @property
+    def follows(self) -> bool:
+        """A follower rank of a TP group: call follow() instead of generating."""
+        return self.tp_size > 1 and self.tp_rank > 0
+
+    def follow(self):
+        """Follower ranks: replay rank 0's engine commands until rank 0 closes the group."""
+        self.engine.follow()
 
     def health(self):
         h = {"ok": bool(self.engine.healthy), "backend": self.name, "tp": self.tp_size,
@@ -106,6 +135,8 @@ class HipBackend:
     def close(self):
         if self.sched is not None:
             self.sched.shutdown()
+        if self.tp_size > 1 and self.tp_rank == 0:
+            self.engine.tp_stop()
 
     def device_memory(self):
         return {f"hip:{self.device}": int(self.engine.device_bytes)}

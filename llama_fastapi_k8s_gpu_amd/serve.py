@@ -30,15 +30,20 @@ def main() -> int:
     from .parallel.tp_serve import TPLeader, follower_loop, init_tp
     rank, world, ctrl = init_tp(settings)
     llm = build_engine(settings)
+    native = getattr(llm, "backend_name", "") == "hip"   # the engine mirrors its own commands
     if rank == 0:
-        leader = TPLeader(llm, ctrl)
+        front = llm if native else TPLeader(llm, ctrl)
         try:
-            uvicorn.run(create_app(settings, engine=leader), host=host, port=port, workers=1)
+            uvicorn.run(create_app(settings, engine=front), host=host, port=port, workers=1)
         finally:
-            leader.close()
+            front.close()
     else:
         logging.getLogger(__name__).info("rank %d/%d following rank 0", rank, world)
-        follower_loop(llm, ctrl)
+        if native:
+            llm.follow()
+            llm.close()
+        else:
+            follower_loop(llm, ctrl)
     import torch.distributed as dist
     dist.destroy_process_group()
     return 0

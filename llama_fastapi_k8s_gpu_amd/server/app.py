@@ -18,10 +18,15 @@ Documented deviations:
     result (408) is unchanged;
   * OpenAI-compatible ``/v1/*`` routes (``OPENAI_API``, server/openai_api.py) share
     the admission queue and the one-at-a-time consumer.
+  * ``EXACT_TOKEN_GUARD=1``: after the reference's char/4 trim, the oldest messages
+    are dropped by the real (chat-templated) token count, so a token-dense prompt
+    no longer fails at the context limit; ``PARITY_MODE=0`` exempts
+    the system message from the 400-char cap (Appendix C6).
   * ``MAX_BATCH=M`` (default 1 = the reference): M consumer tasks and a
     Semaphore(M) feed the engine's continuous batch, so M generations run at once
     (M in flight + ``MAX_QUEUE_SIZE`` waiting; the next request gets 503). FIFO
-    admission, timeouts and error strings are unchanged.
+    admission, timeouts and error strings are unchanged. M is capped by the
+    engine's ``batch_width`` (1 for engines without a batch scheduler).
 """
 from __future__ import annotations
 
@@ -37,7 +42,7 @@ from fastapi import FastAPI, HTTPException, Request
 from fastapi.responses import JSONResponse, Response
 
 from ..config import Settings
-from .policy import build_messages, truncate_messages_to_fit_context
+from .policy import build_messages, exact_token_trim, truncate_messages_to_fit_context
 from .schema import BotMessageRequest
 
 logging.basicConfig(level=logging.INFO)
@@ -105,7 +110,8 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
         async with semaphore:
             try:
                 messages = truncate_messages_to_fit_context(
-                    messages, settings.max_context_tokens, settings.message_char_cap)
+                    messages, settings.max_context_tokens, settings.message_char_cap,
+                    cap_system=settings.parity_mode)
                 eng = app.state.engine
                 kwargs = dict(messages=messages, stream=False,
                               temperature=sampling.temperature, top_p=sampling.top_p,
@@ -115,9 +121,20 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
                     kwargs["max_tokens"] = sampling.max_tokens
                 if settings.cooperative_cancel and getattr(eng, "supports_cancel", False):
                     kwargs["cancel_event"] = cancel_event
+                count = getattr(eng, "count_chat_tokens", None)
+                if settings.exact_token_guard and count is not None:
+                    n_ctx = int(getattr(eng, "n_ctx", lambda: settings.n_ctx)())
+                    limit = max(1, n_ctx - settings.exact_token_reserve)
+
+                    def guarded(**kw):   # tokenisation off the event loop, with the generation
+                        kw["messages"] = exact_token_trim(kw["messages"], count, limit)
+                        return eng.create_chat_completion(**kw)
+                    call = guarded
+                else:
+                    call = eng.create_chat_completion
                 metrics.in_flight.inc()
                 try:
-                    answer = await asyncio.to_thread(eng.create_chat_completion, **kwargs)
+                    answer = await asyncio.to_thread(call, **kwargs)
                 finally:
                     metrics.in_flight.dec()
 
@@ -179,7 +196,14 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             # before the server accepts traffic, off the event loop.
             app_.state.engine = await asyncio.to_thread(factory, settings)
         app_.state.queue = asyncio.Queue(maxsize=settings.max_queue_size)
+        # generations in flight: MAX_BATCH, capped by what the engine actually runs at once
+        # (its continuous batch); an engine without a scheduler (CPU, hybrid, a backend that
+        # fell back to one row) keeps the reference's one-at-a-time consumer, so requests
+        # never wait on a facade lock while their 408 clock runs
         width = max(1, int(settings.max_batch))
+        eng_width = getattr(app_.state.engine, "batch_width", None)
+        if eng_width is not None:
+            width = max(1, min(width, int(eng_width)))
         app_.state.semaphore = asyncio.Semaphore(width)
         app_.state.consumer_tasks = [asyncio.create_task(consumer(app_)) for _ in range(width)]
         app_.state.consumer_task = app_.state.consumer_tasks[0]

@@ -37,9 +37,14 @@ def count_tokens_roughly(text: str) -> int:
 
 def truncate_messages_to_fit_context(messages: List[Dict[str, str]], max_tokens: int,
                                      char_cap: int = 400,
-                                     count: Callable[[str], int] = count_tokens_roughly
-                                     ) -> List[Dict[str, str]]:
+                                     count: Callable[[str], int] = count_tokens_roughly,
+                                     cap_system: bool = True) -> List[Dict[str, str]]:
+    """Reference api.py:35-46. ``cap_system=False`` (PARITY_MODE=0) exempts system
+    messages from the per-message cap - the reference cuts its own 423-char persona at
+    400 chars and so always loses the gender / appearance suffix."""
     for m in messages:
+        if not cap_system and m.get("role") == "system":
+            continue
         if len(m["content"]) > char_cap:
             m["content"] = m["content"][:char_cap]
     total = sum(count(m["content"]) for m in messages)
@@ -69,4 +74,33 @@ def build_messages(request) -> List[Dict[str, str]]:
     bp = request.bot_profile
     system = build_system_prompt(bp.name, bp.appearance, bp.system_prompt)
     messages.insert(1, {"role": "system", "content": system})
+    return messages
+
+
+def exact_token_trim(messages: List[Dict[str, str]], n_tokens: Callable[[List[Dict[str, str]]], int],
+                     limit: int) -> List[Dict[str, str]]:
+    """Real-token context guard (EXACT_TOKEN_GUARD): the char/4 estimate
+    can undercount badly (non-Latin text is ~1 token per char), and a prompt whose true
+    token count reaches n_ctx fails the request (reference api.py:35-46 -> 500). Drop
+    the oldest message after indices 0 and 1 (the reference's drop order) while the
+    templated prompt's real token count is >= ``limit``; if two messages still do not
+    fit, shorten the last message's text from its start (its newest words survive).
+    ``n_tokens(messages)`` = token count of the chat-templated prompt."""
+    while n_tokens(messages) >= limit and len(messages) > 2:
+        messages.pop(2)
+    if n_tokens(messages) < limit or not messages:
+        return messages
+    last = messages[-1]
+    text = last["content"]
+    lo, hi = 0, len(text)           # smallest cut so the prompt fits: binary search on the prefix dropped
+    while lo < hi:
+        mid = (lo + hi) // 2
+        last["content"] = text[mid:]
+        if n_tokens(messages) < limit:
+            hi = mid
+        else:
+            lo = mid + 1
+    last["content"] = text[lo:]
+    if n_tokens(messages) >= limit:   # the other messages alone exceed the context
+        raise ValueError(f"prompt does not fit the context window of {limit} tokens")
     return messages

@@ -175,3 +175,67 @@ def test_request_log_line(caplog):
     lines = [r.getMessage() for r in caplog.records if r.name == "api"]
     assert any(l.startswith("Request at ") and "GET http://testserver/items/1 completed in " in l
                and l.endswith("s") for l in lines)
+
+
+def test_parity_mode_off_keeps_full_system_prompt():
+    """PARITY_MODE=0: the system message is exempt from the 400-char cap, so the persona's
+    gender / appearance suffix survives (Appendix C6); turns are still capped."""
+    app, eng = make(parity_mode=False)
+    with TestClient(app) as c:
+        c.post("/response", json=body([{"turn": "user", "message": "x" * 900}], name="Zoe.f",
+                                      appearance="1,2,3, tall, blue eyes"))
+    msgs = eng.calls[0]["messages"]
+    assert msgs[1]["content"].endswith("You a girl. tall blue eyes")
+    assert len(msgs[0]["content"]) == 400
+
+
+class _TokenCountingFake(FakeEngine):
+    """A fake engine whose 'tokenizer' counts one token per character (worst-case dense
+    text: the char/4 estimate undercounts it 4x)."""
+
+    def __init__(self, n_ctx):
+        super().__init__("echo")
+        self._n = n_ctx
+
+    def n_ctx(self):
+        return self._n
+
+    def count_chat_tokens(self, messages):
+        return sum(len(m["content"]) + 4 for m in messages)
+
+    def create_chat_completion(self, messages, **kw):
+        if self.count_chat_tokens(messages) >= self._n:
+            raise ValueError("Requested tokens exceed context window")
+        return super().create_chat_completion(messages, **kw)
+
+
+@pytest.mark.parametrize("guard", [False, True])
+def test_exact_token_guard(guard):
+    """EXACT_TOKEN_GUARD=1 drops the oldest turns by real token count (never the first two
+    messages) so a token-dense prompt fits n_ctx; without it the request 500s as in the
+    reference (api.py:35-46)."""
+    s = Settings()
+    s.exact_token_guard = guard
+    s.exact_token_reserve = 16
+    eng = _TokenCountingFake(1024)
+    ctx = [{"turn": "user" if i % 2 == 0 else "assistant", "message": f"{i}" * 300} for i in range(8)]
+    with TestClient(create_app(s, engine=eng)) as c:
+        r = c.post("/response", json=body(ctx, system_prompt="S" * 50))
+    if not guard:
+        assert r.status_code == 500 and "exceed context window" in r.json()["detail"]
+        return
+    assert r.status_code == 200, r.text
+    msgs = eng.calls[-1]["messages"]
+    assert eng.count_chat_tokens(msgs) < 1024 - 16
+    assert msgs[0]["content"] == "0" * 300 and msgs[1]["role"] == "system"
+    assert msgs[-1]["content"] == "7" * 300        # the newest turn survives
+
+
+def test_exact_token_trim_shortens_last_message():
+    from llama_fastapi_k8s_gpu_amd.server.policy import exact_token_trim
+    count = lambda ms: sum(len(m["content"]) for m in ms)   # noqa: E731
+    msgs = [{"role": "system", "content": "s" * 10}, {"role": "user", "content": "a" * 50 + "b" * 50}]
+    out = exact_token_trim(msgs, count, 60)
+    assert count(out) == 59 and out[1]["content"].endswith("b" * 49)
+    with pytest.raises(ValueError):
+        exact_token_trim([{"role": "system", "content": "s" * 80}, {"role": "user", "content": "u"}], count, 60)

@@ -316,12 +316,8 @@ def _run_sampler(torch, logits, ring_tokens, params, seed, step=0):
     state[3] = rl
     state[4] = rl & 63
     dr, ds = torch.from_numpy(ring).cuda(), torch.from_numpy(state).cuda()
-    nb = h.sampler_blocks(V)
-    cv = torch.zeros(nb * 64, device="cuda")
-    ci = torch.zeros(nb * 64, dtype=torch.int32, device="cuda")
-    ct = torch.zeros(2 * nb, dtype=torch.int32, device="cuda")
-    h.sample(dl.data_ptr(), V, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), cv.data_ptr(), ci.data_ptr(), 0, 0, 1,
-             stream(), ct.data_ptr())
+    cand = torch.zeros(h.sampler_cand_words(V), dtype=torch.int32, device="cuda")
+    h.sample(dl.data_ptr(), V, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), cand.data_ptr(), 0, 0, 1, stream())
     torch.cuda.synchronize()
     return int(ds[0].item()), ds.cpu().numpy()
 
@@ -335,6 +331,54 @@ def test_sampler_greedy_with_penalties(torch):
     tok, st = _run_sampler(torch, logits, [top, top, 7], p, 0)
     assert tok == int(np.argmax(apply_penalties(logits, [top, top, 7], p)))
     assert st[1] == 1 and st[2] == 1  # pos and step advanced
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sampler_vocab_parallel_equals_single(torch, world):
+    """Tensor-parallel sampling: stage 1 on each vocabulary shard (global ids offset, equal
+    slice counts), the shards' candidate blocks concatenated as the all-gather leaves them,
+    stage 2 on the gathered blocks == the one-shard sampler (same token, same state)."""
+    from llama_fastapi_k8s_gpu_amd.engine.sampling import SamplingParams
+    h = hip()
+    rng = np.random.default_rng(20 + world)
+    for it in range(6):
+        V = [128256, 32000, 1000][it % 3]
+        logits = (rng.standard_normal(V) * 3).astype(np.float32)
+        hist = [int(t) for t in rng.integers(0, V, 70)]
+        p = SamplingParams(temperature=1.2, top_k=40, top_p=0.9, min_p=0.05, repeat_penalty=1.1,
+                           frequency_penalty=0.7, presence_penalty=0.8, seed=7 + it,
+                           logit_bias={int(hist[3]): 2.5, 5: -1.0})
+        want, want_st = _run_sampler(torch, logits, hist, p, p.seed, step=it)
+        pb = np.frombuffer(h.sampler_params_bytes(p.top_k, p.top_p, p.min_p, p.temperature, p.repeat_penalty,
+                                                  p.frequency_penalty, p.presence_penalty, p.last_n, p.seed, 0,
+                                                  p.tfs_z, p.typical_p, dict(p.logit_bias)), np.uint8)
+        dp = torch.from_numpy(pb.copy()).cuda()
+        V_l = (V + world - 1) // world
+        W = h.sampler_cand_words(V_l)
+        gathered = torch.zeros(world * W, dtype=torch.int32, device="cuda")
+        ring = np.zeros(64, np.int32)
+        ring[:64] = hist[-64:]
+        states = []
+        for r in range(world):
+            shard = np.zeros(V_l, np.float32)
+            n = max(0, min(V_l, V - r * V_l))
+            shard[:n] = logits[r * V_l:r * V_l + n]
+            dl = torch.from_numpy(shard).cuda()
+            st = np.zeros(8, np.int32)
+            st[2], st[3], st[4] = it, 64, 0
+            ds, dr = torch.from_numpy(st).cuda(), torch.from_numpy(ring.copy()).cuda()
+            h.sample(dl.data_ptr(), n, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(),
+                     gathered[r * W:(r + 1) * W].data_ptr(), 0, 0, 1, stream(), vocab_off=r * V_l, V_glob=V,
+                     V_span=V_l, stage=1)
+            states.append((ds, dr, dl))
+        torch.cuda.synchronize()
+        for ds, dr, dl in states:   # every rank runs the identical stage 2
+            h.sample(dl.data_ptr(), V_l, dp.data_ptr(), dr.data_ptr(), ds.data_ptr(), gathered.data_ptr(), 0, 0, 1,
+                     stream(), vocab_off=0, V_glob=V, V_span=V_l, cand_all=gathered.data_ptr(), world=world, stage=2)
+        torch.cuda.synchronize()
+        for ds, _, _ in states:
+            assert int(ds[0].item()) == want, (world, it, int(ds[0].item()), want)
+            assert (ds.cpu().numpy()[:6] == want_st[:6]).all()
 
 
 def test_sampler_matches_host_chain(torch):

@@ -1,4 +1,4 @@
-"""One-shot P2P all-reduce (kernels/p2p_allreduce.hip, runtime/p2p.cpp).
+"""One-shot P2P all-reduce / all-gather (kernels/p2p_allreduce.hip, runtime/p2p.cpp).
 
 Two processes share the ONE GPU of the test box: each exports its receive region
 with a hipIpc handle, the handles are exchanged over a gloo group, and the
@@ -45,6 +45,24 @@ def _worker(rank, world, port, q):
             torch.cuda.synchronize()
             ref = sum(_inputs(r, it, n).astype(np.float32) for r in range(world))
             worst = max(worst, float(np.abs(dst[:n].cpu().numpy() - ref).max()))
+        # back-to-back launches of different sizes with no host barrier in between (the fixed
+        # grid keeps slot reuse safe), all-gathers interleaved with all-reduces
+        outs = []
+        for it in range(12):
+            n = [N, 37, 1000 + it][it % 3]
+            x = torch.from_numpy(_inputs(rank, 200 + it, n)).cuda()
+            if it % 2:
+                y = torch.empty(n, device="cuda")
+                c.allreduce(x.data_ptr(), y.data_ptr(), n, s.cuda_stream)
+            else:
+                y = torch.empty(world * n, device="cuda")
+                c.allgather(x.data_ptr(), y.data_ptr(), n, s.cuda_stream)
+            outs.append((it, n, y))
+        torch.cuda.synchronize()
+        for it, n, y in outs:
+            parts = [_inputs(r, 200 + it, n) for r in range(world)]
+            ref = sum(parts) if it % 2 else np.concatenate(parts)
+            worst = max(worst, float(np.abs(y.cpu().numpy() - ref).max()))
         # graph replay: the captured launch advances its epochs on the device
         g = torch.cuda.CUDAGraph()
         cs = torch.cuda.Stream()

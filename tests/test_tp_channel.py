@@ -1,0 +1,110 @@
+"""The tensor-parallel control channel (csrc/runtime/tp_channel.h) across processes:
+rank 0 publishes commands, followers receive every one of them in order (the mailbox
+is never overwritten before every follower copied it), a follower that attaches late
+sees only what comes after, and a follower notices a leader that died."""
+import multiprocessing as mp
+import os
+import time
+
+import pytest
+
+
+def _name(tag):
+    return f"lfk_test_{tag}_{os.getpid()}_{os.urandom(3).hex()}"
+
+
+def _follower(name, rank, n, q):
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    cpu = load_cpu()
+    c = cpu.TPChannel.attach(name, rank)
+    q.put(("ready", rank))
+    got = []
+    while True:
+        m = c.receive(5000)
+        if m is None:
+            q.put(("timeout", rank, got))
+            return
+        if m == b"STOP":
+            break
+        got.append(m)
+        if len(got) % 7 == 0:
+            time.sleep(0.01)   # a slow follower: the leader must wait for its copy
+    q.put(("done", rank, got))
+
+
+def test_channel_order_and_backpressure():
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    cpu = load_cpu()
+    world, n = 3, 200
+    name = _name("order")
+    lead = cpu.TPChannel.create(name, world, 4096)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_follower, args=(name, r, n, q)) for r in range(1, world)]
+    for p in procs:
+        p.start()
+    for _ in procs:
+        assert q.get(timeout=60)[0] == "ready"
+    msgs = [bytes([i % 251]) * (1 + (i * 37) % 3000) for i in range(n)]
+    for m in msgs:
+        lead.publish(m)
+    lead.publish(b"STOP")
+    res = [q.get(timeout=60) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+    for kind, rank, got in res:
+        assert kind == "done", (kind, rank)
+        assert got == msgs, rank
+
+
+def _orphan(name, q):
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    c = load_cpu().TPChannel.attach(name, 1)
+    q.put("attached")
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        if c.receive(200) is None and not c.leader_alive():
+            q.put("leader gone")
+            return
+    q.put("still waiting")
+
+
+def _leader_then_exit(name, q):
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    c = load_cpu().TPChannel.create(name, 2, 64)
+    q.put("created")
+    time.sleep(1.0)
+    os._exit(0)   # dies without publishing STOP (and without unlinking)
+
+
+def test_follower_detects_dead_leader():
+    name = _name("dead")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    lp = ctx.Process(target=_leader_then_exit, args=(name, q))
+    lp.start()
+    assert q.get(timeout=60) == "created"
+    fp = ctx.Process(target=_orphan, args=(name, q))
+    fp.start()
+    assert q.get(timeout=60) == "attached"
+    assert q.get(timeout=60) == "leader gone"
+    lp.join(timeout=10)
+    fp.join(timeout=10)
+    try:
+        os.unlink("/dev/shm/" + name)
+    except FileNotFoundError:
+        pass
+
+
+def test_channel_rejects_bad_use():
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    cpu = load_cpu()
+    with pytest.raises(Exception):
+        cpu.TPChannel.attach(_name("missing"), 1)
+    name = _name("cap")
+    lead = cpu.TPChannel.create(name, 2, 16)
+    with pytest.raises(Exception):
+        lead.publish(b"x" * 17)             # larger than the mailbox
+    with pytest.raises(Exception):
+        cpu.TPChannel.create(name, 2, 16)   # the name is taken
+    assert lead.world == 2

@@ -1,0 +1,183 @@
+"""Tensor parallelism on the MI355X engine, run for real on the one-GPU test box.
+
+Two ranks share device 0 (``comm="ipc"``: every collective takes the one-shot P2P
+kernel over hipIpc-mapped memory - RCCL refuses two ranks on one device) and form a
+``split_mode="row"`` group exactly as ``torchrun`` ranks would on an 8-GPU node: heads
+/ FFN features / vocabulary sharded, two all-reduces per layer, vocabulary-parallel
+sampling (candidate all-gather), rank 0 driving and rank 1 replaying its commands
+over the native control channel (csrc/runtime/tp_channel.h).
+
+Checked against the same model at TP=1 in the same process and against the exact fp32
+model: prefill and graph-replayed decode logits (TP within 1e-2 of TP=1 - the activation
+quantum of the q8 / bf16 paths, whose rounding the all-reduce's summation order can flip
+- and no further from the exact model than TP=1), greedy generations (identical, or
+diverging only at a near-tie of the exact model), seeded sampling (identical draws until
+rounding noise moves a probability boundary), continuous batching under TP (rows of one
+batched step), cooperative cancel (the followers stop at rank 0's step), and one
+``/response`` through the FastAPI app on rank 0.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [("tiny-llama3-tp", None), ("tiny-mixtral-tp", None), ("tiny-llama3-tp4", [3.0, 1.0])]
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+def _exercise(llm, with_app):
+    """Every serving entry point once; returns what the TP=1 run must reproduce."""
+    eng = llm._backend.engine
+    rng = np.random.default_rng(11)
+    toks = [int(t) for t in rng.integers(3, 400, 44)]
+    out = {"prefill": eng.eval_logits(toks[:39], 0)}
+    out["decode"] = [eng.decode_logits(toks[39 + i], 39 + i) for i in range(4)]
+    out["greedy"] = eng.generate(toks[:20], 0, 32, {"temperature": 0.0}, [], None, None)["tokens"]
+    out["sampled"] = eng.generate(toks[:17], 0, 24, {"temperature": 1.0, "top_k": 40, "top_p": 0.95, "seed": 3},
+                                  [], None, None)["tokens"]
+    calls = {"n": 0}
+
+    def poll():
+        calls["n"] += 1
+        return calls["n"] >= 3
+    r = eng.generate([1, 2, 3], 0, 200, {"temperature": 1.0, "seed": 1}, [], poll, None)
+    out["cancel"] = (r["finish"], len(r["tokens"]))
+    # continuous batching: three concurrent requests decode as rows of one batched step
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(3) as ex:
+        res = list(ex.map(lambda i: llm.create_completion([1, 5 + i, 9, 12 + i, 30 + 2 * i], max_tokens=12,
+                                                          temperature=0.0), range(3)))
+    out["batched"] = [x["choices"][0]["text"] for x in res]
+    out["batched_n"] = [x["usage"]["completion_tokens"] for x in res]
+    # an after-the-batch single-sequence request still works (slot 0 path)
+    out["greedy2"] = eng.generate(toks[:9], 0, 8, {"temperature": 0.0}, [], None, None)["tokens"]
+    if with_app:
+        from fastapi.testclient import TestClient
+
+        from llama_fastapi_k8s_gpu_amd.config import Settings
+        from llama_fastapi_k8s_gpu_amd.server.app import create_app
+        s = Settings()
+        s.max_batch = 3
+        body = {"bot_profile": {"name": "Mia.f", "appearance": "a, b, c, d"}, "user_profile": {"name": "u"},
+                "context": [{"turn": "user", "message": "hello there"}]}
+        with TestClient(create_app(s, engine=llm)) as c:
+            resp = c.post("/response", json=body)
+            out["http"] = (resp.status_code, isinstance(resp.json().get("response"), str))
+            out["health"] = c.get("/health").json()["engine"]["tp"]
+    out["healthy"] = bool(llm.health()["ok"])
+    return out
+
+
+def _worker(rank, world, port, paths, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK="0")
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+        kw = dict(n_gpu_layers=-1, n_ctx=256, n_batch=64, seed=5, verbose=False, max_batch=3)
+        results = []
+        for i, (spec, path, ts) in enumerate(paths):
+            llm = Llama(path, split_mode="row", tensor_split=ts, tp_comm="ipc", device=0, **kw)
+            assert llm._backend.tp_size == world
+            if rank > 0:
+                llm.follow()          # returns when rank 0 closes the group
+                llm.close()
+                continue
+            assert llm.batch_width == 3
+            got = _exercise(llm, with_app=(i == 0))
+            llm.close()               # publishes STOP: the follower's follow() returns
+            ref = _exercise(Llama(path, split_mode="none", **kw), with_app=False)
+            results.append((spec, got, ref))
+        dist.barrier()
+        q.put((rank, results, None))
+        dist.destroy_process_group()
+    except BaseException as e:  # report instead of hanging the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(400)
+def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.multiprocessing as mp
+
+    from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
+    paths = [(spec, write_synthetic_gguf(spec, str(tmp_path / f"{spec}.gguf"), seed=4), ts) for spec, ts in CASES]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29600 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, paths, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in procs:
+            rank, results, err = q.get(timeout=380)
+            res[rank] = (results, err)
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank in (0, 1):
+        assert res[rank][1] is None, f"rank {rank}:\n{res[rank][1]}"
+    from llama_fastapi_k8s_gpu_amd.gguf.reader import GGUFReader
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    toks = [int(t) for t in np.random.default_rng(11).integers(3, 400, 44)]   # as _exercise draws them
+    report, bad = [], []
+    for (spec, got, ref), (_, path, _) in zip(res[0][0], paths):
+        exact = ReferenceLlama(GGUFReader(path), n_ctx=256)
+        x_pre = exact.forward(toks[:39], 0).numpy()
+        x_dec = [exact.forward([toks[39 + i]], 39 + i).numpy() for i in range(4)]
+
+        def near_tie(prompt, a, b, k):
+            """Tokens a (TP) and b (TP=1) at step k of a greedy run from `prompt`: both are
+            argmax candidates of the exact model within the engines' activation-rounding noise."""
+            m = ReferenceLlama(GGUFReader(path), n_ctx=256)
+            lg = m.forward(list(prompt) + list(b[:k]), 0).numpy()
+            return abs(lg[a[k]] - lg[b[k]]) <= 2e-2 * np.abs(lg).max()
+
+        moe = "mixtral" in spec
+
+        def greedy_ok(prompt, a, b):
+            k = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), None)
+            # MoE: a near-tie in the ROUTER (top-2 of 4 experts) flips an expert, which moves
+            # the logits far more than the rounding noise (both engines sit ~0.2 from the exact
+            # model on such steps); past the first token only the teacher-forced logits compare
+            return k is None or near_tie(prompt, a, b, k) or (moe and k >= 1)
+        e_tp = [_rel(got["prefill"], x_pre)] + [_rel(g, x) for g, x in zip(got["decode"], x_dec)]
+        e_1 = [_rel(ref["prefill"], x_pre)] + [_rel(r, x) for r, x in zip(ref["decode"], x_dec)]
+        sd = next((i for i, (x, y) in enumerate(zip(got["sampled"], ref["sampled"])) if x != y), None)
+        checks = {
+            # q8 (decode GEMV) / bf16 (prefill GEMM) activations: the all-reduce's fp32 summation
+            # order can flip a rounding, so TP and TP=1 agree to the activation quantum, and TP is
+            # as close to the exact fp32 model as TP=1 is
+            "logits_vs_tp1": max([_rel(got["prefill"], ref["prefill"])] +
+                                 [_rel(a_, b_) for a_, b_ in zip(got["decode"], ref["decode"])]) <= 1e-2,
+            "logits_vs_exact": all(t <= o + 5e-3 for t, o in zip(e_tp, e_1)),
+            "greedy": greedy_ok(toks[:20], got["greedy"], ref["greedy"]),
+            "greedy2": greedy_ok(toks[:9], got["greedy2"], ref["greedy2"]),
+            # seeded sampling: identical draws until the rounding noise moves a probability boundary
+            "sampled": (sd is None or sd >= 4) and len(got["sampled"]) == len(ref["sampled"]),
+            "cancel": got["cancel"][0] == "cancelled" and got["cancel"][1] < 200,
+            "batched": got["batched_n"] == ref["batched_n"] and
+                       sum(x == y for x, y in zip(got["batched"], ref["batched"])) >= 2,
+            "healthy": got["healthy"],
+        }
+        if "http" in got:
+            checks["http"] = got["http"] == (200, True) and got["health"] == 2
+        report.append((spec, {"err_tp": [round(v, 5) for v in e_tp], "err_tp1": [round(v, 5) for v in e_1],
+                              "sampled_diff_at": sd, "cancel": got["cancel"]},
+                       [k for k, ok in checks.items() if not ok]))
+        bad += [(spec, k) for k, ok in checks.items() if not ok]
+    print("TP report:", report)
+    assert not bad, (bad, report)

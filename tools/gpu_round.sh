@@ -15,9 +15,11 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in "$@"; do
   case $s in
+    tp) step tp 460 python -u -m pytest tests/test_p2p_allreduce.py tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread -p no:cacheprovider ;;
+    samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     kern) step kern 900 python -m pytest tests/test_kernels_gpu.py -q -p no:cacheprovider ;;
     eng) step eng 900 python -m pytest tests/test_engine_gpu.py -q -p no:cacheprovider ;;
-    gputests) step gputests 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    gputests) step gputests 1000 python -u -m pytest tests -m gpu -q --timeout 420 --timeout-method thread -p no:cacheprovider ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
     micro) step micro 300 python tools/launch_microbench.py ;;
@@ -31,6 +33,10 @@ for s in "$@"; do
     gvpmc) export TMPDIR=/tmp; step gvpmc 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/gvpmc -o pmc --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 --only q4k ;;
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
+    bench20) step bench20 900 python bench.py --steps 20 --warmup 2 ;;
+    benchtp2) LFK_BENCH_DEVICE=0 step benchtp2 900 python bench.py --gpus 2 --steps 12 --warmup 2 ;;
+    benchdp2) LFK_BENCH_DEVICE=0 step benchdp2 900 python bench.py --gpus 2 --parallel dp --steps 12 --warmup 2 ;;
+    batch) step batch 600 python -u -m pytest tests/test_batch_gpu.py tests/test_batch_serving_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o decode \
             --output-format csv -- python3 tools/decode_bench.py --steps 64 --no-graph ;;
   esac

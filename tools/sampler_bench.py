@@ -19,15 +19,12 @@ def main():
     dp = torch.from_numpy(pb.copy()).cuda()
     ring = torch.from_numpy(rng.integers(0, V, 64).astype(np.int32)).cuda()
     st = torch.from_numpy(np.array([0, 0, 0, 64, 0, 0, 0, 0], np.int32)).cuda()
-    nb = h.sampler_blocks(V)
-    cv = torch.zeros(nb * 64, device="cuda")
-    ci = torch.zeros(nb * 64, dtype=torch.int32, device="cuda")
-    ct = torch.zeros(2 * nb, dtype=torch.int32, device="cuda")
+    cand = torch.zeros(h.sampler_cand_words(V), dtype=torch.int32, device="cuda")
     clk = torch.zeros(8, dtype=torch.int64, device="cuda")
 
     def run(s, dbg=0):
-        h.sample(dl.data_ptr(), V, dp.data_ptr(), ring.data_ptr(), st.data_ptr(), cv.data_ptr(), ci.data_ptr(), 0, 0,
-                 0, s, ct.data_ptr(), dbg_clk=dbg)
+        h.sample(dl.data_ptr(), V, dp.data_ptr(), ring.data_ptr(), st.data_ptr(), cand.data_ptr(), 0, 0,
+                 0, s, dbg_clk=dbg)
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(3):
         run(s)
