@@ -240,19 +240,22 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("debug") = 0, py::arg("dbg_clk") = 0);
 
   m.def("bprep", [](uintptr_t x, int ldx, bool swiglu, uintptr_t norm, float eps, int K, int B, uintptr_t xh, int ldh,
-                    uintptr_t stream, uintptr_t zero, int zero_n) {
+                    uintptr_t stream, uintptr_t zero, int zero_n, int swiglu_group) {
     BPrepArgs a;
+    a.swiglu_group = swiglu_group;
     a.x = P<float>(x); a.ldx = ldx; a.swiglu = swiglu; a.norm_w = P<float>(norm); a.eps = eps; a.K = K; a.B = B;
     a.xh = P<__half>(xh); a.ldh = ldh; a.zero = P<float>(zero); a.zero_n = zero_n;
     bprep(a, S(stream));
     hip_ok("bprep");
   }, py::arg("x"), py::arg("ldx"), py::arg("swiglu"), py::arg("norm"), py::arg("eps"), py::arg("K"), py::arg("B"),
-     py::arg("xh"), py::arg("ldh"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0);
+     py::arg("xh"), py::arg("ldh"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0,
+     py::arg("swiglu_group") = 32);
   m.def("bmm", [](uintptr_t w, int type, int rows, int K, uintptr_t xh, int ldh, uintptr_t out, int ldo, int B,
                   uintptr_t stream, int debug, uintptr_t h_out, int ldh_out, uintptr_t xf, int ldxf,
-                  uintptr_t norm, float eps, bool store_out) {
+                  uintptr_t norm, float eps, bool store_out, uintptr_t dbg_clk) {
     BmmArgs a;
     a.debug = debug;
+    a.dbg_clk = P<long long>(dbg_clk);
     a.w = make_qmat(P<void>(w), type, rows, K);
     a.xh = P<__half>(xh); a.ldh = ldh; a.out = P<float>(out); a.ldo = ldo; a.n_out = rows; a.B = B;
     if (h_out) {  // SwiGLU epilogue (gate/up rows in 32-row groups)
@@ -267,14 +270,15 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("xh"), py::arg("ldh"), py::arg("out"),
      py::arg("ldo"), py::arg("B"), py::arg("stream"), py::arg("debug") = 0, py::arg("h_out") = 0,
      py::arg("ldh_out") = 0, py::arg("xf") = 0, py::arg("ldxf") = 0, py::arg("norm") = 0, py::arg("eps") = 1e-5f,
-     py::arg("store_out") = false);
+     py::arg("store_out") = false, py::arg("dbg_clk") = 0);
   m.def("bmm_norm_fits", &bmm_norm_fits);
   m.def("bmm_supported", &bmm_supported);
   m.def("t16_bytes", &t16_bytes);
-  m.def("t16_repack", [](uintptr_t w, int type, int rows, int K, uintptr_t dst, uintptr_t stream) {
-    t16_repack(make_qmat(P<void>(w), type, rows, K), P<uint8_t>(dst), S(stream));
+  m.def("t16_repack", [](uintptr_t w, int type, int rows, int K, uintptr_t dst, uintptr_t stream, bool swiglu) {
+    t16_repack(make_qmat(P<void>(w), type, rows, K), P<uint8_t>(dst), S(stream), swiglu);
     hip_ok("t16_repack");
-  });
+  }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("dst"), py::arg("stream"),
+     py::arg("swiglu") = false);
 
   py::class_<P2PComm>(m, "P2PComm")
       .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_n"), py::arg("device"))
@@ -336,8 +340,15 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
                           int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,
-                          int debug_stop, uintptr_t dbg_clk) {
+                          int debug_stop, uintptr_t dbg_clk, int batch, uintptr_t slots, size_t slot_stride,
+                          uintptr_t out_h) {
     AttnDecodeArgs a;
+    if (batch > 0) {  // rows b: query q + b*n_head*hd, slot slots[b], position pos[b], own workspaces
+      a.batch = batch; a.slots = P<int>(slots); a.slot_stride = slot_stride;
+      a.q_stride = (size_t)n_head * hd; a.out_stride = (size_t)n_head * hd;
+      a.part_stride = attn_decode_workspace_floats(n_ctx, n_head, hd);
+      a.out_h = P<__half>(out_h); a.out_h_stride = (size_t)n_head * hd;
+    }
     a.debug_stop = debug_stop;
     a.dbg_clk = P<long long>(dbg_clk);
     a.counters = P<int>(counters);
@@ -348,7 +359,8 @@ PYBIND11_MODULE(_hip, m) {
     hip_ok("attn_decode");
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("pos"), py::arg("n_ctx"), py::arg("n_head"), py::arg("n_kv"),
      py::arg("hd"), py::arg("scale"), py::arg("part"), py::arg("out"), py::arg("stream"), py::arg("counters"),
-     py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0);
+     py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0, py::arg("batch") = 0, py::arg("slots") = 0,
+     py::arg("slot_stride") = 0, py::arg("out_h") = 0);
   m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
   m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
                            int hd, float scale, uintptr_t out, uintptr_t stream, bool out_bf16) {

@@ -87,9 +87,13 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   constexpr int KPW = 16;       // keys per wave
   // TL: timeline instrumentation (microbenchmarks; a separate instantiation so
   // the production kernel's code generation is untouched)
-  const long long t_entry = TL ? wall_clock64() : 0;
-  const bool stamp = TL && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0;
-#define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) a.dbg_clk[i] = wall_clock64() - t_entry; } } while (0)
+  // TL: per-block wall_clock64 stamps (absolute), dbg_clk[16 * linear block + i]: 0 entry, 1 loads
+  // issued + position read, 2 V staged, 3 wave partials met, 4 block partial stored, 5 split
+  // counter taken, 8 / 9 merge start / end (merging block), 7 exit
+  const bool stamp = TL && threadIdx.x == 0;
+  long long* const tl = TL ? a.dbg_clk + 16 * ((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) : nullptr;
+#define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) tl[(i) + 1] = wall_clock64(); } } while (0)
+  if constexpr (TL) { if (stamp) tl[0] = wall_clock64(); }
   if ((int)blockIdx.z == (a.batch > 0 ? a.batch : 1)) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   }
   __syncthreads();
   LFK_STAMP(5);
-  if constexpr (TL) { if (last && threadIdx.x == 0) a.dbg_clk[8] = wall_clock64() - t_entry; }
+  if constexpr (TL) { if (last && threadIdx.x == 0) tl[8] = wall_clock64(); }
   if (!last) return;
   // every element's split values and the split statistics are loaded in one
   // batch of independent sc1 loads (one memory round trip per 16 splits)
@@ -328,7 +332,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
       if (a.out_h) a.out_h[swz4(o)] = __float2half(num[j] / den[j]);
     }
   }
-  if constexpr (TL) { if (threadIdx.x == 0) a.dbg_clk[9] = wall_clock64() - t_entry; }
+  if constexpr (TL) { if (threadIdx.x == 0) tl[9] = wall_clock64(); }
 #undef LFK_STAMP
 }
 

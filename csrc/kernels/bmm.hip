@@ -212,11 +212,16 @@ __device__ __forceinline__ void copy16(uint8_t* d, const uint8_t* s, bool ok) {
 }
 
 template <int T>
-__global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
+__global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst, int swiglu) {
   const int s = blockIdx.x, t = blockIdx.y, steps = gridDim.x;
   const int l = threadIdx.x, r16 = l & 15, kq = l >> 4;
-  const int row = t * 16 + r16;
-  const bool ok = row < w.rows;
+  int row = t * 16 + r16;
+  bool ok = row < w.rows;
+  if (swiglu) {  // tile t: gate rows of features 8t .. 8t+7, then their up rows (32-row groups in `w`)
+    const int f = 8 * t + (r16 & 7);
+    row = 64 * (f >> 5) + (r16 >= 8 ? 32 : 0) + (f & 31);
+    ok = f < w.rows / 2;
+  }
   const size_t r = ok ? (size_t)row : 0;
   uint8_t* blk = dst + ((size_t)t * steps + s) * t16_step_bytes(T);
   const Planes& P = w.P;
@@ -295,14 +300,16 @@ __global__ __launch_bounds__(64) void t16_repack_kernel(QMat w, uint8_t* dst) {
   }
 }
 
-void t16_repack(const QMat& w, uint8_t* dst, hipStream_t st) {
+void t16_repack(const QMat& w, uint8_t* dst, hipStream_t st, bool swiglu) {
   if (!bmm_supported(w.type, w.K)) throw std::runtime_error("t16_repack: unsupported type / K");
+  if (swiglu && w.rows % 64) throw std::runtime_error("t16_repack: SwiGLU copy needs 32-row gate / up groups");
   const dim3 grid(w.K / 256, (w.rows + 15) / 16);
+  const int sw = swiglu ? 1 : 0;
   switch (w.type) {
-    case T_Q4_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q4_K>, grid, dim3(64), 0, st, w, dst); break;
-    case T_Q5_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q5_K>, grid, dim3(64), 0, st, w, dst); break;
-    case T_Q6_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q6_K>, grid, dim3(64), 0, st, w, dst); break;
-    default: hipLaunchKernelGGL(t16_repack_kernel<T_Q8_0>, grid, dim3(64), 0, st, w, dst); break;
+    case T_Q4_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q4_K>, grid, dim3(64), 0, st, w, dst, sw); break;
+    case T_Q5_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q5_K>, grid, dim3(64), 0, st, w, dst, sw); break;
+    case T_Q6_K: hipLaunchKernelGGL(t16_repack_kernel<T_Q6_K>, grid, dim3(64), 0, st, w, dst, sw); break;
+    default: hipLaunchKernelGGL(t16_repack_kernel<T_Q8_0>, grid, dim3(64), 0, st, w, dst, sw); break;
   }
 }
 
@@ -377,6 +384,10 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
+  // microbenchmark timeline: [0] entry [1] weights issued [2] x staged [3] first tile computed
+  // [4] exit [5] tiles done by the block
+  long long* clk = a.dbg_clk ? a.dbg_clk + (size_t)bid * 8 : nullptr;
+  if (clk && tid == 0) clk[0] = wall_clock64();
   // segments (Q|K|V in one launch): tile index -> (matrix, local tile)
   const int t1 = (a.n_out + 15) >> 4;
   const int t2 = t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0);
@@ -390,11 +401,20 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   if (s0 >= s1) return;  // whole block, before any barrier
   const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
   const int gstride = nbk / kparts;
-  // tile order: SwiGLU blocks take 4-tile units (4u .. 4u + 3, then unit u + nbk)
+  // tile order: SwiGLU blocks take a contiguous range of tiles, balanced per CU: blocks b and
+  // b + G (G = a.tile_groups, the CU count; placement only moves speed, never results) split
+  // the quota T / G (+1) of group b % G between them - at 2 blocks per CU and T = 7 G every CU
+  // gets exactly 7 tiles (an even split of whole units left a quarter of the CUs half-loaded)
   const bool sw = a.swiglu_epi;
-  int gt = sw ? 4 * bid : bid / kparts;
-  auto next_tile = [&](int g) { return sw ? ((g & 3) != 3 ? g + 1 : g + 1 + 4 * (nbk - 1)) : g + gstride; };
-  if (gt >= tiles) return;  // whole block, before any barrier
+  int gt = bid / kparts, tiles_end = tiles;
+  if (sw) {
+    const int G = a.tile_groups, g = bid % G, rnd = bid / G, nr = (nbk + G - 1) / G;
+    const int q = tiles / G + (g < tiles % G ? 1 : 0), p0 = g * (tiles / G) + min(g, tiles % G);
+    gt = p0 + rnd * q / nr;
+    tiles_end = p0 + (rnd + 1) * q / nr;
+  }
+  auto next_tile = [&](int g) { return sw ? g + 1 : g + gstride; };
+  if (gt >= tiles_end) return;  // whole block, before any barrier
   const int SB = t16_step_bytes(QT);
   auto tile_base = [&](int g) {  // first byte of global tile g's tile16 data
     const int sg = seg_of(g);
@@ -408,8 +428,8 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   const uint8_t* tb = tile_base(gt);
   // tiles after the first (past the end: an earlier valid tile - loaded, never used)
   const int g1 = next_tile(gt);
-  const uint8_t* tbn = g1 < tiles ? tile_base(g1) : tb;
-  const uint8_t* tbn2 = g1 < tiles && next_tile(g1) < tiles ? tile_base(next_tile(g1)) : tbn;
+  const uint8_t* tbn = g1 < tiles_end ? tile_base(g1) : tb;
+  const uint8_t* tbn2 = g1 < tiles_end && next_tile(g1) < tiles_end ? tile_base(next_tile(g1)) : tbn;
   auto addr = [&](int j) {  // weights of the wave's step j counted from this tile's first
     return j < n_ws ? tb + (size_t)(ws0 + j * NW) * SB
          : j < 2 * n_ws ? tbn + (size_t)(ws0 + (j - n_ws) * NW) * SB : tbn2 + (size_t)ws0 * SB;
@@ -425,6 +445,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       tload<QT>(wb[1], p1, 1, lane, r16, kq);
     }
   }
+  if (clk && tid == 0) clk[1] = wall_clock64();
   // stage x[b][k0, k0 + kn) for the B rows
   if (NW >= 8 && a.xf) {  // (8/16-wave kernels only: keeps the split-K kernels' registers)
     // folded RMSNorm (K = 4096, B <= 8: each thread holds 2 float4 of every row): every load
@@ -456,13 +477,30 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       if (lane == 0) rowss[b * NW + wave] = ss;
     }
   } else {
-    for (int i = tid; i < a.B * (kn >> 3); i += kBlock) {
-      const int b = i / (kn >> 3), v = i - b * (kn >> 3);
-      *reinterpret_cast<uint4*>(xs + b * ldx + 8 * v) =
-          *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * v);
+    // every thread's loads go out before any LDS store: one memory round trip for the slice
+    // (a load-store loop waited for each load in turn: 3-6 round trips, 1.5-3.6 us per launch)
+    constexpr int U = 8;
+    const int nv = kn >> 3, n = a.B * nv;
+    for (int i0 = 0; i0 < n; i0 += U * kBlock) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * kBlock + tid, n - 1);
+        const int b = i / nv, c = i - b * nv;
+        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kBlock + tid;
+        if (i < n) {
+          const int b = i / nv, c = i - b * nv;
+          *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = v[u];
+        }
+      }
     }
   }
   __syncthreads();
+  if (clk && tid == 0) clk[2] = wall_clock64();
   const bool col_ok = r16 < a.B;
   // folded norm: this lane's column scale (applied to the reduced tile before any epilogue)
   float cs = 1.f;
@@ -473,7 +511,6 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     cs = rsqrtf(t / (float)kn + a.eps);
   }
   const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
-  f4_t gate[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};  // SwiGLU: wave 0's gate tiles of the unit
   // the wave's steps as one flattened sequence over its tiles, the buffers alternating
   // (wa, wb, wa, ...) along it: no register copies, and a tile's end is just a point in it
   // two accumulators (chunk h = 0 / 1): the 8 MFMAs of a step form two dependent chains of 4
@@ -516,7 +553,10 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     }
   };
   // reduction + epilogue of tile gt (every wave of the block, once per tile)
+  int ntiles_done = 0;
   auto finish_tile = [&]() {
+    if (clk && tid == 0 && ntiles_done == 0) clk[3] = wall_clock64();
+    ++ntiles_done;
     acc += acc2;
     const int sg = seg_of(gt);   // wave-uniform
     const int tile = gt - seg_first(sg);
@@ -530,15 +570,15 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
       if (NW >= 8 && a.xf) acc *= cs;
       if (sw) {
-        // tiles 4u, 4u+1: gate rows; 4u+2, 4u+3: the up rows of the same features
-        const int qt = gt & 3;
-        if (qt == 0) gate[0] = acc;
-        else if (qt == 1) gate[1] = acc;
-        else if (col_ok) {
-          const f4_t g = qt == 2 ? gate[0] : gate[1];
-          const int f0 = (gt >> 2) * 32 + (qt - 2) * 16 + 4 * kq;  // 4 consecutive features
-          const h2_t p0 = {(_Float16)(silu(g[0]) * acc[0]), (_Float16)(silu(g[2]) * acc[2])};
-          const h2_t p1 = {(_Float16)(silu(g[1]) * acc[1]), (_Float16)(silu(g[3]) * acc[3])};
+        // rows 0-7 of the tile (lanes 0-31): gate of features 8 gt + 4 kq + i; rows 8-15 (lanes
+        // 32-63): the up rows of the same features
+        f4_t up;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(acc[i], 32);
+        if (col_ok && lane < 32) {
+          const int f0 = gt * 8 + 4 * kq;  // 4 consecutive features
+          const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
+          const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
           *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
         }
       } else if (col_ok && a.qkv_epi) {
@@ -591,11 +631,11 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
     finish_tile();
     i = 0;
     gt = next_tile(gt);
-    if (gt >= tiles) return false;
+    if (gt >= tiles_end) return false;
     tb = tbn;
     tbn = tbn2;
-    const int gn2 = next_tile(gt) < tiles ? next_tile(next_tile(gt)) : tiles;
-    tbn2 = gn2 < tiles ? tile_base(gn2) : tbn;
+    const int gn2 = next_tile(gt) < tiles_end ? next_tile(next_tile(gt)) : tiles_end;
+    tbn2 = gn2 < tiles_end ? tile_base(gn2) : tbn;
     return true;
   };
   // one step: load step i + PD into `ld`, compute step i from `cur`
@@ -620,7 +660,11 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       }
     }
   } else {
-    for (; gt < tiles; gt = next_tile(gt)) finish_tile();  // idle waves still join every tile's barriers
+    for (; gt < tiles_end; gt = next_tile(gt)) finish_tile();  // idle waves still join every tile's barriers
+  }
+  if (clk && tid == 0) {
+    clk[4] = wall_clock64();
+    clk[5] = ntiles_done;
   }
 }
 
@@ -652,9 +696,10 @@ __global__ __launch_bounds__(kPrepBlock) void bprep_kernel(BPrepArgs a) {
     v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < a.K) {
       if (a.swiglu) {
-        const int gi = (i >> 5) * 64 + (i & 31);
+        const int G = a.swiglu_group;  // 32 or 8 (a power of two, i % 4 == 0 stays in one group)
+        const int gi = (i / G) * 2 * G + (i % G);
         const float4 g = *reinterpret_cast<const float4*>(xr + gi);
-        const float4 up = *reinterpret_cast<const float4*>(xr + gi + 32);
+        const float4 up = *reinterpret_cast<const float4*>(xr + gi + G);
         v[u] = make_float4(silu(g.x) * up.x, silu(g.y) * up.y, silu(g.z) * up.z, silu(g.w) * up.w);
       } else {
         v[u] = *reinterpret_cast<const float4*>(xr + i);
@@ -691,6 +736,7 @@ __global__ __launch_bounds__(kPrepBlock) void bprep_kernel(BPrepArgs a) {
 void bprep(const BPrepArgs& a, hipStream_t s) {
   if (a.B < 1 || a.K % 128 || a.K > 4 * kPrepBlock * kPrepMaxVec) throw std::runtime_error("bprep: bad shape");
   if (a.zero_n % 4) throw std::runtime_error("bprep: zero_n must be a multiple of 4");
+  if (a.swiglu && a.swiglu_group != 32 && a.swiglu_group != 8) throw std::runtime_error("bprep: swiglu group 8 or 32");
   // zero blocks: >= 4 float4 stores per thread, at most 512 blocks
   const int nz = a.zero && a.zero_n ? std::min(512, std::max(1, (a.zero_n / 4 + 4 * kPrepBlock - 1) / (4 * kPrepBlock))) : 0;
   hipLaunchKernelGGL(bprep_kernel, dim3(a.B + nz), dim3(kPrepBlock), 0, s, a);
@@ -747,10 +793,14 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     a.spp = steps;
     a.kparts = 1;
     const size_t lds = bmm_lds(a.B, steps, nw1);
-    const int units = a.swiglu_epi ? tiles / 4 : tiles;
     // blocks per CU: LDS and the 16 waves a CU holds at this kernel's register count
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 16 / nw1));
-    const int nb = std::max(1, std::min(units, per_cu * bmm_cus()));
+    int nb = std::max(1, std::min(tiles, per_cu * bmm_cus()));
+    if (a.swiglu_epi) {  // every CU group gets the same number of blocks (the range split assumes it)
+      const int G = std::max(1, std::min(bmm_cus(), tiles));
+      nb = G * std::max(1, std::min(per_cu, tiles / G));
+      a.tile_groups = G;
+    }
     if constexpr (QT == T_Q4_K) {
       if (nw1 == 16) {
         hipLaunchKernelGGL((bmm_kernel<QT, 16, 1>), dim3(nb), dim3(1024), lds, s, a);
@@ -776,7 +826,9 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   // blocks per part: ~4 blocks per CU overall (each block loops over tiles, so its staged x
   // slice - as many bytes as a tile's weights at B = 8 - is amortised over several tiles)
   static const int per_cu = env_int("LFK_BMM_GRID", 4);  // tuning
-  const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus() + kparts - 1) / kparts));
+  // blocks past per_cu * CUs would start only when a first-round block retires (a whole
+  // block lifetime of tail): the grid stays within one resident round
+  const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus()) / kparts));
   const size_t lds = bmm_lds(a.B, spp, 4);
   if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 4, 2>), dim3(bpk * kparts), dim3(256), lds, s, a);
   else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a);
@@ -790,7 +842,7 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
   if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
   if (a.qkv_epi && (!bmm_qkv_fits(a.w.K, a.B) || a.qkv.head_dim % 2)) throw std::runtime_error("bmm: qkv epilogue");
-  if (a.swiglu_epi && (a.qkv_epi || a.nseg != 1 || !bmm_qkv_fits(a.w.K, a.B) || a.n_out % 64 || !a.h_out ||
+  if (a.swiglu_epi && (a.qkv_epi || a.nseg != 1 || !bmm_qkv_fits(a.w.K, a.B) || a.n_out % 16 || !a.h_out ||
                        a.ldh_out < a.n_out / 2 || a.ldh_out % 4))
     throw std::runtime_error("bmm: swiglu epilogue");
   if (a.xf && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))

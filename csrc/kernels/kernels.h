@@ -97,14 +97,16 @@ struct BmmArgs {
     const float2* rope = nullptr;  // [n_ctx][head_dim / 2]
   } qkv;
   bool qkv_epi = false;
-  // SwiGLU epilogue (gate/up, one K part, see bmm_qkv_fits): W rows come in 32-row gate / up
-  // groups (rows 64g.. = gate features 32g.., rows 64g+32.. = up features 32g..); a block
-  // takes 4-tile units (gate, gate, up, up of one group) and writes silu(gate) * up as f16 in
-  // bmm's 4-group k order to h_out[b * ldh_out + feature] - the down projection's input -
-  // instead of accumulating into `out` (no zeroed pre-activation buffer, no SwiGLU prep)
+  // SwiGLU epilogue (gate/up, one K part, see bmm_qkv_fits): the tile16 copy is the SwiGLU
+  // form (t16_repack swiglu = true): tile t holds the gate rows of features 8t .. 8t+7, then
+  // their up rows, so every tile finishes its own features - silu(gate) * up as f16 in bmm's
+  // 4-group k order to h_out[b * ldh_out + feature], the down projection's input - instead of
+  // accumulating into `out` (no zeroed pre-activation buffer, no SwiGLU prep). Tiles are
+  // split over the blocks in per-CU-balanced contiguous ranges (see bmm.hip).
   __half* h_out = nullptr;
   int ldh_out = 0;
   bool swiglu_epi = false;
+  int tile_groups = 1;             // SwiGLU tile split: blocks b, b + tile_groups share a CU's quota (launcher)
   // RMSNorm folded into the x staging (one K part, K % 2048 == 0, see bmm_norm_fits): the
   // block reads the fp32 rows xf[b * ldxf + k], stages f16(x * norm_w) and the row sums of
   // squares; the epilogue scales each column by rsqrt(mean + eps) (xh is not read)
@@ -115,6 +117,7 @@ struct BmmArgs {
   bool store_out = false;          // plain epilogue: out = result (default: out += result)
   bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
   bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
+  long long* dbg_clk = nullptr;    // microbenchmarks only: per-block wall_clock64 stamps [grid][8]
 };
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)
@@ -122,7 +125,9 @@ bool bmm_norm_fits(int K, int B);  // one K part + the folded RMSNorm's staging 
 void bmm(const BmmArgs& a, hipStream_t s);
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);
-void t16_repack(const QMat& planar, uint8_t* dst, hipStream_t s);
+// swiglu: `planar` is a gate/up matrix in 32-row gate / up groups (upload_gate_up); the copy
+// regroups it per tile as 8 gate rows + the 8 up rows of the same features
+void t16_repack(const QMat& planar, uint8_t* dst, hipStream_t s, bool swiglu = false);
 // f32 rows -> bmm input: optional SwiGLU (x rows of 2K gate/up pre-activations, 32-feature
 // interleaved groups), optional RMSNorm (* norm_w), f16 swizzled; also zeroes zero[0, zero_n)
 struct BPrepArgs {
@@ -136,6 +141,7 @@ struct BPrepArgs {
   int ldh = 0;
   float* zero = nullptr;
   int zero_n = 0;
+  int swiglu_group = 32;           // gate/up row groups of x: 32 (planar GEMV layout) or 8 (tile16 SwiGLU copy)
 };
 void bprep(const BPrepArgs& a, hipStream_t s);
 
@@ -209,7 +215,7 @@ struct AttnDecodeArgs {
   int* counters = nullptr;        // [n_kv_head] zero-initialised; each launch leaves them at 0
   float* out = nullptr;           // [n_head][hd]
   int debug_stop = 0;             // microbenchmarks only: 1..4 = exit after stage N (0 = full kernel)
-  long long* dbg_clk = nullptr;   // microbenchmarks only: wall_clock64 stamps of block (0,0) / the merging block
+  long long* dbg_clk = nullptr;   // microbenchmarks only: per-block wall_clock64 stamps [grid][16] (attention.hip)
   // optional: a second grid plane (blockIdx.z = 1) touches one dword per 128-B line of
   // [pf, pf + pf_bytes) so the next projection's weights are in the memory-side
   // cache when its GEMV starts (the attention blocks are latency bound and leave

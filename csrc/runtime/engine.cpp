@@ -315,7 +315,7 @@ void Engine::setup_batch_mfma() {
   auto ok = [&](const QMat& m) { return m.base && bmm_supported(m.type, m.K); };
   auto kfit = [](int K) { return K % 128 == 0 && K <= 32768; };  // bprep's row shapes
   bool att = ok(output_) && kfit(hp_.n_embd) && kfit(nq_) && (V_pad_ % 4) == 0 && ((nq_ + 2 * nkvd_) % 4) == 0;
-  bool ffn = hp_.n_expert == 0 && kfit(F_l_);
+  bool ffn = hp_.n_expert == 0 && kfit(F_l_) && (2 * F_l_) % 64 == 0;
   for (int l = 0; l < hp_.n_layer; ++l) {
     const Layer& L = layers_[l];
     att = att && ok(L.wq) && ok(L.wk) && ok(L.wv) && ok(L.wo);
@@ -336,10 +336,10 @@ void Engine::setup_batch_mfma() {
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
   hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_));
   // the batched path reads its own copy of the weights, laid out per 16-row tile (bmm.hip)
-  auto tile = [&](const QMat& m) {
+  auto tile = [&](const QMat& m, bool swiglu = false) {
     QMat t = m;
     uint8_t* dst = (uint8_t*)dalloc(t16_bytes(m.type, m.rows, m.K));
-    t16_repack(m, dst, stream_);
+    t16_repack(m, dst, stream_, swiglu);
     t.base = dst;
     return t;
   };
@@ -347,7 +347,7 @@ void Engine::setup_batch_mfma() {
   for (int l = 0; l < hp_.n_layer; ++l) {
     Layer& L = layers_[l];
     L.t_wq = tile(L.wq); L.t_wk = tile(L.wk); L.t_wv = tile(L.wv); L.t_wo = tile(L.wo);
-    if (bg_ffn_) { L.t_gu = tile(L.w_gu); L.t_down = tile(L.w_down); }
+    if (bg_ffn_) { L.t_gu = tile(L.w_gu, /*swiglu=*/true); L.t_down = tile(L.w_down); }
   }
   HIPCHK(hipStreamSynchronize(stream_));
 }
@@ -773,8 +773,9 @@ void Engine::bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int 
 }
 
 void Engine::bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero,
-                        int zero_n, hipStream_t s) {
+                        int zero_n, hipStream_t s, int swiglu_group) {
   BPrepArgs p;
+  p.swiglu_group = swiglu_group;
   p.x = x; p.ldx = ldx; p.swiglu = swiglu; p.norm_w = norm_w; p.eps = hp_.rms_eps;
   p.K = K; p.B = B; p.xh = xh_b_; p.ldh = K; p.zero = zero; p.zero_n = zero_n;
   bprep(p, s);
@@ -875,7 +876,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s);
   }
   tp_end();
-  if (bg_ffn_ && fused && (2 * F_l_) % 64 == 0) {
+  if (bg_ffn_ && fused) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
     BmmArgs a;
@@ -896,7 +897,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   if (bg_ffn_) {
     bprep_rows(x_, d, false, L.ffn_norm, d, B, gu_b_, B * 2 * F_l_, s);
     bmm_rows(L.t_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
-    bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s);
+    bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s, /*swiglu_group=*/8);  // t_gu: SwiGLU copy
     tp_begin();
     bmm_rows(L.t_down, xh_b_, F_l_, acc, d, d, B, s);
     tp_end();

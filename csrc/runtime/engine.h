@@ -182,7 +182,7 @@ class Engine : public SlotBackend {
   void enqueue_batch_step(int B, hipStream_t s);
   void bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B, hipStream_t s);
   void bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero, int zero_n,
-                  hipStream_t s);
+                  hipStream_t s, int swiglu_group = 32);
   void setup_batch_mfma();
   SamplerParamsDev make_sparams(const SamplingOpts& sp) const;
   void begin_slot_state(int slot, const std::vector<int>& prompt, const SamplingOpts& sp);

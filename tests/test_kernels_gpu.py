@@ -517,11 +517,12 @@ def test_bmm_rows_vs_fp32(torch, t, B, R, K):
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
 @pytest.mark.parametrize("B", [1, 5, 8])
-@pytest.mark.parametrize("F,K", [(256, 4096), (96, 2048)])
+@pytest.mark.parametrize("F,K", [(256, 4096), (96, 2048), (7168, 4096)])
 def test_bmm_swiglu_epilogue_vs_fp32(torch, t, B, F, K):
-    """Gate/up projection with the SwiGLU epilogue: W rows in 32-row gate / up groups, the
-    kernel writes silu(gate) * up as f16 in bprep's (0, 2, 1, 3) 4-group order, against the
-    fp32 product of the same f16 activations."""
+    """Gate/up projection with the SwiGLU epilogue: W rows in 32-row gate / up groups, regrouped
+    by the SwiGLU tile16 copy into 8 gate + 8 up rows per tile; the kernel writes silu(gate) * up
+    as f16 in bprep's (0, 2, 1, 3) 4-group order, against the fp32 product of the same f16
+    activations. F = 7168 (the 8B's TP=2 slice): 896 tiles over the per-CU balanced ranges."""
     rng = np.random.default_rng(B * 100 + F + int(t))
     R = 2 * F
     raw, W = make_matrix(t, R, K, rng)
@@ -532,7 +533,7 @@ def test_bmm_swiglu_epilogue_vs_fp32(torch, t, B, F, K):
     ldh_out = F + 8
     hout = torch.full((B, ldh_out), 7.0, dtype=torch.float16, device="cuda")
     tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
-    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream(), swiglu=True)
     hip().bmm(tw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, 0, 0, B, stream(),
               h_out=hout.data_ptr(), ldh_out=ldh_out)
     torch.cuda.synchronize()
@@ -569,7 +570,7 @@ def test_bmm_folded_norm_vs_fp32(torch, t, B, mode):
     dx[:, :K] = torch.from_numpy(X).cuda()
     dn = torch.from_numpy(nw).cuda()
     tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
-    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream(), swiglu=(mode == "swiglu"))
     xn = X.astype(np.float64) / np.sqrt((X.astype(np.float64) ** 2).mean(1, keepdims=True) + eps) * nw
     pre = xn @ W.astype(np.float64).T
     if mode == "store":
@@ -614,9 +615,10 @@ def test_bprep_norm_swiglu_zero(torch):
     assert float(z.abs().sum()) == 0.0
     GU = rng.standard_normal((B, 2 * K)).astype(np.float32)
     dgu = torch.from_numpy(GU).cuda()
-    hip().bprep(dgu.data_ptr(), 2 * K, True, 0, 1e-5, K, B, xh.data_ptr(), K, stream())
-    torch.cuda.synchronize()
-    g = GU.reshape(B, -1, 2, 32)[:, :, 0, :].reshape(B, K)
-    u = GU.reshape(B, -1, 2, 32)[:, :, 1, :].reshape(B, K)
-    h = (g / (1 + np.exp(-g)) * u).astype(np.float16)
-    assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(h).astype(np.float32)) < 2e-3
+    for G in (32, 8):   # planar gate / up groups, and the SwiGLU tile16 copy's 8-row groups
+        hip().bprep(dgu.data_ptr(), 2 * K, True, 0, 1e-5, K, B, xh.data_ptr(), K, stream(), swiglu_group=G)
+        torch.cuda.synchronize()
+        g = GU.reshape(B, -1, 2, G)[:, :, 0, :].reshape(B, K)
+        u = GU.reshape(B, -1, 2, G)[:, :, 1, :].reshape(B, K)
+        h = (g / (1 + np.exp(-g)) * u).astype(np.float16)
+        assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(h).astype(np.float32)) < 2e-3, G

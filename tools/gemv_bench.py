@@ -140,14 +140,16 @@ def main():
                                 hd ** -0.5, part.data_ptr(), ao.data_ptr(), st, cnt.data_ptr(), debug_stop=stop)
             timed(f"attn_decode_L{L}" + ("" if stop == 0 else f"_stop{stop}"), fn, 2 * 8 * L * hd * 2)
     # in-kernel timeline (wall_clock64 ticks of 10 ns) of block (0,0) and the merging block
-    stamps = torch.zeros(16, dtype=torch.int64, device="cuda")
+    stamps = torch.zeros(16 * 8 * ((n_ctx + 63) // 64), dtype=torch.int64, device="cuda")
     for L in (128, 1000):
         p = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
         for _ in range(3):
             hip.attn_decode(qa.data_ptr(), kc.data_ptr(), vc.data_ptr(), p.data_ptr(), n_ctx, 32, 8, hd, hd ** -0.5,
                             part.data_ptr(), ao.data_ptr(), s, cnt.data_ptr(), dbg_clk=stamps.data_ptr())
         torch.cuda.synchronize()
-        res[f"attn_timeline_L{L}_us"] = {"us": [round(v / 100.0, 2) for v in stamps.tolist()[:10]], "TB_s": 0}
+        st0 = stamps.tolist()[:16]   # block (0, 0): absolute stamps -> us after its entry
+        res[f"attn_timeline_L{L}_us"] = {"us": [round((v - st0[0]) / 100.0, 2) if v else None for v in st0[1:11]],
+                                        "TB_s": 0}
     # floor: an empty kernel (debug_stop=1 at L=1 exits immediately in every block)
     p1 = torch.tensor([0], dtype=torch.int32, device="cuda")
     timed("empty_kernel_floor", lambda st=s: hip.attn_decode(qa.data_ptr(), kc.data_ptr(), vc.data_ptr(),

@@ -16,6 +16,11 @@ step() {  # step <name> <timeout> <cmd...>
 for s in "$@"; do
   case $s in
     tp) step tp 460 python -u -m pytest tests/test_p2p_allreduce.py tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread -p no:cacheprovider ;;
+    bmmt) step bmmt 400 python -u -m pytest tests/test_kernels_gpu.py -k "bmm or bprep" -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
+    attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
+    attntl1) step attntl1 200 python tools/attn_timeline.py --rows 1 --L 700 ;;
+    bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
     samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     kern) step kern 900 python -m pytest tests/test_kernels_gpu.py -q -p no:cacheprovider ;;
     eng) step eng 900 python -m pytest tests/test_engine_gpu.py -q -p no:cacheprovider ;;
