@@ -62,9 +62,16 @@ def _blocks(data: np.ndarray, ggml_type) -> np.ndarray:
 # ------------------------------------------------------------- dequantise
 
 
-def dequantize(data, ggml_type, n_elements: int | None = None) -> np.ndarray:
-    """Decode raw ggml bytes into float32 (flat)."""
+def dequantize(data, ggml_type, n_elements: int | None = None, arith: str = "f32") -> np.ndarray:
+    """Decode raw ggml bytes into float32 (flat).
+
+    ``arith="f16"`` reproduces the batched decode projection's dequantisation bit for bit
+    (kernels/bmm.hip on its tile16 copy): the per-sub-block scale d*sc and offset -dmin*m are
+    rounded to f16 once, and every weight is ONE f16 rounding of q*scale + offset (a fused
+    v_pk_fma_f16). Returned as float32 (exact f16 values)."""
     t = GGMLType(ggml_type)
+    if arith == "f16" and t in (GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K):
+        return _dequantize_f16(data, t, n_elements)
     if t == GGMLType.F32:
         return np.frombuffer(bytes(data) if not isinstance(data, np.ndarray) else data.tobytes(),
                              dtype=np.float32).copy()
@@ -125,6 +132,55 @@ def dequantize(data, ggml_type, n_elements: int | None = None) -> np.ndarray:
     else:
         raise NotImplementedError(f"dequantize {t.name}")
     out = out.reshape(-1)
+    if n_elements is not None:
+        assert out.size == n_elements
+    return out
+
+def _dequantize_f16(data, t, n_elements):
+    b = _blocks(data, t)
+    nb = b.shape[0]
+    h = lambda v: np.asarray(v, np.float64).astype(np.float16).astype(np.float64)  # noqa: E731
+    if t == GGMLType.Q8_0:
+        d = b[:, 0:2].copy().view(np.float16).astype(np.float64)
+        q = b[:, 2:34].view(np.int8).astype(np.float64)
+        out = h(d * q)
+    elif t in (GGMLType.Q4_K, GGMLType.Q5_K):
+        d = b[:, 0:2].copy().view(np.float16).astype(np.float64)[:, 0]
+        dmin = b[:, 2:4].copy().view(np.float16).astype(np.float64)[:, 0]
+        sc, m = _unpack_scale_min_k4(b[:, 4:16])
+        qs = b[:, 16:144] if t == GGMLType.Q4_K else b[:, 48:176]
+        qh = None if t == GGMLType.Q4_K else b[:, 16:48]
+        out = np.empty((nb, 256), np.float64)
+        for j in range(4):
+            grp = qs[:, 32 * j:32 * j + 32]
+            lo = (grp & 0xF).astype(np.float64)
+            hi = (grp >> 4).astype(np.float64)
+            if qh is not None:
+                lo += ((qh >> (2 * j)) & 1).astype(np.float64) * 16
+                hi += ((qh >> (2 * j + 1)) & 1).astype(np.float64) * 16
+            for half, q in ((0, lo), (1, hi)):
+                sb = 2 * j + half
+                a = h(d * sc[:, sb])
+                mn = h(-dmin * m[:, sb])
+                out[:, 64 * j + 32 * half:64 * j + 32 * half + 32] = h(q * a[:, None] + mn[:, None])
+    else:  # Q6_K
+        ql = b[:, 0:128]
+        qh = b[:, 128:192]
+        scales = b[:, 192:208].view(np.int8).astype(np.float64)
+        d = b[:, 208:210].copy().view(np.float16).astype(np.float64)[:, 0]
+        out = np.empty((nb, 256), np.float64)
+        for n in range(2):
+            l_ = ql[:, 64 * n:64 * n + 64]
+            h_ = qh[:, 32 * n:32 * n + 32]
+            sc = scales[:, 8 * n:8 * n + 8]
+            q1 = ((l_[:, 0:32] & 0xF) | (((h_ >> 0) & 3) << 4)).astype(np.float64) - 32
+            q2 = ((l_[:, 32:64] & 0xF) | (((h_ >> 2) & 3) << 4)).astype(np.float64) - 32
+            q3 = ((l_[:, 0:32] >> 4) | (((h_ >> 4) & 3) << 4)).astype(np.float64) - 32
+            q4 = ((l_[:, 32:64] >> 4) | (((h_ >> 6) & 3) << 4)).astype(np.float64) - 32
+            for k, q in enumerate((q1, q2, q3, q4)):
+                a = np.repeat(h(d[:, None] * sc[:, [2 * k, 2 * k + 1]]), 16, axis=1)
+                out[:, 128 * n + 32 * k:128 * n + 32 * k + 32] = h(q * a)
+    out = out.reshape(-1).astype(np.float32)
     if n_elements is not None:
         assert out.size == n_elements
     return out

@@ -116,10 +116,10 @@ class GGUFReader:
         ti = self.tensors[name]
         return self._mm[ti.offset:ti.offset + ti.nbytes]
 
-    def dequant(self, name: str) -> np.ndarray:
+    def dequant(self, name: str, arith: str = "f32") -> np.ndarray:
         """float32 array in row-major numpy order (reverse of ggml shape)."""
         ti = self.tensors[name]
-        return dequantize(np.asarray(self.raw(name)), ti.ggml_type, ti.n_elements).reshape(ti.shape[::-1])
+        return dequantize(np.asarray(self.raw(name)), ti.ggml_type, ti.n_elements, arith=arith).reshape(ti.shape[::-1])
 
     def get(self, key: str, default=None):
         return self.metadata.get(key, default)

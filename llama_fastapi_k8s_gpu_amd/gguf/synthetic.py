@@ -107,6 +107,9 @@ SPECS: Dict[str, ModelSpec] = {
     # weight touch's per-CU gate/up segments must clamp to the plane end)
     "tiny-q8-oddff": ModelSpec("tiny-q8-oddff", 256, 2, 4, 2, 576, 0, 10000.0, "spm", "q8_0",
                                n_ctx_train=1024),
+    # 32 layers (the 8B's depth) at d 1024: the Q4_K_M bump pattern over a full-depth stack
+    "tiny-llama3-deep32": ModelSpec("tiny-llama3-deep32", 1024, 32, 8, 2, 512, 0, 500000.0, "bpe", "q4_k_m",
+                                    n_ctx_train=1024),
     # d = 4096 with the Llama-3 GQA grouping (32 q heads on 8 kv heads), 4 layers (Q4_K_M mix:
     # layers 0 and 3 bump V/down to Q6_K): full-width kernels at test cost
     "pd-llama-g4": ModelSpec("pd-llama-g4", 4096, 4, 32, 8, 2048, 0, 500000.0, "bpe", "q4_k_m",

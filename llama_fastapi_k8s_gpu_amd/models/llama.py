@@ -72,11 +72,31 @@ def rope_tables(hp: LlamaHParams, n_pos: int):
 
 
 class ReferenceLlama:
-    """float32 torch forward over a GGUFReader (CPU; tiny models only)."""
+    """float32 torch forward over a GGUFReader (CPU; tiny models only).
+
+    ``forward(..., path=...)`` optionally reproduces the activation and weight rounding of
+    one of the MI355X engine's compute paths, so engine-level tests can hold the engine to
+    ~1e-3 instead of the ~5e-2 its roundings cost against the exact model:
+
+      * ``"decode"`` (single-row GEMV, kernels/gemv.hip): every projection input quantised
+        to q8 per 32 (scale amax/127, nearest) - of x * w_norm before the 1/rms scale for the
+        normed inputs - exact weights; attention on f16 q * scale, f16 K/V;
+      * ``"prefill"`` (MFMA GEMM, kernels/gemm.hip + attention.hip): bf16 activations and
+        bf16-rounded dequantised weights; attention with q * scale * log2(e) in f16, f16 P and
+        K/V, bf16 output; the logits row through the decode head (q8);
+      * ``"batch"`` (batched MFMA projections, kernels/bmm.hip): f16(x * w_norm) with the
+        1/rms applied to the f32 result, f16 weights from the tile16 copy's f16 arithmetic
+        (quants.dequantize(arith="f16")), f16 attention output and SwiGLU output; the head
+        input f16(x / rms * w).
+    K/V are stored f16 in every emulated path (the engine's cache). ``path=None`` is the exact
+    fp32 model.
+    """
 
     def __init__(self, reader, n_ctx: int = 512, device: str = "cpu"):
         import torch
         self.torch = torch
+        self.reader = reader
+        self.device = device
         self.hp = LlamaHParams.from_metadata(reader.metadata)
         hp = self.hp
         if not hp.n_vocab:
@@ -85,7 +105,8 @@ class ReferenceLlama:
         t = lambda name: torch.from_numpy(np.ascontiguousarray(reader.dequant(name))).to(device)
         self.tok_embd = t("token_embd.weight")
         self.out_norm = t("output_norm.weight")
-        self.output = t("output.weight") if "output.weight" in reader.tensors else self.tok_embd
+        self._out_name = "output.weight" if "output.weight" in reader.tensors else "token_embd.weight"
+        self.output = t(self._out_name)
         self.layers: List[Dict] = []
         for i in range(hp.n_layer):
             p = f"blk.{i}."
@@ -97,15 +118,78 @@ class ReferenceLlama:
             else:
                 for k in ("ffn_gate", "ffn_up", "ffn_down"):
                     L[k] = t(p + k + ".weight")
+            L["_prefix"] = p
             self.layers.append(L)
         cos, sin = rope_tables(hp, n_ctx)
         self.cos = torch.from_numpy(cos).to(device)
         self.sin = torch.from_numpy(sin).to(device)
         self.k_cache = torch.zeros(hp.n_layer, n_ctx, hp.n_head_kv, hp.head_dim, device=device)
         self.v_cache = torch.zeros_like(self.k_cache)
+        self._wcache: Dict = {}
+
+    # ------------------------------------------------------------ rounding helpers
+    def _f16(self, x):
+        return x.half().float()
+
+    def _bf16(self, x):
+        return x.bfloat16().float()
+
+    def _q8(self, x):
+        """Per-32-block symmetric int8 quantise-dequantise along the last dim."""
+        torch = self.torch
+        shp = x.shape
+        b = x.reshape(*shp[:-1], shp[-1] // 32, 32)
+        amax = b.abs().amax(-1, keepdim=True)
+        s = amax / 127.0
+        q = torch.where(s > 0, torch.round(b / torch.where(s > 0, s, torch.ones_like(s))), torch.zeros_like(b))
+        return (q * s).reshape(shp)
+
+    def _weight(self, key: str, L: Optional[Dict], kind: str):
+        """Weight `key` of layer L (or the output head, L None) as the path reads it."""
+        if kind == "f32":
+            return self.output if L is None else L[key]
+        name = self._out_name if L is None else L["_prefix"] + key + ".weight"
+        ck = (name, kind)
+        if ck not in self._wcache:
+            torch = self.torch
+            if kind == "bf16":
+                w = self._bf16(self.output if L is None else L[key])
+            else:  # "f16": the batched path's tile16 dequantisation (F32/F16 tensors stay exact)
+                ti = self.reader.tensors[name]
+                arr = np.asarray(self.reader.raw(name))
+                from ..gguf.quants import dequantize
+                w = torch.from_numpy(np.ascontiguousarray(
+                    dequantize(arr, ti.ggml_type, ti.n_elements, arith="f16").reshape(ti.shape[::-1]))).to(self.device)
+            self._wcache[ck] = w
+        return self._wcache[ck]
 
     def _rms(self, x, w):
         return x * self.torch.rsqrt((x * x).mean(-1, keepdim=True) + self.hp.rms_eps) * w
+
+    def _normed_input(self, x, w, path):
+        """The normalised projection input the path feeds its matmul."""
+        torch = self.torch
+        rs = torch.rsqrt((x * x).mean(-1, keepdim=True) + self.hp.rms_eps)
+        if path == "decode":
+            return self._q8(x * w) * rs
+        if path == "prefill":
+            return self._bf16(x * rs * w)
+        if path == "batch":
+            return self._f16(x * w) * rs
+        return x * rs * w
+
+    def _plain_input(self, h, path):
+        """A projection input that is not a norm output (attention out, SwiGLU out)."""
+        if path == "decode":
+            return self._q8(h)
+        if path == "prefill":
+            return self._bf16(h)
+        if path == "batch":
+            return self._f16(h)
+        return h
+
+    def _wkind(self, path):
+        return {"prefill": "bf16", "batch": "f16"}.get(path, "f32")
 
     def _rope(self, x, pos):
         # x [T, H, D]; adjacent pairs (2i, 2i+1)
@@ -117,60 +201,104 @@ class ReferenceLlama:
         out[..., 1::2] = x0 * s + x1 * c
         return out
 
-    def _ffn(self, L, h):
+    def _ffn(self, L, x, path):
         torch = self.torch
         F = torch.nn.functional
+        wk = self._wkind(path)
+        h = self._normed_input(x, L["ffn_norm"], path)
         if not self.hp.n_expert:
-            return (F.silu(h @ L["ffn_gate"].T) * (h @ L["ffn_up"].T)) @ L["ffn_down"].T
-        logits = h @ L["ffn_gate_inp"].T                      # [T, E]
+            a = F.silu(h @ self._weight("ffn_gate", L, wk).T) * (h @ self._weight("ffn_up", L, wk).T)
+            return self._plain_input(a, path) @ self._weight("ffn_down", L, wk).T
+        # MoE: the batched path runs the prefill GEMM FFN (bf16), the decode path the GEMV
+        # experts (q8) with the f32 router
+        if path == "batch":
+            path, wk = "prefill", "bf16"
+            h = self._normed_input(x, L["ffn_norm"], path)
+        rw = L["ffn_gate_inp"] if path != "prefill" else self._bf16(L["ffn_gate_inp"])
+        hr = self._normed_input(x, L["ffn_norm"], None) if path == "decode" else h
+        logits = hr @ rw.T                                    # [T, E]
         probs = torch.softmax(logits, -1)
         w, ids = torch.topk(probs, self.hp.n_expert_used, dim=-1)
         w = w / w.sum(-1, keepdim=True)
         out = torch.zeros_like(h)
+        ge = L["ffn_gate_exps"] if path is None else self._bf16(L["ffn_gate_exps"]) if path == "prefill" else L["ffn_gate_exps"]
+        ue = L["ffn_up_exps"] if path is None else self._bf16(L["ffn_up_exps"]) if path == "prefill" else L["ffn_up_exps"]
+        de = L["ffn_down_exps"] if path is None else self._bf16(L["ffn_down_exps"]) if path == "prefill" else L["ffn_down_exps"]
         for t in range(h.shape[0]):
             for j in range(self.hp.n_expert_used):
                 e = int(ids[t, j])
-                g = F.silu(L["ffn_gate_exps"][e] @ h[t]) * (L["ffn_up_exps"][e] @ h[t])
-                out[t] += w[t, j] * (L["ffn_down_exps"][e] @ g)
+                g = F.silu(ge[e] @ h[t]) * (ue[e] @ h[t])
+                out[t] += w[t, j] * (de[e] @ self._plain_input(g[None], path)[0])
         return out
 
-    def forward(self, tokens, n_past: int, all_logits: bool = False, trace: Optional[List[Dict]] = None):
-        """Evaluate ``tokens`` at positions n_past.. ; returns logits [T,V] or [V].
-        ``trace`` (a list) receives per layer the last token's q / k / v (roped), the attention
-        output, x after the attention residual, the SwiGLU output and x after the FFN residual."""
+    def _attention(self, q, li, pos, n_past, T, path):
         torch = self.torch
         hp = self.hp
+        scale = 1.0 / np.sqrt(hp.head_dim)
+        Lk = n_past + T
+        K = self.k_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)   # [Lk, H, D]
+        V = self.v_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)
+        mask = torch.arange(Lk)[None, :] > pos[:, None]
+        if path == "prefill":
+            l2e = 1.4426950408889634
+            s = torch.einsum("thd,lhd->htl", self._f16(q * (scale * l2e)), K)
+            s = s.masked_fill(mask[None], float("-inf"))
+            p = torch.exp2(s - s.amax(-1, keepdim=True))
+            a = torch.einsum("htl,lhd->thd", self._f16(p), V) / p.sum(-1).permute(1, 0)[..., None]
+            return a.reshape(T, -1)
+        if path in ("decode", "batch"):
+            q = self._f16(q * scale)
+            s = torch.einsum("thd,lhd->htl", q, K)
+        else:
+            s = torch.einsum("thd,lhd->htl", q, K) * scale
+        s = s.masked_fill(mask[None], float("-inf"))
+        return torch.einsum("htl,lhd->thd", torch.softmax(s, -1), V).reshape(T, -1)
+
+    def forward(self, tokens, n_past: int, all_logits: bool = False, trace: Optional[List[Dict]] = None,
+                path: Optional[str] = None):
+        """Evaluate ``tokens`` at positions n_past.. ; returns logits [T,V] or [V].
+        ``trace`` (a list) receives per layer the last token's q / k / v (roped), the attention
+        output, x after the attention residual, the SwiGLU output and x after the FFN residual.
+        ``path``: None (exact fp32) or the engine path whose rounding to reproduce (class doc)."""
+        torch = self.torch
+        hp = self.hp
+        if path not in (None, "decode", "prefill", "batch"):
+            raise ValueError(f"unknown path {path!r}")
         T = len(tokens)
         pos = torch.arange(n_past, n_past + T)
         x = self.tok_embd[torch.as_tensor(list(tokens))]
-        scale = 1.0 / np.sqrt(hp.head_dim)
+        wk = self._wkind(path)
         for li, L in enumerate(self.layers):
-            h = self._rms(x, L["attn_norm"])
-            q = (h @ L["attn_q"].T).view(T, hp.n_head, hp.head_dim)
-            k = (h @ L["attn_k"].T).view(T, hp.n_head_kv, hp.head_dim)
-            v = (h @ L["attn_v"].T).view(T, hp.n_head_kv, hp.head_dim)
+            h = self._normed_input(x, L["attn_norm"], path)
+            q = (h @ self._weight("attn_q", L, wk).T).view(T, hp.n_head, hp.head_dim)
+            k = (h @ self._weight("attn_k", L, wk).T).view(T, hp.n_head_kv, hp.head_dim)
+            v = (h @ self._weight("attn_v", L, wk).T).view(T, hp.n_head_kv, hp.head_dim)
             q, k = self._rope(q, pos), self._rope(k, pos)
+            if path is not None:   # the engine's KV cache is f16
+                k, v = self._f16(k), self._f16(v)
             self.k_cache[li, n_past:n_past + T] = k
             self.v_cache[li, n_past:n_past + T] = v
-            Lk = n_past + T
-            K = self.k_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)   # [Lk, H, D]
-            V = self.v_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)
-            s = torch.einsum("thd,lhd->htl", q, K) * scale
-            mask = torch.arange(Lk)[None, :] > pos[:, None]
-            s = s.masked_fill(mask[None], float("-inf"))
-            a = torch.einsum("htl,lhd->thd", torch.softmax(s, -1), V).reshape(T, -1)
-            x = x + a @ L["attn_output"].T
-            h = self._rms(x, L["ffn_norm"])
+            a = self._attention(q, li, pos, n_past, T, path)
+            x = x + self._plain_input(a, path) @ self._weight("attn_output", L, wk).T
             if trace is not None and not self.hp.n_expert:
                 F = torch.nn.functional
-                hh = F.silu(h @ L["ffn_gate"].T) * (h @ L["ffn_up"].T)
+                hn = self._rms(x, L["ffn_norm"])
+                hh = F.silu(hn @ L["ffn_gate"].T) * (hn @ L["ffn_up"].T)
                 trace.append({"q": q[-1].reshape(-1).clone(), "k": k[-1].reshape(-1).clone(),
                               "v": v[-1].reshape(-1).clone(), "o": a[-1].clone(), "x_attn": x[-1].clone(),
                               "h": hh[-1].clone()})
-            x = x + self._ffn(L, h)
+            x = x + self._ffn(L, x, path)
             if trace is not None and not self.hp.n_expert:
                 trace[-1]["x_ffn"] = x[-1].clone()
-        x = self._rms(x, self.out_norm)
+        # the logits: prefill and decode both end on the GEMV head (q8); the batched head
+        # stages f16(x / rms * w) for the tile16 f16 output weights
+        hpath = {"prefill": "decode"}.get(path, path)
+        if hpath == "batch":
+            rs = torch.rsqrt((x * x).mean(-1, keepdim=True) + hp.rms_eps)
+            xo = self._f16(x * rs * self.out_norm)
+        else:
+            xo = self._normed_input(x, self.out_norm, hpath)
+        W = self._weight(None, None, self._wkind(hpath))
         if all_logits:
-            return x @ self.output.T
-        return x[-1] @ self.output.T
+            return xo @ W.T
+        return xo[-1] @ W.T

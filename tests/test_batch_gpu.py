@@ -29,27 +29,46 @@ def test_batch_step_rows_match_reference(models, spec):
     eng = load_hip().Engine(path, n_ctx=256, n_batch=64, device=0, use_graph=False, n_slots=4)
     assert eng.n_slots == 4 and eng.max_batch == 4
     ref = ReferenceLlama(GGUFReader(path), n_ctx=256)
+    emu = ReferenceLlama(GGUFReader(path), n_ctx=256)
     rng = np.random.default_rng(3)
     greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
     slots = [3, 0, 1]                      # not in order, slot 2 unused
-    seqs = {}
+    seqs, plen, paths = {}, {}, {}
     for s, n in zip(slots, (5, 40, 17)):
         prompt = [int(t) for t in rng.integers(3, 300, n)]
         first = eng.slot_begin(s, prompt, 0, greedy)
         seqs[s] = prompt + [first]
+        plen[s] = n
+        paths[s] = []
+
+    def emulated(s):
+        """The slot's history as the engine computed it: the prompt on the prefill path, each
+        fed token on the path of the step that fed it (batched rows; one row = the GEMV decode)."""
+        out = emu.forward(seqs[s][:plen[s]], 0, path="prefill")
+        for i, p in enumerate(paths[s]):
+            out = emu.forward([seqs[s][plen[s] + i]], plen[s] + i, path=p)
+        return out.numpy()
     for step in range(3):
         toks = eng.batch_step(slots)
         logits = eng.batch_logits(len(slots))
         for b, s in enumerate(slots):
+            paths[s].append("batch")
             want = ref.forward(seqs[s], 0).numpy()
             assert rel_err(logits[b], want) < 5e-2, (spec, step, s, rel_err(logits[b], want))
+            e = rel_err(logits[b], emulated(s))
+            assert e < TIGHT[spec], (spec, step, s, e)
             assert toks[b] == int(np.argmax(logits[b]))
             seqs[s].append(toks[b])
-    # a sub-batch of the slots continues where each slot stands
+    # a sub-batch of the slots continues where each slot stands (one row: the GEMV decode graph)
     toks = eng.batch_step([1])
+    paths[1].append("decode")
     want = ref.forward(seqs[1], 0).numpy()
     assert rel_err(eng.batch_logits(1)[0], want) < 5e-2
+    assert rel_err(eng.batch_logits(1)[0], emulated(1)) < TIGHT[spec]
     assert eng.healthy, eng.last_error
+
+
+TIGHT = {"tiny-llama3-q4_k_m": 5e-3, "tiny-tinyllama-q8_0": 5e-3, "tiny-mixtral-q4_k_m": 2e-2}
 
 
 def test_batch_step_d4096_fused_paths(tmp_path):
@@ -63,18 +82,25 @@ def test_batch_step_d4096_fused_paths(tmp_path):
     path = write_synthetic_gguf("pd-llama-g4", str(tmp_path / "g4.gguf"))
     eng = load_hip().Engine(path, n_ctx=128, n_batch=64, device=0, use_graph=True, n_slots=4)
     ref = ReferenceLlama(GGUFReader(path), n_ctx=128)
+    emu = ReferenceLlama(GGUFReader(path), n_ctx=128)
     rng = np.random.default_rng(5)
     greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
-    seqs = {}
+    seqs, plen = {}, {}
     for s, n in zip((2, 0, 3), (6, 11, 9)):
         prompt = [int(t) for t in rng.integers(3, 300, n)]
         seqs[s] = prompt + [eng.slot_begin(s, prompt, 0, greedy)]
+        plen[s] = n
     for rows in ([2, 0, 3], [0, 3]):
         toks = eng.batch_step(rows)
         logits = eng.batch_logits(len(rows))
         for b, s in enumerate(rows):
             want = ref.forward(seqs[s], 0).numpy()
             assert rel_err(logits[b], want) < 5e-2, (s, rel_err(logits[b], want))
+            out = emu.forward(seqs[s][:plen[s]], 0, path="prefill")
+            for i in range(plen[s], len(seqs[s])):
+                out = emu.forward([seqs[s][i]], i, path="batch")
+            e = rel_err(logits[b], out.numpy())
+            assert e < 5e-3, (s, e)
             assert toks[b] == int(np.argmax(logits[b]))
             seqs[s].append(toks[b])
     assert eng.healthy, eng.last_error

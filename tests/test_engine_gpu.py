@@ -29,20 +29,49 @@ def _engine(path, n_ctx=256, graph=True):
 
 @pytest.mark.parametrize("spec", SPECS)
 def test_prefill_and_decode_logits_match_reference(models, spec):
+    """Prefill (MFMA GEMM) and decode (GEMV) logits against the fp32 model that reproduces
+    each path's rounding (ReferenceLlama path=...): tight; and against the exact model: the
+    rounding's own size."""
     from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
     path = models[spec]
     ref = ReferenceLlama(GGUFReader(path), n_ctx=256)
+    emu = ReferenceLlama(GGUFReader(path), n_ctx=256)
     eng = _engine(path)
     rng = np.random.default_rng(0)
-    toks = [int(t) for t in rng.integers(0, ref.hp.n_vocab, 40)]
-    ref_pre = ref.forward(toks[:39], 0).numpy()
+    toks = [int(t) for t in rng.integers(0, ref.hp.n_vocab, 44)]
     got_pre = eng.eval_logits(toks[:39], 0)
-    assert rel_err(got_pre, ref_pre) < 5e-2, spec
-    ref_dec = ref.forward([toks[39]], 39).numpy()
-    got_dec = eng.decode_logits(toks[39], 39)
-    assert rel_err(got_dec, ref_dec) < 5e-2, spec
+    assert rel_err(got_pre, ref.forward(toks[:39], 0).numpy()) < 5e-2, spec
+    e = rel_err(got_pre, emu.forward(toks[:39], 0, path="prefill").numpy())
+    assert e < TIGHT[spec], (spec, "prefill", e)
+    for i in range(39, 44):   # several graph-replayed decode steps on the prefilled cache
+        ref_dec = ref.forward([toks[i]], i).numpy()
+        got_dec = eng.decode_logits(toks[i], i)
+        assert rel_err(got_dec, ref_dec) < 5e-2, spec
+        e = rel_err(got_dec, emu.forward([toks[i]], i, path="decode").numpy())
+        assert e < TIGHT[spec], (spec, "decode", i, e)
     assert np.argmax(got_dec) == np.argmax(ref_dec) or \
         ref_dec[np.argmax(got_dec)] > ref_dec.max() - 0.05 * np.abs(ref_dec).max()
+
+
+# engine vs the rounding-emulating reference; MoE: a near-tie in the router flips an expert on
+# one side only (the router logits differ by the emulation's residual order of ~1e-6)
+TIGHT = {s: 5e-3 for s in SPECS}
+TIGHT["tiny-mixtral-q4_k_m"] = 2e-2
+
+
+def test_deep_model_no_drift(tmp_path):
+    """32 layers (d 1024, Q4_K_M mix incl. the bumped Q6_K V / down layers): prefill and
+    decode logits stay on the rounding-emulating reference through the whole depth."""
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    path = write_synthetic_gguf("tiny-llama3-deep32", str(tmp_path / "deep.gguf"), seed=2)
+    emu = ReferenceLlama(GGUFReader(path), n_ctx=128)
+    eng = _engine(path, n_ctx=128)
+    toks = [int(t) for t in np.random.default_rng(9).integers(3, 500, 24)]
+    e = rel_err(eng.eval_logits(toks[:20], 0), emu.forward(toks[:20], 0, path="prefill").numpy())
+    assert e < 5e-3, ("prefill", e)
+    for i in range(20, 24):
+        e = rel_err(eng.decode_logits(toks[i], i), emu.forward([toks[i]], i, path="decode").numpy())
+        assert e < 5e-3, ("decode", i, e)
 
 
 @pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m", "tiny-q8-oddff"])
