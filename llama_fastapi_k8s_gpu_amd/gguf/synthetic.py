@@ -107,6 +107,15 @@ SPECS: Dict[str, ModelSpec] = {
     # weight touch's per-CU gate/up segments must clamp to the plane end)
     "tiny-q8-oddff": ModelSpec("tiny-q8-oddff", 256, 2, 4, 2, 576, 0, 10000.0, "spm", "q8_0",
                                n_ctx_train=1024),
+    # one layer: each engine path against the rounding-emulating reference op for op (with more
+    # layers, 1e-7 summation-order differences flip q8 / bf16 roundings downstream)
+    "tiny-llama3-1l": ModelSpec("tiny-llama3-1l", 256, 1, 4, 2, 512, 0, 500000.0, "bpe", "q4_k_m",
+                                n_ctx_train=1024),
+    "tiny-mixed-1l": ModelSpec("tiny-mixed-1l", 256, 1, 4, 2, 512, 0, 500000.0, "bpe", "mixed-test",
+                               n_ctx_train=1024),
+    "tiny-q8-1l": ModelSpec("tiny-q8-1l", 512, 1, 8, 1, 768, 0, 10000.0, "spm", "q8_0", n_ctx_train=1024),
+    "tiny-mixtral-1l": ModelSpec("tiny-mixtral-1l", 256, 1, 4, 2, 512, 0, 1e6, "spm", "q4_k_m",
+                                 n_expert=4, n_expert_used=2, n_ctx_train=1024),
     # 32 layers (the 8B's depth) at d 1024: the Q4_K_M bump pattern over a full-depth stack
     "tiny-llama3-deep32": ModelSpec("tiny-llama3-deep32", 1024, 32, 8, 2, 512, 0, 500000.0, "bpe", "q4_k_m",
                                     n_ctx_train=1024),

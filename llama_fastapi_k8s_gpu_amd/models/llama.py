@@ -85,7 +85,7 @@ class ReferenceLlama:
         bf16-rounded dequantised weights; attention with q * scale * log2(e) in f16, f16 P and
         K/V, bf16 output; the logits row through the decode head (q8);
       * ``"batch"`` (batched MFMA projections, kernels/bmm.hip): f16(x * w_norm) with the
-        1/rms applied to the f32 result, f16 weights from the tile16 copy's f16 arithmetic
+        1/rms applied to the f32 result (d = 4096, the folded norm; f16(x / rms * w) below), f16 weights from the tile16 copy's f16 arithmetic
         (quants.dequantize(arith="f16")), f16 attention output and SwiGLU output; the head
         input f16(x / rms * w).
     K/V are stored f16 in every emulated path (the engine's cache). ``path=None`` is the exact
@@ -175,7 +175,9 @@ class ReferenceLlama:
         if path == "prefill":
             return self._bf16(x * rs * w)
         if path == "batch":
-            return self._f16(x * w) * rs
+            # d = 4096 (B <= 8): the norm folded into the projection's x staging applies 1/rms
+            # to the f32 result; otherwise bmm's prep kernel stages f16(x / rms * w)
+            return self._f16(x * w) * rs if x.shape[-1] == 4096 else self._f16(x * rs * w)
         return x * rs * w
 
     def _plain_input(self, h, path):
