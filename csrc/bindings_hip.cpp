@@ -124,6 +124,14 @@ PYBIND11_MODULE(_hip, m) {
              py::gil_scoped_release nogil;
              return e.slot_begin(slot, prompt, n_keep, o);
            })
+      .def("slots_begin",
+           [](Engine& e, const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+              const std::vector<int>& n_keep, py::list sps) {
+             std::vector<SamplingOpts> o;
+             for (auto h : sps) o.push_back(sampling_opts(h.cast<py::dict>()));
+             py::gil_scoped_release nogil;
+             return e.slots_begin(slots, prompts, n_keep, o);
+           })
       .def("batch_step",
            [](Engine& e, const std::vector<int>& slots) {
              py::gil_scoped_release nogil;

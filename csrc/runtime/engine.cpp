@@ -69,6 +69,44 @@ void* Engine::dalloc(size_t bytes) {
   return p;
 }
 
+uint8_t* Engine::stage_acquire(size_t bytes) {
+  const int i = stage_.cur;
+  if (!upload_stream_) {
+    HIPCHK(hipStreamCreateWithFlags(&upload_stream_, hipStreamNonBlocking));
+    for (auto& e : stage_.done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  HIPCHK(hipEventSynchronize(stage_.done[i]));   // its previous copy has left the buffer
+  if (stage_.cap[i] < bytes) {
+    if (stage_.buf[i]) HIPCHK(hipHostFree(stage_.buf[i]));
+    stage_.buf[i] = nullptr;
+    const size_t cap = (bytes + (4u << 20) - 1) & ~(size_t)((4u << 20) - 1);
+    HIPCHK(hipHostMalloc((void**)&stage_.buf[i], cap, hipHostMallocDefault));
+    stage_.cap[i] = cap;
+  }
+  return stage_.buf[i];
+}
+
+void Engine::stage_commit(void* dev, size_t bytes) {
+  const int i = stage_.cur;
+  HIPCHK(hipMemcpyAsync(dev, stage_.buf[i], bytes, hipMemcpyHostToDevice, upload_stream_));
+  HIPCHK(hipEventRecord(stage_.done[i], upload_stream_));
+  stage_.cur ^= 1;
+}
+
+void Engine::stage_release() {
+  if (!upload_stream_) return;
+  HIPCHK(hipStreamSynchronize(upload_stream_));
+  for (int i = 0; i < 2; ++i) {
+    if (stage_.buf[i]) HIPCHK(hipHostFree(stage_.buf[i]));
+    stage_.buf[i] = nullptr;
+    stage_.cap[i] = 0;
+    if (stage_.done[i]) HIPCHK(hipEventDestroy(stage_.done[i]));
+    stage_.done[i] = nullptr;
+  }
+  HIPCHK(hipStreamDestroy(upload_stream_));
+  upload_stream_ = nullptr;
+}
+
 Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) {
   HIPCHK(hipSetDevice(opt_.device));
   HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -106,6 +144,7 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
     comm_ = c;
   }
   load(f);
+  stage_release();   // every weight is on the device before anything reads it
   alloc_buffers();
   build_rope();
   setup_batch_mfma();
@@ -125,10 +164,15 @@ Engine::~Engine() {
   if (graph_) hipGraphDestroy(graph_);
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   for (void* p : allocs_) hipFree(p);
+  try {
+    stage_release();
+  } catch (...) {
+  }
   if (h_ring_) hipHostFree(h_ring_);
   if (h_tokens_) hipHostFree(h_tokens_);
   if (h_bslots_) hipHostFree(h_bslots_);
   if (h_btok_) hipHostFree(h_btok_);
+  if (h_rmeta_) hipHostFree(h_rmeta_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -142,17 +186,17 @@ QMat Engine::upload_matrix(const GGUFFile& f, const std::string& name, size_t r0
   const size_t R_src = (size_t)t->ne[1];
   const int E = n_expert > 0 ? n_expert : 1;
   const size_t one = qbytes(t->type, R, K);
-  std::vector<uint8_t> host(one * E);
   const TypeInfo ti = type_info(t->type);
   const size_t src_expert = R_src * (K_src / ti.block) * ti.bytes;
   f.prefetch(*t);
+  uint8_t* host = stage_acquire(one * E);
   for (int e = 0; e < E; ++e) {
     const size_t rows_avail = r0 < R_src ? std::min(R, R_src - r0) : 0;
-    if (rows_avail < R) std::memset(host.data() + one * e, 0, one);
-    repack_planar(t->type, f.data(*t) + src_expert * e, K_src, r0, rows_avail, c0, K, host.data() + one * e, R, 0, 0);
+    if (rows_avail < R) std::memset(host + one * e, 0, one);
+    repack_planar(t->type, f.data(*t) + src_expert * e, K_src, r0, rows_avail, c0, K, host + one * e, R, 0, 0);
   }
-  void* d = dalloc(host.size());
-  HIPCHK(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
+  void* d = dalloc(one * E);
+  stage_commit(d, one * E);
   return make_qmat(d, t->type, (int)R, (int)K, n_expert > 0 ? one : 0);
 }
 
@@ -166,17 +210,17 @@ QMat Engine::upload_gate_up(const GGUFFile& f, const std::string& gate, const st
   const size_t K = (size_t)tg->ne[0];
   const int E = n_expert > 0 ? n_expert : 1;
   const size_t one = qbytes(tg->type, 2 * F, K);
-  std::vector<uint8_t> host(one * E);
   const TypeInfo ti = type_info(tg->type);
   const size_t src_expert = (size_t)tg->ne[1] * (K / ti.block) * ti.bytes;
   f.prefetch(*tg);
   f.prefetch(*tu);
+  uint8_t* host = stage_acquire(one * E);
   for (int e = 0; e < E; ++e) {
-    repack_planar(tg->type, f.data(*tg) + src_expert * e, K, f0, F, 0, K, host.data() + one * e, 2 * F, 32, 0);
-    repack_planar(tu->type, f.data(*tu) + src_expert * e, K, f0, F, 0, K, host.data() + one * e, 2 * F, 32, 32);
+    repack_planar(tg->type, f.data(*tg) + src_expert * e, K, f0, F, 0, K, host + one * e, 2 * F, 32, 0);
+    repack_planar(tu->type, f.data(*tu) + src_expert * e, K, f0, F, 0, K, host + one * e, 2 * F, 32, 32);
   }
-  void* d = dalloc(host.size());
-  HIPCHK(hipMemcpy(d, host.data(), host.size(), hipMemcpyHostToDevice));
+  void* d = dalloc(one * E);
+  stage_commit(d, one * E);
   return make_qmat(d, tg->type, (int)(2 * F), (int)K, n_expert > 0 ? one : 0);
 }
 
@@ -185,7 +229,8 @@ float* Engine::upload_f32(const GGUFFile& f, const std::string& name) {
   if (!t) throw std::runtime_error("missing tensor " + name);
   if (t->type != T_F32) throw std::runtime_error(name + ": expected F32");
   float* d = static_cast<float*>(dalloc(t->nbytes));
-  HIPCHK(hipMemcpy(d, f.data(*t), t->nbytes, hipMemcpyHostToDevice));
+  std::memcpy(stage_acquire(t->nbytes), f.data(*t), t->nbytes);
+  stage_commit(d, t->nbytes);
   return d;
 }
 
@@ -288,6 +333,9 @@ void Engine::alloc_buffers() {
     gu_b_ = (float*)dalloc(sizeof(float) * bmax_ * 2 * F_l_);
     HIPCHK(hipHostMalloc((void**)&h_bslots_, sizeof(int) * bmax_, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
+    rpos_ = (int*)dalloc(sizeof(int) * B);
+    rslots_ = (int*)dalloc(sizeof(int) * B);
+    HIPCHK(hipHostMalloc((void**)&h_rmeta_, sizeof(int) * 3 * B, hipHostMallocDefault));
   }
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
   dev_err_ = (int*)dalloc(sizeof(int) * 4);
@@ -597,7 +645,20 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
     g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
     g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
-    if (!batched) {
+    if (!batched && segs_) {  // packed prompts: per-row slot / position, attention per piece
+      __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; + slot * slot_stride_
+      __half* vcl = vc_ + kv_layer * l;
+      rope_kv_prefill(qkv_, T, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, rpos_, rslots_, slot_stride_);
+      for (const PrefillSeg& g : *segs_) {
+        AttnPrefillArgs pa;
+        pa.q = q_ + (size_t)g.row * nq_;
+        pa.k_cache = kcl + slot_stride_ * g.slot; pa.v_cache = vcl + slot_stride_ * g.slot;
+        pa.T = g.n; pa.pos0 = g.pos; pa.n_ctx = opt_.n_ctx;
+        pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
+        pa.out_bf16 = attnb_ + (size_t)g.row * nq_; pa.out_stride = nq_;
+        attn_prefill(pa, s);
+      }
+    } else if (!batched) {
       __half* kcl = kc_ + slot_stride_ * kv_slot_ + kv_layer * l;
       __half* vcl = vc_ + slot_stride_ * kv_slot_ + kv_layer * l;
       rope_kv_prefill(qkv_, T, pos0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s);
@@ -951,6 +1012,7 @@ enum TPOp : int32_t {
   TPO_DECODE_LOGITS,
   TPO_BATCH_LOGITS,
   TPO_BENCH_DECODE,
+  TPO_SLOTS_BEGIN,  // slots_begin(): n, slots, n_keep, then n x (prompt, sampling)
 };
 
 static void put_sp(TPMsg& m, const SamplingOpts& sp) {
@@ -980,8 +1042,10 @@ void Engine::mirror(const TPMsg& m) {
 
 void Engine::tp_ctl_create(const std::string& name) {
   if (opt_.tp_size < 2 || opt_.tp_rank != 0) throw std::runtime_error("tp_ctl_create: rank 0 of a TP group only");
-  // largest command: a prefill chunk / a whole prompt plus sampling options
-  const size_t cap = 4096 + sizeof(int) * (size_t)std::max(opt_.n_ctx, opt_.n_batch) + 16 * kMaxLogitBias;
+  // largest command: a prefill chunk / a whole prompt plus sampling options - or one of those
+  // per KV slot (a joint admission, slots_begin)
+  const size_t one = 256 + sizeof(int) * (size_t)std::max(opt_.n_ctx, opt_.n_batch) + 16 * kMaxLogitBias;
+  const size_t cap = 4096 + one * (size_t)std::max(1, bmax_);
   tp_ctl_ = TPChannel::create(name, opt_.tp_size, cap);
 }
 
@@ -1039,6 +1103,18 @@ void Engine::follow() {
           const int slot = m.get<int>(), n_keep = m.get<int>();
           const std::vector<int> prompt = m.get_vec<int>();
           slot_begin_impl(slot, prompt, n_keep, get_sp(m));
+          break;
+        }
+        case TPO_SLOTS_BEGIN: {
+          const int n = m.get<int>();
+          const std::vector<int> slots = m.get_vec<int>(), keep = m.get_vec<int>();
+          std::vector<std::vector<int>> prompts(n);
+          std::vector<SamplingOpts> sps(n);
+          for (int i = 0; i < n; ++i) {
+            prompts[i] = m.get_vec<int>();
+            sps[i] = get_sp(m);
+          }
+          slots_begin_impl(slots, prompts, keep, sps);
           break;
         }
         case TPO_BATCH_STEP: batch_step_impl(m.get_vec<int>()); break;
@@ -1117,6 +1193,91 @@ int Engine::slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep
   HIPCHK(hipMemcpy(&tok, state_ + (size_t)S_NSTATE * slot + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
   check_device_err();
   return tok;
+}
+
+std::vector<int> Engine::slots_begin(const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+                                     const std::vector<int>& n_keep, const std::vector<SamplingOpts>& sps) {
+  ExecGuard guard(this);
+  const size_t n = slots.size();
+  if (!bmax_) throw std::runtime_error("slots_begin: the engine was built with one KV slot");
+  if (prompts.size() != n || n_keep.size() != n || sps.size() != n) throw std::runtime_error("slots_begin: sizes");
+  std::vector<int> keep(n_keep);
+  for (size_t i = 0; i < n; ++i) {
+    if (slots[i] < 0 || slots[i] >= opt_.n_slots) throw std::runtime_error("slots_begin: slot out of range");
+    for (size_t j = 0; j < i; ++j)
+      if (slots[j] == slots[i]) throw std::runtime_error("slots_begin: duplicate slot");
+    const int np = (int)prompts[i].size();
+    if (np == 0) throw std::runtime_error("empty prompt");
+    if (np >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+    (void)make_sparams(sps[i]);
+    if (keep[i] < 0 || keep[i] >= np) keep[i] = 0;
+  }
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_SLOTS_BEGIN); m.put((int)n); m.put_vec(slots); m.put_vec(keep);
+    for (size_t i = 0; i < n; ++i) {
+      m.put_vec(prompts[i]);
+      put_sp(m, sps[i]);
+    }
+    mirror(m);
+  }
+  return slots_begin_impl(slots, prompts, keep, sps);
+}
+
+std::vector<int> Engine::slots_begin_impl(const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+                                          const std::vector<int>& n_keep, const std::vector<SamplingOpts>& sps) {
+  const size_t n = slots.size();
+  for (size_t i = 0; i < n; ++i) begin_slot_state(slots[i], prompts[i], sps[i]);
+  const int NB = opt_.n_batch, d = hp_.n_embd;
+  int* h_tok = h_rmeta_;
+  int* h_pos = h_rmeta_ + NB;
+  int* h_slot = h_rmeta_ + 2 * NB;
+  std::vector<PrefillSeg> segs;
+  int rows = 0;
+  // one packed chunk: tokens / positions / slots up, every layer over its rows, then the
+  // logits row of each prompt that ends in it (sampled into that slot's state)
+  auto flush = [&]() {
+    if (!rows) return;
+    HIPCHK(hipMemcpyAsync(tokens_, h_tok, sizeof(int) * rows, hipMemcpyHostToDevice, stream_));
+    HIPCHK(hipMemcpyAsync(rpos_, h_pos, sizeof(int) * rows, hipMemcpyHostToDevice, stream_));
+    HIPCHK(hipMemcpyAsync(rslots_, h_slot, sizeof(int) * rows, hipMemcpyHostToDevice, stream_));
+    segs_ = &segs;
+    try {
+      enqueue_prefill(rows, 0, stream_);
+    } catch (...) {
+      segs_ = nullptr;
+      throw;
+    }
+    segs_ = nullptr;
+    for (const PrefillSeg& g : segs)
+      if (g.last) enqueue_head(x_ + (size_t)(g.row + g.n - 1) * d, 0, stream_, g.slot);
+    HIPCHK(hipStreamSynchronize(stream_));  // the pinned row metadata is rewritten next
+    segs.clear();
+    rows = 0;
+  };
+  for (size_t i = 0; i < n; ++i) {
+    const std::vector<int>& pr = prompts[i];
+    int pos = n_keep[i];
+    const int np = (int)pr.size();
+    while (pos < np) {
+      if (rows == NB) flush();
+      const int take = std::min(NB - rows, np - pos);
+      for (int j = 0; j < take; ++j) {
+        h_tok[rows + j] = pr[pos + j];
+        h_pos[rows + j] = pos + j;
+        h_slot[rows + j] = slots[i];
+      }
+      segs.push_back({rows, take, slots[i], pos, pos + take == np});
+      rows += take;
+      pos += take;
+    }
+  }
+  flush();
+  std::vector<int> out(n);
+  for (size_t i = 0; i < n; ++i)
+    HIPCHK(hipMemcpy(&out[i], state_ + (size_t)S_NSTATE * slots[i] + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
+  check_device_err();
+  return out;
 }
 
 std::vector<int> Engine::batch_step(const std::vector<int>& slots) {

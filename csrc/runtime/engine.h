@@ -124,6 +124,12 @@ class Engine : public SlotBackend {
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
   int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
+  // Admission of several requests in ONE prefill: the prompts' rows are packed into shared
+  // chunks of up to n_batch rows (per-row KV slot / position for RoPE and the KV append,
+  // one attention launch per prompt piece), so every weight is streamed once per chunk for
+  // all of them instead of once per prompt; returns each slot's first token.
+  std::vector<int> slots_begin(const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+                               const std::vector<int>& n_keep, const std::vector<SamplingOpts>& sps) override;
   // One decode step of every listed slot, each at its own position: embeds each slot's
   // current token, runs all layers over the B rows (MFMA GEMMs, per-row RoPE/KV append,
   // batched split-L attention), the lm_head GEMM and the batched sampler; returns the
@@ -144,6 +150,18 @@ class Engine : public SlotBackend {
   std::mutex exec_mu_;
 
   void* dalloc(size_t bytes);
+  // model load: two pinned staging buffers alternate - the host repacks tensor i + 1 into one
+  // while the DMA engine copies tensor i out of the other (upload_stream_)
+  struct Staging {
+    uint8_t* buf[2] = {nullptr, nullptr};
+    size_t cap[2] = {0, 0};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    int cur = 0;
+  } stage_;
+  hipStream_t upload_stream_ = nullptr;
+  uint8_t* stage_acquire(size_t bytes);          // the free buffer, >= bytes
+  void stage_commit(void* dev, size_t bytes);    // async copy of it to dev; flips buffers
+  void stage_release();                          // waits for the copies, frees the buffers
   QMat upload_matrix(const GGUFFile& f, const std::string& name, size_t r0, size_t R, size_t c0, size_t K,
                      int n_expert = 0);
   QMat upload_gate_up(const GGUFFile& f, const std::string& gate, const std::string& up, size_t f0, size_t F,
@@ -164,6 +182,18 @@ class Engine : public SlotBackend {
   void mirror(const TPMsg& m);
   void prefill_chunk(int slot, const int* toks, int T, int pos, bool head);
   int slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp);
+  std::vector<int> slots_begin_impl(const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+                                    const std::vector<int>& n_keep, const std::vector<SamplingOpts>& sps);
+  // a piece of one prompt inside a packed prefill chunk: rows [row, row + n) at positions
+  // pos.. of KV slot `slot`; `last` = the prompt ends here (its logits row is sampled)
+  struct PrefillSeg {
+    int row, n, slot, pos;
+    bool last;
+  };
+  const std::vector<PrefillSeg>* segs_ = nullptr;  // set while a packed chunk is enqueued
+  int* rpos_ = nullptr;     // [n_batch] per-row position of a packed chunk
+  int* rslots_ = nullptr;   // [n_batch] per-row KV slot
+  int* h_rmeta_ = nullptr;  // pinned [3][n_batch]: tokens | positions | slots
   std::vector<int> batch_step_impl(const std::vector<int>& slots);
   std::vector<float> eval_logits_impl(const std::vector<int>& tokens, int pos0);
   std::vector<float> decode_logits_impl(int token, int pos);

@@ -162,46 +162,66 @@ void BatchScheduler::loop() {
     // 1. rows whose request was cancelled / abandoned leave before anything runs
     for (int s = first_slot_; s < n_slots_; ++s)
       if (slot_req_[s] && slot_req_[s]->cancel) finish(*slot_req_[s], "cancelled");
-    // 2. admission: queued requests into free slots (prefill + first token each)
-    while (!pending_.empty()) {
-      std::shared_ptr<Req> r = pending_.front();
-      if (r->cancel) {
+    // 2. admission: queued requests into free slots, prefilled TOGETHER (one packed prefill
+    //    pass streams every weight once for all of them) + the first token of each
+    {
+      std::vector<std::shared_ptr<Req>> adm;
+      std::vector<int> a_slot, a_keep;
+      while (!pending_.empty()) {
+        std::shared_ptr<Req> r = pending_.front();
+        if (r->cancel) {
+          pending_.pop_front();
+          finish(*r, "cancelled");
+          continue;
+        }
+        int lcp = 0;
+        const int slot = pick_slot(r->prompt, &lcp);
+        if (slot < 0) break;
         pending_.pop_front();
-        finish(*r, "cancelled");
-        continue;
+        r->slot = slot;
+        slot_req_[slot] = r;
+        slot_used_[slot] = ++tick_;
+        r->t_start = sched_now();
+        adm.push_back(r);
+        a_slot.push_back(slot);
+        a_keep.push_back(std::min(lcp, (int)r->prompt.size() - 1));
       }
-      int lcp = 0;
-      const int slot = pick_slot(r->prompt, &lcp);
-      if (slot < 0) break;
-      pending_.pop_front();
-      const int n_prompt = (int)r->prompt.size();
-      const int n_keep = std::min(lcp, n_prompt - 1);
-      r->slot = slot;
-      slot_req_[slot] = r;
-      slot_used_[slot] = ++tick_;
-      r->t_start = sched_now();
-      std::string err;
-      int tok = 0;
-      lk.unlock();
-      try {
-        tok = eng_.slot_begin(slot, r->prompt, n_keep, r->sp);
-      } catch (const std::exception& e) {
-        err = e.what();
+      if (!adm.empty()) {
+        std::vector<std::vector<int>> prompts;
+        std::vector<SamplingOpts> sps;
+        for (auto& r : adm) {
+          prompts.push_back(r->prompt);
+          sps.push_back(r->sp);
+        }
+        std::string err;
+        std::vector<int> toks;
+        lk.unlock();
+        try {
+          toks = adm.size() == 1 ? std::vector<int>{eng_.slot_begin(a_slot[0], prompts[0], a_keep[0], sps[0])}
+                                 : eng_.slots_begin(a_slot, prompts, a_keep, sps);
+        } catch (const std::exception& e) {
+          err = e.what();
+        }
+        lk.lock();
+        const double t = sched_now();
+        for (size_t i = 0; i < adm.size(); ++i) {
+          Req& r = *adm[i];
+          r.t_first = t;
+          if (!err.empty()) {
+            slot_hist_[a_slot[i]].clear();
+            r.error = err;
+            finish(r, "error");
+            continue;
+          }
+          ++st_.admitted;
+          st_.reused_tokens += a_keep[i];
+          r.n_prefilled = (int)r.prompt.size() - a_keep[i];
+          slot_hist_[a_slot[i]] = r.prompt;
+          push_token(r, toks[i]);
+        }
+        if (adm.size() > 1) ++st_.joint_admissions;
+        cv_out_.notify_all();  // the first tokens reach their waiters now, not after the next step
       }
-      lk.lock();
-      r->t_first = sched_now();
-      if (!err.empty()) {
-        slot_hist_[slot].clear();
-        r->error = err;
-        finish(*r, "error");
-        continue;
-      }
-      ++st_.admitted;
-      st_.reused_tokens += n_keep;
-      r->n_prefilled = n_prompt - n_keep;
-      slot_hist_[slot] = r->prompt;
-      push_token(*r, tok);
-      cv_out_.notify_all();  // the first token reaches its waiter now, not after the next step
     }
     // 3. one decode step over every active row
     rows.clear();

@@ -7,9 +7,10 @@
 // ONE batch costs one. This scheduler owns a host thread that keeps the engine's KV slots
 // busy:
 //
-//   loop:  retire cancelled requests  ->  admit queued requests into free slots
-//          (slot_begin: prefill + first token; the free slot whose resident tokens share
-//          the longest prefix with the prompt is chosen and that prefix is not recomputed)
+//   loop:  retire cancelled requests  ->  admit every queued request that finds a free slot
+//          (slots_begin: ONE packed prefill of all their prompts + each first token; the
+//          free slot whose resident tokens share the longest prefix with the prompt is
+//          chosen and that prefix is not recomputed)
 //          ->  one batch_step over every active slot  ->  hand each row its token,
 //          finish rows on a stop id / max_new / context end.
 //
@@ -49,6 +50,7 @@ struct SchedStats {
   long long rows = 0;         // rows decoded over all steps
   long long admitted = 0;
   long long reused_tokens = 0;  // prompt tokens served from a slot's resident KV prefix
+  long long joint_admissions = 0;  // admissions that prefilled several prompts in one pass
   int active = 0, pending = 0, slots = 0;
 };
 

@@ -27,6 +27,14 @@ class SlotBackend {
   // prefill prompt[n_keep:] into `slot` (its first n_keep positions are reused), set the
   // slot's sampling state, return its first token
   virtual int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) = 0;
+  // several admissions at once (slot_begin of each, in order); an engine that can prefill
+  // the prompts together (one pass of every weight for all of them) overrides it
+  virtual std::vector<int> slots_begin(const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
+                                       const std::vector<int>& n_keep, const std::vector<SamplingOpts>& sps) {
+    std::vector<int> out;
+    for (size_t i = 0; i < slots.size(); ++i) out.push_back(slot_begin(slots[i], prompts[i], n_keep[i], sps[i]));
+    return out;
+  }
   // one decode step of every listed slot at its own position -> each slot's next token
   virtual std::vector<int> batch_step(const std::vector<int>& slots) = 0;
 };

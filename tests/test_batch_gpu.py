@@ -108,6 +108,35 @@ def test_batch_step_d4096_fused_paths(tmp_path):
     assert eng.healthy, eng.last_error
 
 
+@pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
+def test_joint_admission_matches_sequential(models, spec):
+    """slots_begin packs several prompts into shared prefill chunks (per-row KV slot and
+    position, one attention launch per prompt piece; n_batch 32 makes pieces cross chunk
+    boundaries, one prompt reuses its slot's resident prefix): first tokens and the rows of
+    the following batched steps equal slot-by-slot admission."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    hip = load_hip()
+    kw = dict(n_ctx=256, n_batch=32, device=0, use_graph=False, n_slots=4)
+    joint, seq = hip.Engine(models[spec], **kw), hip.Engine(models[spec], **kw)
+    rng = np.random.default_rng(12)
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    base = [int(t) for t in rng.integers(3, 300, 21)]
+    for e in (joint, seq):                 # slot 1 holds `base`: the second round reuses it
+        e.slot_begin(1, base, 0, greedy)
+    prompts = [[int(t) for t in rng.integers(3, 300, n)] for n in (45, 7)] + [base + [11, 12, 13]]
+    slots, keep = [3, 0, 1], [0, 0, len(base)]
+    a = joint.slots_begin(slots, prompts, keep, [greedy] * 3)
+    b = [seq.slot_begin(s, p, k, greedy) for s, p, k in zip(slots, prompts, keep)]
+    assert a == b
+    for _ in range(3):
+        ta, tb = joint.batch_step(slots), seq.batch_step(slots)
+        la, lb = joint.batch_logits(3), seq.batch_logits(3)
+        for r in range(3):
+            assert rel_err(la[r], lb[r]) < 1e-3, (r, rel_err(la[r], lb[r]))
+        assert ta == tb
+    assert joint.healthy, joint.last_error
+
+
 def test_batch_sampling_params_are_per_slot(models):
     """Each slot samples with its own parameters, penalty ring and seed."""
     from llama_fastapi_k8s_gpu_amd.runtime import load_hip

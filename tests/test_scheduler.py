@@ -149,3 +149,20 @@ def test_concurrent_submitters_and_shutdown():
     assert r["done"] and r["finish"] == "cancelled"
     with pytest.raises(RuntimeError):
         sched.submit([1], 1, {}, [])
+
+
+def test_requests_queued_together_are_admitted_together():
+    """Requests that queue while a step runs are admitted in one slots_begin call (one packed
+    prefill on the MI355X engine); their tokens still equal their sequential runs."""
+    eng, sched = make(n_slots=5, max_batch=4, n_ctx=256, step_us=3000)
+    first = sched.submit([1, 2, 3], 50, {}, [])
+    time.sleep(0.02)                       # the scheduler is inside a 3 ms step now
+    reqs = [([7, i, 9, 10 + i], 12) for i in range(3)]
+    ids = [sched.submit(p, m, {}, []) for p, m in reqs]
+    for rid, (p, m) in zip(ids, reqs):
+        toks, r = run(sched, rid)
+        assert toks == sequential(p, m, 256) and r["n_prefilled"] == len(p)
+    run(sched, first)
+    st = sched.stats()
+    assert st["joint_admissions"] >= 1 and st["admitted"] == 4
+    sched.shutdown()
