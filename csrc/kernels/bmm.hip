@@ -399,6 +399,12 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   const int kp = bid % kparts;
   const int s0 = kp * spp, s1 = min(steps, s0 + spp);
   if (s0 >= s1) return;  // whole block, before any barrier
+  if (a.ew && a.steps_per_expert > 0) {  // MoE down: the part of an unrouted expert adds nothing
+    const int e = s0 / a.steps_per_expert;  // (the launcher keeps every part inside one expert)
+    bool any = false;
+    for (int b = 0; b < a.B; ++b) any = any || a.ew[(size_t)b * a.ew_ld + e] != 0.f;
+    if (!any) return;  // whole block (uniform), before any barrier
+  }
   const int k0 = s0 * 256, kn = (s1 - s0) * 256, ldx = kn + 8;
   const int gstride = nbk / kparts;
   // tile order: SwiGLU blocks take a contiguous range of tiles, balanced per CU: blocks b and
@@ -407,13 +413,41 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   // gets exactly 7 tiles (an even split of whole units left a quarter of the CUs half-loaded)
   const bool sw = a.swiglu_epi;
   int gt = bid / kparts, tiles_end = tiles;
-  if (sw) {
-    const int G = a.tile_groups, g = bid % G, rnd = bid / G, nr = (nbk + G - 1) / G;
-    const int q = tiles / G + (g < tiles % G ? 1 : 0), p0 = g * (tiles / G) + min(g, tiles % G);
-    gt = p0 + rnd * q / nr;
-    tiles_end = p0 + (rnd + 1) * q / nr;
+  // MoE gate/up: only the experts some row is routed to are computed - the split below runs
+  // over their tiles alone ("active" index space: expert rank * tpe + local tile), so the
+  // blocks share the routed experts' work evenly (E <= 64: one bit per expert, block-uniform)
+  const bool moe_sw = sw && a.ew;
+  const int tpe = moe_sw ? a.tiles_per_expert : 1;
+  unsigned long long act = ~0ull;
+  if (moe_sw) {
+    bool any = false;
+    if (lane < tiles / tpe)
+      for (int b = 0; b < a.B; ++b) any = any || a.ew[(size_t)b * a.ew_ld + lane] != 0.f;
+    act = __ballot(any);
   }
-  auto next_tile = [&](int g) { return sw ? g + 1 : g + gstride; };
+  auto glob = [&](int ai) {  // active index -> global tile
+    if (!moe_sw) return ai;
+    unsigned long long m = act;
+    for (int r = ai / tpe; r > 0; --r) m &= m - 1;  // drop the lowest set bits: the rank-th expert
+    return m ? (int)__builtin_ctzll(m) * tpe + ai % tpe : tiles;
+  };
+  if (sw) {
+    const int ta = moe_sw ? __popcll(act) * tpe : tiles;  // tiles to compute
+    const int G = a.tile_groups, g = bid % G, rnd = bid / G, nr = (nbk + G - 1) / G;
+    const int q = ta / G + (g < ta % G ? 1 : 0), p0 = g * (ta / G) + min(g, ta % G);
+    const int a0 = p0 + rnd * q / nr, a1 = p0 + (rnd + 1) * q / nr;
+    gt = a0 < a1 ? glob(a0) : tiles;
+    tiles_end = a1 >= ta ? tiles : glob(a1);
+  }
+  auto next_tile = [&](int g) {
+    if (!sw) return g + gstride;
+    ++g;
+    if (moe_sw && g % tpe == 0 && g < tiles) {  // past an expert: the next routed one
+      const unsigned long long m = act >> (g / tpe);
+      g = m ? g + (int)__builtin_ctzll(m) * tpe : tiles;
+    }
+    return g;
+  };
   if (gt >= tiles_end) return;  // whole block, before any barrier
   const int SB = t16_step_bytes(QT);
   auto tile_base = [&](int g) {  // first byte of global tile g's tile16 data
@@ -577,8 +611,10 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
         for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(acc[i], 32);
         if (col_ok && lane < 32) {
           const int f0 = gt * 8 + 4 * kq;  // 4 consecutive features
-          const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
-          const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
+          // MoE: the row's routing weight of this tile's expert (0: the row is not routed here)
+          const float rw = a.ew ? a.ew[(size_t)r16 * a.ew_ld + gt / a.tiles_per_expert] : 1.f;
+          const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
+          const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
           *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
         }
       } else if (col_ok && a.qkv_epi) {
@@ -820,6 +856,10 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   static const int want_b = env_int("LFK_BMM_BLOCKS", 4);  // per CU (tuning)
   const int want = want_b * bmm_cus();
   while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
+  // MoE down: every K part inside ONE expert - an unrouted expert's SwiGLU rows were never
+  // written (its gate/up tiles are skipped), so its parts must be skipped whole, not mixed in
+  if (a.ew && a.steps_per_expert > 0)
+    while (a.steps_per_expert % spp) --spp;
   const int kparts = (steps + spp - 1) / spp;
   a.spp = spp;
   a.kparts = kparts;
@@ -850,6 +890,12 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
   if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi && !a.one_part)
     throw std::runtime_error("bmm: store_out needs one K part");
   if (a.one_part && !bmm_qkv_fits(a.w.K, a.B)) throw std::runtime_error("bmm: one_part x slice exceeds LDS");
+  if (a.ew && (a.ew_ld < 1 || (a.swiglu_epi ? a.tiles_per_expert < 1 || ((a.n_out + 15) / 16) % a.tiles_per_expert
+                                            : a.steps_per_expert < 1 || (a.w.K / 256) % a.steps_per_expert)))
+    throw std::runtime_error("bmm: expert routing weights need whole experts of tiles / K steps");
+  if (a.ew && a.swiglu_epi && (a.n_out + 15) / 16 / a.tiles_per_expert > 64) throw std::runtime_error("bmm: <= 64 experts");
+  if (a.ew && !a.swiglu_epi && (a.xf || a.qkv_epi || a.one_part))
+    throw std::runtime_error("bmm: the MoE down projection runs split-K (whole-expert parts)");
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;

@@ -115,6 +115,15 @@ struct BmmArgs {
   const float* norm_w = nullptr;
   float eps = 1e-5f;
   bool store_out = false;          // plain epilogue: out = result (default: out += result)
+  // MoE experts as ONE matrix (the batched decode FFN): gate/up = the experts' SwiGLU tile16
+  // copies stacked (tile t belongs to expert t / tiles_per_expert), down = the experts' down
+  // rows concatenated along K (256-k step s to expert s / steps_per_expert) over the stacked
+  // SwiGLU output. ew [B][ew_ld] holds each row's routing weight per expert (0 = not routed):
+  // the SwiGLU epilogue scales row b of expert e's features by ew[b][e] (so unrouted rows
+  // contribute exactly 0 through the down projection) and the down blocks whose K part
+  // covers no expert with a routed row exit before loading a byte.
+  const float* ew = nullptr;
+  int ew_ld = 0, tiles_per_expert = 0, steps_per_expert = 0;
   bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
   bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block wall_clock64 stamps [grid][8]
@@ -175,6 +184,10 @@ void gemv_moe_down(const MoeDownArgs& a, hipStream_t s);
 bool moe_down_splitk(const MoeDownArgs& a, hipStream_t s);
 // decode router fused with the routing (F32 router weights, E <= 16): one launch
 bool moe_router_fused_ok(int router_type, int E, int d);
+// batched decode rows: RMSNorm(x_b) * w_norm -> f32 router -> softmax / top-k / renormalise
+// per row, written DENSE: wd[b * ld + e] = the row's weight of expert e, 0 if not selected
+void moe_router_rows(const float* x, int ldx, int B, const float* nw, float eps, const float* W, int d, int E, int k,
+                     float* wd, int ld, hipStream_t s);
 void moe_router_fused(const float* x, const float* nw, float eps, const float* W, int d, int E, int k, float* logits,
                       int* ids, float* w, hipStream_t s);
 

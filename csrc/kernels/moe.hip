@@ -119,12 +119,16 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 // (two kernel boundaries per MoE layer). The router stays in f32 end to end.
 static constexpr int kRouterMaxE = 16;
 
+// (batched rows: block b routes row b - x + b * ldx - and writes the dense weight row
+// wd + b * ld_dense instead of ids / wout)
 template <int EM>
 __global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __restrict__ x, const float* __restrict__ nw,
                                                                 float eps, const float* __restrict__ W, int d, int E,
-                                                                int k, float* logits, int* ids, float* wout) {
+                                                                int k, float* logits, int* ids, float* wout, int ldx,
+                                                                float* wd, int ld_dense) {
   __shared__ float red[16][EM + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  x += (size_t)blockIdx.x * ldx;
   float ss = 0.f, acc[EM];
 #pragma unroll
   for (int e = 0; e < EM; ++e) acc[e] = 0.f;
@@ -182,6 +186,18 @@ __global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __r
     sel_sum += best;
     if (lane == bi) taken = -1.f;
   }
+  if (wd) {
+    // dense row: lane e < E finds its own weight among the k picks (lanes 0..k-1 hold them)
+    float* row = wd + (size_t)blockIdx.x * ld_dense;
+    float mine = 0.f;
+    for (int j = 0; j < k; ++j) {
+      const int id = __shfl(my_id, j);
+      const float w = __shfl(my_w, j);
+      if (id == lane) mine = w / sel_sum;
+    }
+    if (lane < E) row[lane] = mine;
+    return;
+  }
   if (lane < k) {
     ids[lane] = my_id;
     wout[lane] = my_w / sel_sum;
@@ -196,9 +212,22 @@ void moe_router_fused(const float* x, const float* nw, float eps, const float* W
                       int* ids, float* w, hipStream_t s) {
   if (E > kRouterMaxE || k > E || d % 4) throw std::runtime_error("moe_router_fused: unsupported shape");
   if (E <= 8)  // rows padded to EM are loaded (clamped) and masked: size EM to the expert count
-    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
+    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w,
+                       0, nullptr, 0);
   else
-    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w);
+    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w,
+                       0, nullptr, 0);
+}
+
+void moe_router_rows(const float* x, int ldx, int B, const float* nw, float eps, const float* W, int d, int E, int k,
+                     float* wd, int ld, hipStream_t s) {
+  if (E > kRouterMaxE || k > E || d % 4 || B < 1 || ld < E || ldx % 4) throw std::runtime_error("moe_router_rows: unsupported shape");
+  if (E <= 8)
+    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(B), dim3(1024), 0, s, x, nw, eps, W, d, E, k, nullptr, nullptr,
+                       nullptr, ldx, wd, ld);
+  else
+    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(B), dim3(1024), 0, s, x, nw, eps, W, d, E, k, nullptr, nullptr,
+                       nullptr, ldx, wd, ld);
 }
 
 // ------------------------------------------------------------------ decode: grouped down, split-K

@@ -369,8 +369,16 @@ void Engine::setup_batch_mfma() {
     att = att && ok(L.wq) && ok(L.wk) && ok(L.wv) && ok(L.wo);
     ffn = ffn && ok(L.w_gu) && ok(L.w_down);
   }
+  bool moe = hp_.n_expert > 0 && moe_router_fused_ok(layers_[0].router.type, hp_.n_expert, hp_.n_embd) &&
+             F_l_ % 256 == 0 && (2 * F_l_) % 64 == 0 && kfit(hp_.n_embd);
+  for (int l = 0; moe && l < hp_.n_layer; ++l) {
+    const Layer& L = layers_[l];
+    moe = moe_router_fused_ok(L.router.type, hp_.n_expert, hp_.n_embd) && ok(L.gu_exps) && ok(L.down_exps);
+  }
+  const char* bm = std::getenv("LFK_BATCH_MOE");
   bg_ = att;
   bg_ffn_ = att && ffn;
+  moe_b_ = att && moe && !(bm && bm[0] == '0');
   const char* wo1 = std::getenv("LFK_BMM_WO1");
   wo_one_part_ = wo1 && wo1[0] == '1';
   const char* bt = std::getenv("LFK_BATT_TOUCH");
@@ -381,8 +389,10 @@ void Engine::setup_batch_mfma() {
   const char* hf = std::getenv("LFK_BMM_HEAD1");
   head_fold_ = hf && hf[0] == '1';
   if (!bg_) return;
+  const int E = std::max(1, hp_.n_expert);
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
-  hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_));
+  hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_) * (moe_b_ ? E : 1));
+  if (moe_b_) ew_b_ = (float*)dalloc(sizeof(float) * bmax_ * E);
   // the batched path reads its own copy of the weights, laid out per 16-row tile (bmm.hip)
   auto tile = [&](const QMat& m, bool swiglu = false) {
     QMat t = m;
@@ -396,6 +406,36 @@ void Engine::setup_batch_mfma() {
     Layer& L = layers_[l];
     L.t_wq = tile(L.wq); L.t_wk = tile(L.wk); L.t_wv = tile(L.wv); L.t_wo = tile(L.wo);
     if (bg_ffn_) { L.t_gu = tile(L.w_gu, /*swiglu=*/true); L.t_down = tile(L.w_down); }
+    if (moe_b_) {
+      // gate/up: the experts' SwiGLU tile16 copies back to back (expert e = tiles [e T, (e+1) T))
+      const size_t gu1 = t16_bytes(L.gu_exps.type, L.gu_exps.rows, L.gu_exps.K);
+      uint8_t* gdst = (uint8_t*)dalloc(gu1 * E);
+      // down: every 16-row tile's 256-k steps run expert 0's F_l, then expert 1's, ... (K = E F_l):
+      // each expert's copy goes through `tmp` and is strided into its step range of every tile
+      const int dsteps = L.down_exps.K / 256, dtiles = (L.down_exps.rows + 15) / 16;
+      const size_t dn1 = t16_bytes(L.down_exps.type, L.down_exps.rows, L.down_exps.K);
+      const size_t run = dn1 / dtiles;  // one tile's steps of one expert
+      uint8_t* ddst = (uint8_t*)dalloc(dn1 * E);
+      // (kept allocated: freeing device memory between the engine's setup and the TP group's
+      // collectives was followed by corrupted decode logits on the 2-rank IPC test)
+      uint8_t* tmp = (uint8_t*)dalloc(dn1);
+      for (int e = 0; e < E; ++e) {
+        QMat g = L.gu_exps;
+        g.base += L.gu_exps.expert_stride * e;
+        g.expert_stride = 0;
+        t16_repack(g, gdst + gu1 * e, stream_, /*swiglu=*/true);
+        QMat dm = L.down_exps;
+        dm.base += L.down_exps.expert_stride * e;
+        dm.expert_stride = 0;
+        t16_repack(dm, tmp, stream_);
+        HIPCHK(hipMemcpy2DAsync(ddst + run * e, run * E, tmp, run, run, dtiles, hipMemcpyDeviceToDevice, stream_));
+      }
+      HIPCHK(hipStreamSynchronize(stream_));
+      L.t_gu = L.gu_exps;
+      L.t_gu.base = gdst; L.t_gu.rows = L.gu_exps.rows * E; L.t_gu.expert_stride = 0;
+      L.t_down = L.down_exps;
+      L.t_down.base = ddst; L.t_down.K = dsteps * 256 * E; L.t_down.expert_stride = 0;
+    }
   }
   HIPCHK(hipStreamSynchronize(stream_));
 }
@@ -937,6 +977,34 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s);
   }
   tp_end();
+  if (moe_b_ && fused) {
+    // MoE: dense per-row expert weights (f32 router on the normed rows), then every expert's
+    // SwiGLU rows in ONE gate/up launch (epilogue scaled by the row's weight for that expert,
+    // 0 when unrouted) and ONE down launch over the K-concatenated experts (parts of unrouted
+    // experts skipped): two weight streams per layer instead of a GEMM pair per expert
+    const int E = hp_.n_expert;
+    moe_router_rows(x_, d, B, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, E,
+                    hp_.n_expert_used, ew_b_, E, s);
+    BmmArgs a;
+    if (fnorm) {
+      a.xf = x_; a.ldxf = d; a.norm_w = L.ffn_norm; a.eps = hp_.rms_eps;
+    } else {
+      bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
+    }
+    a.w = L.t_gu; a.xh = xh_b_; a.ldh = d;
+    a.out = nullptr; a.ldo = 0; a.n_out = L.t_gu.rows; a.B = B;
+    a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = E * F_l_;
+    a.ew = ew_b_; a.ew_ld = E; a.tiles_per_expert = 2 * F_l_ / 16;
+    bmm(a, s);
+    tp_begin();
+    BmmArgs dn;
+    dn.w = L.t_down; dn.xh = hh_b_; dn.ldh = E * F_l_;
+    dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
+    dn.ew = ew_b_; dn.ew_ld = E; dn.steps_per_expert = F_l_ / 256;
+    bmm(dn, s);
+    tp_end();
+    return;
+  }
   if (bg_ffn_ && fused) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
@@ -1350,18 +1418,20 @@ void Engine::gather_logits_rows(int B, size_t ld_src, const float* src, std::vec
     return;
   }
   // pack the shard rows [B][V_l] contiguously, all-gather -> [tp][B][V_l]
-  float* packed = nullptr;
-  float* all = nullptr;
-  HIPCHK(hipMalloc((void**)&packed, sizeof(float) * B * V_l_));
-  HIPCHK(hipMalloc((void**)&all, sizeof(float) * B * V_l_ * tp));
+  // persistent (grow-only) scratch: no device alloc / free churn between TP collectives
+  const size_t need = (size_t)B * V_l_ * (1 + tp);
+  if (gather_cap_ < need) {
+    gather_buf_ = (float*)dalloc(sizeof(float) * need);
+    gather_cap_ = need;
+  }
+  float* packed = gather_buf_;
+  float* all = gather_buf_ + (size_t)B * V_l_;
   HIPCHK(hipMemcpy2DAsync(packed, sizeof(float) * V_l_, src, sizeof(float) * ld_src, sizeof(float) * V_l_, B,
                           hipMemcpyDeviceToDevice, stream_));
   allgather_into(packed, all, (size_t)B * V_l_, stream_);
   std::vector<float> h((size_t)B * V_l_ * tp);
   HIPCHK(hipMemcpyAsync(h.data(), all, sizeof(float) * h.size(), hipMemcpyDeviceToHost, stream_));
   HIPCHK(hipStreamSynchronize(stream_));
-  HIPCHK(hipFree(packed));
-  HIPCHK(hipFree(all));
   for (int r = 0; r < tp; ++r) {
     const int n = std::max(0, std::min(V_l_, V - r * V_l_));
     for (int b = 0; b < B; ++b)

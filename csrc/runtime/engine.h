@@ -229,6 +229,8 @@ class Engine : public SlotBackend {
   std::unique_ptr<TPChannel> tp_ctl_;
   bool tp_stopped_ = false;
   std::vector<void*> allocs_;
+  float* gather_buf_ = nullptr;  // gather_logits_rows scratch (TP), grow-only
+  size_t gather_cap_ = 0;
   size_t dev_bytes_ = 0;
   bool healthy_ = true;
   std::string last_error_;
@@ -307,10 +309,15 @@ class Engine : public SlotBackend {
   // step for all rows) instead of the prefill GEMM: attention/head (bg_) and the dense FFN
   // (bg_ffn_); LFK_BATCH_MFMA=0 keeps the GEMM path (A/B)
   bool bg_ = false, bg_ffn_ = false;
+  // MoE FFN on the batched projections: the experts as one stacked SwiGLU matrix and one
+  // K-concatenated down matrix (t_gu / t_down of each layer), routed by dense per-row expert
+  // weights ew_b_ [bmax][E] (bmm.hip, BmmArgs::ew); LFK_BATCH_MOE=0 keeps the grouped GEMM
+  bool moe_b_ = false;
+  float* ew_b_ = nullptr;
   __half* xh_b_ = nullptr;    // [bmax][max(d, nq, F)] prepared f16 projection input
   QMat t_output_;             // tile16 copy of the output head
   float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
-  __half* hh_b_ = nullptr;    // [bmax][F_l] down-projection input written by the SwiGLU epilogue
+  __half* hh_b_ = nullptr;    // [bmax][F_l] (MoE: [bmax][E F_l]) down input written by the SwiGLU epilogue
   // RMSNorm folded into the one-part projections' staging (Q|K|V, gate/up: no prep launch;
   // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
   // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)

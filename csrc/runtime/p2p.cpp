@@ -17,6 +17,10 @@ P2PComm::P2PComm(int rank, int world, int max_n, int device)
   data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n_;
   data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
   region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
+  // a whole, 2 MiB-granular allocation of its own: an exported IPC handle names the
+  // underlying allocation, and a small hipMalloc can be carved out of a freed block at an
+  // offset the peer's mapping does not carry (peer writes then land elsewhere in our memory)
+  region_bytes_ = (region_bytes_ + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
   p2pchk(hipMalloc(&region_, region_bytes_), "hipMalloc region");
   p2pchk(hipMemset(region_, 0, region_bytes_), "hipMemset region");
   p2pchk(hipMalloc((void**)&epochs_, sizeof(int) * kP2PMaxBlocks), "hipMalloc epochs");

@@ -211,11 +211,22 @@ class ReferenceLlama:
         if not self.hp.n_expert:
             a = F.silu(h @ self._weight("ffn_gate", L, wk).T) * (h @ self._weight("ffn_up", L, wk).T)
             return self._plain_input(a, path) @ self._weight("ffn_down", L, wk).T
-        # MoE: the batched path runs the prefill GEMM FFN (bf16), the decode path the GEMV
-        # experts (q8) with the f32 router
+        # MoE: the decode path runs the GEMV experts (q8) with the f32 router; the batched path
+        # the stacked-expert bmm (f16 tile16 weights, f16 input, f32 router, the SwiGLU output
+        # scaled by the routing weight before its f16 rounding)
         if path == "batch":
-            path, wk = "prefill", "bf16"
-            h = self._normed_input(x, L["ffn_norm"], path)
+            hr = self._normed_input(x, L["ffn_norm"], None)
+            probs = torch.softmax(hr @ L["ffn_gate_inp"].T, -1)
+            w, ids = torch.topk(probs, self.hp.n_expert_used, dim=-1)
+            w = w / w.sum(-1, keepdim=True)
+            ge, ue, de = (self._weight(k, L, "f16") for k in ("ffn_gate_exps", "ffn_up_exps", "ffn_down_exps"))
+            out = torch.zeros_like(h)
+            for t in range(h.shape[0]):
+                for j in range(self.hp.n_expert_used):
+                    e = int(ids[t, j])
+                    g = F.silu(ge[e] @ h[t]) * (ue[e] @ h[t])
+                    out[t] += de[e] @ self._f16(g * w[t, j])
+            return out
         rw = L["ffn_gate_inp"] if path != "prefill" else self._bf16(L["ffn_gate_inp"])
         hr = self._normed_input(x, L["ffn_norm"], None) if path == "decode" else h
         logits = hr @ rw.T                                    # [T, E]

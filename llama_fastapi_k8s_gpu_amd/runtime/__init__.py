@@ -32,6 +32,16 @@ def _load(name: str, builder: str):
 
 
 def load_hip():
+    # torch first: its libtorch_hip loads the HIP runtime torch ships (soname libamdhip64.so.7,
+    # file name libamdhip64.so), and the extension's libamdhip64.so.7 / librccl.so.1 then
+    # resolve to those same copies by soname. Loaded the other way round, the extension pulls
+    # in /opt/rocm's runtime and torch adds its own by file name - two HIP runtimes in one
+    # process, and torch.cuda reports no device.
+    if "_hip" not in _MODS:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
     return _load("_hip", "build_hip")
 
 

@@ -33,6 +33,11 @@ def main():
         prompt = [int(t) for t in rng.integers(0, eng.hparams["n_vocab"], args.prompt)]
         eng.slot_begin(s, prompt, 0, sp)
     res["slot_begin_ms"] = round((time.perf_counter() - t0) * 1e3 / args.slots, 2)
+    # joint admission: the same prompts prefilled together (packed chunks of n_batch rows)
+    prompts = [[int(t) for t in rng.integers(0, eng.hparams["n_vocab"], args.prompt)] for _ in range(args.slots)]
+    t0 = time.perf_counter()
+    eng.slots_begin(list(range(args.slots)), prompts, [0] * args.slots, [sp] * args.slots)
+    res["slots_begin_ms_per_prompt"] = round((time.perf_counter() - t0) * 1e3 / args.slots, 2)
     for B in [int(b) for b in args.batches.split(",")]:
         if B > eng.max_batch:
             continue
