@@ -1,11 +1,15 @@
 """Headline benchmark: output tokens/s + p50 /response latency, Llama-3-8B Q4_K_M
 (BASELINE.json metric), measured through the real FastAPI ``/response`` path.
 
-One "step" = one ``POST /response`` request, served exactly as the reference
-serves it (reference api.py:118-173): persona system prompt, context
+One "step" = one round of ``POST /response`` requests, one per concurrent client
+(``--clients``, default 6: K steps post K x C requests), each served exactly as the
+reference serves it (reference api.py:118-173): persona system prompt, context
 truncation, admission queue, ``create_chat_completion(temperature=1.2,
 top_p=0.9, frequency_penalty=0.7, presence_penalty=0.8)`` with no max_tokens -
-so each request decodes until EOS or the 1024-token context is full.
+so each request decodes until EOS or the 1024-token context is full. Whole rounds keep
+every client busy to the end of the timed region: a request count that is not a multiple
+of C left a last partial wave decoding 1-5 rows alone (round 2's 20 requests at C = 6 spent
+~20 % of the timed region on a 2-row tail), which measured the tail, not the serving rate.
 
 GPUs: ``--gpus N`` runs N ranks, one process per GPU. Without ``WORLD_SIZE`` in the
 environment and N > 1, bench.py starts ``torch.distributed.run`` itself (before anything
@@ -208,14 +212,15 @@ def main() -> int:
                             if lat is not None:
                                 lat.append(time.perf_counter() - t)
                     await asyncio.gather(*[client() for _ in range(max(1, clients))])
-                await drive(range(1000, 1000 + args.warmup), None, args.clients)
+                nc = max(1, args.clients)
+                await drive(range(1000, 1000 + args.warmup * nc), None, args.clients)
                 if not tp:
                     barrier()
                 else:
                     torch.cuda.synchronize(device)
                 n0 = len(eng.completion_tokens)
                 t_start = time.perf_counter()
-                await drive(range(args.steps), latencies, args.clients)
+                await drive(range(args.steps * nc), latencies, args.clients)
                 # TP: rank 0's last step completed its all-reduces, so every rank is done with it
                 if not tp:
                     barrier()
@@ -260,8 +265,9 @@ def main() -> int:
                        "clients_per_group": args.clients, "max_batch": max_batch,
                        "p50_response_ms": round(p50, 1),
                        "decode_tokens_per_s_per_request": round(toks / dec, 1) if dec > 0 else None,
-                       "avg_prompt_tokens": round(ptoks / max(1, args.steps), 1),
-                       "avg_output_tokens": round(toks / max(1, args.steps), 1),
+                       "requests": n1 - n0, "step": f"one round of {args.clients} concurrent /response requests",
+                       "avg_prompt_tokens": round(ptoks / max(1, n1 - n0), 1),
+                       "avg_output_tokens": round(toks / max(1, n1 - n0), 1),
                        "serial": {"requests": serial_steps, "clients": 1,
                                   "tokens_per_s": round(s_toks / serial_s, 2) if serial_steps else None,
                                   "p50_response_ms": round(statistics.median(serial_lat) * 1e3, 1)

@@ -342,6 +342,97 @@ __device__ __forceinline__ int raw_word(const BRawT<T>& w) {
   else return w.a.x;
 }
 
+// One 256-k step of a 16-row tile: lane l's chunks 8s + 4h + kq (h = 0, 1) dequantised into
+// MFMA A fragments, B = the staged x row of column r16 (xrow indexed by global k), one
+// accumulator per chunk h (two dependent chains of 4 MFMAs instead of one of 8: the MFMA
+// read-after-write stalls were 24 % of the gate/up kernel's wave cycles)
+template <int QT>
+__device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, const __half* xrow, f4_t& acc, f4_t& acc2) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = 8 * s + 4 * h + kq;
+    int off_lo, off_hi;
+    chunk_runs<QT>(c, off_lo, off_hi);
+    const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+    const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+    const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
+    HFrag F;
+    dequant_frags<QT>(wc[h], c, F);
+    const uint4 xr[4] = {x0, x1, x2, x3};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      // MFMA m takes 8 weights of ONE run: the low run's 0-7 / 8-15 (m = 0 / 1), then the high
+      // run's (m = 2 / 3) - pairs of quant dwords 2(m % 2), 2(m % 2) + 1 - so its B operand is
+      // the 16-byte LDS read as it stands (taking 4 halves from each run cost 3 v_mov per MFMA)
+      const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
+      const uint4 av = make_uint4(F.w[4 * dw + sh], F.w[4 * dw + sh + 1], F.w[4 * dw + 4 + sh], F.w[4 * dw + 5 + sh]);
+      f4_t& ac = h == 0 ? acc : acc2;
+      ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
+                                                  __builtin_bit_cast(h8_t, xr[m]), ac, 0, 0, 0);
+    }
+  }
+}
+
+// Stage x[b][k0, k0 + kn) of the B rows in LDS (f16, row stride ldx halves): from xh, or -
+// with the RMSNorm folded in (a.xf, K = 4096, B <= 8, kBlock >= 512: each thread holds 2
+// float4 of every row) - from the fp32 residual rows: every load is issued first (one memory
+// round trip, like the f16 staging), then f16(x * w) goes to LDS in bprep's 4-group order and
+// each wave leaves its per-row partial sum of squares in rowss[b * NW + wave] (rows past B load
+// row B - 1 and are dropped: straight-line code, no predicated loads)
+template <int NW>
+__device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
+                                            int tid, int lane, int wave) {
+  constexpr int kBlock = NW * 64;
+  if (NW >= 8 && a.xf) {
+    constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
+    float4 xv[8 * J], w[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) w[j] = *reinterpret_cast<const float4*>(a.norm_w + 4 * (tid + j * kBlock));
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
+#pragma unroll
+      for (int j = 0; j < J; ++j) xv[J * b + j] = *reinterpret_cast<const float4*>(xr + 4 * (tid + j * kBlock));
+    }
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const float4 x = xv[J * b + j], ww = w[j];
+        ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+        const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
+        const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
+        if (b < a.B) *reinterpret_cast<uint2*>(xs + b * ldx + 4 * (tid + j * kBlock)) = make_uint2(as_u(p0), as_u(p1));
+      }
+      ss = wave_sum_fast(ss);
+      if (lane == 0) rowss[b * NW + wave] = ss;
+    }
+  } else {
+    // every thread's loads go out before any LDS store: one memory round trip for the slice
+    // (a load-store loop waited for each load in turn: 3-6 round trips, 1.5-3.6 us per launch)
+    constexpr int U = 8;
+    const int nv = kn >> 3, n = a.B * nv;
+    for (int i0 = 0; i0 < n; i0 += U * kBlock) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * kBlock + tid, n - 1);
+        const int b = i / nv, c = i - b * nv;
+        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kBlock + tid;
+        if (i < n) {
+          const int b = i / nv, c = i - b * nv;
+          *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = v[u];
+        }
+      }
+    }
+  }
+}
+
 // Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global loads. __syncthreads() is a workgroup release/acquire, which makes every wave drain
 // its outstanding global loads (s_waitcnt vmcnt(0)) - at every tile boundary that emptied
@@ -374,8 +465,7 @@ __device__ __forceinline__ void lds_barrier(bool fence) {
 // (second launch bound = minimum waves per SIMD: 4, except the 8-wave Q6_K kernel, which
 // would spill at 128 VGPRs)
 template <int QT, int NW, int PD>
-__global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 : 4) void bmm_kernel(BmmArgs a) {
-  const int bid = blockIdx.x, nbk = gridDim.x;
+__device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs& a, const int bid, const int nbk) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
@@ -481,58 +571,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   }
   if (clk && tid == 0) clk[1] = wall_clock64();
   // stage x[b][k0, k0 + kn) for the B rows
-  if (NW >= 8 && a.xf) {  // (8/16-wave kernels only: keeps the split-K kernels' registers)
-    // folded RMSNorm (K = 4096, B <= 8: each thread holds 2 float4 of every row): every load
-    // is issued first - one memory round trip, like the f16 staging - then f16(x * w) goes to
-    // LDS in bprep's 4-group order and each wave leaves its per-row partial sum of squares
-    // (rows past B load row B - 1 and are dropped: straight-line code, no predicated loads)
-    constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
-    float4 xv[8 * J], w[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) w[j] = *reinterpret_cast<const float4*>(a.norm_w + 4 * (tid + j * kBlock));
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
-#pragma unroll
-      for (int j = 0; j < J; ++j) xv[J * b + j] = *reinterpret_cast<const float4*>(xr + 4 * (tid + j * kBlock));
-    }
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const float4 x = xv[J * b + j], ww = w[j];
-        ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
-        const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
-        const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
-        if (b < a.B) *reinterpret_cast<uint2*>(xs + b * ldx + 4 * (tid + j * kBlock)) = make_uint2(as_u(p0), as_u(p1));
-      }
-      ss = wave_sum_fast(ss);
-      if (lane == 0) rowss[b * NW + wave] = ss;
-    }
-  } else {
-    // every thread's loads go out before any LDS store: one memory round trip for the slice
-    // (a load-store loop waited for each load in turn: 3-6 round trips, 1.5-3.6 us per launch)
-    constexpr int U = 8;
-    const int nv = kn >> 3, n = a.B * nv;
-    for (int i0 = 0; i0 < n; i0 += U * kBlock) {
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = min(i0 + u * kBlock + tid, n - 1);
-        const int b = i / nv, c = i - b * nv;
-        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * kBlock + tid;
-        if (i < n) {
-          const int b = i / nv, c = i - b * nv;
-          *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = v[u];
-        }
-      }
-    }
-  }
+  bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
   __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
   const bool col_ok = r16 < a.B;
@@ -561,30 +600,7 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
       acc[0] += (float)raw_word<QT>(wc[0]) + (float)raw_word<QT>(wc[1]);
       return;
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = 8 * s + 4 * h + kq;
-      int off_lo, off_hi;
-      chunk_runs<QT>(c, off_lo, off_hi);
-      const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
-      const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
-      const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
-      HFrag F;
-      dequant_frags<QT>(wc[h], c, F);
-      const uint4 xr[4] = {x0, x1, x2, x3};
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        // MFMA m takes 8 weights of ONE run: the low run's 0-7 / 8-15 (m = 0 / 1), then the high
-        // run's (m = 2 / 3) - pairs of quant dwords 2(m % 2), 2(m % 2) + 1 - so its B operand is
-        // the 16-byte LDS read as it stands (taking 4 halves from each run cost 3 v_mov per MFMA)
-        const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
-        const uint4 av = make_uint4(F.w[4 * dw + sh], F.w[4 * dw + sh + 1], F.w[4 * dw + 4 + sh], F.w[4 * dw + 5 + sh]);
-        const uint4 bv = xr[m];
-        f4_t& ac = h == 0 ? acc : acc2;
-        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
-                                                    __builtin_bit_cast(h8_t, bv), ac, 0, 0, 0);
-      }
-    }
+    bmm_step<QT>(wc, s, kq, xrow, acc, acc2);
   };
   // reduction + epilogue of tile gt (every wave of the block, once per tile)
   int ntiles_done = 0;
@@ -704,6 +720,149 @@ __global__ __launch_bounds__(NW * 64, (QT == T_Q6_K && NW == 8) || PD == 2 ? 3 :
   }
 }
 
+// Q|K|V of the bumped layers in ONE launch: blocks [0, a.nb1) run the Q|K run (type QT, args a),
+// the rest the V run (type QT2, args a2; Q4_K_M bumps V to Q6_K on half the layers). As its own
+// launch the 64-tile V projection cost 10.4 us on a 3.6 MB matrix (B = 6, r3c profile); a
+// side-stream graph branch for it measured no gain (r2 profiles).
+template <int QT, int NW, int PD, int QT2 = 0>
+__global__ __launch_bounds__(NW * 64, ((QT == T_Q6_K || QT2 == T_Q6_K) && NW == 8) || PD == 2 ? 3 : 4)
+void bmm_kernel(BmmArgs a, BmmArgs a2) {
+  // the body reads its arguments through the kernarg segment pointer: a reference to the
+  // by-value parameter made the compiler copy the whole block to scratch (544 B per lane)
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if constexpr (QT2 != 0) {
+    if ((int)blockIdx.x >= ka[0].nb1) {
+      bmm_body<QT2, NW, PD>(ka[1], blockIdx.x - ka[0].nb1, gridDim.x - ka[0].nb1);
+      return;
+    }
+    bmm_body<QT, NW, PD>(ka[0], blockIdx.x, ka[0].nb1);
+  } else {
+    bmm_body<QT, NW, PD>(ka[0], blockIdx.x, gridDim.x);
+  }
+  (void)a;
+  (void)a2;
+}
+
+// ---------------------------------------------------------------- wave-owned tiles
+// One-part projections with many tiles (dense SwiGLU gate/up: 1792 tiles = 7 per CU for the 8B
+// shape; the head): every WAVE streams whole tiles - all K steps - with PD steps of weights in
+// flight in registers, so there is no cross-wave reduction and no barrier after the x staging.
+// bmm_kernel splits a tile's steps over the block's 8 waves (2 steps per wave at K = 4096):
+// every tile ended in an LDS reduction behind two block barriers, each wave had one step in
+// flight, and 46 % of the wave cycles sat in s_waitcnt / barriers (r2g PMC).
+// One block per CU (the launcher asks for more than half the LDS, so two never share a CU):
+// the x slice is staged once per CU (bmm_kernel staged it twice), and block b takes the
+// contiguous tile range [t0, t0 + tn) of an even split - wave w its tiles t0 + w + i * NW.
+// Weights rotate through PD + 1 register buffers with fixed roles (the step loop unrolled by
+// PD + 1): no register copies, so no wait on in-flight loads before they are needed.
+template <int QT, int PD>
+__global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
+  constexpr int NW = 8, R = PD + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* rowss = reinterpret_cast<float*>(smem);            // [8 rows][NW waves] folded norm
+  __half* xs = reinterpret_cast<__half*>(smem + 256);
+  const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int K = a.w.K, steps = K >> 8;
+  // block = (K part kp, tile group grp): parts > 1 add their partial tiles atomically (Wo /
+  // down: 8 parts x 32 groups of 8 tiles = one block per CU for the 256-tile shapes)
+  const int kparts = a.kparts, kp = blockIdx.x % kparts, grp = blockIdx.x / kparts, G = gridDim.x / kparts;
+  const int s0 = kp * a.spp, ns = min(steps, s0 + a.spp) - s0;  // this part's steps [s0, s0 + ns)
+  const int k0 = s0 * 256, kn = ns * 256, ldx = kn + 8;
+  const int tiles = (a.n_out + 15) >> 4, bid = blockIdx.x;
+  const int t0 = grp * (tiles / G) + min(grp, tiles % G);
+  const int tn = tiles / G + (grp < tiles % G ? 1 : 0);
+  const int nt = wave < tn ? (tn - 1 - wave) / NW + 1 : 0;  // this wave's tiles (wave-uniform)
+  const int N = nt * ns;                                    // ... as one sequence of steps
+  const int SB = t16_step_bytes(QT);
+  auto tile_of = [&](int i) { return t0 + wave + i * NW; };
+  auto tbase = [&](int i) { return a.w.base + ((size_t)tile_of(i) * steps + s0) * SB; };
+  BRawT<QT> buf[R][2];
+  int li = 0, ls = 0;  // load cursor: the wave's tile, step
+  const uint8_t* lp = nt > 0 ? tbase(0) : a.w.base;
+  auto load_next = [&](BRawT<QT>* dst) {
+    tload<QT>(dst[0], lp + (size_t)ls * SB, 0, lane, r16, kq);
+    tload<QT>(dst[1], lp + (size_t)ls * SB, 1, lane, r16, kq);
+    if (++ls == ns) {
+      ls = 0;
+      if (++li < nt) lp = tbase(li);
+    }
+  };
+  // microbenchmark timeline (wave 0, as bmm_kernel's): [0] entry [1] weights issued [2] x staged
+  // [3] first tile computed [4] exit [5] tiles of wave 0
+  long long* clk = a.dbg_clk ? a.dbg_clk + (size_t)bid * 8 : nullptr;
+  if (clk && tid == 0) clk[0] = wall_clock64();
+  // the first PD steps go out before the x staging round trip
+#pragma unroll
+  for (int p = 0; p < PD; ++p)
+    if (p < N) load_next(buf[p]);
+  if (clk && tid == 0) clk[1] = wall_clock64();
+  bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+  __syncthreads();
+  if (clk && tid == 0) clk[2] = wall_clock64();
+  if (N == 0) return;
+  const bool col_ok = r16 < a.B;
+  float cs = 1.f;  // folded norm: this lane's column scale
+  if (a.xf) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += rowss[(col_ok ? r16 : 0) * NW + w];
+    cs = rsqrtf(t / (float)K + a.eps);
+  }
+  const __half* xrow = xs + (col_ok ? r16 : 0) * ldx - k0;  // indexed by global k
+  f4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  int ci = 0, cstep = 0;  // compute cursor (step s0 + cstep of tile ci)
+  auto finish = [&]() {   // tile ci is complete in acc + acc2: C[row 4kq + i][col r16]
+    acc += acc2;
+    if (a.xf) acc *= cs;
+    const int gt = tile_of(ci);
+    if (a.swiglu_epi) {
+      // rows 0-7 (lanes 0-31): gate of features 8 gt + 4 kq + i; rows 8-15 (lanes 32-63): up
+      f4_t up;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(acc[i], 32);
+      if (col_ok && lane < 32) {
+        const int f0 = gt * 8 + 4 * kq;
+        const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
+        const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
+        *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
+      }
+    } else if (col_ok) {
+      float* o = a.out + (size_t)r16 * a.ldo;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = gt * 16 + 4 * kq + i;
+        if (row < a.n_out) {
+          if (kparts > 1) atomicAdd(o + row, acc[i]);
+          else if (a.store_out) o[row] = acc[i];
+          else o[row] += acc[i];  // one owner per (row, column)
+        }
+      }
+    }
+    acc = f4_t{0.f, 0.f, 0.f, 0.f};
+    acc2 = acc;
+  };
+  for (int j0 = 0; j0 < N; j0 += R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (j0 + r >= N) break;  // wave-uniform
+      if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
+      __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
+      bmm_step<QT>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
+      if (++cstep == ns) {
+        finish();
+        cstep = 0;
+        ++ci;
+        if (clk && tid == 0 && ci == 1) clk[3] = wall_clock64();
+      }
+    }
+  }
+  if (clk && tid == 0) {
+    clk[4] = wall_clock64();
+    clk[5] = nt;
+  }
+}
+
 // ---------------------------------------------------------------- activation prep
 // One block per activation row: optional SwiGLU (gate/up pre-activations in 32-feature
 // interleaved groups), optional RMSNorm (* w), f16, k order (0,2,1,3) inside every 4-group.
@@ -819,6 +978,37 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
   for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
   const int steps = a.w.K / 256;
+  // dense SwiGLU gate/up: wave-owned tiles (LFK_BMM_WT=0: the block-split kernel, A/B), PD
+  // steps of weights in flight per wave (LFK_BMM_WTPD: 1-3)
+  static const int wt_env = env_int("LFK_BMM_WT", 1);
+  static const int wtpd = std::min(3, std::max(1, env_int("LFK_BMM_WTPD", 2)));
+  // plain split-K projections (Wo, down): the same kernel over (K part, 8-tile group) blocks
+  // (LFK_BMM_WTK=0: the block-split kernel)
+  static const int wtk_env = env_int("LFK_BMM_WTK", 1);
+  const bool wt_sw = wt_env && a.swiglu_epi && !a.ew && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
+                     a.B <= 8;
+  const bool wt_k = wtk_env && !a.swiglu_epi && !a.ew && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
+                    a.nseg == 1 && a.B <= 8;
+  if (wt_sw || wt_k) {
+    const int cus = bmm_cus();
+    int kparts = 1;
+    if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
+      kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
+      // the staged slice (B rows x part) stays within the LDS
+      while (kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
+    }
+    a.spp = (steps + kparts - 1) / kparts;
+    a.kparts = kparts = (steps + a.spp - 1) / a.spp;
+    // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K group
+    const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
+    // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
+    const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
+    const dim3 grid(G * kparts);
+    if (wtpd == 1) hipLaunchKernelGGL((bmm_wt_kernel<QT, 1>), grid, dim3(512), lds, s, a);
+    else if (wtpd == 3) hipLaunchKernelGGL((bmm_wt_kernel<QT, 3>), grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+    return;
+  }
   if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
     // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
     static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4, 8 or 16
@@ -839,13 +1029,13 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     }
     if constexpr (QT == T_Q4_K) {
       if (nw1 == 16) {
-        hipLaunchKernelGGL((bmm_kernel<QT, 16, 1>), dim3(nb), dim3(1024), lds, s, a);
+        hipLaunchKernelGGL((bmm_kernel<QT, 16, 1>), dim3(nb), dim3(1024), lds, s, a, a);
         return;
       }
     }
-    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(nb), dim3(256), lds, s, a);
-    else if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 8, 2>), dim3(nb), dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((bmm_kernel<QT, 8, 1>), dim3(nb), dim3(512), lds, s, a);
+    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(nb), dim3(256), lds, s, a, a);
+    else if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 8, 2>), dim3(nb), dim3(512), lds, s, a, a);
+    else hipLaunchKernelGGL((bmm_kernel<QT, 8, 1>), dim3(nb), dim3(512), lds, s, a, a);
     return;
   }
   // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
@@ -870,14 +1060,11 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   // block lifetime of tail): the grid stays within one resident round
   const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus()) / kparts));
   const size_t lds = bmm_lds(a.B, spp, 4);
-  if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 4, 2>), dim3(bpk * kparts), dim3(256), lds, s, a);
-  else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a);
+  if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 4, 2>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
+  else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
 }
 
-void bmm(const BmmArgs& a0, hipStream_t s) {
-  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
-  BmmArgs a = a0;
-  a.fence_sync = fence;
+static void bmm_check(const BmmArgs& a) {
   if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
   if (a.nseg < 1 || a.nseg > 3) throw std::runtime_error("bmm: 1 to 3 segments");
@@ -896,6 +1083,13 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
   if (a.ew && a.swiglu_epi && (a.n_out + 15) / 16 / a.tiles_per_expert > 64) throw std::runtime_error("bmm: <= 64 experts");
   if (a.ew && !a.swiglu_epi && (a.xf || a.qkv_epi || a.one_part))
     throw std::runtime_error("bmm: the MoE down projection runs split-K (whole-expert parts)");
+}
+
+void bmm(const BmmArgs& a0, hipStream_t s) {
+  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
+  BmmArgs a = a0;
+  a.fence_sync = fence;
+  bmm_check(a);
   if (a.n_out <= 0) return;
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;
@@ -904,6 +1098,42 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
     case T_Q8_0: launch_bmm<T_Q8_0>(a, s); break;
     default: throw std::runtime_error("bmm: unsupported weight type");
   }
+}
+
+bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
+  static const int on = env_int("LFK_BMM_QKV2", 1);  // 0: one launch per run (A/B)
+  if (!on || !a0.qkv_epi || !b0.qkv_epi || a0.B != b0.B || a0.w.K != b0.w.K || a0.n_out <= 0 || b0.n_out <= 0)
+    return false;
+  if ((a0.xf == nullptr) != (b0.xf == nullptr)) return false;
+  static const int nw1_env = env_int("LFK_BMM_NW1", 8);
+  if (nw1_env != 8) return false;  // the one-part tuning knob picks other block shapes: separate launches
+  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
+  BmmArgs a = a0, b = b0;
+  a.fence_sync = b.fence_sync = fence;
+  bmm_check(a);
+  bmm_check(b);
+  auto tiles_of = [](const BmmArgs& x) {
+    int t = (x.n_out + 15) / 16;
+    for (int i = 1; i < x.nseg; ++i) t += (x.seg_rows[i] + 15) / 16;
+    return t;
+  };
+  const int steps = a.w.K / 256;
+  a.spp = b.spp = steps;
+  a.kparts = b.kparts = 1;
+  const size_t lds = bmm_lds(a.B, steps, 8);
+  const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 2));
+  const int cap = per_cu * bmm_cus();
+  const int ta = tiles_of(a), tb = tiles_of(b);
+  // blocks in proportion to the runs' tiles, each run at least one block, within one resident round
+  int na = std::min(ta, std::max(1, (int)((long long)cap * ta / (ta + tb))));
+  int nbb = std::min(tb, std::max(1, cap - na));
+  a.nb1 = na;
+  const dim3 grid(na + nbb), blk(512);
+  const int ta_ = a.w.type, tb_ = b.w.type;
+  if (ta_ == T_Q4_K && tb_ == T_Q6_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q6_K>), grid, blk, lds, s, a, b);
+  else if (ta_ == T_Q4_K && tb_ == T_Q5_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q5_K>), grid, blk, lds, s, a, b);
+  else return false;
+  return true;
 }
 
 }  // namespace lfk

@@ -127,11 +127,16 @@ struct BmmArgs {
   bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
   bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block wall_clock64 stamps [grid][8]
+  int nb1 = 0;                     // bmm_qkv2: blocks of the first run (set by the launcher)
 };
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)
 bool bmm_norm_fits(int K, int B);  // one K part + the folded RMSNorm's staging shape
 void bmm(const BmmArgs& a, hipStream_t s);
+// two one-part Q|K|V runs of different weight types (Q|K Q4_K + V Q6_K / Q5_K: the bumped
+// layers of the K-quant mixes) in one launch; false = unsupported pair or shape (caller
+// launches them one by one)
+bool bmm_qkv2(const BmmArgs& a, const BmmArgs& b, hipStream_t s);
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);
 // swiglu: `planar` is a gate/up matrix in 32-row gate / up groups (upload_gate_up); the copy

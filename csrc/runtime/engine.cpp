@@ -941,7 +941,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
       }
       i = j;
     }
-    for (const BmmArgs& a : rl) bmm(a, s);
+    // bumped layers (Q|K Q4_K + V Q6_K): both runs in one launch
+    if (!(rl.size() == 2 && B <= kBmmMaxRows && bmm_qkv2(rl[0], rl[1], s)))
+      for (const BmmArgs& a : rl) bmm(a, s);
   }
   if (!fused)
     rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
