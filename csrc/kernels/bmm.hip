@@ -433,6 +433,38 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
   }
 }
 
+// Q|K|V epilogue of one reduced 16-row tile (lane: rows 4kq .. 4kq+3, column r16): RoPE on the
+// adjacent pairs (0,1), (2,3) this lane holds for Q and K, Q rows to q_out, K / V rows as f16
+// into the row's KV slot at its position (the batched rope_kv_prefill folded in)
+__device__ __forceinline__ void qkv_epilogue(const BmmArgs& a, int sg, int tile, int n_out, const f4_t& acc, int r16,
+                                             int kq) {
+  const auto& q = a.qkv;
+  const int kind = sg == 0 ? q.kind[0] : sg == 1 ? q.kind[1] : q.kind[2], b = r16, hd = q.head_dim;
+  const int pos = min(max(q.pos[b], 0), q.n_ctx - 1);
+  const size_t so = (size_t)q.slots[b] * q.slot_stride;
+#pragma unroll
+  for (int i = 0; i < 4; i += 2) {
+    const int row = tile * 16 + 4 * kq + i;
+    if (row < n_out) {  // rows come in (even, odd) pairs: n_out is even
+      float y0 = acc[i], y1 = acc[i + 1];
+      const int dd = row % hd;
+      if (kind < 2) {
+        const float2 cs = q.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
+        y0 = acc[i] * cs.x - acc[i + 1] * cs.y;
+        y1 = acc[i] * cs.y + acc[i + 1] * cs.x;
+      }
+      if (kind == 0) {
+        q.q_out[(size_t)b * q.q_ld + row] = y0;
+        q.q_out[(size_t)b * q.q_ld + row + 1] = y1;
+      } else {
+        __half* c = (kind == 1 ? q.k_cache : q.v_cache) + so + ((size_t)(row / hd) * q.n_ctx + pos) * hd + dd;
+        c[0] = __float2half(y0);
+        c[1] = __float2half(y1);
+      }
+    }
+  }
+}
+
 // Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global loads. __syncthreads() is a workgroup release/acquire, which makes every wave drain
 // its outstanding global loads (s_waitcnt vmcnt(0)) - at every tile boundary that emptied
@@ -465,7 +497,8 @@ __device__ __forceinline__ void lds_barrier(bool fence) {
 // (second launch bound = minimum waves per SIMD: 4, except the 8-wave Q6_K kernel, which
 // would spill at 128 VGPRs)
 template <int QT, int NW, int PD>
-__device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs& a, const int bid, const int nbk) {
+__device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __restrict__ ap, const int bid, const int nbk) {
+  const BmmArgs& a = *ap;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
@@ -634,32 +667,7 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs& a,
           *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
         }
       } else if (col_ok && a.qkv_epi) {
-        // rows 4kq .. 4kq+3 of the tile: RoPE pairs (0,1), (2,3) are in this lane
-        const auto& q = a.qkv;
-        const int kind = sg == 0 ? q.kind[0] : sg == 1 ? q.kind[1] : q.kind[2], b = r16, hd = q.head_dim;
-        const int pos = min(max(q.pos[b], 0), q.n_ctx - 1);
-        const size_t so = (size_t)q.slots[b] * q.slot_stride;
-#pragma unroll
-        for (int i = 0; i < 4; i += 2) {
-          const int row = tile * 16 + 4 * kq + i;
-          if (row < n_out) {  // rows come in (even, odd) pairs: n_out is even
-            float y0 = acc[i], y1 = acc[i + 1];
-            const int dd = row % hd;
-            if (kind < 2) {
-              const float2 cs = q.rope[(size_t)pos * (hd >> 1) + (dd >> 1)];
-              y0 = acc[i] * cs.x - acc[i + 1] * cs.y;
-              y1 = acc[i] * cs.y + acc[i + 1] * cs.x;
-            }
-            if (kind == 0) {
-              q.q_out[(size_t)b * q.q_ld + row] = y0;
-              q.q_out[(size_t)b * q.q_ld + row + 1] = y1;
-            } else {
-              __half* c = (kind == 1 ? q.k_cache : q.v_cache) + so + ((size_t)(row / hd) * q.n_ctx + pos) * hd + dd;
-              c[0] = __float2half(y0);
-              c[1] = __float2half(y1);
-            }
-          }
-        }
+        qkv_epilogue(a, sg, tile, n_out, acc, r16, kq);
       } else if (col_ok) {
         float* o = out + (size_t)r16 * a.ldo;
 #pragma unroll
@@ -732,12 +740,12 @@ void bmm_kernel(BmmArgs a, BmmArgs a2) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   if constexpr (QT2 != 0) {
     if ((int)blockIdx.x >= ka[0].nb1) {
-      bmm_body<QT2, NW, PD>(ka[1], blockIdx.x - ka[0].nb1, gridDim.x - ka[0].nb1);
+      bmm_body<QT2, NW, PD>(ka + 1, blockIdx.x - ka[0].nb1, gridDim.x - ka[0].nb1);
       return;
     }
-    bmm_body<QT, NW, PD>(ka[0], blockIdx.x, ka[0].nb1);
+    bmm_body<QT, NW, PD>(ka, blockIdx.x, ka[0].nb1);
   } else {
-    bmm_body<QT, NW, PD>(ka[0], blockIdx.x, gridDim.x);
+    bmm_body<QT, NW, PD>(ka, blockIdx.x, gridDim.x);
   }
   (void)a;
   (void)a2;

@@ -338,8 +338,6 @@ void Engine::alloc_buffers() {
     HIPCHK(hipHostMalloc((void**)&h_rmeta_, sizeof(int) * 3 * B, hipHostMallocDefault));
   }
   HIPCHK(hipMemset(out_tokens_, 0, sizeof(int) * 64));
-  dev_err_ = (int*)dalloc(sizeof(int) * 4);
-  HIPCHK(hipMemset(dev_err_, 0, sizeof(int) * 4));
   // P2P messages: a decode step's hidden rows and the sampler's candidate blocks; in "ipc"
   // mode (no RCCL) also prefill chunks and the test hooks' logit gathers
   {
@@ -441,9 +439,10 @@ void Engine::setup_batch_mfma() {
 }
 
 void Engine::check_device_err() {
+  // the only bounded in-kernel wait left is the P2P all-reduce's (TP); a blocking read of an
+  // error word nothing else writes cost every step a synchronous copy
   int e = 0;
-  HIPCHK(hipMemcpy(&e, dev_err_, sizeof(int), hipMemcpyDeviceToHost));
-  if (e == 0 && p2p_ && p2p_->ready()) e = p2p_->error();
+  if (p2p_ && p2p_->ready()) e = p2p_->error();
   if (e != 0) {
     healthy_ = false;
     last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
@@ -1383,8 +1382,13 @@ std::vector<int> Engine::batch_step_impl(const std::vector<int>& slots) {
     return std::vector<int>(h_btok_, h_btok_ + 1);
   }
   last_b1_ = false;
-  std::memcpy(h_bslots_, slots.data(), sizeof(int) * B);
-  HIPCHK(hipMemcpyAsync(bslots_, h_bslots_, sizeof(int) * B, hipMemcpyHostToDevice, stream_));
+  // the row -> slot map goes up only when it changed (a steady batch re-sends nothing; each
+  // step ends in a stream sync, so the pinned copy is never rewritten under an in-flight copy)
+  if (B != bslots_n_ || std::memcmp(h_bslots_, slots.data(), sizeof(int) * B) != 0) {
+    std::memcpy(h_bslots_, slots.data(), sizeof(int) * B);
+    HIPCHK(hipMemcpyAsync(bslots_, h_bslots_, sizeof(int) * B, hipMemcpyHostToDevice, stream_));
+    bslots_n_ = B;
+  }
   if (opt_.use_graph) {
     if ((int)bgraph_.size() <= B) bgraph_.resize(B + 1, nullptr);
     if (!bgraph_[B]) {

@@ -284,7 +284,6 @@ class Engine : public SlotBackend {
   __hip_bfloat16* moe_xg_ = nullptr; __hip_bfloat16* moe_hg_ = nullptr; float* moe_yg_ = nullptr;
   int* moe_ids_ = nullptr;
   float* moe_w_ = nullptr;
-  int* dev_err_ = nullptr;    // device error word (bounded in-kernel waits that timed out)
   int* h_ring_ = nullptr;     // pinned [64]
   int* h_tokens_ = nullptr;   // pinned [n_batch]
 
@@ -304,6 +303,7 @@ class Engine : public SlotBackend {
   int* attn_cnt_b_ = nullptr;      // [bmax][64]
   int* h_bslots_ = nullptr;   // pinned [bmax]
   int* h_btok_ = nullptr;     // pinned [bmax]
+  int bslots_n_ = -1;         // rows of the row -> slot map last uploaded to bslots_
   int last_batch_ = 0;
   // batch_step projections on the MFMA batched projection (bmm.hip: weights streamed once per
   // step for all rows) instead of the prefill GEMM: attention/head (bg_) and the dense FFN

@@ -28,3 +28,13 @@ def main(path):
 
 if __name__ == "__main__":
     main(sys.argv[1])
+
+
+def one_step(path, layer_from=2, layers=2):
+    """The kernel sequence of one step (the second to last), durations in order."""
+    rows = list(csv.DictReader(open(path)))
+    idx = [i for i, r in enumerate(rows) if "sample_stage1" in r["Kernel_Name"]]
+    a, b = idx[-3], idx[-2]
+    for r in rows[a + 1:b + 1]:
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000
+        print(f"{r['Kernel_Name'].split('(')[0][-40:]:40s} grid {int(r['Grid_Size_X']) // int(r['Workgroup_Size_X']):5d} {d:7.2f}")
