@@ -285,51 +285,52 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   if constexpr (TL) { if (last && threadIdx.x == 0) tl[8] = wall_clock64(); }
   if (!last) return;
   // every element's split values and the split statistics are loaded in one
-  // batch of independent sc1 loads (one memory round trip per 16 splits)
+  // batch of independent sc1 loads (one memory round trip per 16 splits). A thread
+  // takes EPT adjacent dims of ONE head, so the split statistics (m, l) are loaded
+  // once per thread, not once per element: 64 instead of 96 VGPRs of loads at G = 4,
+  // which keeps the kernel at 4 waves per SIMD (a B = 6 grid of 768 blocks then fits
+  // the chip in one dispatch round instead of leaving a third of it for a second one).
   constexpr int EPT = (G * HD + 255) / 256;
+  static_assert(HD % EPT == 0, "a thread's elements must share one head");
   constexpr int NSB = 16;
-  float M[EPT], num[EPT], den[EPT];
+  const int e0 = min(tid * EPT, G * HD - EPT);
+  const int h = kvh * G + e0 / HD, d0 = e0 % HD;
+  float M = -FLT_MAX, num[EPT], den = 0.f;
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) { M[j] = -FLT_MAX; num[j] = 0.f; den[j] = 0.f; }
+  for (int j = 0; j < EPT; ++j) num[j] = 0.f;
   for (int s0 = 0; s0 < ns; s0 += NSB) {
-    float mv[EPT][NSB], lv[EPT][NSB], pv[EPT][NSB];
+    float mv[NSB], lv[NSB], pv[NSB][EPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int e = min(tid + 256 * j, G * HD - 1);
-      const int h = kvh * G + e / HD, d = e % HD;
+    for (int i = 0; i < NSB; ++i) {
+      const int s2 = min(s0 + i, ns - 1);
+      const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
+      mv[i] = ld_sc1(p + HD);
+      lv[i] = ld_sc1(p + HD + 1);
 #pragma unroll
-      for (int i = 0; i < NSB; ++i) {
-        const int s2 = min(s0 + i, ns - 1);
-        const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
-        mv[j][i] = ld_sc1(p + HD);
-        lv[j][i] = ld_sc1(p + HD + 1);
-        pv[j][i] = ld_sc1(p + d);
-      }
+      for (int j = 0; j < EPT; ++j) pv[i][j] = ld_sc1(p + d0 + j);
     }
+    float mb = M;
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      float mb = M[j];
+    for (int i = 0; i < NSB; ++i) mb = (s0 + i < ns) ? fmaxf(mb, mv[i]) : mb;
+    const float r = __expf(M - mb);
+    den *= r;
 #pragma unroll
-      for (int i = 0; i < NSB; ++i) mb = (s0 + i < ns) ? fmaxf(mb, mv[j][i]) : mb;
-      const float r = __expf(M[j] - mb);
-      num[j] *= r;
-      den[j] *= r;
+    for (int j = 0; j < EPT; ++j) num[j] *= r;
 #pragma unroll
-      for (int i = 0; i < NSB; ++i) {
-        const float f = (s0 + i < ns) ? __expf(mv[j][i] - mb) : 0.f;
-        num[j] += f * pv[j][i];
-        den[j] += f * lv[j][i];
-      }
-      M[j] = mb;
+    for (int i = 0; i < NSB; ++i) {
+      const float f = (s0 + i < ns) ? __expf(mv[i] - mb) : 0.f;
+      den += f * lv[i];
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) num[j] += f * pv[i][j];
     }
+    M = mb;
   }
+  if (tid * EPT < G * HD) {
 #pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = tid + 256 * j;
-    if (e < G * HD) {
-      const int o = (kvh * G + e / HD) * HD + e % HD;
-      a.out[o] = num[j] / den[j];
-      if (a.out_h) a.out_h[swz4(o)] = __float2half(num[j] / den[j]);
+    for (int j = 0; j < EPT; ++j) {
+      const int o = h * HD + d0 + j;
+      a.out[o] = num[j] / den;
+      if (a.out_h) a.out_h[swz4(o)] = __float2half(num[j] / den);
     }
   }
   if constexpr (TL) { if (threadIdx.x == 0) tl[9] = wall_clock64(); }

@@ -37,6 +37,11 @@ for s in "$@"; do
             --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
     gvpmc) export TMPDIR=/tmp; step gvpmc 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/gvpmc -o pmc --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 --only q4k ;;
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
+    gemmb) step gemmb 300 bash -c 'python tools/gemm_bench.py --T 512 && python tools/gemm_bench.py --T 2048' ;;
+    gemmpmc) export TMPDIR=/tmp; step gemmpmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
+            -d gpurun_out/gemmpmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup
+            step gemmpmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+            -d gpurun_out/gemmpmcB -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup ;;
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
     bench20) step bench20 900 python bench.py --steps 20 --warmup 2 ;;
     benchtp2) LFK_BENCH_DEVICE=0 step benchtp2 900 python bench.py --gpus 2 --steps 12 --warmup 2 ;;
