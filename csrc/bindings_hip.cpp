@@ -118,6 +118,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("n_slots", &Engine::n_slots)
       .def_property_readonly("max_batch", &Engine::max_batch)
       .def_property_readonly("batch_gemv", &Engine::batch_gemv)
+      .def_property_readonly("prefill_t16", &Engine::prefill_t16)
       .def("slot_begin",
            [](Engine& e, int slot, const std::vector<int>& prompt, int n_keep, py::dict sp) {
              const SamplingOpts o = sampling_opts(sp);
@@ -346,6 +347,17 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
+  m.def("gemm_t16", [](uintptr_t w, int type, int rows, int K, uintptr_t x, int T, uintptr_t out, int ldo,
+                       uintptr_t out_h, int ldh, int epi, uintptr_t stream, uintptr_t resid) {
+    GemmT16Args a;
+    a.w = make_qmat(P<void>(w), type, rows, K);
+    a.x = P<__half>(x); a.T = T; a.out = P<float>(out); a.ldo = ldo; a.resid = P<float>(resid);
+    a.out_h = P<__half>(out_h); a.ldh = ldh;
+    gemm_t16(a, epi, S(stream));
+    hip_ok("gemm_t16");
+  }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
+     py::arg("ldo"), py::arg("out_h"), py::arg("ldh"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
+
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
                           int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,
                           int debug_stop, uintptr_t dbg_clk, int batch, uintptr_t slots, size_t slot_stride,
@@ -371,25 +383,29 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("slot_stride") = 0, py::arg("out_h") = 0);
   m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
   m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
-                           int hd, float scale, uintptr_t out, uintptr_t stream, bool out_bf16) {
+                           int hd, float scale, uintptr_t out, uintptr_t stream, bool out_bf16, bool out_h) {
     AttnPrefillArgs a;
     a.q = P<float>(q); a.k_cache = P<__half>(kc); a.v_cache = P<__half>(vc); a.T = T; a.pos0 = pos0;
     a.n_ctx = n_ctx; a.n_head = n_head; a.n_kv_head = n_kv; a.head_dim = hd; a.scale = scale;
-    if (out_bf16) a.out_bf16 = P<__hip_bfloat16>(out);
+    if (out_h) a.out_h = P<__half>(out);
+    else if (out_bf16) a.out_bf16 = P<__hip_bfloat16>(out);
     else a.out = P<float>(out);
     a.out_stride = n_head * hd;
     attn_prefill(a, S(stream));
     hip_ok("attn_prefill");
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("T"), py::arg("pos0"), py::arg("n_ctx"), py::arg("n_head"),
-     py::arg("n_kv"), py::arg("hd"), py::arg("scale"), py::arg("out"), py::arg("stream"), py::arg("out_bf16") = false);
+     py::arg("n_kv"), py::arg("hd"), py::arg("scale"), py::arg("out"), py::arg("stream"), py::arg("out_bf16") = false,
+     py::arg("out_h") = false);
   m.def("embed", [](uintptr_t w, int type, int V, int d, uintptr_t tokens, int T, uintptr_t x, uintptr_t stream) {
     embed_rows(make_qmat(P<void>(w), type, V, d), P<int>(tokens), T, P<float>(x), S(stream));
     hip_ok("embed");
   });
-  m.def("rmsnorm_bf16", [](uintptr_t x, uintptr_t w, float eps, int T, int d, uintptr_t y, uintptr_t stream) {
-    rmsnorm_bf16(P<float>(x), P<float>(w), eps, T, d, P<__hip_bfloat16>(y), S(stream));
+  m.def("rmsnorm_bf16", [](uintptr_t x, uintptr_t w, float eps, int T, int d, uintptr_t y, uintptr_t stream,
+                           bool f16sw) {
+    rmsnorm_bf16(P<float>(x), P<float>(w), eps, T, d, P<__hip_bfloat16>(y), S(stream), nullptr, 0, f16sw);
     hip_ok("rmsnorm_bf16");
-  });
+  }, py::arg("x"), py::arg("w"), py::arg("eps"), py::arg("T"), py::arg("d"), py::arg("y"), py::arg("stream"),
+     py::arg("f16sw") = false);
   m.def("launch_probe", [](int threads, int blocks, size_t lds, int iters, uintptr_t out, uintptr_t stream) {
     launch_probe(threads, blocks, lds, iters, P<float>(out), S(stream));
   });

@@ -493,7 +493,8 @@ typedef float f32x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
-template <int HD, bool OUTBF>
+// OUT: 0 f32, 1 bf16, 2 f16 in bmm's 4-group k order (gemm_t16's input)
+template <int HD, int OUT>
 __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs a, int HB) {
   constexpr int KT = 64, KP = HD + 8, VP = HD + 32, NKK = HD / 16, NDT = HD / 32;
   constexpr int CPR = HD / 8, NCH = KT * CPR / 256;  // 16-B chunks per row / per thread
@@ -633,9 +634,13 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs 
         const size_t off = (size_t)t * a.out_stride + (size_t)head * HD + d;
         const float v0 = o[dt][4 * rg] * inv, v1 = o[dt][4 * rg + 1] * inv;
         const float v2 = o[dt][4 * rg + 2] * inv, v3 = o[dt][4 * rg + 3] * inv;
-        if constexpr (OUTBF) {
+        if constexpr (OUT == 1) {
           const uint2 pk = make_uint2(pk_bf16_pair(v0, v1), pk_bf16_pair(v2, v3));
           *reinterpret_cast<uint2*>(a.out_bf16 + off) = pk;
+        } else if constexpr (OUT == 2) {  // positions (0, 2, 1, 3) of the 4-group
+          const __half2 p0 = __floats2half2_rn(v0, v2), p1 = __floats2half2_rn(v1, v3);
+          *reinterpret_cast<uint2*>(a.out_h + off) =
+              make_uint2(__builtin_bit_cast(unsigned, p0), __builtin_bit_cast(unsigned, p1));
         } else {
           *reinterpret_cast<float4*>(a.out + off) = make_float4(v0, v1, v2, v3);
         }
@@ -647,8 +652,9 @@ template <int HD>
 static void launch_attn_prefill_mfma(const AttnPrefillArgs& a, int G, hipStream_t s) {
   const int HB = std::min(G, 4), QTB = 4 / HB;
   dim3 grid(a.n_kv_head, (a.T + 32 * QTB - 1) / (32 * QTB), G / HB);
-  if (a.out_bf16) hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, true>), grid, dim3(256), 0, s, a, HB);
-  else hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, false>), grid, dim3(256), 0, s, a, HB);
+  if (a.out_h) hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 2>), grid, dim3(256), 0, s, a, HB);
+  else if (a.out_bf16) hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 1>), grid, dim3(256), 0, s, a, HB);
+  else hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 0>), grid, dim3(256), 0, s, a, HB);
 }
 
 void attn_prefill(const AttnPrefillArgs& a, hipStream_t s) {
@@ -663,7 +669,7 @@ void attn_prefill(const AttnPrefillArgs& a, hipStream_t s) {
     else launch_attn_prefill_mfma<64>(a, G, s);
     return;
   }
-  if (!a.out) throw std::runtime_error("attn_prefill: the scalar path writes f32 only");
+  if (!a.out) throw std::runtime_error("attn_prefill: the scalar path writes f32 only (no bf16 / f16 output)");
   dim3 grid(a.n_head, (a.T + 15) / 16);
   if (a.head_dim == 128) hipLaunchKernelGGL(attn_prefill_kernel<128>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(attn_prefill_kernel<64>, grid, dim3(256), 0, s, a);

@@ -313,24 +313,31 @@ void t16_repack(const QMat& w, uint8_t* dst, hipStream_t st, bool swiglu) {
   }
 }
 
-// raw loads of lane l's chunk h (8s + 4h + kq) from a tile16 step block
-template <int T>
+// raw loads of lane l's chunk h (8s + 4h + kq) from a tile16 step block (NT: the quant
+// bytes non-temporal - decode reads every weight once; the prefill GEMM's token blocks
+// re-read them, so it loads them plainly)
+template <int T, bool NT = true>
+__device__ __forceinline__ int4 ld_q16(const uint8_t* p) {
+  if constexpr (NT) return ld_nt16(p);
+  else return *reinterpret_cast<const int4*>(p);
+}
+template <int T, bool NT = true>
 __device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, int l, int r16, int kq) {
   if constexpr (T == T_Q4_K) {
-    w.q = ld_nt16(blk + h * 1024 + l * 16);
+    w.q = ld_q16<T, NT>(blk + h * 1024 + l * 16);
     // chunk 4h + kq covers sub-blocks 2g, 2g + 1 with g = 2h + kq / 2
     w.m = *reinterpret_cast<const uint2*>(blk + 2048 + r16 * 32 + 8 * (2 * h + (kq >> 1)));
   } else if constexpr (T == T_Q5_K) {
-    w.q = ld_nt16(blk + h * 1024 + l * 16);
+    w.q = ld_q16<T, NT>(blk + h * 1024 + l * 16);
     w.h = *reinterpret_cast<const int4*>(blk + 2048 + r16 * 32 + 16 * (kq & 1));
     w.m = *reinterpret_cast<const uint2*>(blk + 2560 + r16 * 32 + 8 * (2 * h + (kq >> 1)));
   } else if constexpr (T == T_Q6_K) {
-    w.l = ld_nt16(blk + h * 1024 + l * 16);
+    w.l = ld_q16<T, NT>(blk + h * 1024 + l * 16);
     w.x = *reinterpret_cast<const uint2*>(blk + 2048 + h * 512 + l * 8);
     w.s = *reinterpret_cast<const unsigned*>(blk + 3072 + r16 * 32 + (4 * h + kq) * 4);
   } else {
-    w.a = ld_nt16(blk + h * 2048 + l * 16);
-    w.b = ld_nt16(blk + h * 2048 + 1024 + l * 16);
+    w.a = ld_q16<T, NT>(blk + h * 2048 + l * 16);
+    w.b = ld_q16<T, NT>(blk + h * 2048 + 1024 + l * 16);
     w.d = *reinterpret_cast<const unsigned short*>(blk + 4096 + h * 128 + l * 2);
   }
 }
@@ -1142,6 +1149,240 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
   else if (ta_ == T_Q4_K && tb_ == T_Q5_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q5_K>), grid, blk, lds, s, a, b);
   else return false;
   return true;
+}
+
+// ---------------------------------------------------------------- prefill GEMM on the tile16 copy
+// Y[T][N] = X[T][K] . W^T for prompt chunks, reading the same tile16 copy and the
+// same dequantisation as the batched decode - but where a decode wave's A fragments meet one
+// B column block (<= 16 rows), here they serve TM / 16 token groups: the per-weight VALU work
+// is spread over TM tokens and the kernel is paced by the matrix cores, not by issue.
+//
+// Block = 8 waves x 2 tiles (256 weight rows) x TM tokens; per 128-k half step h of 256-k step
+// s (the chunks 8s + 4h + kq cover k [256s + 128h, +128) for every type, see chunk_runs):
+//   X[t0 .. t0 + TM)[that k range] f16 staged in LDS (double buffered, the next half's global
+//   loads held in registers during this half's MFMAs), each wave's two tiles' raw weights one
+//   half ahead (ping-pong, fixed roles), dequantised once per half into A fragments; per token
+//   group g and run m ONE ds_read_b128 (the B operand, 16 tokens x 8 k) feeds the MFMAs of both
+//   tiles (LDS at half rate: 512 B per 16-cycle MFMA per SIMD).
+// Split-K (grid z) for the narrow projections: partial tiles meet by atomic add.
+// Epilogues: STORE (+ resid), ADD (residual in place), SWIGLU (the tile16 SwiGLU copy's tile =
+// 8 gate + 8 up rows of the same features: lane kq < 2 takes up from lane + 32 and writes
+// silu(g) * u as f16 in the 4-group k order - the next gemm_t16's X).
+static constexpr int kT16Pitch = 128 + 8;  // halves per staged token row (16-B pad: conflict-free b128 reads)
+
+template <int QT, int EPI, int TM, int NWV>
+__global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
+  constexpr int NG = TM / 16, NT = NWV * 64;
+  constexpr int XL = TM * 16 / NT;  // 16-B X pieces per thread per half step
+  constexpr int SB = t16_step_bytes(QT);
+  __shared__ __attribute__((aligned(16))) __half xs[2][TM * kT16Pitch];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, kq = lane >> 4;
+  const int K = a.w.K, steps = K >> 8;
+  const int ntiles = (a.w.rows + 15) >> 4;
+  const int tile0 = blockIdx.x * 2 * NWV + 2 * wave;  // this wave's tiles: tile0, tile0 + 1
+  const int t0 = blockIdx.y * TM;
+  const int spz = (steps + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int sb = blockIdx.z * spz, se = min(steps, sb + spz);
+  if (sb >= se) return;  // whole block, before any barrier
+  const int nh = 2 * (se - sb);
+  const uint8_t* wt0 = a.w.base + (size_t)min(tile0, ntiles - 1) * steps * SB;
+  const uint8_t* wt1 = a.w.base + (size_t)min(tile0 + 1, ntiles - 1) * steps * SB;
+  f4_t acc[2][NG];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[j][g] = f4_t{0.f, 0.f, 0.f, 0.f};
+  static_assert(XL == 2 || XL == 4, "X pieces per thread");
+  // X piece p = tid + NT j: token p / 16, 16-B column p % 16 of the 128-k slice (rows past T
+  // load row T - 1: finite values whose outputs are never stored). Named registers, not an
+  // array: the array was put in scratch.
+  uint4 x0, x1, x2, x3;
+  const __half* xrow[XL];
+#pragma unroll
+  for (int j = 0; j < XL; ++j) xrow[j] = a.x + (size_t)min(t0 + ((tid + NT * j) >> 4), a.T - 1) * K + 8 * (tid & 15);
+  auto load_x = [&](int i) __attribute__((always_inline)) {
+    const int k0 = (sb + (i >> 1)) * 256 + 128 * (i & 1);
+    x0 = *reinterpret_cast<const uint4*>(xrow[0] + k0);
+    x1 = *reinterpret_cast<const uint4*>(xrow[1] + k0);
+    if constexpr (XL == 4) {
+      x2 = *reinterpret_cast<const uint4*>(xrow[2] + k0);
+      x3 = *reinterpret_cast<const uint4*>(xrow[3] + k0);
+    }
+  };
+  auto store_x = [&](int buf) __attribute__((always_inline)) {
+    __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * (tid & 15)];
+    constexpr int J = (NT / 16) * kT16Pitch;  // piece j + 1 is NT / 16 tokens further
+    *reinterpret_cast<uint4*>(d) = x0;
+    *reinterpret_cast<uint4*>(d + J) = x1;
+    if constexpr (XL == 4) {
+      *reinterpret_cast<uint4*>(d + 2 * J) = x2;
+      *reinterpret_cast<uint4*>(d + 3 * J) = x3;
+    }
+  };
+  auto load_w = [&](int i, BRawT<QT>& w0, BRawT<QT>& w1) __attribute__((always_inline)) {
+    const int s = sb + (i >> 1), h = i & 1;
+    tload<QT, false>(w0, wt0 + (size_t)s * SB, h, lane, r16, kq);
+    tload<QT, false>(w1, wt1 + (size_t)s * SB, h, lane, r16, kq);
+  };
+  auto half = [&](int i, const BRawT<QT>& w0, const BRawT<QT>& w1) __attribute__((always_inline)) {
+    const int s = sb + (i >> 1), h = i & 1;
+    const int c = 8 * s + 4 * h + kq;
+    int off_lo, off_hi;
+    chunk_runs<QT>(c, off_lo, off_hi);
+    off_lo -= 256 * s + 128 * h;
+    off_hi -= 256 * s + 128 * h;
+    HFrag F0, F1;
+    dequant_frags<QT>(w0, c, F0);
+    dequant_frags<QT>(w1, c, F1);
+    const __half* xb = &xs[i & 1][r16 * kT16Pitch];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const uint4 bv = *reinterpret_cast<const uint4*>(xb + g * 16 * kT16Pitch + (m < 2 ? off_lo : off_hi) + 8 * (m & 1));
+        const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
+        const uint4 a0 = make_uint4(F0.w[4 * dw + sh], F0.w[4 * dw + sh + 1], F0.w[4 * dw + 4 + sh], F0.w[4 * dw + 5 + sh]);
+        const uint4 a1 = make_uint4(F1.w[4 * dw + sh], F1.w[4 * dw + sh + 1], F1.w[4 * dw + 4 + sh], F1.w[4 * dw + 5 + sh]);
+        acc[0][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, a0), __builtin_bit_cast(h8_t, bv), acc[0][g], 0, 0, 0);
+        acc[1][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, a1), __builtin_bit_cast(h8_t, bv), acc[1][g], 0, 0, 0);
+      }
+    }
+  };
+  BRawT<QT> wa0, wa1, wb0, wb1;  // ping-pong weight buffers with fixed roles (no rotating copy)
+  load_x(0);
+  load_w(0, wa0, wa1);
+  store_x(0);
+  lds_barrier(false);
+  // nh is even (whole 256-k steps). The loads past the last half are clamped repeats and the
+  // last stores go to the buffer nobody reads any more: no conditional around a load (a
+  // load under a branch drains vmcnt at the join, and the conditional X slice went to scratch)
+  for (int i = 0; i < nh; i += 2) {
+    // even half: compute from A, load B (and the next X slice)
+    load_w(i + 1, wb0, wb1);
+    load_x(i + 1);
+    half(i, wa0, wa1);
+    store_x((i + 1) & 1);
+    lds_barrier(false);
+    // odd half: compute from B, load A
+    load_w(min(i + 2, nh - 1), wa0, wa1);
+    load_x(min(i + 2, nh - 1));
+    half(i + 1, wb0, wb1);
+    store_x(i & 1);
+    lds_barrier(false);
+  }
+  // ---- epilogue: acc[j][g][e] = (weight row 16 tile + 4 kq + e, token t0 + 16 g + r16)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int tile = tile0 + j;
+    if (tile >= ntiles) continue;  // wave-uniform
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int t = t0 + 16 * g + r16;
+      const f4_t v = acc[j][g];
+      if constexpr (EPI == GEMM_SWIGLU) {
+        f4_t u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u[e] = __shfl_xor(v[e], 32);
+        const int f = 8 * tile + 4 * kq;
+        if (kq < 2 && t < a.T && f < (a.w.rows >> 1)) {
+          float hv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hv[e] = v[e] / (1.f + __expf(-v[e])) * u[e];
+          const __half2 p0 = __floats2half2_rn(hv[0], hv[2]), p1 = __floats2half2_rn(hv[1], hv[3]);
+          *reinterpret_cast<uint2*>(a.out_h + (size_t)t * a.ldh + f) =
+              make_uint2(__builtin_bit_cast(unsigned, p0), __builtin_bit_cast(unsigned, p1));
+        }
+      } else {
+        const int n = 16 * tile + 4 * kq;
+        if (t < a.T && n < a.w.rows) {
+          float* o = a.out + (size_t)t * a.ldo + n;
+          if (gridDim.z > 1) {  // split-K partials (STORE outputs pre-zeroed, resid added once)
+            f4_t w = v;
+            if (EPI == GEMM_STORE && a.resid && blockIdx.z == 0) {
+              const float4 r = *reinterpret_cast<const float4*>(a.resid + (size_t)t * a.ldo + n);
+              w += f4_t{r.x, r.y, r.z, r.w};
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) atomicAdd(o + e, w[e]);
+          } else {
+            float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (EPI == GEMM_ADD) r = *reinterpret_cast<const float4*>(o);
+            else if (a.resid) r = *reinterpret_cast<const float4*>(a.resid + (size_t)t * a.ldo + n);
+            *reinterpret_cast<float4*>(o) = make_float4(r.x + v[0], r.y + v[1], r.z + v[2], r.w + v[3]);
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int QT, int EPI>
+static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
+  // block shape (waves x 32 rows, TM tokens): the widest one whose grid covers the CUs without
+  // split-K (8 x 128: twice the fragment reuse of 64-token blocks; 4 x 64 for the 4096-row
+  // projections of a few hundred tokens), else the one with the most blocks, split over K
+  // (partials by atomic add) until the grid covers the CUs with >= 2 steps (512 k) per part.
+  // LFK_T16_CFG="waves,tokens" pins one (tuning).
+  static const char* cfg_env = getenv("LFK_T16_CFG");
+  const int ntiles = (a.w.rows + 15) / 16, steps = a.w.K / 256, cus = bmm_cus();
+  static const int shapes[3][2] = {{8, 128}, {8, 64}, {4, 64}};
+  int nw = 4, tm = 64;
+  int pin_nw = 0, pin_tm = 0;
+  if (cfg_env && sscanf(cfg_env, "%d,%d", &pin_nw, &pin_tm) == 2 &&
+      ((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && pin_tm == 64))) {
+    nw = pin_nw;
+    tm = pin_tm;
+  } else {
+    for (const auto& sh : shapes) {
+      const long blocks = (long)((ntiles + 2 * sh[0] - 1) / (2 * sh[0])) * ((a.T + sh[1] - 1) / sh[1]);
+      nw = sh[0];
+      tm = sh[1];
+      if (blocks >= cus) break;
+    }
+  }
+  const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm;
+  int split = 1;
+  if (EPI != GEMM_SWIGLU)
+    while (gx * gy * split < cus && steps / (split * 2) >= 2) split *= 2;
+  const int spz = (steps + split - 1) / split;
+  split = (steps + spz - 1) / spz;  // no empty parts
+  if (split > 1 && EPI == GEMM_STORE && !a.out_zeroed) {
+    const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
+    if (e != hipSuccess) throw std::runtime_error("gemm_t16: memset failed");
+  }
+  const dim3 grid(gx, gy, split);
+  if (nw == 8 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 8>), grid, dim3(512), 0, s, a);
+  else if (nw == 8) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 8>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 4>), grid, dim3(256), 0, s, a);
+}
+
+template <int QT>
+static void gemm_t16_epi(const GemmT16Args& a, int epi, hipStream_t s) {
+  switch (epi) {
+    case GEMM_STORE: launch_gemm_t16<QT, GEMM_STORE>(a, s); break;
+    case GEMM_ADD: launch_gemm_t16<QT, GEMM_ADD>(a, s); break;
+    case GEMM_SWIGLU: launch_gemm_t16<QT, GEMM_SWIGLU>(a, s); break;
+    default: throw std::runtime_error("gemm_t16: bad epilogue");
+  }
+}
+
+void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s) {
+  if (a.T <= 0) return;
+  if (!bmm_supported(a.w.type, a.w.K) || !a.w.base || !a.x) throw std::runtime_error("gemm_t16: unsupported type / K");
+  if (a.w.rows % 16) throw std::runtime_error("gemm_t16: rows must be a multiple of 16");
+  if (epi == GEMM_SWIGLU) {
+    if (!a.out_h || a.ldh % 4 || a.ldh < a.w.rows / 2) throw std::runtime_error("gemm_t16: SwiGLU output");
+  } else if (!a.out || a.ldo % 4 || a.ldo < a.w.rows || (a.resid && epi != GEMM_STORE)) {
+    throw std::runtime_error("gemm_t16: output");
+  }
+  if (reinterpret_cast<uintptr_t>(a.x) % 16) throw std::runtime_error("gemm_t16: X must be 16-byte aligned");
+  switch (a.w.type) {
+    case T_Q4_K: gemm_t16_epi<T_Q4_K>(a, epi, s); break;
+    case T_Q5_K: gemm_t16_epi<T_Q5_K>(a, epi, s); break;
+    case T_Q6_K: gemm_t16_epi<T_Q6_K>(a, epi, s); break;
+    default: gemm_t16_epi<T_Q8_0>(a, epi, s); break;
+  }
 }
 
 }  // namespace lfk

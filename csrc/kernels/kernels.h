@@ -269,6 +269,7 @@ struct AttnPrefillArgs {
   float scale = 1.f;
   float* out = nullptr;           // [T][n_head][hd] f32, or
   __hip_bfloat16* out_bf16 = nullptr;  // bf16 (the Wo GEMM's input; MFMA path only)
+  __half* out_h = nullptr;        // or f16 in bmm's 4-group k order (gemm_t16's input; MFMA path)
   int out_stride = 0;
 };
 void attn_prefill(const AttnPrefillArgs& a, hipStream_t s);
@@ -292,6 +293,23 @@ struct GemmArgs {
 };
 void gemm_dq(const GemmArgs& a, int epi, hipStream_t s);
 
+// Prefill GEMM on the tile16 weight copy (bmm.hip): Y[T][N] = X[T][K] . W^T with X f16 in bmm's
+// 4-group k order (rmsnorm_bf16(..., f16sw), attention prefill out_h, this kernel's SwiGLU
+// epilogue) and W dequantised with bmm's f16 arithmetic into v_mfma_f32_16x16x32_f16 A
+// fragments that serve 128 tokens each (the planar gemm_dq decodes to bf16 per 64-k step).
+struct GemmT16Args {
+  QMat w;                          // base = tile16 copy (the SwiGLU form for GEMM_SWIGLU)
+  const __half* x = nullptr;       // [T][K] f16, bmm k order (row stride K)
+  int T = 0;
+  float* out = nullptr;            // f32 [T][ldo] (STORE / ADD)
+  int ldo = 0;
+  const float* resid = nullptr;    // STORE: out = acc + resid[t][n] (TP rank 0)
+  bool out_zeroed = false;         // STORE: `out` already zeroed (no memset before split-K)
+  __half* out_h = nullptr;         // SWIGLU: silu(gate) * up as f16 [T][ldh], bmm k order
+  int ldh = 0;
+};
+void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s);
+
 // ---------------------------------------------------------------- MoE prefill (grouped experts)
 // Device-side routing: per-expert row lists in ascending token order (moe.hip).
 void moe_route_group(const float* logits, int T, int n_expert, int k, int* sel, float* selw, int* cnt_off, int* tok,
@@ -305,8 +323,9 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s);
 // y_bf16[t] = rmsnorm(x[t]) * w
 // zero (optional): also zero rows [T][zero_ld] f32 (the next split-K GEMM's output)
+// f16sw: write y as f16 in bmm's 4-group k order instead (gemm_t16's input; same 2-byte rows)
 void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s,
-                  float* zero = nullptr, int zero_ld = 0);
+                  float* zero = nullptr, int zero_ld = 0, bool f16sw = false);
 // f32 activation [T][d] -> bf16 (for the next GEMM)
 void to_bf16(const float* x, int n, __hip_bfloat16* y, hipStream_t s);
 // prefill: rope q/k of QKV rows, write q (f32) and k/v to the caches at pos0+t.

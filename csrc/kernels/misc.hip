@@ -33,6 +33,7 @@ void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t
   hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(128), 0, s, emb, tokens, T, x);
 }
 
+template <bool F16SW>
 __global__ __launch_bounds__(256) void rmsnorm_bf16_kernel(const float* x, const float* w, float eps, int d,
                                                           __hip_bfloat16* y, float* zero, int zero_ld) {
   const int t = blockIdx.x, tid = threadIdx.x;
@@ -54,17 +55,25 @@ __global__ __launch_bounds__(256) void rmsnorm_bf16_kernel(const float* x, const
   for (int i = tid * 4; i < d; i += 1024) {
     float4 v = *reinterpret_cast<const float4*>(xr + i);
     float4 g = *reinterpret_cast<const float4*>(w + i);
-    *reinterpret_cast<uint2*>(y + (size_t)t * d + i) =
-        make_uint2(pk_bf16_pair(v.x * sc * g.x, v.y * sc * g.y), pk_bf16_pair(v.z * sc * g.z, v.w * sc * g.w));
+    if constexpr (F16SW) {  // 4-group order (0, 2, 1, 3): the pairs (0, 2) and (1, 3)
+      const __half2 p0 = __floats2half2_rn(v.x * sc * g.x, v.z * sc * g.z);
+      const __half2 p1 = __floats2half2_rn(v.y * sc * g.y, v.w * sc * g.w);
+      *reinterpret_cast<uint2*>(y + (size_t)t * d + i) =
+          make_uint2(__builtin_bit_cast(unsigned, p0), __builtin_bit_cast(unsigned, p1));
+    } else {
+      *reinterpret_cast<uint2*>(y + (size_t)t * d + i) =
+          make_uint2(pk_bf16_pair(v.x * sc * g.x, v.y * sc * g.y), pk_bf16_pair(v.z * sc * g.z, v.w * sc * g.w));
+    }
   }
 }
 
 void rmsnorm_bf16(const float* x, const float* w, float eps, int T, int d, __hip_bfloat16* y, hipStream_t s,
-                  float* zero, int zero_ld) {
+                  float* zero, int zero_ld, bool f16sw) {
   if (T <= 0) return;
   if (zero && (zero_ld % 4 || reinterpret_cast<uintptr_t>(zero) % 16))
     throw std::runtime_error("rmsnorm_bf16: zeroed rows must be float4 aligned");
-  hipLaunchKernelGGL(rmsnorm_bf16_kernel, dim3(T), dim3(256), 0, s, x, w, eps, d, y, zero, zero_ld);
+  if (f16sw) hipLaunchKernelGGL(rmsnorm_bf16_kernel<true>, dim3(T), dim3(256), 0, s, x, w, eps, d, y, zero, zero_ld);
+  else hipLaunchKernelGGL(rmsnorm_bf16_kernel<false>, dim3(T), dim3(256), 0, s, x, w, eps, d, y, zero, zero_ld);
 }
 
 __global__ void to_bf16_kernel(const float* x, int n, __hip_bfloat16* y) {

@@ -436,6 +436,15 @@ void Engine::setup_batch_mfma() {
     }
   }
   HIPCHK(hipStreamSynchronize(stream_));
+  // dense models: prompt chunks on the same tile16 copies (gemm_t16: the dequantisation spread
+  // over 128 tokens per fragment, f16 activations - measured against gemm_dq in profiles/)
+  const char* pt = std::getenv("LFK_PREFILL_T16");
+  bool t16 = bg_ffn_ && !moe_b_ && !(pt && pt[0] == '0');
+  for (int l = 0; t16 && l < hp_.n_layer; ++l) {
+    const Layer& L = layers_[l];
+    for (const QMat* m : {&L.t_wq, &L.t_wk, &L.t_wv, &L.t_wo, &L.t_gu, &L.t_down}) t16 = t16 && m->base && m->rows % 16 == 0;
+  }
+  prefill_t16_ = t16;
 }
 
 void Engine::check_device_err() {
@@ -678,12 +687,24 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
   const int ncol = nq_ + 2 * nkvd_;
   {
     const Layer& L = layers_[l];
-    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, qkv_, ncol);  // + zero the q|k|v rows
-    GemmArgs g;
-    g.x = xb_; g.T = T; g.ldo = ncol; g.out_zeroed = true;
-    g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
-    g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
-    g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
+    // prompt chunks on the tile16 copies: f16 activations in bmm's k order (same 2-byte buffers)
+    const bool t16 = prefill_t16_ && !batched;
+    __half* const xh16 = reinterpret_cast<__half*>(xb_);
+    __half* const attnh16 = reinterpret_cast<__half*>(attnb_);
+    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, qkv_, ncol, t16);  // + zero the q|k|v rows
+    if (t16) {
+      GemmT16Args g;
+      g.x = xh16; g.T = T; g.ldo = ncol; g.out_zeroed = true;
+      g.w = L.t_wq; g.out = qkv_; gemm_t16(g, GEMM_STORE, s);
+      g.w = L.t_wk; g.out = qkv_ + nq_; gemm_t16(g, GEMM_STORE, s);
+      g.w = L.t_wv; g.out = qkv_ + nq_ + nkvd_; gemm_t16(g, GEMM_STORE, s);
+    } else {
+      GemmArgs g;
+      g.x = xb_; g.T = T; g.ldo = ncol; g.out_zeroed = true;
+      g.w = L.wq; g.out = qkv_; gemm_dq(g, GEMM_STORE, s);
+      g.w = L.wk; g.out = qkv_ + nq_; gemm_dq(g, GEMM_STORE, s);
+      g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
+    }
     if (!batched && segs_) {  // packed prompts: per-row slot / position, attention per piece
       __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; + slot * slot_stride_
       __half* vcl = vc_ + kv_layer * l;
@@ -694,7 +715,9 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
         pa.k_cache = kcl + slot_stride_ * g.slot; pa.v_cache = vcl + slot_stride_ * g.slot;
         pa.T = g.n; pa.pos0 = g.pos; pa.n_ctx = opt_.n_ctx;
         pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
-        pa.out_bf16 = attnb_ + (size_t)g.row * nq_; pa.out_stride = nq_;
+        if (t16) pa.out_h = attnh16 + (size_t)g.row * nq_;
+        else pa.out_bf16 = attnb_ + (size_t)g.row * nq_;
+        pa.out_stride = nq_;
         attn_prefill(pa, s);
       }
     } else if (!batched) {
@@ -704,7 +727,9 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       AttnPrefillArgs pa;
       pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
       pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
-      pa.out_bf16 = attnb_; pa.out_stride = nq_;  // bf16 straight into the Wo GEMM's input
+      if (t16) pa.out_h = attnh16;  // straight into the Wo GEMM's input (f16 / bf16)
+      else pa.out_bf16 = attnb_;
+      pa.out_stride = nq_;
       attn_prefill(pa, s);
     } else {  // T decode rows, each of its own KV slot and position
       __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
@@ -721,28 +746,61 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       attn_decode(aa, s);
       to_bf16(attn_, T * nq_, attnb_, s);
     }
-    GemmArgs o;
-    o.w = L.wo; o.x = attnb_; o.T = T; o.ldo = d;
-    if (!tp) {
-      o.out = x_;
-      gemm_dq(o, GEMM_ADD, s);
+    if (t16) {
+      GemmT16Args o;
+      o.w = L.t_wo; o.x = attnh16; o.T = T; o.ldo = d;
+      if (!tp) {
+        o.out = x_;
+        gemm_t16(o, GEMM_ADD, s);
+      } else {
+        o.out = tmp_;
+        o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+        gemm_t16(o, GEMM_STORE, s);
+        allreduce_into(tmp_, x_, (size_t)T * d, s);
+      }
     } else {
-      o.out = tmp_;
-      o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
-      gemm_dq(o, GEMM_STORE, s);
-      allreduce_into(tmp_, x_, (size_t)T * d, s);
+      GemmArgs o;
+      o.w = L.wo; o.x = attnb_; o.T = T; o.ldo = d;
+      if (!tp) {
+        o.out = x_;
+        gemm_dq(o, GEMM_ADD, s);
+      } else {
+        o.out = tmp_;
+        o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+        gemm_dq(o, GEMM_STORE, s);
+        allreduce_into(tmp_, x_, (size_t)T * d, s);
+      }
     }
   }
-  enqueue_rows_ffn(l, T, s);
+  enqueue_rows_ffn(l, T, s, prefill_t16_ && !batched);
 }
 
 // The FFN half of a layer over T rows (prompt chunk or batched decode rows): RMSNorm ->
 // gate/up (or MoE routing + grouped experts) -> down, residual into x_.
-void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s) {
+void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd;
   const bool tp = opt_.tp_size > 1;
-  rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s);
+  t16 = t16 && hp_.n_expert == 0;
+  rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s, nullptr, 0, t16);
+  if (t16) {
+    GemmT16Args gu;
+    gu.w = L.t_gu; gu.x = reinterpret_cast<const __half*>(xb_); gu.T = T;
+    gu.out_h = reinterpret_cast<__half*>(h_); gu.ldh = F_l_;
+    gemm_t16(gu, GEMM_SWIGLU, s);
+    GemmT16Args dn;
+    dn.w = L.t_down; dn.x = reinterpret_cast<const __half*>(h_); dn.T = T; dn.ldo = d;
+    if (!tp) {
+      dn.out = x_;
+      gemm_t16(dn, GEMM_ADD, s);
+    } else {
+      dn.out = tmp_;
+      dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;
+      gemm_t16(dn, GEMM_STORE, s);
+      allreduce_into(tmp_, x_, (size_t)T * d, s);
+    }
+    return;
+  }
   if (hp_.n_expert > 0) {
     const int E = hp_.n_expert;
     GemmArgs ra;

@@ -121,6 +121,8 @@ class Engine : public SlotBackend {
   int max_batch() const override { return bmax_; }
   // 0: batch_step on the prefill GEMM; 1: attention/head on the batched GEMV; 2: every projection
   int batch_gemv() const { return bg_ffn_ ? 2 : bg_ ? 1 : 0; }
+  // prompt chunks run on the tile16 copies (gemm_t16, f16 activations) instead of gemm_dq
+  bool prefill_t16() const { return prefill_t16_; }
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
   int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
@@ -205,7 +207,7 @@ class Engine : public SlotBackend {
   // one layer over T activation rows: a prompt chunk at positions pos0.. of KV slot kv_slot_
   // (batched == false) or T decode rows of slots bslots_ at positions bpos_ (batched == true)
   void enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s);
-  void enqueue_rows_ffn(int l, int T, hipStream_t s);
+  void enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16 = false);
   void enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int slot = 0);
   // batch_step on the MFMA batched projections (bmm.hip): one layer over the B decode rows
   void enqueue_batch_layer(int l, int B, hipStream_t s);
@@ -309,6 +311,7 @@ class Engine : public SlotBackend {
   // step for all rows) instead of the prefill GEMM: attention/head (bg_) and the dense FFN
   // (bg_ffn_); LFK_BATCH_MFMA=0 keeps the GEMM path (A/B)
   bool bg_ = false, bg_ffn_ = false;
+  bool prefill_t16_ = false;  // LFK_PREFILL_T16=0: the planar bf16 gemm_dq (A/B)
   // MoE FFN on the batched projections: the experts as one stacked SwiGLU matrix and one
   // K-concatenated down matrix (t_gu / t_down of each layer), routed by dense per-row expert
   // weights ew_b_ [bmax][E] (bmm.hip, BmmArgs::ew); LFK_BATCH_MOE=0 keeps the grouped GEMM

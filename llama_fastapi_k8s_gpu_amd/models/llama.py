@@ -84,6 +84,9 @@ class ReferenceLlama:
       * ``"prefill"`` (MFMA GEMM, kernels/gemm.hip + attention.hip): bf16 activations and
         bf16-rounded dequantised weights; attention with q * scale * log2(e) in f16, f16 P and
         K/V, bf16 output; the logits row through the decode head (q8);
+      * ``"prefill16"`` (the tile16 prefill GEMM, gemm_t16 in kernels/bmm.hip, dense models with
+        batching on): f16(x / rms * w) inputs, f16 attention and SwiGLU outputs, the tile16 copy's
+        f16-arithmetic weights; attention and head as ``"prefill"``;
       * ``"batch"`` (batched MFMA projections, kernels/bmm.hip): f16(x * w_norm) with the
         1/rms applied to the f32 result (d = 4096, the folded norm; f16(x / rms * w) below), f16 weights from the tile16 copy's f16 arithmetic
         (quants.dequantize(arith="f16")), f16 attention output and SwiGLU output; the head
@@ -174,6 +177,8 @@ class ReferenceLlama:
             return self._q8(x * w) * rs
         if path == "prefill":
             return self._bf16(x * rs * w)
+        if path == "prefill16":
+            return self._f16(x * rs * w)
         if path == "batch":
             # d = 4096 (B <= 8): the norm folded into the projection's x staging applies 1/rms
             # to the f32 result; otherwise bmm's prep kernel stages f16(x / rms * w)
@@ -186,12 +191,12 @@ class ReferenceLlama:
             return self._q8(h)
         if path == "prefill":
             return self._bf16(h)
-        if path == "batch":
+        if path in ("batch", "prefill16"):
             return self._f16(h)
         return h
 
     def _wkind(self, path):
-        return {"prefill": "bf16", "batch": "f16"}.get(path, "f32")
+        return {"prefill": "bf16", "batch": "f16", "prefill16": "f16"}.get(path, "f32")
 
     def _rope(self, x, pos):
         # x [T, H, D]; adjacent pairs (2i, 2i+1)
@@ -252,7 +257,7 @@ class ReferenceLlama:
         K = self.k_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)   # [Lk, H, D]
         V = self.v_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)
         mask = torch.arange(Lk)[None, :] > pos[:, None]
-        if path == "prefill":
+        if path in ("prefill", "prefill16"):
             l2e = 1.4426950408889634
             s = torch.einsum("thd,lhd->htl", self._f16(q * (scale * l2e)), K)
             s = s.masked_fill(mask[None], float("-inf"))
@@ -275,7 +280,7 @@ class ReferenceLlama:
         ``path``: None (exact fp32) or the engine path whose rounding to reproduce (class doc)."""
         torch = self.torch
         hp = self.hp
-        if path not in (None, "decode", "prefill", "batch"):
+        if path not in (None, "decode", "prefill", "prefill16", "batch"):
             raise ValueError(f"unknown path {path!r}")
         T = len(tokens)
         pos = torch.arange(n_past, n_past + T)
@@ -305,7 +310,7 @@ class ReferenceLlama:
                 trace[-1]["x_ffn"] = x[-1].clone()
         # the logits: prefill and decode both end on the GEMV head (q8); the batched head
         # stages f16(x / rms * w) for the tile16 f16 output weights
-        hpath = {"prefill": "decode"}.get(path, path)
+        hpath = {"prefill": "decode", "prefill16": "decode"}.get(path, path)
         if hpath == "batch":
             rs = torch.rsqrt((x * x).mean(-1, keepdim=True) + hp.rms_eps)
             xo = self._f16(x * rs * self.out_norm)

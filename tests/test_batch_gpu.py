@@ -44,7 +44,7 @@ def test_batch_step_rows_match_reference(models, spec):
     def emulated(s):
         """The slot's history as the engine computed it: the prompt on the prefill path, each
         fed token on the path of the step that fed it (batched rows; one row = the GEMV decode)."""
-        out = emu.forward(seqs[s][:plen[s]], 0, path="prefill")
+        out = emu.forward(seqs[s][:plen[s]], 0, path="prefill16" if eng.prefill_t16 else "prefill")
         for i, p in enumerate(paths[s]):
             out = emu.forward([seqs[s][plen[s] + i]], plen[s] + i, path=p)
         return out.numpy()
@@ -98,7 +98,7 @@ def test_batch_step_d4096_fused_paths(tmp_path):
         for b, s in enumerate(rows):
             want = ref.forward(seqs[s], 0).numpy()
             assert rel_err(logits[b], want) < 5e-2, (s, rel_err(logits[b], want))
-            out = emu.forward(seqs[s][:plen[s]], 0, path="prefill")
+            out = emu.forward(seqs[s][:plen[s]], 0, path="prefill16" if eng.prefill_t16 else "prefill")
             for i in range(plen[s], len(seqs[s])):
                 out = emu.forward([seqs[s][i]], i, path="batch")
             e = rel_err(logits[b], out.numpy())

@@ -83,6 +83,11 @@ def test_one_layer_paths_match_emulation(tmp_path, spec):
                                            emu.forward([toks[i]], i, path="decode").numpy())))
     # batched rows (two slots at different lengths); B = 2 takes the batched projections
     beng = load_hip().Engine(path, n_ctx=128, n_batch=64, device=0, use_graph=True, n_slots=3)
+    ppath = "prefill16" if beng.prefill_t16 else "prefill"
+    if spec == "tiny-llama3-1l":   # dense models with batching prefill on the tile16 copies
+        assert beng.prefill_t16, spec
+    errs.append((ppath, rel_err(beng.eval_logits(toks[:20], 0),
+                                ReferenceLlama(GGUFReader(path), n_ctx=128).forward(toks[:20], 0, path=ppath).numpy())))
     greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
     seqs = {0: toks[:9], 2: toks[:14]}
     for s in seqs:
@@ -93,7 +98,7 @@ def test_one_layer_paths_match_emulation(tmp_path, spec):
         for b, s in enumerate((0, 2)):
             n = len(seqs[s])
             em = ReferenceLlama(GGUFReader(path), n_ctx=128)
-            em.forward(seqs[s][:n - 1 - step], 0, path="prefill")
+            em.forward(seqs[s][:n - 1 - step], 0, path=ppath)
             for i in range(n - 1 - step, n - 1):
                 em.forward([seqs[s][i]], i, path="batch")
             errs.append((f"batch{step}.{s}", rel_err(lg[b], em.forward([seqs[s][n - 1]], n - 1, path="batch").numpy())))

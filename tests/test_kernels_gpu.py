@@ -232,6 +232,13 @@ def test_attn_prefill(torch, hd, T, pos0, H, Hkv):
                            ob.data_ptr(), stream(), True)
         torch.cuda.synchronize()
         assert rel_err(ob.float().cpu().numpy(), ref) < 8e-3
+        # f16 in bmm's 4-group k order (the tile16 prefill GEMM's input)
+        oh = torch.zeros(T, H * hd, device="cuda", dtype=torch.float16)
+        hip().attn_prefill(dq.data_ptr(), dK.data_ptr(), dV.data_ptr(), T, pos0, n_ctx, H, Hkv, hd, scale,
+                           oh.data_ptr(), stream(), out_h=True)
+        torch.cuda.synchronize()
+        got = _swizzle4(oh.float().cpu().numpy()).reshape(T, H, hd)
+        assert rel_err(got, ref) < 3e-3
 
 
 @pytest.mark.parametrize("t", QTYPES)
@@ -622,3 +629,75 @@ def test_bprep_norm_swiglu_zero(torch):
         u = GU.reshape(B, -1, 2, G)[:, :, 1, :].reshape(B, K)
         h = (g / (1 + np.exp(-g)) * u).astype(np.float16)
         assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(h).astype(np.float32)) < 2e-3, G
+
+
+@pytest.mark.parametrize("t", BM_TYPES)
+@pytest.mark.parametrize("T,R,K", [(17, 256, 512), (100, 4096, 1024), (300, 272, 4096), (130, 1024, 14336)])
+def test_gemm_t16_vs_fp32(torch, t, T, R, K):
+    """Prefill GEMM on the tile16 copy: Y = X W^T with X f16 in the 4-group k order and W the
+    tile16 dequantisation (f16 arithmetic), against the fp64 product of the same f16 X and the
+    exact weights; STORE (split-K on the narrow shapes), STORE + resid, and ADD."""
+    rng = np.random.default_rng(T + R + K + int(t))
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+    Xh = rng.standard_normal((T, K)).astype(np.float16)
+    dx = torch.from_numpy(_swizzle4(Xh)).cuda()
+    ref = Xh.astype(np.float64) @ W.astype(np.float64).T
+    ldo = R + 4
+    out = torch.full((T, ldo), 3.0, device="cuda")
+    hip().gemm_t16(tw.data_ptr(), int(t), R, K, dx.data_ptr(), T, out.data_ptr(), ldo, 0, 0, 0, stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert rel_err(got[:, :R], ref) < 2e-3, rel_err(got[:, :R], ref)
+    assert np.all(got[:, R:] == 3.0)
+    res = torch.randn(T, ldo, device="cuda")
+    hip().gemm_t16(tw.data_ptr(), int(t), R, K, dx.data_ptr(), T, out.data_ptr(), ldo, 0, 0, 0, stream(),
+                   resid=res.data_ptr())
+    torch.cuda.synchronize()
+    assert rel_err(out.cpu().numpy()[:, :R] - res.cpu().numpy()[:, :R], ref) < 2e-3
+    base = torch.randn(T, ldo, device="cuda")
+    acc = base.clone()
+    hip().gemm_t16(tw.data_ptr(), int(t), R, K, dx.data_ptr(), T, acc.data_ptr(), ldo, 0, 0, 1, stream())
+    torch.cuda.synchronize()
+    assert rel_err((acc - base).cpu().numpy()[:, :R], ref) < 2e-3
+    assert torch.equal(acc[:, R:], base[:, R:])
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("T,F,K", [(40, 96, 2048), (200, 256, 4096), (129, 1792, 1024)])
+def test_gemm_t16_swiglu_vs_fp32(torch, t, T, F, K):
+    """Prefill gate/up on the SwiGLU tile16 copy: silu(gate) * up as f16 in the 4-group k order."""
+    rng = np.random.default_rng(T * 3 + F + int(t))
+    R = 2 * F
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream(), swiglu=True)
+    Xh = rng.standard_normal((T, K)).astype(np.float16)
+    dx = torch.from_numpy(_swizzle4(Xh)).cuda()
+    ldh = F + 8
+    h = torch.full((T, ldh), 7.0, dtype=torch.float16, device="cuda")
+    hip().gemm_t16(tw.data_ptr(), int(t), R, K, dx.data_ptr(), T, 0, 0, h.data_ptr(), ldh, 2, stream())
+    torch.cuda.synchronize()
+    pre = Xh.astype(np.float64) @ W.astype(np.float64).T
+    g = pre.reshape(T, F // 32, 2, 32)[:, :, 0].reshape(T, F)
+    u = pre.reshape(T, F // 32, 2, 32)[:, :, 1].reshape(T, F)
+    ref = g / (1.0 + np.exp(-g)) * u
+    got = h.cpu().numpy().astype(np.float64)
+    assert rel_err(_swizzle4(got[:, :F]), ref) < 3e-3, rel_err(_swizzle4(got[:, :F]), ref)
+    assert np.all(got[:, F:] == 7.0)
+
+
+def test_rmsnorm_f16_swizzled(torch):
+    rng = np.random.default_rng(5)
+    T, d = 7, 4096
+    x = torch.from_numpy((rng.standard_normal((T, d)) * 2).astype(np.float32)).cuda()
+    w = torch.from_numpy((0.5 + rng.random(d)).astype(np.float32)).cuda()
+    y = torch.zeros(T, d, dtype=torch.float16, device="cuda")
+    hip().rmsnorm_bf16(x.data_ptr(), w.data_ptr(), 1e-5, T, d, y.data_ptr(), stream(), f16sw=True)
+    torch.cuda.synchronize()
+    xf = x.cpu().double()
+    ref = (xf / torch.sqrt((xf * xf).mean(1, keepdim=True) + 1e-5) * w.cpu().double()).numpy()
+    assert rel_err(_swizzle4(y.float().cpu().numpy()), ref) < 1e-3

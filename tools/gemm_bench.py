@@ -23,12 +23,13 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--eager", action="store_true")
+    ap.add_argument("--t16", action="store_true", help="the tile16 prefill GEMM (gemm_t16, f16 X)")
     args = ap.parse_args()
     from llama_fastapi_k8s_gpu_amd.runtime import load_hip
     hip = load_hip()
     s = torch.cuda.current_stream().cuda_stream
     d, F, T = 4096, 14336, args.T
-    res = {"T": T}
+    res = {"T": T, "kernel": "gemm_t16" if args.t16 else "gemm_dq"}
     for name, t, R, K, epi in [
         ("gateup_q4k_swiglu", Q4_K, 2 * F, d, SWIGLU),
         ("down_q4k_add", Q4_K, d, F, ADD),
@@ -40,12 +41,18 @@ def main():
             continue
         w = torch.empty(hip.qbytes(t, R, K), dtype=torch.uint8, device="cuda")
         hip.fill_random(w.data_ptr(), t, R, K, 0.02, 7, s)
-        x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
+        x = torch.randn(T, K, device="cuda").to(torch.float16 if args.t16 else torch.bfloat16)
         out = torch.zeros(T, R, device="cuda")
         ob = torch.zeros(T, R // 2, device="cuda", dtype=torch.bfloat16)
+        if args.t16:
+            tw = torch.empty(hip.t16_bytes(t, R, K), dtype=torch.uint8, device="cuda")
+            hip.t16_repack(w.data_ptr(), t, R, K, tw.data_ptr(), s, epi == SWIGLU)
 
         def fn():
-            hip.gemm(w.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), ob.data_ptr(), R, epi, s)
+            if args.t16:
+                hip.gemm_t16(tw.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), R, ob.data_ptr(), R // 2, epi, s)
+            else:
+                hip.gemm(w.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), ob.data_ptr(), R, epi, s)
 
         fn()
         torch.cuda.synchronize()

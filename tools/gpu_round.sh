@@ -38,6 +38,8 @@ for s in "$@"; do
     gvpmc) export TMPDIR=/tmp; step gvpmc 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/gvpmc -o pmc --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 --only q4k ;;
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
     gemmb) step gemmb 300 bash -c 'python tools/gemm_bench.py --T 512 && python tools/gemm_bench.py --T 2048' ;;
+    gemmt) step gemmt 300 bash -c 'for T in 384 512 2048 2304; do python tools/gemm_bench.py --T $T && python tools/gemm_bench.py --T $T --t16 || exit 1; done; for c in 8,128 8,64 4,64; do LFK_T16_CFG=$c python tools/gemm_bench.py --T 512 --t16 || exit 1; done' ;;
+    t16t) step t16t 400 python -u -m pytest tests/test_kernels_gpu.py -k "t16 or rmsnorm_f16 or attn_prefill" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     gemmpmc) export TMPDIR=/tmp; step gemmpmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
             -d gpurun_out/gemmpmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup
             step gemmpmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
