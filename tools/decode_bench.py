@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--prompt", type=int, default=256)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--slots", type=int, default=1, help="KV slots (> 1: batching on, tile16 copies + tile16 prefill)")
     ap.add_argument("--gen", type=int, default=0, help="also time a full generate() of this many tokens")
     args = ap.parse_args()
     from llama_fastapi_k8s_gpu_amd.gguf.synthetic import cached_synthetic_gguf
@@ -24,7 +25,8 @@ def main():
     path = cached_synthetic_gguf(args.model)
     t1 = time.time()
     hip = load_hip()
-    eng = hip.Engine(path, n_ctx=args.n_ctx, n_batch=512, device=0, use_graph=not args.no_graph)
+    eng = hip.Engine(path, n_ctx=args.n_ctx, n_batch=512, device=0, use_graph=not args.no_graph,
+                     **({"n_slots": args.slots} if args.slots > 1 else {}))
     t2 = time.time()
     import numpy as np
     toks = [int(t) for t in np.random.default_rng(0).integers(0, eng.hparams["n_vocab"], args.prompt)]
@@ -34,7 +36,7 @@ def main():
     prefill_ms = (time.time() - t3) * 1e3
     res = {"model": args.model, "gen_s": round(t1 - t0, 1), "load_s": round(t2 - t1, 1),
            "device_GB": round(eng.device_bytes / 1e9, 2), "prefill_tokens": args.prompt,
-           "prefill_ms": round(prefill_ms, 2), "prefill_tok_s": round(args.prompt / prefill_ms * 1e3, 1)}
+           "prefill_ms": round(prefill_ms, 2), "prefill_t16": bool(getattr(eng, "prefill_t16", False)), "prefill_tok_s": round(args.prompt / prefill_ms * 1e3, 1)}
     for pos0 in (args.prompt, min(args.n_ctx - args.steps - 2, 768)):
         ms = eng.bench_decode(args.steps, pos0)
         res[f"decode_ms_at_{pos0}"] = round(ms, 4)

@@ -44,6 +44,11 @@ for s in "$@"; do
             -d gpurun_out/gemmpmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup
             step gemmpmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
             -d gpurun_out/gemmpmcB -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup ;;
+    t16pmc) export TMPDIR=/tmp; step t16pmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
+            -d gpurun_out/t16pmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --T 512 --t16
+            step t16pmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
+            -d gpurun_out/t16pmcB -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --T 512 --t16
+            step prefprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prefprof -o pre --output-format csv -- python3 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
     bench20) step bench20 900 python bench.py --steps 20 --warmup 2 ;;
     benchtp2) LFK_BENCH_DEVICE=0 step benchtp2 900 python bench.py --gpus 2 --steps 12 --warmup 2 ;;
