@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 
@@ -77,6 +78,23 @@ class FakeSlotEngine : public SlotBackend {
     if (fail_at_ > 0 && steps_ == fail_at_) throw std::runtime_error("fake: injected device fault");
     return out;
   }
+  // pipelined form (the scheduler's batch_launch / batch_collect path): a launch runs the step
+  // at once - its KV effects happen in launch order, as on the device - and queues the tokens
+  bool can_pipeline() const override { return pipeline_; }
+  void batch_launch(const std::vector<int>& slots) override {
+    std::vector<int> out = batch_step(slots);
+    std::lock_guard<std::mutex> g(mu_);
+    if (queued_.size() >= 2) throw std::runtime_error("fake: two steps already in flight");
+    queued_.push_back(std::move(out));
+  }
+  std::vector<int> batch_collect() override {
+    std::lock_guard<std::mutex> g(mu_);
+    if (queued_.empty()) throw std::runtime_error("fake: no step in flight");
+    std::vector<int> out = std::move(queued_.front());
+    queued_.pop_front();
+    return out;
+  }
+  void set_pipeline(bool on) { pipeline_ = on; }
   long long prefilled() { std::lock_guard<std::mutex> g(mu_); return prefilled_; }
   long long steps() { std::lock_guard<std::mutex> g(mu_); return steps_; }
   int max_rows() { std::lock_guard<std::mutex> g(mu_); return max_rows_; }
@@ -89,6 +107,8 @@ class FakeSlotEngine : public SlotBackend {
   std::vector<int> cur_;
   long long prefilled_ = 0, steps_ = 0, fail_at_ = 0;
   int max_rows_ = 0;
+  bool pipeline_ = false;
+  std::deque<std::vector<int>> queued_;
 };
 
 PYBIND11_MODULE(_cpu, m) {
@@ -206,7 +226,8 @@ PYBIND11_MODULE(_cpu, m) {
       .def_property_readonly("prefilled", &FakeSlotEngine::prefilled)
       .def_property_readonly("steps", &FakeSlotEngine::steps)
       .def_property_readonly("max_rows", &FakeSlotEngine::max_rows)
-      .def("fail_at", &FakeSlotEngine::fail_at);
+      .def("fail_at", &FakeSlotEngine::fail_at)
+      .def("set_pipeline", &FakeSlotEngine::set_pipeline);
   bind_scheduler<FakeSlotEngine>(m);
 
   // the tensor-parallel control channel (runtime/tp_channel.h), for host-side tests of its

@@ -138,6 +138,17 @@ PYBIND11_MODULE(_hip, m) {
              py::gil_scoped_release nogil;
              return e.batch_step(slots);
            })
+      .def("batch_launch",
+           [](Engine& e, const std::vector<int>& slots) {
+             py::gil_scoped_release nogil;
+             e.batch_launch(slots);
+           })
+      .def("batch_collect",
+           [](Engine& e) {
+             py::gil_scoped_release nogil;
+             return e.batch_collect();
+           })
+      .def_property_readonly("can_pipeline", &Engine::can_pipeline)
       .def("batch_logits",
            [](Engine& e, int B) {
              std::vector<float> v = e.batch_logits(B);

@@ -161,6 +161,8 @@ Engine::~Engine() {
     if (sgraph_[i]) hipGraphExecDestroy(sgraph_[i]);
   for (hipGraphExec_t g : bgraph_)
     if (g) hipGraphExecDestroy(g);
+  for (hipGraphExec_t g : bgraph2_)
+    if (g) hipGraphExecDestroy(g);
   if (graph_) hipGraphDestroy(graph_);
   if (comm_) ncclCommDestroy(static_cast<ncclComm_t>(comm_));
   for (void* p : allocs_) hipFree(p);
@@ -172,6 +174,10 @@ Engine::~Engine() {
   if (h_tokens_) hipHostFree(h_tokens_);
   if (h_bslots_) hipHostFree(h_bslots_);
   if (h_btok_) hipHostFree(h_btok_);
+  for (int i = 0; i < 2; ++i) {
+    if (h_btok2_[i]) hipHostFree(h_btok2_[i]);
+    if (bev_[i]) hipEventDestroy(bev_[i]);
+  }
   if (h_rmeta_) hipHostFree(h_rmeta_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
   if (stream_) hipStreamDestroy(stream_);
@@ -333,6 +339,10 @@ void Engine::alloc_buffers() {
     gu_b_ = (float*)dalloc(sizeof(float) * bmax_ * 2 * F_l_);
     HIPCHK(hipHostMalloc((void**)&h_bslots_, sizeof(int) * bmax_, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(hipHostMalloc((void**)&h_btok2_[i], sizeof(int) * bmax_, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&bev_[i], hipEventDisableTiming));
+    }
     rpos_ = (int*)dalloc(sizeof(int) * B);
     rslots_ = (int*)dalloc(sizeof(int) * B);
     HIPCHK(hipHostMalloc((void**)&h_rmeta_, sizeof(int) * 3 * B, hipHostMallocDefault));
@@ -1407,8 +1417,7 @@ std::vector<int> Engine::slots_begin_impl(const std::vector<int>& slots, const s
   return out;
 }
 
-std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
-  ExecGuard guard(this);
+void Engine::check_batch_rows(const std::vector<int>& slots) const {
   const int B = (int)slots.size();
   if (!bmax_) throw std::runtime_error("batch_step: the engine was built with one KV slot");
   if (B < 1 || B > bmax_) throw std::runtime_error("batch_step: 1 <= rows <= max_batch");
@@ -1417,6 +1426,45 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
     for (int c = 0; c < b; ++c)
       if (slots[c] == slots[b]) throw std::runtime_error("batch_step: duplicate slot");
   }
+}
+
+void Engine::batch_launch(const std::vector<int>& slots) {
+  ExecGuard guard(this);
+  if (!can_pipeline()) throw std::runtime_error("batch_launch: not available on this engine (TP)");
+  if (fl_n_ >= 2) throw std::runtime_error("batch_launch: two steps already in flight");
+  check_batch_rows(slots);
+  const int B = (int)slots.size();
+  // a changed row -> slot map is rewritten in pinned memory: no copy of it may still be queued
+  const bool remap = B != bslots_n_ || std::memcmp(h_bslots_, slots.data(), sizeof(int) * B) != 0;
+  if (remap && fl_n_ > 0) HIPCHK(hipStreamSynchronize(stream_));
+  const int i = (fl_head_ + fl_n_) & 1;
+  launch_par_ = i;
+  enqueue_batch_launch(slots, h_btok2_[i]);
+  launch_par_ = 0;
+  HIPCHK(hipEventRecord(bev_[i], stream_));
+  fl_B_[i] = B;
+  fl_b1_[i] = last_b1_;
+  ++fl_n_;
+}
+
+std::vector<int> Engine::batch_collect() {
+  ExecGuard guard(this);
+  if (fl_n_ <= 0) throw std::runtime_error("batch_collect: no step in flight");
+  const int i = fl_head_;
+  fl_head_ ^= 1;
+  --fl_n_;
+  HIPCHK(hipEventSynchronize(bev_[i]));
+  HIPCHK(hipGetLastError());
+  check_device_err();
+  last_batch_ = fl_B_[i];
+  last_b1_ = fl_b1_[i];
+  return std::vector<int>(h_btok2_[i], h_btok2_[i] + fl_B_[i]);
+}
+
+std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
+  ExecGuard guard(this);
+  if (fl_n_ > 0) throw std::runtime_error("batch_step: pipelined steps in flight (batch_collect them first)");
+  check_batch_rows(slots);
   if (leader()) {
     TPMsg m;
     m.put<int32_t>(TPO_BATCH_STEP); m.put_vec(slots);
@@ -1427,17 +1475,24 @@ std::vector<int> Engine::batch_step(const std::vector<int>& slots) {
 
 std::vector<int> Engine::batch_step_impl(const std::vector<int>& slots) {
   const int B = (int)slots.size();
+  enqueue_batch_launch(slots, h_btok_);
+  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(hipGetLastError());
+  check_device_err();
+  last_batch_ = B;
+  return std::vector<int>(h_btok_, h_btok_ + B);
+}
+
+// Queue one batch step of `slots` and the copy of its tokens to the pinned h_dst (no sync).
+void Engine::enqueue_batch_launch(const std::vector<int>& slots, int* h_dst) {
+  const int B = (int)slots.size();
   if (B == 1 && b1_gemv_) {
     // one active row: the single-row GEMV decode of that slot beats the batched projections
     launch_step(slots[0]);
-    HIPCHK(hipMemcpyAsync(h_btok_, state_ + (size_t)S_NSTATE * slots[0] + S_TOKEN, sizeof(int),
+    HIPCHK(hipMemcpyAsync(h_dst, state_ + (size_t)S_NSTATE * slots[0] + S_TOKEN, sizeof(int),
                           hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
-    HIPCHK(hipGetLastError());
-    check_device_err();
-    last_batch_ = 1;
     last_b1_ = true;
-    return std::vector<int>(h_btok_, h_btok_ + 1);
+    return;
   }
   last_b1_ = false;
   // the row -> slot map goes up only when it changed (a steady batch re-sends nothing; each
@@ -1448,26 +1503,25 @@ std::vector<int> Engine::batch_step_impl(const std::vector<int>& slots) {
     bslots_n_ = B;
   }
   if (opt_.use_graph) {
-    if ((int)bgraph_.size() <= B) bgraph_.resize(B + 1, nullptr);
+    if ((int)bgraph_.size() <= B) {
+      bgraph_.resize(B + 1, nullptr);
+      bgraph2_.resize(B + 1, nullptr);
+    }
     if (!bgraph_[B]) {
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
       enqueue_batch_step(B, stream_);
       HIPCHK(hipStreamEndCapture(stream_, &g));
-      const hipError_t e = hipGraphInstantiate(&bgraph_[B], g, nullptr, nullptr, 0);
+      hipError_t e = hipGraphInstantiate(&bgraph_[B], g, nullptr, nullptr, 0);
+      if (e == hipSuccess) e = hipGraphInstantiate(&bgraph2_[B], g, nullptr, nullptr, 0);
       hipGraphDestroy(g);
       HIPCHK(e);
     }
-    HIPCHK(hipGraphLaunch(bgraph_[B], stream_));
+    HIPCHK(hipGraphLaunch(launch_par_ ? bgraph2_[B] : bgraph_[B], stream_));
   } else {
     enqueue_batch_step(B, stream_);
   }
-  HIPCHK(hipMemcpyAsync(h_btok_, btok_out_, sizeof(int) * B, hipMemcpyDeviceToHost, stream_));
-  HIPCHK(hipStreamSynchronize(stream_));
-  HIPCHK(hipGetLastError());
-  check_device_err();
-  last_batch_ = B;
-  return std::vector<int>(h_btok_, h_btok_ + B);
+  HIPCHK(hipMemcpyAsync(h_dst, btok_out_, sizeof(int) * B, hipMemcpyDeviceToHost, stream_));
 }
 
 // Rows [0, B) of a logits buffer with row pitch ld_src holding this rank's vocabulary shard

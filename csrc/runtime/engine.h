@@ -137,6 +137,13 @@ class Engine : public SlotBackend {
   // batched split-L attention), the lm_head GEMM and the batched sampler; returns the
   // next token of each slot (synchronous).
   std::vector<int> batch_step(const std::vector<int>& slots) override;
+  // Pipelined batch_step (the scheduler's decode loop, slots.h): without it the host turnaround
+  // between steps - stream-sync wake-up, token hand-off, graph launch - left the GPU idle
+  // ~60-80 us per 2.3 ms step. Single-GPU engines only (TP followers replay the leader's
+  // synchronous commands).
+  bool can_pipeline() const override { return opt_.tp_size == 1 && bmax_ > 0; }
+  void batch_launch(const std::vector<int>& slots) override;
+  std::vector<int> batch_collect() override;
   std::vector<float> batch_logits(int B);  // test hook: logits [B][n_vocab] of the last batch_step
 
  private:
@@ -305,6 +312,15 @@ class Engine : public SlotBackend {
   int* attn_cnt_b_ = nullptr;      // [bmax][64]
   int* h_bslots_ = nullptr;   // pinned [bmax]
   int* h_btok_ = nullptr;     // pinned [bmax]
+  // steps in flight (batch_launch / batch_collect): a ring of two, each with its own pinned
+  // token buffer and completion event
+  int* h_btok2_[2] = {nullptr, nullptr};
+  hipEvent_t bev_[2] = {nullptr, nullptr};
+  int fl_B_[2] = {0, 0};
+  bool fl_b1_[2] = {false, false};
+  int fl_head_ = 0, fl_n_ = 0;
+  void check_batch_rows(const std::vector<int>& slots) const;
+  void enqueue_batch_launch(const std::vector<int>& slots, int* h_dst);
   int bslots_n_ = -1;         // rows of the row -> slot map last uploaded to bslots_
   int last_batch_ = 0;
   // batch_step projections on the MFMA batched projection (bmm.hip: weights streamed once per
@@ -329,6 +345,11 @@ class Engine : public SlotBackend {
   bool wo_one_part_ = false;  // Wo as one K part (LFK_BMM_WO1=1, A/B)
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
+  // a second instantiation of each, for the pipelined launches: consecutive in-flight steps
+  // alternate between the two (a graph exec relaunched while its previous launch is still
+  // queued may be held back by the runtime until that one completes)
+  std::vector<hipGraphExec_t> bgraph2_;
+  int launch_par_ = 0;  // which instantiation enqueue_batch_launch uses (0: bgraph_, 1: bgraph2_)
   // single-row decode (GEMV path) of KV slot dslot_: enqueue_decode reads it while capturing;
   // one graph per slot (slot 0's is graph_exec_). batch_step over ONE row takes this path
   // (LFK_B1_GEMV=0: the batched projections), the faster one at B = 1

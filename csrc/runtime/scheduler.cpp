@@ -1,6 +1,8 @@
 // Continuous-batching scheduler: see scheduler.h.
 #include "scheduler.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <chrono>
 #include <stdexcept>
@@ -21,6 +23,8 @@ BatchScheduler::BatchScheduler(SlotBackend& e) : eng_(e) {
   slot_hist_.resize(n_slots_);
   slot_used_.assign(n_slots_, 0);
   st_.slots = n_slots_ - first_slot_;
+  const char* pe = std::getenv("LFK_SCHED_PIPELINE");
+  pipeline_ = e.can_pipeline() && !(pe && pe[0] == '0');
   th_ = std::thread([this] { loop(); });
 }
 
@@ -151,9 +155,14 @@ void BatchScheduler::loop() {
   std::unique_lock<std::mutex> lk(mu_);
   std::vector<int> rows;
   std::vector<std::shared_ptr<Req>> row_req;
+  struct Flight {
+    std::vector<int> rows;
+    std::vector<std::shared_ptr<Req>> req;
+  };
+  std::deque<Flight> flights;  // pipelined steps queued on the engine, oldest first
   while (true) {
     cv_work_.wait(lk, [&] {
-      if (stop_ || !pending_.empty()) return true;
+      if (stop_ || !pending_.empty() || !flights.empty()) return true;
       for (int s = first_slot_; s < n_slots_; ++s)
         if (slot_req_[s]) return true;
       return false;
@@ -223,7 +232,12 @@ void BatchScheduler::loop() {
         cv_out_.notify_all();  // the first tokens reach their waiters now, not after the next step
       }
     }
-    // 3. one decode step over every active row
+    // 3. one decode step over every active row. Pipelined (engines that can): the step of
+    //    the current rows is queued and, while nothing waits for admission and the rows are
+    //    those of the step already in flight, the NEXT step is queued too before the host
+    //    handles this one's tokens - the device runs back to back through the host turnaround.
+    //    A row that finishes on a step whose successor is already queued just has one extra
+    //    token computed and dropped (its request is done; the KV slot is free either way).
     rows.clear();
     row_req.clear();
     for (int s = first_slot_; s < n_slots_; ++s)
@@ -231,32 +245,85 @@ void BatchScheduler::loop() {
         rows.push_back(s);
         row_req.push_back(slot_req_[s]);
       }
-    if (rows.empty()) continue;
+    if (rows.empty() && flights.empty()) continue;
     std::vector<int> out;
     std::string err;
+    Flight cur;
     lk.unlock();
     try {
-      out = eng_.batch_step(rows);
+      if (!pipeline_) {
+        out = eng_.batch_step(rows);
+        cur.rows = rows;
+        cur.req = row_req;
+      } else {
+        if (flights.empty()) {
+          eng_.batch_launch(rows);
+          flights.push_back(Flight{rows, row_req});
+        }
+        // the next step feeds each row's newest token at position prompt + tokens - 1 + 1:
+        // only while that stays inside the context (a row finishing on the context end must
+        // not get a KV write past n_ctx from a step queued before its end was seen)
+        bool more;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          more = pending_.empty() && !stop_;
+          for (size_t b = 0; more && b < row_req.size(); ++b) {
+            const Req& r = *row_req[b];
+            more = !r.done && !r.cancel && (int)(r.prompt.size() + r.tokens.size()) < eng_.n_ctx();
+          }
+        }
+        if (more && flights.size() == 1 && !rows.empty() && flights.back().rows == rows) {
+          eng_.batch_launch(rows);
+          flights.push_back(Flight{rows, row_req});
+        }
+        cur = flights.front();
+        flights.pop_front();
+        out = eng_.batch_collect();
+      }
     } catch (const std::exception& e) {
       err = e.what();
+      if (cur.rows.empty()) {
+        cur.rows = rows;
+        cur.req = row_req;
+      }
+      // the engine's state after a failed step is unknown: drop every queued step
+      for (int k = (int)flights.size(); k > 0; --k) {
+        try {
+          eng_.batch_collect();
+        } catch (...) {
+        }
+      }
+      flights.clear();
     }
     lk.lock();
     ++st_.steps;
-    st_.rows += (long long)rows.size();
-    for (size_t b = 0; b < rows.size(); ++b) {
-      Req& r = *row_req[b];
+    st_.rows += (long long)cur.rows.size();
+    for (size_t b = 0; b < cur.rows.size(); ++b) {
+      Req& r = *cur.req[b];
       if (!err.empty()) {
-        slot_hist_[rows[b]].clear();
-        r.error = err;
-        finish(r, "error");
+        slot_hist_[cur.rows[b]].clear();
+        if (!r.done) {
+          r.error = err;
+          finish(r, "error");
+        }
         continue;
       }
-      slot_hist_[rows[b]].push_back(r.tokens.back());  // the token this step fed is now in the KV
-      if (r.done) continue;
+      if (r.done) continue;  // finished (or cancelled) after this step was queued: its token is dropped
+      slot_hist_[cur.rows[b]].push_back(r.tokens.back());  // the token this step fed is now in the KV
       push_token(r, out[b]);
     }
     cv_out_.notify_all();
   }
+  // drain what is still queued before anything else uses the engine
+  lk.unlock();
+  for (size_t k = 0; k < flights.size(); ++k) {
+    try {
+      eng_.batch_collect();
+    } catch (...) {
+    }
+  }
+  flights.clear();
+  lk.lock();
   // shutdown: nothing runs any more
   for (auto& r : pending_) finish(*r, "cancelled");
   pending_.clear();

@@ -94,6 +94,7 @@ class BatchScheduler {
 
   SlotBackend& eng_;
   int first_slot_ = 1, n_slots_ = 1;
+  bool pipeline_ = false;  // batch_launch / batch_collect (LFK_SCHED_PIPELINE=0: synchronous steps)
   std::mutex mu_;
   std::condition_variable cv_work_, cv_out_;
   std::deque<std::shared_ptr<Req>> pending_;

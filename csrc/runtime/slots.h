@@ -37,6 +37,13 @@ class SlotBackend {
   }
   // one decode step of every listed slot at its own position -> each slot's next token
   virtual std::vector<int> batch_step(const std::vector<int>& slots) = 0;
+  // Pipelined form (optional): batch_launch queues one step and returns, batch_collect waits
+  // for the OLDEST queued step and returns its tokens. Steps run in launch order, each feeding
+  // from the tokens its predecessor sampled on the device, so the scheduler can queue step
+  // k + 1 before it has handled step k's tokens. At most two steps in flight.
+  virtual bool can_pipeline() const { return false; }
+  virtual void batch_launch(const std::vector<int>& slots) { (void)slots; }
+  virtual std::vector<int> batch_collect() { return {}; }
 };
 
 }  // namespace lfk

@@ -162,3 +162,40 @@ def test_single_slot_engine_rejects_batching(models):
     eng = load_hip().Engine(models["tiny-llama3-q4_k_m"], n_ctx=128, n_batch=32, device=0, use_graph=False)
     with pytest.raises(RuntimeError):
         eng.batch_step([0])
+
+
+def test_pipelined_steps_equal_synchronous(models):
+    """batch_launch / batch_collect (step k + 1 queued before step k's tokens are read, the
+    scheduler's mode) produce exactly the tokens of synchronous batch_step calls - the steps
+    feed from device-resident tokens - including a one-row step (the single-row graph) and a
+    row set change."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-llama3-q4_k_m"]
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    rng = np.random.default_rng(8)
+    prompts = {s: [int(t) for t in rng.integers(3, 300, n)] for s, n in ((1, 7), (2, 19), (3, 12))}
+    plan = [[1, 2, 3]] * 4 + [[2]] * 3 + [[1, 3]] * 3
+
+    def run(pipelined):
+        eng = load_hip().Engine(path, n_ctx=256, n_batch=64, device=0, use_graph=True, n_slots=4)
+        assert eng.can_pipeline
+        first = {s: eng.slot_begin(s, p, 0, greedy) for s, p in prompts.items()}
+        out = []
+        if not pipelined:
+            for rows in plan:
+                out.append(list(eng.batch_step(rows)))
+        else:
+            i = 0
+            while i < len(plan):
+                eng.batch_launch(plan[i])
+                if i + 1 < len(plan) and plan[i + 1] == plan[i]:
+                    eng.batch_launch(plan[i + 1])
+                    out.append(list(eng.batch_collect()))
+                    out.append(list(eng.batch_collect()))
+                    i += 2
+                else:
+                    out.append(list(eng.batch_collect()))
+                    i += 1
+        assert eng.healthy, eng.last_error
+        return first, out
+    assert run(False) == run(True)

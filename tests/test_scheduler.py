@@ -38,9 +38,22 @@ def run(sched, rid, timeout=20.0):
     raise AssertionError("request did not finish")
 
 
+PIPELINE = {"on": False}
+
+
+@pytest.fixture(autouse=True, params=[False, True], ids=["sync", "pipelined"])
+def _pipeline(request):
+    """Every scheduler test runs twice: synchronous batch_step, and the pipelined
+    batch_launch / batch_collect loop (the next step queued before this one's tokens are
+    handled - the MI355X engine's mode)."""
+    PIPELINE["on"] = request.param
+    yield
+
+
 def make(n_slots=5, max_batch=4, n_ctx=64, step_us=200):
     cpu = load_cpu()
     eng = cpu.FakeSlotEngine(n_slots, max_batch, n_ctx, VOCAB, step_us)
+    eng.set_pipeline(PIPELINE["on"])
     return eng, cpu.BatchScheduler(eng)
 
 

@@ -49,6 +49,16 @@ def main():
         ms = (time.perf_counter() - t0) * 1e3 / args.steps
         res[f"B{B}_ms_per_step"] = round(ms, 3)
         res[f"B{B}_tok_s"] = round(B / ms * 1e3, 1)
+        if getattr(eng, "can_pipeline", False):
+            # the scheduler's mode: step k + 1 queued before step k's tokens are collected
+            t0 = time.perf_counter()   # exactly args.steps steps launched and collected in here
+            eng.batch_launch(slots)
+            for _ in range(args.steps - 1):
+                eng.batch_launch(slots)
+                eng.batch_collect()
+            eng.batch_collect()
+            ms = (time.perf_counter() - t0) * 1e3 / args.steps
+            res[f"B{B}_pipelined_ms_per_step"] = round(ms, 3)
     print(json.dumps(res), flush=True)
 
 
