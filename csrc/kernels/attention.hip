@@ -33,6 +33,16 @@ __device__ __forceinline__ void st_sc1(float* p, float v) {
 __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the same for an 8-byte aligned pair (one dwordx2 access instead of two)
+__device__ __forceinline__ void st2_sc1(float* p, float a, float b) {
+  const unsigned long long v = ((unsigned long long)__float_as_uint(b) << 32) | __float_as_uint(a);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld2_sc1(const float* p) {
+  const unsigned long long v = __hip_atomic_load(reinterpret_cast<unsigned long long*>(const_cast<float*>(p)),
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_float2(__uint_as_float((unsigned)v), __uint_as_float((unsigned)(v >> 32)));
+}
 
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 
@@ -245,28 +255,31 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     if (tid < G) a.out[tid] = wl[0][tid];
     return;
   }
-  // ---- 3. block partial: element e = (g, d) per thread
-  for (int e = tid; e < G * HD; e += 256) {
-    const int g = e / HD, d = e % HD;
+  // ---- 3. block partial: a pair of adjacent dims (g, d, d + 1) per thread (8-byte sc1 stores;
+  //      the (M, l) statistics of a head are one pair too - HD + 2 keeps every pair aligned)
+  for (int e2 = tid; e2 < G * HD / 2; e2 += 256) {
+    const int g = (2 * e2) / HD, d = (2 * e2) % HD;
     const float M = fmaxf(fmaxf(wm[0][g], wm[1][g]), fmaxf(wm[2][g], wm[3][g]));
-    float l = 0.f, acc = 0.f;
+    float l = 0.f, acc0 = 0.f, acc1 = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const float f = wm[w][g] == -FLT_MAX ? 0.f : __expf(wm[w][g] - M);
       l += f * wl[w][g];
-      acc += f * wo[w][g][d];
+      acc0 += f * wo[w][g][d];
+      acc1 += f * wo[w][g][d + 1];
     }
     if (ns == 1) {
       const int o = (kvh * G + g) * HD + d;
-      a.out[o] = acc / l;
-      if (a.out_h) a.out_h[swz4(o)] = __float2half(acc / l);
+      a.out[o] = acc0 / l;
+      a.out[o + 1] = acc1 / l;
+      if (a.out_h) {
+        a.out_h[swz4(o)] = __float2half(acc0 / l);
+        a.out_h[swz4(o + 1)] = __float2half(acc1 / l);
+      }
     } else {
       float* dst = a.part + ((size_t)split * a.n_head + kvh * G + g) * (HD + 2);
-      st_sc1(dst + d, acc);
-      if (d == 0) {
-        st_sc1(dst + HD, M);
-        st_sc1(dst + HD + 1, l);
-      }
+      st2_sc1(dst + d, acc0, acc1);
+      if (d == 0) st2_sc1(dst + HD, M, l);
     }
   }
   LFK_STAMP(4);
@@ -304,10 +317,19 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     for (int i = 0; i < NSB; ++i) {
       const int s2 = min(s0 + i, ns - 1);
       const float* p = a.part + ((size_t)s2 * a.n_head + h) * (HD + 2);
-      mv[i] = ld_sc1(p + HD);
-      lv[i] = ld_sc1(p + HD + 1);
+      const float2 st = ld2_sc1(p + HD);
+      mv[i] = st.x;
+      lv[i] = st.y;
+      if constexpr (EPT == 1) {
+        pv[i][0] = ld_sc1(p + d0);
+      } else {
 #pragma unroll
-      for (int j = 0; j < EPT; ++j) pv[i][j] = ld_sc1(p + d0 + j);
+        for (int j = 0; j < EPT; j += 2) {
+          const float2 v = ld2_sc1(p + d0 + j);
+          pv[i][j] = v.x;
+          pv[i][j + 1] = v.y;
+        }
+      }
     }
     float mb = M;
 #pragma unroll
