@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
 
   __shared__ __attribute__((aligned(16))) h2v qs[G][HD / 2];   // q * scale in f16 pairs
   __shared__ __attribute__((aligned(16))) __half vs[4][KPW][HD + 8];
-  __shared__ float ps[4][G][KPW];
+  __shared__ __attribute__((aligned(16))) float ps[4][G][KPW];
   __shared__ float wm[4][G], wl[4][G];
   __shared__ __attribute__((aligned(16))) float wo[4][G][HD];
   __shared__ int last;
@@ -223,21 +223,29 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int j = 0; j < DV; ++j) o[g][j] = 0.f;
+  // the weights of 4 keys per head in one 16-byte LDS read (16 instead of 64 reads at G = 4)
 #pragma unroll
-  for (int k = 0; k < KPW; ++k) {
-    float v[DV];
-    if constexpr (DV == 2) {
-      const __half2 h2 = *reinterpret_cast<const __half2*>(&vs[wave][k][2 * lane]);
-      v[0] = __low2float(h2);
-      v[1] = __high2float(h2);
-    } else {
-      v[0] = __half2float(vs[wave][k][lane]);
-    }
+  for (int k4 = 0; k4 < KPW; k4 += 4) {
+    float4 pg[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const float p = ps[wave][g][k];
+    for (int g = 0; g < G; ++g) pg[g] = *reinterpret_cast<const float4*>(&ps[wave][g][k4]);
 #pragma unroll
-      for (int j = 0; j < DV; ++j) o[g][j] += p * v[j];
+    for (int kk = 0; kk < 4; ++kk) {
+      const int k = k4 + kk;
+      float v[DV];
+      if constexpr (DV == 2) {
+        const __half2 h2 = *reinterpret_cast<const __half2*>(&vs[wave][k][2 * lane]);
+        v[0] = __low2float(h2);
+        v[1] = __high2float(h2);
+      } else {
+        v[0] = __half2float(vs[wave][k][lane]);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float p = kk == 0 ? pg[g].x : kk == 1 ? pg[g].y : kk == 2 ? pg[g].z : pg[g].w;
+#pragma unroll
+        for (int j = 0; j < DV; ++j) o[g][j] += p * v[j];
+      }
     }
   }
 #pragma unroll
