@@ -256,8 +256,8 @@ def main() -> int:
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong" if tp else "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "q4_k_m weights; f16 (batched MFMA) / int8 (single-row GEMV) / bf16 (prefill MFMA) "
-                     "activations; fp32 accumulate",
+            "dtype": "q4_k_m weights; f16 (batched decode and prompt prefill MFMA, tile16 copies) / int8 "
+                     "(single-row GEMV) activations; fp32 accumulate",
             "data": "synthetic (random-init Llama-3-8B Q4_K_M GGUF, synthetic chat requests)",
             "config": {"model": "Llama-3-8B Q4_K_M",
                        "global_batch": (1 if tp else world) * min(args.clients, max_batch),

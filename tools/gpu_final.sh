@@ -11,3 +11,7 @@ cat gpurun_out/final_bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fprof -o bstep --output-format csv -- \
   python3 tools/batch_bench.py --batches 6 --steps 32 > gpurun_out/fprof.log 2>&1 || { tail -20 gpurun_out/fprof.log; exit 1; }
 echo done
+# single-row decode (the reference's serving mode): kernel stats of graph-free decode steps
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fdec -o dec --output-format csv -- \
+  python3 tools/decode_bench.py --steps 64 --no-graph > gpurun_out/fdec.log 2>&1 || { tail -20 gpurun_out/fdec.log; exit 1; }
+echo done2
