@@ -1037,6 +1037,10 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     // blocks per CU: LDS and the 16 waves a CU holds at this kernel's register count
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 16 / nw1));
     int nb = std::max(1, std::min(tiles, per_cu * bmm_cus()));
+    // Q|K|V (tuning, LFK_BMM_QKV_TPB): tiles per block - every block stages the whole x slice
+    // (B rows x K), so fewer blocks over more tiles each trade x staging for weight parallelism
+    static const int qkv_tpb = std::max(1, env_int("LFK_BMM_QKV_TPB", 1));
+    if (a.qkv_epi && qkv_tpb > 1) nb = std::max(1, std::min(nb, (tiles + qkv_tpb - 1) / qkv_tpb));
     if (a.swiglu_epi) {  // every CU group gets the same number of blocks (the range split assumes it)
       const int G = std::max(1, std::min(bmm_cus(), tiles));
       nb = G * std::max(1, std::min(per_cu, tiles / G));
@@ -1137,8 +1141,9 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
   a.kparts = b.kparts = 1;
   const size_t lds = bmm_lds(a.B, steps, 8);
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 2));
-  const int cap = per_cu * bmm_cus();
   const int ta = tiles_of(a), tb = tiles_of(b);
+  static const int qkv_tpb = std::max(1, env_int("LFK_BMM_QKV_TPB", 1));  // as in launch_bmm
+  const int cap = std::max(2, std::min(per_cu * bmm_cus(), (ta + tb + qkv_tpb - 1) / qkv_tpb));
   // blocks in proportion to the runs' tiles, each run at least one block, within one resident round
   int na = std::min(ta, std::max(1, (int)((long long)cap * ta / (ta + tb))));
   int nbb = std::min(tb, std::max(1, cap - na));
