@@ -1009,6 +1009,8 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     int kparts = 1;
     if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
       kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
+      static const int parts_env = env_int("LFK_BMM_WTK_PARTS", 0);  // tuning: K parts (Wo / down)
+      if (parts_env > 0) kparts = std::max(1, std::min(steps, parts_env));
       // the staged slice (B rows x part) stays within the LDS
       while (kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
     }
