@@ -1189,12 +1189,21 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   const int ntiles = (a.w.rows + 15) >> 4;
   const int tile0 = blockIdx.x * 2 * NWV + 2 * wave;  // this wave's tiles: tile0, tile0 + 1
   const int t0 = blockIdx.y * TM;
+  if (a.seg_dev) {  // grouped form: this expert's rows of the gathered buffers
+    const int r0 = a.seg_dev[0];
+    a.T = a.seg_dev[1] - r0;
+    if (t0 >= a.T) return;  // whole block, before any barrier
+    a.x += (size_t)r0 * K;
+    if (a.out) a.out += (size_t)r0 * a.ldo;
+    if (a.out_h) a.out_h += (size_t)r0 * a.ldh;
+  }
   const int spz = (steps + (int)gridDim.z - 1) / (int)gridDim.z;
   const int sb = blockIdx.z * spz, se = min(steps, sb + spz);
   if (sb >= se) return;  // whole block, before any barrier
   const int nh = 2 * (se - sb);
-  const uint8_t* wt0 = a.w.base + (size_t)min(tile0, ntiles - 1) * steps * SB;
-  const uint8_t* wt1 = a.w.base + (size_t)min(tile0 + 1, ntiles - 1) * steps * SB;
+  const size_t tstride = a.tile_stride ? a.tile_stride : (size_t)steps * SB;
+  const uint8_t* wt0 = a.w.base + (size_t)min(tile0, ntiles - 1) * tstride + (size_t)a.step0 * SB;
+  const uint8_t* wt1 = a.w.base + (size_t)min(tile0 + 1, ntiles - 1) * tstride + (size_t)a.step0 * SB;
   f4_t acc[2][NG];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -1333,6 +1342,8 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   // LFK_T16_CFG="waves,tokens" pins one (tuning).
   static const char* cfg_env = getenv("LFK_T16_CFG");
   const int ntiles = (a.w.rows + 15) / 16, steps = a.w.K / 256, cus = bmm_cus();
+  // grouped: size the shape and split for the expected rows, launch for the most
+  const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
   static const int shapes[3][2] = {{8, 128}, {8, 64}, {4, 64}};
   int nw = 4, tm = 64;
   int pin_nw = 0, pin_tm = 0;
@@ -1342,19 +1353,21 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
     tm = pin_tm;
   } else {
     for (const auto& sh : shapes) {
-      const long blocks = (long)((ntiles + 2 * sh[0] - 1) / (2 * sh[0])) * ((a.T + sh[1] - 1) / sh[1]);
+      const long blocks = (long)((ntiles + 2 * sh[0] - 1) / (2 * sh[0])) * ((rows + sh[1] - 1) / sh[1]);
       nw = sh[0];
       tm = sh[1];
       if (blocks >= cus) break;
     }
   }
-  const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm;
+  const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm, gy_busy = (rows + tm - 1) / tm;
   int split = 1;
   if (EPI != GEMM_SWIGLU)
-    while (gx * gy * split < cus && steps / (split * 2) >= 2) split *= 2;
+    while (gx * gy_busy * split < cus && steps / (split * 2) >= 2) split *= 2;
   const int spz = (steps + split - 1) / split;
   split = (steps + spz - 1) / spz;  // no empty parts
+  if (a.seg_dev && split > 1 && EPI != GEMM_STORE) throw std::runtime_error("gemm_t16: grouped split-K needs STORE");
   if (split > 1 && EPI == GEMM_STORE && !a.out_zeroed) {
+    if (a.seg_dev) throw std::runtime_error("gemm_t16: grouped split-K STORE needs a pre-zeroed output");
     const hipError_t e = hipMemset2DAsync(a.out, sizeof(float) * a.ldo, 0, sizeof(float) * a.w.rows, a.T, s);
     if (e != hipSuccess) throw std::runtime_error("gemm_t16: memset failed");
   }

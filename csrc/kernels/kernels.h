@@ -307,6 +307,16 @@ struct GemmT16Args {
   bool out_zeroed = false;         // STORE: `out` already zeroed (no memset before split-K)
   __half* out_h = nullptr;         // SWIGLU: silu(gate) * up as f16 [T][ldh], bmm k order
   int ldh = 0;
+  // grouped (MoE) form: rows [seg_dev[0], seg_dev[1]) of x / out / out_h, read on the device; T
+  // is then only the launch bound and rows_hint the expected count (shape and split-K sizing;
+  // split-K STORE partials are atomically added, so the caller pre-zeroes `out`)
+  const int* seg_dev = nullptr;
+  int rows_hint = 0;
+  // a matrix inside a wider tile16 copy (the MoE down experts concatenated along K): bytes
+  // between consecutive 16-row tiles (0: the matrix's own K / 256 steps) and its first 256-k
+  // step inside each tile
+  size_t tile_stride = 0;
+  int step0 = 0;
 };
 void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s);
 

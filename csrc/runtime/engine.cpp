@@ -448,11 +448,13 @@ void Engine::setup_batch_mfma() {
   HIPCHK(hipStreamSynchronize(stream_));
   // dense models: prompt chunks on the same tile16 copies (gemm_t16: the dequantisation spread
   // over 128 tokens per fragment, f16 activations - measured against gemm_dq in profiles/)
+  // (MoE: the experts run on the stacked SwiGLU copy and the K-concatenated down copy)
   const char* pt = std::getenv("LFK_PREFILL_T16");
-  bool t16 = bg_ffn_ && !moe_b_ && !(pt && pt[0] == '0');
+  bool t16 = (hp_.n_expert > 0 ? moe_b_ : bg_ffn_) && !(pt && pt[0] == '0');
   for (int l = 0; t16 && l < hp_.n_layer; ++l) {
     const Layer& L = layers_[l];
     for (const QMat* m : {&L.t_wq, &L.t_wk, &L.t_wv, &L.t_wo, &L.t_gu, &L.t_down}) t16 = t16 && m->base && m->rows % 16 == 0;
+    if (hp_.n_expert > 0) t16 = t16 && L.down_exps.K % 256 == 0 && L.gu_exps.rows % 16 == 0;
   }
   prefill_t16_ = t16;
 }
@@ -791,9 +793,9 @@ void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd;
   const bool tp = opt_.tp_size > 1;
-  t16 = t16 && hp_.n_expert == 0;
-  rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s, nullptr, 0, t16);
-  if (t16) {
+  // MoE: the router GEMM reads the bf16 norm; the experts' f16 norm is written after it
+  rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s, nullptr, 0, t16 && hp_.n_expert == 0);
+  if (t16 && hp_.n_expert == 0) {
     GemmT16Args gu;
     gu.w = L.t_gu; gu.x = reinterpret_cast<const __half*>(xb_); gu.T = T;
     gu.out_h = reinterpret_cast<__half*>(h_); gu.ldh = F_l_;
@@ -819,7 +821,8 @@ void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
     const int KU = hp_.n_expert_used;
     // device-side routing -> per-expert row lists; gather the routed rows once
     moe_route_group(router_logits_, T, E, KU, moe_sel_, moe_selw_, moe_off_, moe_tok_, moe_gw_, moe_pos_, s);
-    gather_rows_bf16(xb_, moe_tok_, T * KU, d, moe_xg_, s);
+    if (t16) rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s, nullptr, 0, true);  // after the router read xb_
+    gather_rows_bf16(xb_, moe_tok_, T * KU, d, moe_xg_, s);  // 2-byte rows: bf16 or f16 alike
     if (tp) {
       if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * T * d, hipMemcpyDeviceToDevice, s));
       else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * T * d, s));
@@ -828,7 +831,23 @@ void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
     // split-K partials of the grouped down GEMMs meet by atomic add: zero the gathered output
     HIPCHK(hipMemsetAsync(moe_yg_, 0, sizeof(float) * (size_t)T * KU * d, s));
     const int hint = std::max(1, T * KU / E);
-    for (int e = 0; e < E; ++e) {  // each expert multiplies only its rows (count/offset read on the device)
+    for (int e = 0; t16 && e < E; ++e) {  // the tile16 expert copies (stacked gate/up, K-concatenated down)
+      GemmT16Args gu;
+      gu.w = L.gu_exps; gu.w.expert_stride = 0;
+      gu.w.base = L.t_gu.base + t16_bytes(L.gu_exps.type, L.gu_exps.rows, L.gu_exps.K) * e;
+      gu.x = reinterpret_cast<const __half*>(moe_xg_); gu.T = T;
+      gu.out_h = reinterpret_cast<__half*>(moe_hg_); gu.ldh = F_l_;
+      gu.seg_dev = moe_off_ + e; gu.rows_hint = hint;
+      gemm_t16(gu, GEMM_SWIGLU, s);
+      GemmT16Args dn;
+      dn.w = L.down_exps; dn.w.expert_stride = 0; dn.w.base = L.t_down.base;
+      dn.tile_stride = t16_bytes(L.down_exps.type, 16, L.t_down.K);  // one tile over all experts' K
+      dn.step0 = e * (L.down_exps.K / 256);
+      dn.x = reinterpret_cast<const __half*>(moe_hg_); dn.T = T; dn.ldo = d; dn.out = moe_yg_; dn.out_zeroed = true;
+      dn.seg_dev = moe_off_ + e; dn.rows_hint = hint;
+      gemm_t16(dn, GEMM_STORE, s);
+    }
+    for (int e = 0; !t16 && e < E; ++e) {  // each expert multiplies only its rows (count/offset read on the device)
       GemmArgs gu;
       gu.w = L.gu_exps; gu.w.base += L.gu_exps.expert_stride * e;
       gu.x = moe_xg_; gu.T = T; gu.out_bf16 = moe_hg_; gu.seg_dev = moe_off_ + e; gu.rows_hint = hint;

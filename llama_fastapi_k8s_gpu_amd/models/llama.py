@@ -84,9 +84,10 @@ class ReferenceLlama:
       * ``"prefill"`` (MFMA GEMM, kernels/gemm.hip + attention.hip): bf16 activations and
         bf16-rounded dequantised weights; attention with q * scale * log2(e) in f16, f16 P and
         K/V, bf16 output; the logits row through the decode head (q8);
-      * ``"prefill16"`` (the tile16 prefill GEMM, gemm_t16 in kernels/bmm.hip, dense models with
+      * ``"prefill16"`` (the tile16 prefill GEMM, gemm_t16 in kernels/bmm.hip, engines with
         batching on): f16(x / rms * w) inputs, f16 attention and SwiGLU outputs, the tile16 copy's
-        f16-arithmetic weights; attention and head as ``"prefill"``;
+        f16-arithmetic weights (MoE: the router on the bf16 norm as ``"prefill"``); attention and
+        head as ``"prefill"``;
       * ``"batch"`` (batched MFMA projections, kernels/bmm.hip): f16(x * w_norm) with the
         1/rms applied to the f32 result (d = 4096, the folded norm; f16(x / rms * w) below), f16 weights from the tile16 copy's f16 arithmetic
         (quants.dequantize(arith="f16")), f16 attention output and SwiGLU output; the head
@@ -231,6 +232,21 @@ class ReferenceLlama:
                     e = int(ids[t, j])
                     g = F.silu(ge[e] @ h[t]) * (ue[e] @ h[t])
                     out[t] += de[e] @ self._f16(g * w[t, j])
+            return out
+        if path == "prefill16":
+            # the router GEMM reads the bf16 norm (planar gemm_dq); the experts run on the tile16
+            # copies with the f16 norm, f16 SwiGLU output, routing weight applied after down
+            hr = self._normed_input(x, L["ffn_norm"], "prefill")
+            probs = torch.softmax(hr @ self._bf16(L["ffn_gate_inp"]).T, -1)
+            w, ids = torch.topk(probs, self.hp.n_expert_used, dim=-1)
+            w = w / w.sum(-1, keepdim=True)
+            ge, ue, de = (self._weight(k, L, "f16") for k in ("ffn_gate_exps", "ffn_up_exps", "ffn_down_exps"))
+            out = torch.zeros_like(h)
+            for t in range(h.shape[0]):
+                for j in range(self.hp.n_expert_used):
+                    e = int(ids[t, j])
+                    g = F.silu(ge[e] @ h[t]) * (ue[e] @ h[t])
+                    out[t] += w[t, j] * (de[e] @ self._f16(g))
             return out
         rw = L["ffn_gate_inp"] if path != "prefill" else self._bf16(L["ffn_gate_inp"])
         hr = self._normed_input(x, L["ffn_norm"], None) if path == "decode" else h
