@@ -1209,11 +1209,11 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[j][g] = f4_t{0.f, 0.f, 0.f, 0.f};
-  static_assert(XL == 2 || XL == 4, "X pieces per thread");
+  static_assert(XL >= 2 && XL <= 6 && XL * NT == TM * 16, "X pieces per thread");
   // X piece p = tid + NT j: token p / 16, 16-B column p % 16 of the 128-k slice (rows past T
   // load row T - 1: finite values whose outputs are never stored). Named registers, not an
   // array: the array was put in scratch.
-  uint4 x0, x1, x2, x3;
+  uint4 x0, x1, x2, x3, x4, x5;
   const __half* xrow[XL];
 #pragma unroll
   for (int j = 0; j < XL; ++j) xrow[j] = a.x + (size_t)min(t0 + ((tid + NT * j) >> 4), a.T - 1) * K + 8 * (tid & 15);
@@ -1221,20 +1221,20 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     const int k0 = (sb + (i >> 1)) * 256 + 128 * (i & 1);
     x0 = *reinterpret_cast<const uint4*>(xrow[0] + k0);
     x1 = *reinterpret_cast<const uint4*>(xrow[1] + k0);
-    if constexpr (XL == 4) {
-      x2 = *reinterpret_cast<const uint4*>(xrow[2] + k0);
-      x3 = *reinterpret_cast<const uint4*>(xrow[3] + k0);
-    }
+    if constexpr (XL > 2) x2 = *reinterpret_cast<const uint4*>(xrow[XL > 2 ? 2 : 0] + k0);
+    if constexpr (XL > 3) x3 = *reinterpret_cast<const uint4*>(xrow[XL > 3 ? 3 : 0] + k0);
+    if constexpr (XL > 4) x4 = *reinterpret_cast<const uint4*>(xrow[XL > 4 ? 4 : 0] + k0);
+    if constexpr (XL > 5) x5 = *reinterpret_cast<const uint4*>(xrow[XL > 5 ? 5 : 0] + k0);
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
     __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * (tid & 15)];
     constexpr int J = (NT / 16) * kT16Pitch;  // piece j + 1 is NT / 16 tokens further
     *reinterpret_cast<uint4*>(d) = x0;
     *reinterpret_cast<uint4*>(d + J) = x1;
-    if constexpr (XL == 4) {
-      *reinterpret_cast<uint4*>(d + 2 * J) = x2;
-      *reinterpret_cast<uint4*>(d + 3 * J) = x3;
-    }
+    if constexpr (XL > 2) *reinterpret_cast<uint4*>(d + 2 * J) = x2;
+    if constexpr (XL > 3) *reinterpret_cast<uint4*>(d + 3 * J) = x3;
+    if constexpr (XL > 4) *reinterpret_cast<uint4*>(d + 4 * J) = x4;
+    if constexpr (XL > 5) *reinterpret_cast<uint4*>(d + 5 * J) = x5;
   };
   auto load_w = [&](int i, BRawT<QT>& w0, BRawT<QT>& w1) __attribute__((always_inline)) {
     const int s = sb + (i >> 1), h = i & 1;
@@ -1335,29 +1335,25 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
 
 template <int QT, int EPI>
 static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
-  // block shape (waves x 32 rows, TM tokens): the widest one whose grid covers the CUs without
-  // split-K (8 x 128: twice the fragment reuse of 64-token blocks; 4 x 64 for the 4096-row
-  // projections of a few hundred tokens), else the one with the most blocks, split over K
-  // (partials by atomic add) until the grid covers the CUs with >= 2 steps (512 k) per part.
+  // block shape (waves x 32 rows, TM tokens), measured over T = 384-2304 on the 8B shapes
+  // (profiles/README.md, round 3): the SwiGLU gate/up (28672 rows) on 8 x 64 (8 x 128 from
+  // 2048 tokens: twice the fragment reuse once the grid is many rounds deep); the 4096- and
+  // 1024-row projections on 4 x 64 - 4 blocks per CU - then split over K (partials by atomic
+  // add) only while the grid does not cover the CUs, >= 2 steps (512 k) per part.
   // LFK_T16_CFG="waves,tokens" pins one (tuning).
   static const char* cfg_env = getenv("LFK_T16_CFG");
   const int ntiles = (a.w.rows + 15) / 16, steps = a.w.K / 256, cus = bmm_cus();
   // grouped: size the shape and split for the expected rows, launch for the most
   const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
-  static const int shapes[3][2] = {{8, 128}, {8, 64}, {4, 64}};
   int nw = 4, tm = 64;
   int pin_nw = 0, pin_tm = 0;
   if (cfg_env && sscanf(cfg_env, "%d,%d", &pin_nw, &pin_tm) == 2 &&
       ((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && pin_tm == 64))) {
     nw = pin_nw;
     tm = pin_tm;
-  } else {
-    for (const auto& sh : shapes) {
-      const long blocks = (long)((ntiles + 2 * sh[0] - 1) / (2 * sh[0])) * ((rows + sh[1] - 1) / sh[1]);
-      nw = sh[0];
-      tm = sh[1];
-      if (blocks >= cus) break;
-    }
+  } else if (EPI == GEMM_SWIGLU) {
+    nw = 8;
+    tm = rows >= 2048 ? 128 : 64;
   }
   const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm, gy_busy = (rows + tm - 1) / tm;
   int split = 1;

@@ -631,8 +631,9 @@ def test_bprep_norm_swiglu_zero(torch):
         assert rel_err(xh.cpu().numpy().astype(np.float32), _swizzle4(h).astype(np.float32)) < 2e-3, G
 
 
-@pytest.mark.parametrize("t", BM_TYPES)
-@pytest.mark.parametrize("T,R,K", [(17, 256, 512), (100, 4096, 1024), (300, 272, 4096), (130, 1024, 14336)])
+@pytest.mark.parametrize("t,T,R,K", [(t, T, R, K) for t in BM_TYPES
+                                     for T, R, K in [(17, 256, 512), (100, 4096, 1024), (300, 272, 4096), (130, 1024, 14336)]]
+                         + [(GGMLType.Q4_K, 2304, 4096, 512)])   # a joint-admission sized grid
 def test_gemm_t16_vs_fp32(torch, t, T, R, K):
     """Prefill GEMM on the tile16 copy: Y = X W^T with X f16 in the 4-group k order and W the
     tile16 dequantisation (f16 arithmetic), against the fp64 product of the same f16 X and the

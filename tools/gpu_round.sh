@@ -39,6 +39,9 @@ for s in "$@"; do
     opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
     gemmb) step gemmb 300 bash -c 'python tools/gemm_bench.py --T 512 && python tools/gemm_bench.py --T 2048' ;;
     gemmt) step gemmt 300 bash -c 'for T in 384 512 2048 2304; do python tools/gemm_bench.py --T $T && python tools/gemm_bench.py --T $T --t16 || exit 1; done; for c in 8,128 8,64 4,64; do LFK_T16_CFG=$c python tools/gemm_bench.py --T 512 --t16 || exit 1; done' ;;
+    gemmt2) step gemmt2 300 bash -c 'for T in 2304 2400 1536; do python tools/gemm_bench.py --T $T --t16 && LFK_T16_CFG=8,128 python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
+    gemmt4) step gemmt4 300 bash -c 'for T in 384 512 1024 2304; do python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
+    gemmt3) step gemmt3 400 bash -c 'for T in 384 1024 1536 2304; do for c in 8,128 8,64 4,64; do echo cfg=$c; LFK_T16_CFG=$c python tools/gemm_bench.py --T $T --t16 || exit 1; done; done' ;;
     t16t) step t16t 400 python -u -m pytest tests/test_kernels_gpu.py -k "t16 or rmsnorm_f16 or attn_prefill" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     gemmpmc) export TMPDIR=/tmp; step gemmpmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
             -d gpurun_out/gemmpmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup
