@@ -1457,9 +1457,12 @@ void Engine::batch_launch(const std::vector<int>& slots) {
   const bool remap = B != bslots_n_ || std::memcmp(h_bslots_, slots.data(), sizeof(int) * B) != 0;
   if (remap && fl_n_ > 0) HIPCHK(hipStreamSynchronize(stream_));
   const int i = (fl_head_ + fl_n_) & 1;
+  struct Par {  // the flight's graph instantiation, reset on every exit
+    int& p;
+    ~Par() { p = 0; }
+  } par{launch_par_};
   launch_par_ = i;
   enqueue_batch_launch(slots, h_btok2_[i]);
-  launch_par_ = 0;
   HIPCHK(hipEventRecord(bev_[i], stream_));
   fl_B_[i] = B;
   fl_b1_[i] = last_b1_;
