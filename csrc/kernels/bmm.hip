@@ -1017,9 +1017,13 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     a.spp = (steps + kparts - 1) / kparts;
     a.kparts = kparts = (steps + a.spp - 1) / a.spp;
     // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K group
-    const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
+    // (LFK_BMM_WT_BPC=2, tuning: two blocks per CU - twice the weight bytes in flight per CU -
+    // where the LDS and the 4 waves / SIMD of the 8-wave block allow it)
+    static const int bpc = std::max(1, std::min(2, env_int("LFK_BMM_WT_BPC", 1)));
+    const int G = std::max(1, std::min(std::max(1, cus * bpc / kparts), wt_k ? (tiles + 7) / 8 : tiles));
     // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
-    const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
+    const size_t lds_need = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
+    const size_t lds = bpc > 1 && lds_need <= 78 * 1024 ? lds_need : std::max<size_t>(lds_need, 81 * 1024);
     const dim3 grid(G * kparts);
     if (wtpd == 1) hipLaunchKernelGGL((bmm_wt_kernel<QT, 1>), grid, dim3(512), lds, s, a);
     else if (wtpd == 3) hipLaunchKernelGGL((bmm_wt_kernel<QT, 3>), grid, dim3(512), lds, s, a);
