@@ -507,7 +507,6 @@ template <int QT, int NW, int PD>
 __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __restrict__ ap, const int bid, const int nbk) {
   const BmmArgs& a = *ap;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int kBlock = NW * 64;
   float* red = reinterpret_cast<float*>(smem);                       // [NW-1][64][4]
   float* rowss = reinterpret_cast<float*>(smem + (NW - 1) * 64 * 16);  // [8 rows][NW waves] folded norm
   __half* xs = reinterpret_cast<__half*>(smem + (NW - 1) * 64 * 16 + 512);
@@ -968,8 +967,9 @@ bool bmm_supported(int type, int K) {
 static int bmm_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      throw std::runtime_error("bmm: cannot query the device's CU count");
     return std::max(1, n);
   }();
   return cus;

@@ -164,9 +164,10 @@ static int resident_blocks(F kern, size_t lds, int block = 256) {
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   int dev = 0, cus = 0, per_cu = 0;
-  hipGetDevice(&dev);
-  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds);
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, block, lds) != hipSuccess)
+    throw std::runtime_error("gemv: device / occupancy query failed");
   const int r = std::max(1, per_cu) * std::max(1, cus);
   cache[key] = r;
   return r;

@@ -82,7 +82,6 @@ __device__ __forceinline__ float wave_superset_threshold(const float (&v)[NE], i
 template <int NE>
 __device__ __forceinline__ int wave_collect(const float (&v)[NE], const int (&idx)[NE], float T, int cap, float* ov,
                                             int* oi) {
-  const int lane = threadIdx.x & 63;
   int base = 0;
 #pragma unroll
   for (int e = 0; e < NE; ++e) {
