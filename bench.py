@@ -251,6 +251,11 @@ def main() -> int:
     p50 = statistics.median(latencies) * 1e3
     dec = sum(eng.decode_s[n0:n1])
     if rank == 0:
+        # the model this run served (the headline config is the default llama3-8b-q4_k_m)
+        from llama_fastapi_k8s_gpu_amd.gguf.synthetic import SPECS
+        _spec = SPECS.get(args.model)
+        model_label = ("Llama-3-8B Q4_K_M" if args.model == "llama3-8b-q4_k_m"
+                       else f"{_spec.name} {_spec.quant.upper()}" if _spec is not None else args.model)
         res = {
             "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
@@ -258,8 +263,8 @@ def main() -> int:
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "q4_k_m weights; f16 (batched decode and prompt prefill MFMA, tile16 copies) / int8 "
                      "(single-row GEMV) activations; fp32 accumulate",
-            "data": "synthetic (random-init Llama-3-8B Q4_K_M GGUF, synthetic chat requests)",
-            "config": {"model": "Llama-3-8B Q4_K_M",
+            "data": f"synthetic (random-init {model_label} GGUF, synthetic chat requests)",
+            "config": {"model": model_label,
                        "global_batch": (1 if tp else world) * min(args.clients, max_batch),
                        "seq_len": args.n_ctx, "parallelism": f"{'tp' if tp else 'dp'}{world}",
                        "clients_per_group": args.clients, "max_batch": max_batch,
