@@ -156,6 +156,17 @@ PYBIND11_MODULE(_hip, m) {
              std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
              return a;
            })
+      .def("step_clk", [](Engine& e) {
+        std::vector<long long> v;
+        {
+          py::gil_scoped_release nogil;
+          v = e.step_clk();
+        }
+        py::array_t<long long> out({(py::ssize_t)5, (py::ssize_t)Engine::kStepClkBlocks, (py::ssize_t)16});
+        std::copy(v.begin(), v.end(), out.mutable_data());
+        return out;
+      })
+      .def("step_clk_zero", &Engine::step_clk_zero)
       .def("kv_state_bytes", &Engine::kv_state_bytes)
       .def("kv_save",
            [](Engine& e, int n) {
@@ -372,8 +383,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
                           int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,
                           int debug_stop, uintptr_t dbg_clk, int batch, uintptr_t slots, size_t slot_stride,
-                          uintptr_t out_h) {
+                          uintptr_t out_h, uintptr_t qkv_raw, size_t qkv_ld, size_t k_off, size_t v_off, uintptr_t ss,
+                          float inv_k, float eps) {
     AttnDecodeArgs a;
+    a.qkv_raw = P<float>(qkv_raw); a.qkv_ld = qkv_ld; a.k_off = k_off; a.v_off = v_off;
+    a.ss = P<float>(ss); a.inv_k = inv_k; a.eps = eps;
     if (batch > 0) {  // rows b: query q + b*n_head*hd, slot slots[b], position pos[b], own workspaces
       a.batch = batch; a.slots = P<int>(slots); a.slot_stride = slot_stride;
       a.q_stride = (size_t)n_head * hd; a.out_stride = (size_t)n_head * hd;
@@ -391,7 +405,33 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("pos"), py::arg("n_ctx"), py::arg("n_head"), py::arg("n_kv"),
      py::arg("hd"), py::arg("scale"), py::arg("part"), py::arg("out"), py::arg("stream"), py::arg("counters"),
      py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0, py::arg("batch") = 0, py::arg("slots") = 0,
-     py::arg("slot_stride") = 0, py::arg("out_h") = 0);
+     py::arg("slot_stride") = 0, py::arg("out_h") = 0, py::arg("qkv_raw") = 0, py::arg("qkv_ld") = 0,
+     py::arg("k_off") = 0, py::arg("v_off") = 0, py::arg("ss") = 0, py::arg("inv_k") = 0.f, py::arg("eps") = 1e-5f);
+  // split-K Q|K|V (BmmArgs::qkv_sk) over tile16 copies: RoPE'd partial sums added into out [B][ldo]
+  // (Q at 0, K at nq, V at nq + nkv), the rows' sums of squares into ss_out [B]
+  m.def("bmm_qkv_sk", [](uintptr_t wq, int tq, int nq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nkv, int K,
+                         uintptr_t xf, int ldxf, uintptr_t norm, float eps, int B, uintptr_t out, int ldo,
+                         uintptr_t ss_out, uintptr_t pos, uintptr_t rope, int head_dim, int n_ctx, uintptr_t stream,
+                         uintptr_t zero, int zero_n, uintptr_t dbg_clk) {
+    BmmArgs a;
+    a.w = make_qmat(P<void>(wq), tq, nq, K); a.n_out = nq; a.out = P<float>(out); a.ldo = ldo; a.B = B;
+    a.nseg = 3;
+    a.seg_base[1] = P<uint8_t>(wk); a.seg_rows[1] = nkv; a.seg_out[1] = P<float>(out) + nq;
+    a.seg_base[2] = P<uint8_t>(wv); a.seg_rows[2] = nkv; a.seg_out[2] = P<float>(out) + nq + nkv;
+    a.seg_split = tk != tq ? 1 : tv != tq ? 2 : 3;
+    a.type2 = tk != tq ? tk : tv != tq ? tv : 0;
+    a.qkv_sk = true;
+    a.qkv.pos = P<int>(pos); a.qkv.rope = P<float2>(rope); a.qkv.head_dim = head_dim; a.qkv.n_ctx = n_ctx;
+    a.xf = P<float>(xf); a.ldxf = ldxf; a.norm_w = P<float>(norm); a.eps = eps; a.ss_out = P<float>(ss_out);
+    a.zero = P<float>(zero); a.zero_n = zero_n;
+    a.dbg_clk = P<long long>(dbg_clk);
+    bmm(a, S(stream));
+    hip_ok("bmm_qkv_sk");
+  }, py::arg("wq"), py::arg("tq"), py::arg("nq"), py::arg("wk"), py::arg("tk"), py::arg("wv"), py::arg("tv"),
+     py::arg("nkv"), py::arg("K"), py::arg("xf"), py::arg("ldxf"), py::arg("norm"), py::arg("eps"), py::arg("B"),
+     py::arg("out"), py::arg("ldo"), py::arg("ss_out"), py::arg("pos"), py::arg("rope"), py::arg("head_dim"),
+     py::arg("n_ctx"), py::arg("stream"), py::arg("zero") = 0, py::arg("zero_n") = 0, py::arg("dbg_clk") = 0);
+  m.def("bmm_qkv_sk_supported", &bmm_qkv_sk_supported);
   m.def("attn_decode_workspace_floats", &attn_decode_workspace_floats);
   m.def("attn_prefill", [](uintptr_t q, uintptr_t kc, uintptr_t vc, int T, int pos0, int n_ctx, int n_head, int n_kv,
                            int hd, float scale, uintptr_t out, uintptr_t stream, bool out_bf16, bool out_h) {

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   const bool stamp = TL && threadIdx.x == 0;
   long long* const tl = TL ? a.dbg_clk + 16 * ((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) : nullptr;
 #define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) tl[(i) + 1] = wall_clock64(); } } while (0)
-  if constexpr (TL) { if (stamp) tl[0] = wall_clock64(); }
+  if constexpr (TL) { if (stamp) { tl[0] = wall_clock64(); tl[15] = xcc_id(); } }
   if ((int)blockIdx.z == (a.batch > 0 ? a.batch : 1)) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;
@@ -133,6 +133,14 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     a.counters += 64 * b;
     a.out += (size_t)b * a.out_stride;
     if (a.out_h) a.out_h += (size_t)b * a.out_h_stride;
+    if (a.qkv_raw) a.qkv_raw += (size_t)b * a.qkv_ld;
+  }
+  // split-K Q|K|V (batched): q / k / v are RoPE'd unnormalised sums, this row's RMSNorm scale is
+  // applied here (q is read from the raw sums)
+  float rs = 1.f;
+  if (a.qkv_raw) {
+    rs = rsqrtf(a.ss[a.batch > 0 ? blockIdx.z : 0] * a.inv_k + a.eps);
+    a.q = a.qkv_raw;
   }
   const int kvh = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -146,6 +154,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   __shared__ float wm[4][G], wl[4][G];
   __shared__ __attribute__((aligned(16))) float wo[4][G][HD];
   __shared__ int last;
+  __shared__ __attribute__((aligned(16))) h2v kvn[2][HD / 2];  // split-K Q|K|V: the new key / value (f16)
 
   // ---- 1. loads (speculative), then the position
   const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
@@ -154,9 +163,15 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   for (int i = 0; i < NLD; ++i) kr[i] = *reinterpret_cast<const uint4*>(a.k_cache + row + 8 * i);
 #pragma unroll
   for (int i = 0; i < NLD; ++i) vr[i] = *reinterpret_cast<const uint4*>(a.v_cache + row + 8 * i);
+  const float qscale = a.scale * rs;
   for (int i = tid; i < G * HD / 2; i += 256) {
     const float2 qv = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
-    qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv.x * a.scale), (_Float16)(qv.y * a.scale)};
+    qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv.x * qscale), (_Float16)(qv.y * qscale)};
+  }
+  if (a.qkv_raw && tid < HD) {  // the new key (tid < HD / 2) and value pairs, normalised, f16
+    const int kv = tid / (HD / 2), pr = tid % (HD / 2);
+    const float2 v = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
+    kvn[kv][pr] = h2v{(_Float16)(v.x * rs), (_Float16)(v.y * rs)};
   }
   const int L = min(*a.pos + 1, a.n_ctx);
   LFK_STAMP(0);
@@ -167,6 +182,20 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = vr[i];
   __syncthreads();  // qs (and this wave's vs rows)
   LFK_STAMP(1);
+  if (a.qkv_raw && key == L - 1) {
+    // the new position: its cache rows are written here (this launch's only reader of them is
+    // this lane), and its key / value slices replace the speculatively loaded stale rows
+    const uint4* kn = reinterpret_cast<const uint4*>(&kvn[0][sub * (DPL / 2)]);
+    const uint4* vn = reinterpret_cast<const uint4*>(&kvn[1][sub * (DPL / 2)]);
+#pragma unroll
+    for (int i = 0; i < NLD; ++i) {
+      kr[i] = kn[i];
+      const uint4 v = vn[i];
+      *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = v;
+      *reinterpret_cast<uint4*>(const_cast<__half*>(a.k_cache) + row + 8 * i) = kr[i];
+      *reinterpret_cast<uint4*>(const_cast<__half*>(a.v_cache) + row + 8 * i) = v;
+    }
+  }
   if (a.debug_stop == 2) {
     if (__half2float(vs[wave][kw][sub]) == 1234.f) a.out[tid] = 1.f;
     return;
@@ -401,6 +430,8 @@ void attn_decode(const AttnDecodeArgs& a, hipStream_t s) {
     if (!a.slots || a.n_kv_head > 64 || a.part_stride < attn_decode_workspace_floats(a.n_ctx, a.n_head, a.head_dim))
       throw std::runtime_error("attn_decode: bad batched arguments");
   }
+  if (a.qkv_raw && (a.batch < 1 || !a.ss || a.qkv_ld % 2 || a.k_off % 2 || a.v_off % 2 || touch))
+    throw std::runtime_error("attn_decode: split-K Q|K|V arguments");
   // z: the rows (batched) or one; the weight-touch plane, if any, is the next z index
   dim3 grid(a.n_kv_head, (a.n_ctx + CH - 1) / CH, (a.batch > 0 ? a.batch : 1) + (touch ? 1 : 0));
   if (a.head_dim == 128) launch_attn_decode<128>(a, G, grid, s);

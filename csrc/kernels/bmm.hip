@@ -516,7 +516,10 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __
   // microbenchmark timeline: [0] entry [1] weights issued [2] x staged [3] first tile computed
   // [4] exit [5] tiles done by the block
   long long* clk = a.dbg_clk ? a.dbg_clk + (size_t)bid * 8 : nullptr;
-  if (clk && tid == 0) clk[0] = wall_clock64();
+  if (clk && tid == 0) {
+    clk[0] = wall_clock64();
+    clk[6] = xcc_id();
+  }
   // segments (Q|K|V in one launch): tile index -> (matrix, local tile)
   const int t1 = (a.n_out + 15) >> 4;
   const int t2 = t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0);
@@ -759,18 +762,56 @@ void bmm_kernel(BmmArgs a, BmmArgs a2) {
 
 // ---------------------------------------------------------------- wave-owned tiles
 // One-part projections with many tiles (dense SwiGLU gate/up: 1792 tiles = 7 per CU for the 8B
-// shape; the head): every WAVE streams whole tiles - all K steps - with PD steps of weights in
-// flight in registers, so there is no cross-wave reduction and no barrier after the x staging.
-// bmm_kernel splits a tile's steps over the block's 8 waves (2 steps per wave at K = 4096):
-// every tile ended in an LDS reduction behind two block barriers, each wave had one step in
-// flight, and 46 % of the wave cycles sat in s_waitcnt / barriers (r2g PMC).
-// One block per CU (the launcher asks for more than half the LDS, so two never share a CU):
-// the x slice is staged once per CU (bmm_kernel staged it twice), and block b takes the
-// contiguous tile range [t0, t0 + tn) of an even split - wave w its tiles t0 + w + i * NW.
+// shape; the head) and the split-K ones (Wo, down, Q|K|V): every WAVE streams whole tiles of its
+// block's K part with PD steps of weights in flight in registers, so there is no cross-wave
+// reduction and no barrier after the x staging. bmm_kernel splits a tile's steps over the block's
+// 8 waves (2 steps per wave at K = 4096): every tile ended in an LDS reduction behind two block
+// barriers, each wave had one step in flight, and 46 % of the wave cycles sat in s_waitcnt /
+// barriers (r2g PMC).
+// Blocks are (K part kp, tile group): part > 1 adds its partial tiles atomically. Gate/up, Wo and
+// down run one block per CU (the launcher asks for more than half the LDS, so two never share a
+// CU): the x slice is staged once per CU, and block b takes the contiguous tile range
+// [t0, t0 + tn) of an even split - wave w its tiles t0 + w + i * NW. Split-K Q|K|V groups are
+// a.tpg tiles of one weight type (run A: segments [0, seg_split), run B: the rest, type QT2).
 // Weights rotate through PD + 1 register buffers with fixed roles (the step loop unrolled by
 // PD + 1): no register copies, so no wait on in-flight loads before they are needed.
+
+// x staging of one K part with the RMSNorm folded in (split-K Q|K|V): rows xf[b][k0, k0 + kn) as
+// f16(x * norm_w) in bmm's 4-group order, each row's sum of squares over the part added to
+// rowss[b] (LDS, zeroed by the caller). All loads of a batch go out before any use (one memory
+// round trip); kn % 256 == 0, so the 64 float4 of a wave lie in one row.
+template <int NW>
+__device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
+                                                  int tid, int lane) {
+  constexpr int kBlock = NW * 64, U = 4;
+  const int nv = kn >> 2, n = a.B * nv;
+  for (int i0 = 0; i0 < n; i0 += U * kBlock) {
+    float4 v[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * kBlock + tid, n - 1);
+      const int b = i / nv, c = i - b * nv;
+      v[u] = *reinterpret_cast<const float4*>(a.xf + (size_t)b * a.ldxf + k0 + 4 * c);
+      w[u] = *reinterpret_cast<const float4*>(a.norm_w + k0 + 4 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int iw = i0 + u * kBlock + (tid & ~63);  // the wave's first index (wave-uniform)
+      if (iw >= n) break;
+      const int i = iw + lane;
+      const int b = i / nv, c = i - b * nv;
+      const float4 x = v[u], ww = w[u];
+      const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
+      const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
+      *reinterpret_cast<uint2*>(xs + b * ldx + 4 * c) = make_uint2(as_u(p0), as_u(p1));
+      const float ss = wave_sum_fast(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+      if (lane == 0) atomicAdd(rowss + b, ss);
+    }
+  }
+}
+
 template <int QT, int PD>
-__global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
+__device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   constexpr int NW = 8, R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* rowss = reinterpret_cast<float*>(smem);            // [8 rows][NW waves] folded norm
@@ -783,14 +824,33 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const int kparts = a.kparts, kp = blockIdx.x % kparts, grp = blockIdx.x / kparts, G = gridDim.x / kparts;
   const int s0 = kp * a.spp, ns = min(steps, s0 + a.spp) - s0;  // this part's steps [s0, s0 + ns)
   const int k0 = s0 * 256, kn = ns * 256, ldx = kn + 8;
-  const int tiles = (a.n_out + 15) >> 4, bid = blockIdx.x;
-  const int t0 = grp * (tiles / G) + min(grp, tiles % G);
-  const int tn = tiles / G + (grp < tiles % G ? 1 : 0);
+  const int bid = blockIdx.x;
+  // segments (split-K Q|K|V): global tile g -> (segment, local tile)
+  const int t1 = (a.n_out + 15) >> 4;
+  const int t2 = t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0);
+  const int t3 = t2 + (a.nseg > 2 ? (a.seg_rows[2] + 15) >> 4 : 0);
+  const int tiles = a.nseg == 1 ? t1 : a.nseg == 2 ? t2 : t3;
+  auto seg_of = [&](int g) { return g >= t1 ? (g >= t2 ? 2 : 1) : 0; };
+  auto seg_first = [&](int sg) { return sg == 0 ? 0 : sg == 1 ? t1 : t2; };
+  int t0, tn;
+  if (a.qkv_sk) {  // groups of a.tpg tiles inside one run (run B: from segment seg_split on)
+    const int ta = a.seg_split >= a.nseg ? tiles : a.seg_split == 1 ? t1 : t2;
+    const int gl = run == 0 ? grp : grp - a.nb1;
+    t0 = (run == 0 ? 0 : ta) + gl * a.tpg;
+    tn = max(0, min(a.tpg, (run == 0 ? ta : tiles) - t0));
+  } else {
+    t0 = grp * (tiles / G) + min(grp, tiles % G);
+    tn = tiles / G + (grp < tiles % G ? 1 : 0);
+  }
   const int nt = wave < tn ? (tn - 1 - wave) / NW + 1 : 0;  // this wave's tiles (wave-uniform)
   const int N = nt * ns;                                    // ... as one sequence of steps
   const int SB = t16_step_bytes(QT);
   auto tile_of = [&](int i) { return t0 + wave + i * NW; };
-  auto tbase = [&](int i) { return a.w.base + ((size_t)tile_of(i) * steps + s0) * SB; };
+  auto tbase = [&](int i) {
+    const int g = tile_of(i), sg = seg_of(g);
+    const uint8_t* base = sg == 0 ? a.w.base : sg == 1 ? a.seg_base[1] : a.seg_base[2];
+    return base + ((size_t)(g - seg_first(sg)) * steps + s0) * SB;
+  };
   BRawT<QT> buf[R][2];
   int li = 0, ls = 0;  // load cursor: the wave's tile, step
   const uint8_t* lp = nt > 0 ? tbase(0) : a.w.base;
@@ -805,19 +865,47 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   // microbenchmark timeline (wave 0, as bmm_kernel's): [0] entry [1] weights issued [2] x staged
   // [3] first tile computed [4] exit [5] tiles of wave 0
   long long* clk = a.dbg_clk ? a.dbg_clk + (size_t)bid * 8 : nullptr;
-  if (clk && tid == 0) clk[0] = wall_clock64();
+  if (clk && tid == 0) {
+    clk[0] = wall_clock64();
+    clk[6] = xcc_id();
+  }
+  const bool col_ok = r16 < a.B;
+  // split-K Q|K|V: the row's position and the RoPE factors of the wave's first tile, loaded
+  // beside the weights (the epilogue of each tile prefetches the next tile's)
+  int pos = 0;
+  float2 rc[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
+  auto rope_load = [&](int i) {
+    const int g = tile_of(i), sg = seg_of(g);
+    const int row = (g - seg_first(sg)) * 16 + 4 * kq, hd = a.qkv.head_dim;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) rc[j] = a.qkv.rope[(size_t)pos * (hd >> 1) + ((row + 2 * j) % hd >> 1)];
+  };
+  if (a.qkv_sk) {
+    pos = min(max(a.qkv.pos[col_ok ? r16 : 0], 0), a.qkv.n_ctx - 1);
+    if (nt > 0) rope_load(0);
+    if (tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
+  }
   // the first PD steps go out before the x staging round trip
 #pragma unroll
   for (int p = 0; p < PD; ++p)
     if (p < N) load_next(buf[p]);
   if (clk && tid == 0) clk[1] = wall_clock64();
-  bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+  if (a.zero) {  // side job: zero the next consumer's accumulation rows
+    float4* z = reinterpret_cast<float4*>(a.zero);
+    for (int i = bid * 512 + tid; i < (a.zero_n >> 2); i += gridDim.x * 512) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (a.ss_out) {
+    lds_barrier(false);  // rowss zeroed
+    stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
+  } else {
+    bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+  }
   __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
+  if (a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
-  const bool col_ok = r16 < a.B;
-  float cs = 1.f;  // folded norm: this lane's column scale
-  if (a.xf) {
+  float cs = 1.f;  // folded norm (one K part): this lane's column scale
+  if (a.xf && !a.ss_out) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) t += rowss[(col_ok ? r16 : 0) * NW + w];
@@ -828,9 +916,28 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   int ci = 0, cstep = 0;  // compute cursor (step s0 + cstep of tile ci)
   auto finish = [&]() {   // tile ci is complete in acc + acc2: C[row 4kq + i][col r16]
     acc += acc2;
-    if (a.xf) acc *= cs;
+    if (a.xf && !a.ss_out) acc *= cs;
     const int gt = tile_of(ci);
-    if (a.swiglu_epi) {
+    if (a.qkv_sk) {
+      const int sg = seg_of(gt), kind = sg == 0 ? a.qkv.kind[0] : sg == 1 ? a.qkv.kind[1] : a.qkv.kind[2];
+      const int n_out = sg == 0 ? a.n_out : sg == 1 ? a.seg_rows[1] : a.seg_rows[2];
+      float* o = (sg == 0 ? a.out : sg == 1 ? a.seg_out[1] : a.seg_out[2]) + (size_t)r16 * a.ldo;
+      const int row0 = (gt - seg_first(sg)) * 16 + 4 * kq;
+      f4_t y = acc;
+      if (kind < 2) {  // RoPE on the adjacent pairs (0, 1), (2, 3) of this lane's rows
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          y[2 * j] = acc[2 * j] * rc[j].x - acc[2 * j + 1] * rc[j].y;
+          y[2 * j + 1] = acc[2 * j] * rc[j].y + acc[2 * j + 1] * rc[j].x;
+        }
+      }
+      if (ci + 1 < nt) rope_load(ci + 1);
+      if (col_ok) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (row0 + i < n_out) atomicAdd(o + row0 + i, y[i]);
+      }
+    } else if (a.swiglu_epi) {
       // rows 0-7 (lanes 0-31): gate of features 8 gt + 4 kq + i; rows 8-15 (lanes 32-63): up
       f4_t up;
 #pragma unroll
@@ -875,6 +982,26 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
     clk[4] = wall_clock64();
     clk[5] = nt;
   }
+}
+
+// (the body reads its arguments through the kernarg segment pointer: a reference to the by-value
+// parameter made the compiler copy the whole block to scratch, as in bmm_kernel)
+template <int QT, int PD>
+__global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  wt_body<QT, PD>(*ka, 0);
+  (void)a;
+}
+
+// split-K Q|K|V over two weight types (Q|K Q4_K + V Q6_K / Q5_K on the bumped layers of the
+// K-quant mixes, Q Q4_K + K|V Q8_0 in Mixtral's): groups from a.nb1 on are run B, type QT2 (a
+// uniform branch per block; each run's body keeps its own registers)
+template <int QT, int QT2, int PD>
+__global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD>(*ka, 1);
+  else wt_body<QT, PD>(*ka, 0);
+  (void)a;
 }
 
 // ---------------------------------------------------------------- activation prep
@@ -1030,6 +1157,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), grid, dim3(512), lds, s, a);
     return;
   }
+  if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");
   if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
     // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
     static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4, 8 or 16
@@ -1089,6 +1217,42 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
 }
 
+// split-K Q|K|V: (K part, group of a.tpg tiles of one run) blocks, every wave one tile of the
+// part (tuning: LFK_QKV_SK_PARTS K parts, LFK_QKV_SK_TPG tiles per group)
+template <int QT, int QT2>
+static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
+  int ta = 0, tb = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    const int t = ((i == 0 ? a.n_out : a.seg_rows[i]) + 15) / 16;
+    if (i < a.seg_split) ta += t;
+    else tb += t;
+  }
+  const int steps = a.w.K / 256;
+  static const int parts_env = env_int("LFK_QKV_SK_PARTS", 8);
+  static const int tpg_env = env_int("LFK_QKV_SK_TPG", 8);
+  const int kparts = std::max(1, std::min(steps, parts_env));
+  a.spp = (steps + kparts - 1) / kparts;
+  a.kparts = (steps + a.spp - 1) / a.spp;
+  a.tpg = std::max(1, tpg_env);
+  const int ga = (ta + a.tpg - 1) / a.tpg, gb = (tb + a.tpg - 1) / a.tpg;
+  a.nb1 = ga;
+  const dim3 grid((ga + gb) * a.kparts);
+  const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
+  if constexpr (QT2 == 0) {
+    hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+  } else {
+    hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
+  }
+}
+
+bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B) {
+  if (B < 1 || B > 8 || K % 256 || !bmm_supported(tq, K) || !bmm_supported(tk, K) || !bmm_supported(tv, K)) return false;
+  const int t2 = tk != tq ? tk : tv;
+  if (tk != tq && tv != tk) return false;  // at most two runs: Q [| K] of one type, the rest of another
+  if (t2 == tq) return true;
+  return tq == T_Q4_K && (t2 == T_Q6_K || t2 == T_Q5_K || t2 == T_Q8_0);
+}
+
 static void bmm_check(const BmmArgs& a) {
   if (!bmm_supported(a.w.type, a.w.K)) throw std::runtime_error("bmm: unsupported type / K");
   if (a.B < 1 || a.B > kBmmMaxRows) throw std::runtime_error("bmm: 1 <= B <= 16");
@@ -1097,7 +1261,7 @@ static void bmm_check(const BmmArgs& a) {
   if (a.swiglu_epi && (a.qkv_epi || a.nseg != 1 || !bmm_qkv_fits(a.w.K, a.B) || a.n_out % 16 || !a.h_out ||
                        a.ldh_out < a.n_out / 2 || a.ldh_out % 4))
     throw std::runtime_error("bmm: swiglu epilogue");
-  if (a.xf && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))
+  if (a.xf && !a.qkv_sk && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))
     throw std::runtime_error("bmm: folded norm");
   if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi && !a.one_part)
     throw std::runtime_error("bmm: store_out needs one K part");
@@ -1108,6 +1272,15 @@ static void bmm_check(const BmmArgs& a) {
   if (a.ew && a.swiglu_epi && (a.n_out + 15) / 16 / a.tiles_per_expert > 64) throw std::runtime_error("bmm: <= 64 experts");
   if (a.ew && !a.swiglu_epi && (a.xf || a.qkv_epi || a.one_part))
     throw std::runtime_error("bmm: the MoE down projection runs split-K (whole-expert parts)");
+  if (a.qkv_sk) {
+    if (a.B > 8 || a.qkv_epi || a.swiglu_epi || a.ew || a.one_part || a.store_out || !a.qkv.pos || !a.qkv.rope ||
+        a.qkv.head_dim % 2 || a.qkv.n_ctx < 1 || a.seg_split < 1 || a.seg_split > a.nseg ||
+        (a.seg_split < a.nseg && !bmm_qkv_sk_supported(a.w.type, a.type2, a.type2, a.w.K, a.B)))
+      throw std::runtime_error("bmm: split-K Q|K|V arguments");
+    if (a.xf && (!a.norm_w || !a.ss_out || a.ldxf < a.w.K || a.ldxf % 4)) throw std::runtime_error("bmm: split-K Q|K|V norm");
+  }
+  if (a.ss_out && !(a.qkv_sk && a.xf)) throw std::runtime_error("bmm: ss_out needs the split-K Q|K|V norm");
+  if (a.zero && (a.zero_n % 4 || reinterpret_cast<uintptr_t>(a.zero) % 16)) throw std::runtime_error("bmm: zero side job alignment");
 }
 
 void bmm(const BmmArgs& a0, hipStream_t s) {
@@ -1116,6 +1289,19 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
   a.fence_sync = fence;
   bmm_check(a);
   if (a.n_out <= 0) return;
+  if (a.qkv_sk) {
+    const bool two = a.seg_split < a.nseg;
+    const int t2 = two ? a.type2 : 0;
+    if (a.w.type == T_Q4_K && t2 == T_Q6_K) launch_qkv_sk<T_Q4_K, T_Q6_K>(a, s);
+    else if (a.w.type == T_Q4_K && t2 == T_Q5_K) launch_qkv_sk<T_Q4_K, T_Q5_K>(a, s);
+    else if (a.w.type == T_Q4_K && t2 == T_Q8_0) launch_qkv_sk<T_Q4_K, T_Q8_0>(a, s);
+    else if (t2 != 0) throw std::runtime_error("bmm: split-K Q|K|V type pair");
+    else if (a.w.type == T_Q4_K) launch_qkv_sk<T_Q4_K, 0>(a, s);
+    else if (a.w.type == T_Q5_K) launch_qkv_sk<T_Q5_K, 0>(a, s);
+    else if (a.w.type == T_Q6_K) launch_qkv_sk<T_Q6_K, 0>(a, s);
+    else launch_qkv_sk<T_Q8_0, 0>(a, s);
+    return;
+  }
   switch (a.w.type) {
     case T_Q4_K: launch_bmm<T_Q4_K>(a, s); break;
     case T_Q5_K: launch_bmm<T_Q5_K>(a, s); break;

@@ -127,8 +127,25 @@ struct BmmArgs {
   bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
   bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block wall_clock64 stamps [grid][8]
-  int nb1 = 0;                     // bmm_qkv2: blocks of the first run (set by the launcher)
+  int nb1 = 0;                     // bmm_qkv2: blocks of the first run; split-K Q|K|V: first group of run B
+  // Split-K Q|K|V (qkv_sk, batched decode, B <= 8): segments 0..nseg-1 (Q, K, V rows; kinds in
+  // qkv.kind) are summed over K parts into seg_out (atomic adds into zeroed rows, ldo shared),
+  // Q and K partial tiles rotated by RoPE first (a rotation is linear, so the sum of rotated
+  // partials is the rotated sum). The RMSNorm is folded in as: x staged as f16(x * norm_w) per
+  // K part from xf, each row's partial sum of squares over the part added to ss_out[b] (by the
+  // part's first tile group only); the consumer (the batched attention) scales row b by
+  // rsqrt(ss_out[b] / K + eps). Segments [seg_split, nseg) are of the launch's second weight type.
+  bool qkv_sk = false;
+  float* ss_out = nullptr;
+  int seg_split = 1;
+  int type2 = 0;                   // weight type of segments [seg_split, nseg)
+  int tpg = 8;                    // tiles per (K part) block group (set by the launcher)
+  // side job of the split-K launches: zero [zero, zero + zero_n) floats (zero_n % 4 == 0)
+  float* zero = nullptr;
+  int zero_n = 0;
 };
+// split-K Q|K|V (BmmArgs::qkv_sk): false = unsupported shape / type mix (caller: one-part path)
+bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B);
 bool bmm_supported(int type, int K);
 bool bmm_qkv_fits(int K, int B);   // the Q|K|V epilogue needs one K part (x slice in LDS)
 bool bmm_norm_fits(int K, int B);  // one K part + the folded RMSNorm's staging shape
@@ -250,6 +267,14 @@ struct AttnDecodeArgs {
   // batched: also write the output as the next projection's bmm input (f16, bmm k swizzle)
   __half* out_h = nullptr;
   size_t out_h_stride = 0;
+  // batched, split-K Q|K|V (BmmArgs::qkv_sk): q / k / v of row b are the RoPE'd but unnormalised
+  // sums qkv_raw[b * qkv_ld + ...] (q at 0, k at k_off, v at v_off), the row's RMSNorm scale is
+  // rsqrt(ss[b] * inv_k + eps); the block holding the new position scales its k / v, writes them
+  // to the caches and uses them in place of the (not yet written) cache rows
+  const float* qkv_raw = nullptr;
+  size_t qkv_ld = 0, k_off = 0, v_off = 0;
+  const float* ss = nullptr;
+  float inv_k = 0.f, eps = 1e-5f;
   static constexpr int kTouchRanges = 6;
   const uint8_t* pf[kTouchRanges] = {};
   size_t pf_bytes[kTouchRanges] = {};

@@ -387,18 +387,24 @@ void Engine::setup_batch_mfma() {
   bg_ = att;
   bg_ffn_ = att && ffn;
   moe_b_ = att && moe && !(bm && bm[0] == '0');
-  const char* wo1 = std::getenv("LFK_BMM_WO1");
-  wo_one_part_ = wo1 && wo1[0] == '1';
-  const char* bt = std::getenv("LFK_BATT_TOUCH");
-  batt_touch_ = bt ? std::atoi(bt) : 0;
-  if (nkv_l_ >= 63) batt_touch_ = 0;
   const char* nf = std::getenv("LFK_BMM_NORM");
   norm_fold_ = !(nf && nf[0] == '0');
-  const char* hf = std::getenv("LFK_BMM_HEAD1");
-  head_fold_ = hf && hf[0] == '1';
+  const char* sk = std::getenv("LFK_QKV_SK");
+  qkv_sk_ = !(sk && sk[0] == '0');
+  if (const char* sc = std::getenv("LFK_STEP_CLK")) {
+    step_clk_layer_ = std::atoi(sc);
+    step_clk_ = (long long*)dalloc(sizeof(long long) * 5 * kStepClkBlocks * 16);
+    HIPCHK(hipMemsetAsync(step_clk_, 0, sizeof(long long) * 5 * kStepClkBlocks * 16, stream_));
+  }
   if (!bg_) return;
   const int E = std::max(1, hp_.n_expert);
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
+  {
+    const size_t n = (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16;  // + ss_b_
+    qkv_b_ = (float*)dalloc(sizeof(float) * n);
+    HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * n, stream_));
+    ss_b_ = qkv_b_ + (size_t)bmax_ * (nq_ + 2 * nkvd_);
+  }
   hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_) * (moe_b_ ? E : 1));
   if (moe_b_) ew_b_ = (float*)dalloc(sizeof(float) * bmax_ * E);
   // the batched path reads its own copy of the weights, laid out per 16-row tile (bmm.hip)
@@ -457,6 +463,21 @@ void Engine::setup_batch_mfma() {
     if (hp_.n_expert > 0) t16 = t16 && L.down_exps.K % 256 == 0 && L.gu_exps.rows % 16 == 0;
   }
   prefill_t16_ = t16;
+}
+
+std::vector<long long> Engine::step_clk() {
+  std::vector<long long> h((size_t)5 * kStepClkBlocks * 16, 0);
+  if (step_clk_) {
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(h.data(), step_clk_, sizeof(long long) * h.size(), hipMemcpyDeviceToHost));
+  }
+  return h;
+}
+
+void Engine::step_clk_zero() {
+  if (!step_clk_) return;
+  HIPCHK(hipStreamSynchronize(stream_));
+  HIPCHK(hipMemset(step_clk_, 0, sizeof(long long) * 5 * kStepClkBlocks * 16));
 }
 
 void Engine::check_device_err() {
@@ -949,9 +970,10 @@ void Engine::begin_slot_state(int slot, const std::vector<int>& prompt, const Sa
 
 // bmm over B rows: groups of kBmmMaxRows columns (one more weight stream per group)
 void Engine::bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B,
-                      hipStream_t s) {
+                      hipStream_t s, long long* dbg) {
   for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
     BmmArgs a;
+    a.dbg_clk = b0 == 0 ? dbg : nullptr;
     a.w = w; a.xh = xh + (size_t)b0 * ldh; a.ldh = ldh;
     a.out = out + (size_t)b0 * ldo; a.ldo = ldo; a.n_out = n_out;
     a.B = std::min(kBmmMaxRows, B - b0);
@@ -993,10 +1015,27 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
   // attention / FFN RMSNorm folded into the one-part projections' x staging (no prep launch)
   const bool fnorm = fused && norm_fold_ && bmm_norm_fits(d, B);
-  if (!fnorm) bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
-  // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers;
-  // a side-stream graph branch for the V run measured no gain)
-  {
+  // Q|K|V split over K (the default at B <= 8): RoPE'd partial sums into qkv_b_, normalised and
+  // appended to the caches by the attention
+  const bool sk = qkv_sk_ && bmm_qkv_sk_supported(L.t_wq.type, L.t_wk.type, L.t_wv.type, d, B);
+  if (sk) {
+    BmmArgs a;
+    a.w = L.t_wq; a.n_out = L.t_wq.rows; a.out = qkv_b_; a.ldo = ncol; a.B = B;
+    a.nseg = 3;
+    a.seg_base[1] = L.t_wk.base; a.seg_rows[1] = L.t_wk.rows; a.seg_out[1] = qkv_b_ + nq_;
+    a.seg_base[2] = L.t_wv.base; a.seg_rows[2] = L.t_wv.rows; a.seg_out[2] = qkv_b_ + nq_ + nkvd_;
+    const int tq = L.t_wq.type, tk = L.t_wk.type, tv = L.t_wv.type;
+    a.seg_split = tk != tq ? 1 : tv != tq ? 2 : 3;
+    a.type2 = tk != tq ? tk : tv != tq ? tv : 0;
+    a.qkv_sk = true;
+    a.qkv.pos = bpos_; a.qkv.rope = rope_; a.qkv.head_dim = hd; a.qkv.n_ctx = opt_.n_ctx;
+    a.xf = x_; a.ldxf = d; a.norm_w = L.attn_norm; a.eps = hp_.rms_eps; a.ss_out = ss_b_;
+    a.dbg_clk = clk_of(l, 0);
+    bmm(a, s);
+  } else {
+    if (!fnorm) bprep_rows(x_, d, false, L.attn_norm, d, B, fused ? nullptr : qkv_, fused ? 0 : B * ncol, s);
+    // Q|K|V: one launch per run of equal weight type (Q4_K_M: one, or Q|K + V on bumped layers;
+    // a side-stream graph branch for the V run measured no gain)
     const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
     float* o[3] = {qkv_, qkv_ + nq_, qkv_ + nq_ + nkvd_};
     std::vector<BmmArgs> rl;
@@ -1015,6 +1054,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
         if (fnorm) {
           a.xf = x_ + (size_t)b0 * d; a.ldxf = d; a.norm_w = L.attn_norm; a.eps = hp_.rms_eps;
         }
+        if (rl.empty() && b0 == 0) a.dbg_clk = clk_of(l, 0);
         if (fused) {
           a.qkv_epi = true;
           for (int k = 0; k < a.nseg; ++k) a.qkv.kind[k] = i + k;
@@ -1030,9 +1070,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     // bumped layers (Q|K Q4_K + V Q6_K): both runs in one launch
     if (!(rl.size() == 2 && B <= kBmmMaxRows && bmm_qkv2(rl[0], rl[1], s)))
       for (const BmmArgs& a : rl) bmm(a, s);
+    if (!fused)
+      rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
   }
-  if (!fused)
-    rope_kv_prefill(qkv_, B, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
   AttnDecodeArgs aa;
   aa.q = q_; aa.k_cache = kcl; aa.v_cache = vcl; aa.pos = bpos_;
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
@@ -1042,27 +1082,21 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.q_stride = nq_; aa.out_stride = nq_;
   aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
   aa.out_h = xh_b_; aa.out_h_stride = nq_;   // the Wo input, already in bmm's f16 layout
-  // weight touch (LFK_BATT_TOUCH bit mask: 1 this layer's Wo, 2 the next layer's Q|K|V - tile16
-  // copies): the latency-bound attention pulls them into the memory-side cache
-  if (batt_touch_ & 1) {
-    aa.pf[0] = L.t_wo.base; aa.pf_bytes[0] = t16_bytes(L.t_wo.type, L.t_wo.rows, L.t_wo.K);
+  if (sk) {
+    aa.qkv_raw = qkv_b_; aa.qkv_ld = ncol; aa.k_off = nq_; aa.v_off = nq_ + nkvd_;
+    aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
   }
-  if ((batt_touch_ & 2) && l + 1 < hp_.n_layer) {
-    const Layer& N = layers_[l + 1];
-    const QMat* nm[3] = {&N.t_wq, &N.t_wk, &N.t_wv};
-    for (int k = 0; k < 3; ++k) {
-      aa.pf[1 + k] = nm[k]->base; aa.pf_bytes[1 + k] = t16_bytes(nm[k]->type, nm[k]->rows, nm[k]->K);
-    }
-  }
-  if (batt_touch_ & 3) aa.pf_sink = attn_cnt_b_ + 63;   // row 0's word 63: kv heads < 63
+  aa.dbg_clk = clk_of(l, 1);
   attn_decode(aa, s);
   tp_begin();
-  if (wo_one_part_ && B <= kBmmMaxRows && bmm_qkv_fits(nq_, B)) {
+  if (sk) {  // Wo also re-zeroes the split-K Q|K|V rows and sums of squares for the next layer
     BmmArgs a;
-    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = acc; a.ldo = d; a.n_out = d; a.B = B; a.one_part = true;
+    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = acc; a.ldo = d; a.n_out = d; a.B = B;
+    a.zero = qkv_b_; a.zero_n = bmax_ * ncol + 16;
+    a.dbg_clk = clk_of(l, 2);
     bmm(a, s);
   } else {
-    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s);
+    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
   }
   tp_end();
   if (moe_b_ && fused) {
@@ -1105,9 +1139,10 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     a.w = L.t_gu; a.xh = xh_b_; a.ldh = d;
     a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
     a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
+    a.dbg_clk = clk_of(l, 3);
     bmm(a, s);
     tp_begin();
-    bmm_rows(L.t_down, hh_b_, F_l_, acc, d, d, B, s);
+    bmm_rows(L.t_down, hh_b_, F_l_, acc, d, d, B, s, clk_of(l, 4));
     tp_end();
     return;
   }
@@ -1132,16 +1167,8 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
   embed_rows(tok_embd_, btok_, B, x_, s);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
-    if (head_fold_ && B <= kBmmMaxRows && bmm_norm_fits(d, B)) {
-      // final norm folded into a one-part head projection that stores the logits
-      BmmArgs a;
-      a.w = t_output_; a.xf = x_; a.ldxf = d; a.norm_w = out_norm_; a.eps = hp_.rms_eps;
-      a.out = logits_b_; a.ldo = V_pad_; a.n_out = V_l_; a.B = B; a.store_out = true;
-      bmm(a, s);
-    } else {
-      bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
-      bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, V_l_, B, s);
-    }
+    bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
+    bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, V_l_, B, s);
   } else {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
     rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, s);

@@ -88,6 +88,11 @@ class Engine : public SlotBackend {
   // KV state of positions [0, n) for save/load_state and prompt caches: `buf` holds
   // [K|V][n_layer][nkv_l][n][hd] f16, in host OR device memory (one strided copy each way;
   // a device-resident snapshot is an HBM-to-HBM copy)
+  // per-block timeline of one layer of the batch step (LFK_STEP_CLK=<layer>, tools/step_blocks.py):
+  // [5 kernels: Q|K|V, attention, Wo, gate/up, down][kStepClkBlocks][16] wall_clock64 stamps
+  static constexpr int kStepClkBlocks = 8192;
+  std::vector<long long> step_clk();
+  void step_clk_zero();
   size_t kv_state_bytes(int n) const { return 2ull * hp_.n_layer * nkv_l_ * (size_t)n * hp_.head_dim * 2; }
   void kv_transfer(void* buf, int n, bool load);
   // hybrid placement: hidden states [T][d] of layer `layer_begin` in, last-row logits out
@@ -219,7 +224,8 @@ class Engine : public SlotBackend {
   // batch_step on the MFMA batched projections (bmm.hip): one layer over the B decode rows
   void enqueue_batch_layer(int l, int B, hipStream_t s);
   void enqueue_batch_step(int B, hipStream_t s);
-  void bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B, hipStream_t s);
+  void bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B, hipStream_t s,
+                long long* dbg = nullptr);
   void bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero, int zero_n,
                   hipStream_t s, int swiglu_group = 32);
   void setup_batch_mfma();
@@ -340,9 +346,19 @@ class Engine : public SlotBackend {
   // RMSNorm folded into the one-part projections' staging (Q|K|V, gate/up: no prep launch;
   // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
   // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)
-  bool norm_fold_ = true, head_fold_ = false;
-  int batt_touch_ = 0;        // batched attention weight touch (LFK_BATT_TOUCH bit mask)
-  bool wo_one_part_ = false;  // Wo as one K part (LFK_BMM_WO1=1, A/B)
+  bool norm_fold_ = true;
+  // Q|K|V as a split-K projection (bmm.hip BmmArgs::qkv_sk, B <= 8): RoPE'd partial sums added
+  // into qkv_b_ [bmax][nq + 2 nkvd] (+ the rows' sums of squares ss_b_ [16]); the batched
+  // attention normalises them and appends the new K / V, the Wo launch re-zeroes both
+  // (LFK_QKV_SK=0: the one-part Q|K|V with the RoPE / KV-append epilogue, A/B)
+  bool qkv_sk_ = true;
+  long long* step_clk_ = nullptr;
+  int step_clk_layer_ = -1;
+  long long* clk_of(int l, int k) const {
+    return l == step_clk_layer_ && step_clk_ ? step_clk_ + (size_t)k * kStepClkBlocks * 16 : nullptr;
+  }
+  float* qkv_b_ = nullptr;
+  float* ss_b_ = nullptr;
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   // a second instantiation of each, for the pipelined launches: consecutive in-flight steps

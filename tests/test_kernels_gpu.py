@@ -702,3 +702,99 @@ def test_rmsnorm_f16_swizzled(torch):
     xf = x.cpu().double()
     ref = (xf / torch.sqrt((xf * xf).mean(1, keepdim=True) + 1e-5) * w.cpu().double()).numpy()
     assert rel_err(_swizzle4(y.float().cpu().numpy()), ref) < 1e-3
+
+
+def _rope_table(n_ctx, hd, theta=5e5):
+    inv = theta ** (-np.arange(0, hd, 2, dtype=np.float64) / hd)
+    ang = np.arange(n_ctx, dtype=np.float64)[:, None] * inv[None, :]
+    return np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32)   # [n_ctx][hd/2][2]
+
+
+def _rope_pairs(y, pos, tab):
+    """RoPE on adjacent pairs (GGUF normal mode) of y [rows] at position pos, rows % hd per head."""
+    hd2 = tab.shape[1]
+    z = y.reshape(-1, hd2, 2).astype(np.float64)
+    c, s = tab[pos, :, 0].astype(np.float64), tab[pos, :, 1].astype(np.float64)
+    return np.stack([z[..., 0] * c - z[..., 1] * s, z[..., 0] * s + z[..., 1] * c], -1).reshape(y.shape)
+
+
+@pytest.mark.parametrize("types", [(GGMLType.Q4_K,) * 3, (GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q6_K),
+                                   (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0)])
+@pytest.mark.parametrize("B", [1, 6, 8])
+@pytest.mark.parametrize("hd,H,Hkv,K", [(128, 32, 8, 4096), (64, 32, 4, 2048)])
+def test_bmm_qkv_splitk_then_attention(torch, types, B, hd, H, Hkv, K):
+    """Split-K Q|K|V (RoPE'd partial sums of f16(x * norm_w) . W, the rows' sums of squares) and the
+    batched attention that normalises them, appends the new K / V at each row's position and
+    attends over the cache + the new key - against fp64 references of both stages."""
+    tq, tk, tv = types
+    if not hip().bmm_qkv_sk_supported(int(tq), int(tk), int(tv), K, B):
+        pytest.skip("type mix outside the split-K launch")
+    rng = np.random.default_rng(B * 31 + hd + int(tv) + int(tk))
+    n_ctx, nq, nkv = 256, H * hd, Hkv * hd
+    mats = []
+    for t, R in ((tq, nq), (tk, nkv), (tv, nkv)):
+        raw, W = make_matrix(t, R, K, rng)
+        dw = dev_bytes(to_planar(t, raw, R, K))
+        tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+        hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+        mats.append((tw, W, dw))
+    X = (rng.standard_normal((B, K)) * 3).astype(np.float32)
+    nw = (0.5 + rng.random(K)).astype(np.float32)
+    eps = 1e-5
+    tab = _rope_table(n_ctx, hd)
+    pos = rng.integers(1, n_ctx, B).astype(np.int32)
+    slots = rng.permutation(8)[:B].astype(np.int32)
+    ldo = nq + 2 * nkv
+    dx, dn = torch.from_numpy(X).cuda(), torch.from_numpy(nw).cuda()
+    dtab, dpos, dslots = torch.from_numpy(tab).cuda(), torch.from_numpy(pos).cuda(), torch.from_numpy(slots).cuda()
+    out = torch.zeros(B, ldo, device="cuda")
+    ss = torch.zeros(16, device="cuda")
+    hip().bmm_qkv_sk(mats[0][0].data_ptr(), int(tq), nq, mats[1][0].data_ptr(), int(tk), mats[2][0].data_ptr(), int(tv),
+                     nkv, K, dx.data_ptr(), K, dn.data_ptr(), eps, B, out.data_ptr(), ldo, ss.data_ptr(),
+                     dpos.data_ptr(), dtab.data_ptr(), hd, n_ctx, stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().astype(np.float64)
+    xw = (X * nw).astype(np.float16).astype(np.float64)
+    ss_ref = (X.astype(np.float64) ** 2).sum(1)
+    assert np.allclose(ss.cpu().numpy()[:B], ss_ref, rtol=1e-5)
+    raw_ref = []
+    for b in range(B):
+        q = _rope_pairs(xw[b] @ mats[0][1].astype(np.float64).T, pos[b], tab)
+        k = _rope_pairs(xw[b] @ mats[1][1].astype(np.float64).T, pos[b], tab)
+        v = xw[b] @ mats[2][1].astype(np.float64).T
+        for name, g, r in (("q", got[b, :nq], q), ("k", got[b, nq:nq + nkv], k), ("v", got[b, nq + nkv:], v)):
+            assert rel_err(g, r) < 3e-3, (b, name, rel_err(g, r))
+        raw_ref.append((q, k, v))
+    # stage 2: the batched attention over the raw sums
+    slot_stride = Hkv * n_ctx * hd
+    Kc = rng.standard_normal((8, Hkv, n_ctx, hd)).astype(np.float16)
+    Vc = rng.standard_normal((8, Hkv, n_ctx, hd)).astype(np.float16)
+    dK, dV = torch.from_numpy(Kc).cuda(), torch.from_numpy(Vc).cuda()
+    part = torch.zeros(B * hip().attn_decode_workspace_floats(n_ctx, H, hd), device="cuda")
+    cnt = torch.zeros(64 * B, dtype=torch.int32, device="cuda")
+    aout = torch.zeros(B, nq, device="cuda")
+    aouth = torch.zeros(B, nq, dtype=torch.float16, device="cuda")
+    scale = 1 / np.sqrt(hd)
+    hip().attn_decode(out.data_ptr(), dK.data_ptr(), dV.data_ptr(), dpos.data_ptr(), n_ctx, H, Hkv, hd, scale,
+                      part.data_ptr(), aout.data_ptr(), stream(), cnt.data_ptr(), batch=B, slots=dslots.data_ptr(),
+                      slot_stride=slot_stride, out_h=aouth.data_ptr(), qkv_raw=out.data_ptr(), qkv_ld=ldo, k_off=nq,
+                      v_off=nq + nkv, ss=ss.data_ptr(), inv_k=1.0 / K, eps=eps)
+    torch.cuda.synchronize()
+    Kg, Vg, ao = dK.cpu().numpy(), dV.cpu().numpy(), aout.cpu().numpy()
+    for b in range(B):
+        q, k, v = raw_ref[b]
+        rs = 1.0 / np.sqrt(ss_ref[b] / K + eps)
+        kn = (k * rs).astype(np.float16).reshape(Hkv, hd)
+        vn = (v * rs).astype(np.float16).reshape(Hkv, hd)
+        s, p = slots[b], pos[b]
+        assert rel_err(Kg[s, :, p].astype(np.float64), kn.astype(np.float64)) < 3e-3
+        assert rel_err(Vg[s, :, p].astype(np.float64), vn.astype(np.float64)) < 3e-3
+        Kr, Vr = Kc[s].copy(), Vc[s].copy()
+        Kr[:, p], Vr[:, p] = kn, vn
+        ref = _attn_ref((q * rs).reshape(H, hd), Kr, Vr, p + 1, scale)
+        assert rel_err(ao[b].reshape(H, hd), ref) < 5e-3, (b, rel_err(ao[b].reshape(H, hd), ref))
+        # rows of the other slots' caches untouched
+    untouched = [s for s in range(8) if s not in set(slots.tolist())]
+    for s in untouched:
+        assert np.array_equal(Kg[s], Kc[s]) and np.array_equal(Vg[s], Vc[s])
+    assert int(cnt.abs().sum()) == 0

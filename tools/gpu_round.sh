@@ -21,6 +21,15 @@ for s in "$@"; do
     attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
     attntl1) step attntl1 200 python tools/attn_timeline.py --rows 1 --L 700 ;;
     bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
+    qkvsk) step qkvsk 300 python -u -m pytest tests/test_kernels_gpu.py -k "qkv_splitk or attn_decode or bmm_rows" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    absk) step absk0 200 env LFK_QKV_SK=0 python tools/batch_bench.py --batches 6,8 --steps 64
+          step absk1 200 python tools/batch_bench.py --batches 6,8 --steps 64
+          step absk0b 200 env LFK_QKV_SK=0 python tools/batch_bench.py --batches 6,8 --steps 64
+          step absk1b 200 python tools/batch_bench.py --batches 6,8 --steps 64 ;;
+    blocks) step blocks1 200 python tools/step_blocks.py --json gpurun_out/blocks_sk1.json
+            step blocks0 200 env LFK_QKV_SK=0 python tools/step_blocks.py --json gpurun_out/blocks_sk0.json ;;
+    stepprof) export TMPDIR=/tmp; step stepprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/sprof -o bstep --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
+          python3 tools/step_kernels.py gpurun_out/sprof/bstep_kernel_trace.csv > gpurun_out/sprof_kernels.txt ;;
     samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     kern) step kern 900 python -m pytest tests/test_kernels_gpu.py -q -p no:cacheprovider ;;
     eng) step eng 900 python -m pytest tests/test_engine_gpu.py -q -p no:cacheprovider ;;
