@@ -312,7 +312,8 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("swiglu") = false);
 
   py::class_<P2PComm>(m, "P2PComm")
-      .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_n"), py::arg("device"))
+      .def(py::init<int, int, int, int, bool>(), py::arg("rank"), py::arg("world"), py::arg("max_n"), py::arg("device"),
+           py::arg("uncached") = true)
       .def("handle", [](const P2PComm& c) { return py::bytes(c.handle()); })
       .def("open", [](P2PComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
@@ -328,6 +329,8 @@ PYBIND11_MODULE(_hip, m) {
         hip_ok("p2p_allgather");
       })
       .def("error", &P2PComm::error)
+      .def_property_readonly("uncached", &P2PComm::uncached)
+      .def("mappings", &P2PComm::mappings)
       .def("reset_error", &P2PComm::reset_error);
 
   m.def("gemv_qkv", [](uintptr_t wq, int tq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nq, int nkv, int K,

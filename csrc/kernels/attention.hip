@@ -45,6 +45,7 @@ __device__ __forceinline__ float2 ld2_sc1(const float* p) {
 }
 
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // Cross-lane helpers without the LDS crossbar: DPP within a row of 16 lanes,
 // v_readlane across rows (the reduction trees below are 2-4 steps, each a few
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     a.pos += b;
     a.part += (size_t)b * a.part_stride;
     a.counters += 64 * b;
-    a.out += (size_t)b * a.out_stride;
+    if (a.out) a.out += (size_t)b * a.out_stride;
     if (a.out_h) a.out_h += (size_t)b * a.out_h_stride;
     if (a.qkv_raw) a.qkv_raw += (size_t)b * a.qkv_ld;
   }
@@ -156,7 +157,21 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   __shared__ int last;
   __shared__ __attribute__((aligned(16))) h2v kvn[2][HD / 2];  // split-K Q|K|V: the new key / value (f16)
 
-  // ---- 1. loads (speculative), then the position
+  // ---- 1. loads: q (and the split-K new key / value) first, then the K / V rows
+  //      (speculative: they do not wait for the device-resident position), so q goes to LDS
+  //      while K / V are in flight, the scores wait for K only and P.V for V
+  constexpr int QPT = (G * HD / 2 + 255) / 256;  // q pairs per thread
+  float2 qv[QPT];
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int i = min(tid + 256 * j, G * HD / 2 - 1);
+    qv[j] = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
+  }
+  float2 nv = make_float2(0.f, 0.f);
+  if (a.qkv_raw && tid < HD) {  // the new key (tid < HD / 2) and value pairs
+    const int kv = tid / (HD / 2), pr = tid % (HD / 2);
+    nv = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
+  }
   const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
   uint4 kr[NLD], vr[NLD];
 #pragma unroll
@@ -164,40 +179,39 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
 #pragma unroll
   for (int i = 0; i < NLD; ++i) vr[i] = *reinterpret_cast<const uint4*>(a.v_cache + row + 8 * i);
   const float qscale = a.scale * rs;
-  for (int i = tid; i < G * HD / 2; i += 256) {
-    const float2 qv = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
-    qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv.x * qscale), (_Float16)(qv.y * qscale)};
+#pragma unroll
+  for (int j = 0; j < QPT; ++j) {
+    const int i = tid + 256 * j;
+    if (i < G * HD / 2) qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv[j].x * qscale), (_Float16)(qv[j].y * qscale)};
   }
-  if (a.qkv_raw && tid < HD) {  // the new key (tid < HD / 2) and value pairs, normalised, f16
-    const int kv = tid / (HD / 2), pr = tid % (HD / 2);
-    const float2 v = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
-    kvn[kv][pr] = h2v{(_Float16)(v.x * rs), (_Float16)(v.y * rs)};
-  }
+  if (a.qkv_raw && tid < HD) kvn[tid / (HD / 2)][tid % (HD / 2)] = h2v{(_Float16)(nv.x * rs), (_Float16)(nv.y * rs)};
   const int L = min(*a.pos + 1, a.n_ctx);
   LFK_STAMP(0);
   if (start >= L || a.debug_stop == 1) return;
 
   const int ns = (L + CH - 1) / CH;
-#pragma unroll
-  for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = vr[i];
-  __syncthreads();  // qs (and this wave's vs rows)
+  __syncthreads();  // qs, kvn
   LFK_STAMP(1);
-  if (a.qkv_raw && key == L - 1) {
+  const bool newkey = a.qkv_raw && key == L - 1;
+  if (newkey) {
     // the new position: its cache rows are written here (this launch's only reader of them is
-    // this lane), and its key / value slices replace the speculatively loaded stale rows
+    // this lane; write-through stores), and its key / value slices replace the speculatively
+    // loaded stale rows
     const uint4* kn = reinterpret_cast<const uint4*>(&kvn[0][sub * (DPL / 2)]);
     const uint4* vn = reinterpret_cast<const uint4*>(&kvn[1][sub * (DPL / 2)]);
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.k_cache), 0, 0x7FFFFFFF, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.v_cache), 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
       kr[i] = kn[i];
-      const uint4 v = vn[i];
-      *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = v;
-      *reinterpret_cast<uint4*>(const_cast<__half*>(a.k_cache) + row + 8 * i) = kr[i];
-      *reinterpret_cast<uint4*>(const_cast<__half*>(a.v_cache) + row + 8 * i) = v;
+      vr[i] = vn[i];
+      const int off = (int)((row + 8 * i) * sizeof(__half));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, kr[i]), rk, off, 0, 16);  // aux 16: sc1
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vr[i]), rv, off, 0, 16);
     }
   }
   if (a.debug_stop == 2) {
-    if (__half2float(vs[wave][kw][sub]) == 1234.f) a.out[tid] = 1.f;
+    if ((float)qs[0][sub][0] == 1234.f) a.out[tid] = 1.f;
     return;
   }
 
@@ -241,6 +255,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
 #pragma unroll
     for (int g = 0; g < G; ++g) ps[wave][g][kw] = sc[g];
   }
+  // this wave's V rows (the wave's own keys: a wave barrier, no block barrier)
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = vr[i];
   LFK_STAMP(2);
   // ---- 2c. P.V over this wave's keys (LDS written by this wave only)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -307,8 +324,10 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     }
     if (ns == 1) {
       const int o = (kvh * G + g) * HD + d;
-      a.out[o] = acc0 / l;
-      a.out[o + 1] = acc1 / l;
+      if (a.out) {
+        a.out[o] = acc0 / l;
+        a.out[o + 1] = acc1 / l;
+      }
       if (a.out_h) {
         a.out_h[swz4(o)] = __float2half(acc0 / l);
         a.out_h[swz4(o + 1)] = __float2half(acc1 / l);
@@ -384,12 +403,42 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     }
     M = mb;
   }
-  if (tid * EPT < G * HD) {
+  // outputs through write-through stores (no dirty L2 lines for the end-of-kernel write-back the
+  // next launch waits for): f32 as sc1 words, the f16 Wo input as one 8-byte sc1 store per 4-group
+  // (the lanes of a group pass their values to its first lane)
+  float r[EPT];
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) {
-      const int o = h * HD + d0 + j;
-      a.out[o] = num[j] / den;
-      if (a.out_h) a.out_h[swz4(o)] = __float2half(num[j] / den);
+  for (int j = 0; j < EPT; ++j) r[j] = num[j] / den;
+  const bool live = tid * EPT < G * HD;
+  if (a.out && live) {
+#pragma unroll
+    for (int j = 0; j < EPT; ++j) st_sc1(a.out + h * HD + d0 + j, r[j]);
+  }
+  if (a.out_h) {
+    static_assert(EPT == 1 || EPT == 2 || EPT % 4 == 0, "4-groups of the f16 output");
+    constexpr int LPG = EPT >= 4 ? 1 : 4 / EPT;  // lanes per 4-group
+    float g4[4 * ((EPT + 3) / 4)];
+    if constexpr (LPG == 1) {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) g4[j] = r[j];
+    } else {
+#pragma unroll
+      for (int q = 0; q < LPG; ++q)
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) g4[q * EPT + j] = __shfl(r[j], (tid & ~(LPG - 1)) + q, 64);
+    }
+    if (live && (tid & (LPG - 1)) == 0) {
+      const int o0 = h * HD + d0;  // a multiple of 4
+#pragma unroll
+      for (int k = 0; k < (EPT + 3) / 4; ++k) {
+        // swizzled 4-group: (v0, v2, v1, v3)
+        const h2v p0 = {(_Float16)g4[4 * k], (_Float16)g4[4 * k + 2]};
+        const h2v p1 = {(_Float16)g4[4 * k + 1], (_Float16)g4[4 * k + 3]};
+        const unsigned long long w = ((unsigned long long)__builtin_bit_cast(unsigned, p1) << 32) |
+                                     __builtin_bit_cast(unsigned, p0);
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k), w, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
   if constexpr (TL) { if (threadIdx.x == 0) tl[9] = wall_clock64(); }

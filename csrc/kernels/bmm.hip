@@ -207,6 +207,15 @@ size_t t16_bytes(int type, int rows, int K) {
   return (size_t)((rows + 15) / 16) * (size_t)(K / 256) * (size_t)t16_step_bytes(type);
 }
 
+// 8-byte write-through store (global_store_dwordx2 sc1): the line leaves the XCD's L2 with the
+// store instead of staying dirty until the end-of-kernel write-back, which the next launch waits
+// for (the kernel boundaries after the SwiGLU and attention launches were 1.5-2 us longer than
+// after the atomic-only ones: tools/step_blocks.py)
+__device__ __forceinline__ void st8_wt(void* p, unsigned lo, unsigned hi) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)hi << 32) | lo, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ void copy16(uint8_t* d, const uint8_t* s, bool ok) {
   *reinterpret_cast<uint4*>(d) = ok ? *reinterpret_cast<const uint4*>(s) : make_uint4(0, 0, 0, 0);
 }
@@ -386,9 +395,15 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
 // round trip, like the f16 staging), then f16(x * w) goes to LDS in bprep's 4-group order and
 // each wave leaves its per-row partial sum of squares in rowss[b * NW + wave] (rows past B load
 // row B - 1 and are dropped: straight-line code, no predicated loads)
-template <int NW>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+// `between` runs once the (first batch of) x loads are issued, before any of them is used: the
+// wave-owned kernels issue their first weight steps there (x first, a.x_first) - the x round
+// trip then no longer queues behind the weight bytes
+template <int NW, typename F = NoOp>
 __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                            int tid, int lane, int wave) {
+                                            int tid, int lane, int wave, F between = F()) {
   constexpr int kBlock = NW * 64;
   if (NW >= 8 && a.xf) {
     constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
@@ -401,6 +416,7 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
 #pragma unroll
       for (int j = 0; j < J; ++j) xv[J * b + j] = *reinterpret_cast<const float4*>(xr + 4 * (tid + j * kBlock));
     }
+    between();
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       float ss = 0.f;
@@ -428,6 +444,7 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
         const int b = i / nv, c = i - b * nv;
         v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
       }
+      if (i0 == 0) between();
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * kBlock + tid;
@@ -673,7 +690,7 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __
           const float rw = a.ew ? a.ew[(size_t)r16 * a.ew_ld + gt / a.tiles_per_expert] : 1.f;
           const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
           const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
-          *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
+          st8_wt(a.h_out + (size_t)r16 * a.ldh_out + f0, as_u(p0), as_u(p1));
         }
       } else if (col_ok && a.qkv_epi) {
         qkv_epilogue(a, sg, tile, n_out, acc, r16, kq);
@@ -780,9 +797,9 @@ void bmm_kernel(BmmArgs a, BmmArgs a2) {
 // f16(x * norm_w) in bmm's 4-group order, each row's sum of squares over the part added to
 // rowss[b] (LDS, zeroed by the caller). All loads of a batch go out before any use (one memory
 // round trip); kn % 256 == 0, so the 64 float4 of a wave lie in one row.
-template <int NW>
+template <int NW, typename F = NoOp>
 __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                                  int tid, int lane) {
+                                                  int tid, int lane, F between = F()) {
   constexpr int kBlock = NW * 64, U = 4;
   const int nv = kn >> 2, n = a.B * nv;
   for (int i0 = 0; i0 < n; i0 += U * kBlock) {
@@ -794,6 +811,7 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
       v[u] = *reinterpret_cast<const float4*>(a.xf + (size_t)b * a.ldxf + k0 + 4 * c);
       w[u] = *reinterpret_cast<const float4*>(a.norm_w + k0 + 4 * c);
     }
+    if (i0 == 0) between();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int iw = i0 + u * kBlock + (tid & ~63);  // the wave's first index (wave-uniform)
@@ -880,30 +898,39 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) rc[j] = a.qkv.rope[(size_t)pos * (hd >> 1) + ((row + 2 * j) % hd >> 1)];
   };
-  if (a.qkv_sk) {
-    pos = min(max(a.qkv.pos[col_ok ? r16 : 0], 0), a.qkv.n_ctx - 1);
-    if (nt > 0) rope_load(0);
-    if (tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
-  }
-  // the first PD steps go out before the x staging round trip
+  if (a.qkv_sk && tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
+  // the first PD steps of weights go out before the x staging round trip completes: ahead of the
+  // x loads, or (a.x_first) right behind them, so the x round trip does not queue behind them
+  auto issue_w = [&]() {
 #pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (p < N) load_next(buf[p]);
-  if (clk && tid == 0) clk[1] = wall_clock64();
+    for (int p = 0; p < PD; ++p)
+      if (p < N) load_next(buf[p]);
+    if (clk && tid == 0) clk[1] = wall_clock64();
+  };
+  if (!a.x_first) issue_w();
+  // split-K Q|K|V: the row's position (its RoPE factors load after the staging, beside the
+  // first tile's weights - a load issued ahead of the weights held their issue for a round trip)
+  if (a.qkv_sk) pos = a.qkv.pos[col_ok ? r16 : 0];
   if (a.zero) {  // side job: zero the next consumer's accumulation rows
     float4* z = reinterpret_cast<float4*>(a.zero);
     for (int i = bid * 512 + tid; i < (a.zero_n >> 2); i += gridDim.x * 512) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (a.ss_out) {
-    lds_barrier(false);  // rowss zeroed
-    stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
+  if (a.ss_out) lds_barrier(false);  // rowss zeroed
+  if (a.x_first) {
+    if (a.ss_out) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue_w);
+    else bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave, issue_w);
   } else {
-    bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+    if (a.ss_out) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
+    else bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
   }
   __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
   if (a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
+  if (a.qkv_sk) {
+    pos = min(max(pos, 0), a.qkv.n_ctx - 1);
+    rope_load(0);
+  }
   float cs = 1.f;  // folded norm (one K part): this lane's column scale
   if (a.xf && !a.ss_out) {
     float t = 0.f;
@@ -946,7 +973,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
         const int f0 = gt * 8 + 4 * kq;
         const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
         const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
-        *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
+        st8_wt(a.h_out + (size_t)r16 * a.ldh_out + f0, as_u(p0), as_u(p1));
       }
     } else if (col_ok) {
       float* o = a.out + (size_t)r16 * a.ldo;
@@ -1285,8 +1312,10 @@ static void bmm_check(const BmmArgs& a) {
 
 void bmm(const BmmArgs& a0, hipStream_t s) {
   static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
+  static const bool xfirst = env_int("LFK_WT_XFIRST", 0) != 0;
   BmmArgs a = a0;
   a.fence_sync = fence;
+  a.x_first = xfirst;
   bmm_check(a);
   if (a.n_out <= 0) return;
   if (a.qkv_sk) {

@@ -21,10 +21,18 @@
 // order). A per-launch block count would break this: blocks of different launches
 // would advance different epochs and alias slot ranges.
 //
-// Memory model: payload stores are plain (vectorised) stores into the peer's memory,
-// ordered before the flag stores by a system-scope release fence + block barrier; the
-// reader polls its local flags with system-scope acquire loads and reads the slots
-// with system-scope loads (bypassing an L2 that may hold the slot's previous epoch).
+// Memory model (why a peer's bytes are never read stale, across xGMI or on one GPU):
+//   * the receive region is allocated hipDeviceMallocUncached (runtime/p2p.cpp): no L2 /
+//     L1 of the owning GPU or of a writing peer keeps a line of it, so every store lands in
+//     the owner's HBM and every load reads HBM - there is no previous-epoch line to hit;
+//   * payload stores are plain (vectorised) stores into the peer's region, ordered before
+//     the flag stores by a system-scope release fence + block barrier (the fence waits for
+//     the stores to be acknowledged by the peer's memory);
+//   * the reader polls its LOCAL flags with system-scope acquire loads and reads the slots
+//     with system-scope loads; on a cacheable fallback region (hipMalloc, if the uncached
+//     allocation is refused) the system scope still bypasses the non-coherent caches.
+// Slot reuse (a rank overwriting a slot a slower peer still reads) is excluded by the epoch
+// argument above.
 // Every wait is bounded: a timeout sets *err and the launch completes (the engine
 // then reports itself unhealthy) instead of hanging.
 #include "kernels.h"

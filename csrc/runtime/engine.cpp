@@ -135,7 +135,10 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   if (opt_.n_slots < 1) throw std::runtime_error("n_slots must be >= 1");
   if (opt_.n_slots > 1 && opt_.layer_begin > 0)
     throw std::runtime_error("KV slots (batched decode) need the GPU to hold every layer");
-  if (tp > 1 && opt_.comm != "ipc") {
+  // comm=rccl at tp_size 1: the tensor-parallel code paths over a ONE-rank RCCL communicator
+  // (every collective a copy) - how a one-GPU box runs the RCCL branch inside captured graphs
+  tp_on_ = tp > 1 || opt_.comm == "rccl";
+  if (tp_on_ && opt_.comm != "ipc") {
     if (opt_.nccl_id.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad nccl id");
     ncclUniqueId id;
     std::memcpy(&id, opt_.nccl_id.data(), sizeof(id));
@@ -301,7 +304,7 @@ void Engine::alloc_buffers() {
   const int tp = opt_.tp_size;
   cand_words_ = sampler_cand_words(V_l_);
   cand_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_);
-  if (tp > 1) cand_all_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_ * tp);
+  if (tp_on_) cand_all_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_ * tp);
   state_ = (int*)dalloc(sizeof(int) * S_NSTATE * NS);
   ring_ = (int*)dalloc(sizeof(int) * 64 * NS);
   out_tokens_ = (int*)dalloc(sizeof(int) * 64);
@@ -332,7 +335,7 @@ void Engine::alloc_buffers() {
     btok_out_ = (int*)dalloc(sizeof(int) * bmax_);
     logits_b_ = (float*)dalloc(sizeof(float) * bmax_ * V_pad_);
     cand_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * cand_words_);
-    if (tp > 1) cand_all_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * cand_words_ * tp);
+    if (tp_on_) cand_all_b_ = (unsigned*)dalloc(sizeof(unsigned) * bmax_ * cand_words_ * tp);
     attn_part_b_ = (float*)dalloc(sizeof(float) * bmax_ * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
     attn_cnt_b_ = (int*)dalloc(sizeof(int) * 64 * bmax_);
     HIPCHK(hipMemset(attn_cnt_b_, 0, sizeof(int) * 64 * bmax_));
@@ -430,9 +433,10 @@ void Engine::setup_batch_mfma() {
       const size_t dn1 = t16_bytes(L.down_exps.type, L.down_exps.rows, L.down_exps.K);
       const size_t run = dn1 / dtiles;  // one tile's steps of one expert
       uint8_t* ddst = (uint8_t*)dalloc(dn1 * E);
-      // (kept allocated: freeing device memory between the engine's setup and the TP group's
-      // collectives was followed by corrupted decode logits on the 2-rank IPC test)
-      uint8_t* tmp = (uint8_t*)dalloc(dn1);
+      // one expert's copy, strided into place, then freed (the P2P receive region checks that it
+      // is a whole allocation of its own, runtime/p2p.cpp, so a reuse of this block cannot alias it)
+      uint8_t* tmp = nullptr;
+      HIPCHK(hipMalloc((void**)&tmp, dn1));
       for (int e = 0; e < E; ++e) {
         QMat g = L.gu_exps;
         g.base += L.gu_exps.expert_stride * e;
@@ -445,6 +449,7 @@ void Engine::setup_batch_mfma() {
         HIPCHK(hipMemcpy2DAsync(ddst + run * e, run * E, tmp, run, run, dtiles, hipMemcpyDeviceToDevice, stream_));
       }
       HIPCHK(hipStreamSynchronize(stream_));
+      HIPCHK(hipFree(tmp));
       L.t_gu = L.gu_exps;
       L.t_gu.base = gdst; L.t_gu.rows = L.gu_exps.rows * E; L.t_gu.expert_stride = 0;
       L.t_down = L.down_exps;
@@ -562,7 +567,7 @@ void Engine::enqueue_sample(const float* logits, int rows, size_t ld, int slot, 
     }
   }
   sample_stage1(sa, s);
-  if (opt_.tp_size > 1) {
+  if (tp_on_) {
     const size_t words = cand_words_ * (batched ? rows : 1);
     unsigned* all = batched ? cand_all_b_ : cand_all_;
     allgather_into(reinterpret_cast<const float*>(sa.cand), reinterpret_cast<float*>(all), words, s);
@@ -575,7 +580,7 @@ void Engine::enqueue_sample(const float* logits, int rows, size_t ld, int slot, 
 void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd, hd = hp_.head_dim;
-  const bool tp = opt_.tp_size > 1;
+  const bool tp = tp_on_;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   int* st = state_ + (size_t)S_NSTATE * dslot_;
   QkvArgs qa;
@@ -694,7 +699,7 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int
   GemvArgs h;
   h.w = output_; h.x = xrow; h.norm_w = out_norm_; h.eps = hp_.rms_eps;
   h.n_out = V_real_l_;
-  h.out = opt_.tp_size > 1 ? logits_l_ : logits_;
+  h.out = tp_on_ ? logits_l_ : logits_;
   if (h.n_out > 0) gemv(h, EPI_STORE, s);
   // vocabulary-parallel sampling: stage 1 on this rank's shard, all-gather of the candidate
   // blocks (a few KB), identical stage 2 on every rank (no logit all-gather)
@@ -715,7 +720,7 @@ void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
 
 void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim;
-  const bool tp = opt_.tp_size > 1;
+  const bool tp = tp_on_;
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   const int ncol = nq_ + 2 * nkvd_;
   {
@@ -813,7 +818,7 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
 void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
   const Layer& L = layers_[l];
   const int d = hp_.n_embd;
-  const bool tp = opt_.tp_size > 1;
+  const bool tp = tp_on_;
   // MoE: the router GEMM reads the bf16 norm; the experts' f16 norm is written after it
   rmsnorm_bf16(x_, L.ffn_norm, hp_.rms_eps, T, d, xb_, s, nullptr, 0, t16 && hp_.n_expert == 0);
   if (t16 && hp_.n_expert == 0) {
@@ -998,7 +1003,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
   // row-parallel Wo / down under TP: accumulate this rank's partial into tmp_ (holding the
   // residual on rank 0, zeros elsewhere), then all-reduce into x_
-  const bool tp = opt_.tp_size > 1;
+  const bool tp = tp_on_;
   float* acc = tp ? tmp_ : x_;
   auto tp_begin = [&]() {
     if (!tp) return;
@@ -1082,6 +1087,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.q_stride = nq_; aa.out_stride = nq_;
   aa.part_stride = attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd);
   aa.out_h = xh_b_; aa.out_h_stride = nq_;   // the Wo input, already in bmm's f16 layout
+  aa.out = nullptr;                          // (nothing reads an f32 copy of it)
   if (sk) {
     aa.qkv_raw = qkv_b_; aa.qkv_ld = ncol; aa.k_off = nq_; aa.v_off = nq_ + nkvd_;
     aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
@@ -1620,7 +1626,7 @@ std::vector<float> Engine::batch_logits(int B) {
 
 std::vector<float> Engine::batch_logits_impl(int B) {
   std::vector<float> out;
-  if (last_b1_) gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
+  if (last_b1_) gather_logits_rows(1, V_l_, tp_on_ ? logits_l_ : logits_, out);
   else gather_logits_rows(B, V_pad_, logits_b_, out);
   return out;
 }
@@ -1741,13 +1747,13 @@ std::vector<float> Engine::eval_logits_impl(const std::vector<int>& tokens, int 
   enqueue_prefill(T, pos0, stream_);
   enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
   std::vector<float> out;
-  gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
+  gather_logits_rows(1, V_l_, tp_on_ ? logits_l_ : logits_, out);
   return out;
 }
 
 std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
   ExecGuard guard(this);
-  if (opt_.tp_size > 1) throw std::runtime_error("eval_hidden: not available with tensor parallelism");
+  if (tp_on_) throw std::runtime_error("eval_hidden: not available with tensor parallelism");
   if (T <= 0 || T > opt_.n_batch || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_hidden: bad size");
   HIPCHK(hipMemcpyAsync(x_, x, sizeof(float) * T * hp_.n_embd, hipMemcpyHostToDevice, stream_));
   enqueue_prefill(T, pos0, stream_, /*embed=*/false);
@@ -1760,7 +1766,7 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
 
 void Engine::kv_transfer(void* buf, int n, bool load) {
   ExecGuard guard(this);
-  if (opt_.tp_size > 1)
+  if (tp_on_)
     throw std::runtime_error("KV snapshots hold one rank's heads: not available with tensor parallelism");
   if (n < 0 || n > opt_.n_ctx) throw std::runtime_error("kv_transfer: n out of range");
   if (n == 0) return;
@@ -1799,7 +1805,7 @@ std::vector<float> Engine::decode_logits_impl(int token, int pos) {
   HIPCHK(hipMemcpyAsync(state_, hstate, sizeof(hstate), hipMemcpyHostToDevice, stream_));
   launch_step();
   std::vector<float> out;
-  gather_logits_rows(1, V_l_, opt_.tp_size > 1 ? logits_l_ : logits_, out);
+  gather_logits_rows(1, V_l_, tp_on_ ? logits_l_ : logits_, out);
   check_device_err();
   return out;
 }

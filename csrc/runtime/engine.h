@@ -352,6 +352,7 @@ class Engine : public SlotBackend {
   // attention normalises them and appends the new K / V, the Wo launch re-zeroes both
   // (LFK_QKV_SK=0: the one-part Q|K|V with the RoPE / KV-append epilogue, A/B)
   bool qkv_sk_ = true;
+  bool tp_on_ = false;        // the tensor-parallel code paths (tp_size > 1, or comm=rccl at one rank)
   long long* step_clk_ = nullptr;
   int step_clk_layer_ = -1;
   long long* clk_of(int l, int k) const {

@@ -9,19 +9,37 @@ static void p2pchk(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("p2p: ") + what + ": " + hipGetErrorString(e));
 }
 
-P2PComm::P2PComm(int rank, int world, int max_n, int device)
-    : rank_(rank), world_(world), max_n_((max_n + 3) & ~3), device_(device) {
+P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached)
+    : rank_(rank), world_(world), max_n_((max_n + 3) & ~3), device_(device), uncached_(uncached) {
   if (world < 1 || world > kP2PMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("p2p: bad rank/world");
   if (max_n <= 0) throw std::runtime_error("p2p: bad max_n");
   p2pchk(hipSetDevice(device_), "hipSetDevice");
   data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n_;
   data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
   region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
-  // a whole, 2 MiB-granular allocation of its own: an exported IPC handle names the
-  // underlying allocation, and a small hipMalloc can be carved out of a freed block at an
-  // offset the peer's mapping does not carry (peer writes then land elsewhere in our memory)
+  // A whole, 2 MiB-granular allocation of its own, UNCACHED (hipDeviceMallocUncached): peers
+  // store payloads and flags into it over xGMI while this GPU polls and reads it, so no L2 of
+  // either side may hold a line of it (a stale line of the previous epoch is the classic
+  // cross-device failure; the kernel's system-scope fences order the accesses, the memory type
+  // keeps every one of them at the memory). Ranks sharing a GPU (the one-GPU IPC rehearsal)
+  // import it the same way (tests/test_p2p_allreduce.py runs both region types).
+  // An exported IPC handle names the underlying allocation: the region must BE that allocation
+  // (checked below), or the peer's mapping would start at the allocation's base.
   region_bytes_ = (region_bytes_ + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-  p2pchk(hipMalloc(&region_, region_bytes_), "hipMalloc region");
+  if (!uncached_ || hipExtMallocWithFlags(&region_, region_bytes_, hipDeviceMallocUncached) != hipSuccess) {
+    if (uncached_) (void)hipGetLastError();
+    region_ = nullptr;
+    p2pchk(hipMalloc(&region_, region_bytes_), "hipMalloc region");
+    uncached_ = false;
+  }
+  {
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    p2pchk(hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)region_), "hipMemGetAddressRange region");
+    if ((void*)base != region_ || sz < region_bytes_)
+      throw std::runtime_error("p2p: the receive region is not a whole allocation of its own (IPC peers would map "
+                               "its base, not the region)");
+  }
   p2pchk(hipMemset(region_, 0, region_bytes_), "hipMemset region");
   p2pchk(hipMalloc((void**)&epochs_, sizeof(int) * kP2PMaxBlocks), "hipMalloc epochs");
   p2pchk(hipMemset(epochs_, 0, sizeof(int) * kP2PMaxBlocks), "hipMemset epochs");
@@ -58,8 +76,15 @@ void P2PComm::open(const std::vector<std::string>& handles) {
       void* ptr = nullptr;
       p2pchk(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
       imported_.push_back(ptr);
+      // the mapping must cover the peer's whole region (same layout on every rank)
+      hipDeviceptr_t mbase = nullptr;
+      size_t msz = 0;
+      p2pchk(hipMemGetAddressRange(&mbase, &msz, (hipDeviceptr_t)ptr), "hipMemGetAddressRange peer");
+      if ((char*)mbase + msz < (char*)ptr + region_bytes_)
+        throw std::runtime_error("p2p: rank " + std::to_string(p) + "'s imported region is smaller than the layout");
       base = static_cast<char*>(ptr);
     }
+    if (!base) throw std::runtime_error("p2p: no mapping for rank " + std::to_string(p));
     peers_.data[p] = reinterpret_cast<float*>(base);
     peers_.flags[p] = reinterpret_cast<int*>(base + data_bytes_);
   }
@@ -78,6 +103,22 @@ void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_
 void P2PComm::allreduce(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 0, s); }
 
 void P2PComm::allgather(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 1, s); }
+
+std::vector<std::vector<unsigned long long>> P2PComm::mappings() const {
+  std::vector<std::vector<unsigned long long>> out;
+  for (int p = 0; p < world_; ++p) {
+    void* ptr = p == rank_ ? region_ : (ready_ ? (void*)peers_.data[p] : nullptr);
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    if (ptr && hipMemGetAddressRange(&base, &sz, (hipDeviceptr_t)ptr) != hipSuccess) {
+      (void)hipGetLastError();
+      base = nullptr;
+      sz = 0;
+    }
+    out.push_back({(unsigned long long)(uintptr_t)ptr, (unsigned long long)(uintptr_t)base, (unsigned long long)sz});
+  }
+  return out;
+}
 
 int P2PComm::error() const {
   int e = 0;

@@ -15,7 +15,7 @@ namespace lfk {
 
 class P2PComm {
  public:
-  P2PComm(int rank, int world, int max_n, int device);
+  P2PComm(int rank, int world, int max_n, int device, bool uncached = true);
   ~P2PComm();
   P2PComm(const P2PComm&) = delete;
   P2PComm& operator=(const P2PComm&) = delete;
@@ -27,6 +27,9 @@ class P2PComm {
   void allreduce(const float* src, float* dst, int n, hipStream_t s);
   void allgather(const float* src, float* dst, int n, hipStream_t s);  // dst [world][n]
   int error() const;                                   // device error word (0 = ok)
+  bool uncached() const { return uncached_; }          // region allocated hipDeviceMallocUncached
+  // diagnostics: per rank (mapped pointer, allocation base, allocation size) as seen here
+  std::vector<std::vector<unsigned long long>> mappings() const;
   void reset_error();
 
  private:
@@ -38,6 +41,7 @@ class P2PComm {
   int* err_ = nullptr;
   P2PPeers peers_;
   bool ready_ = false;
+  bool uncached_ = false;
   void launch(const float* src, float* dst, int n, int gather, hipStream_t s);
 };
 

@@ -72,6 +72,12 @@ class Settings:
     # continuous batching (MI355X engine, one rank): up to max_batch generations decode
     # together as rows of one batched step. 1 = the reference's one-at-a-time serving.
     max_batch: int = 1
+    # tensor parallelism (split_mode=row over torchrun ranks): the engine's collectives -
+    # "auto" (one-shot P2P kernel for decode, RCCL for prefill), "rccl", or "ipc" (the P2P
+    # kernel only: ranks may share a GPU). tp_device puts EVERY rank on that GPU (the one-GPU
+    # rehearsal of an N-rank deployment; None = the rank's LOCAL_RANK GPU)
+    tp_comm: str = "auto"
+    tp_device: Optional[int] = None
     # --- service (reference api.py:17-19) ---
     max_context_tokens: int = 1024
     timeout_seconds: float = 25.0
@@ -113,6 +119,9 @@ class Settings:
         s.engine = _env("ENGINE", s.engine).lower()
         s.verbose = _env("VERBOSE", s.verbose, bool)
         s.max_batch = max(1, _env("MAX_BATCH", s.max_batch, int))
+        s.tp_comm = _env("TP_COMM", s.tp_comm).lower()
+        tpd = _env("TP_DEVICE", None)
+        s.tp_device = int(tpd) if tpd is not None else None
         s.max_context_tokens = _env("MAX_CONTEXT_TOKENS", s.max_context_tokens, int)
         s.timeout_seconds = _env("TIMEOUT_SECONDS", s.timeout_seconds, float)
         s.max_queue_size = _env("MAX_QUEUE_SIZE", s.max_queue_size, int)

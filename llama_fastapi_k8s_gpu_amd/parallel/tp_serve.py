@@ -93,20 +93,20 @@ def follower_loop(llm, group=None) -> None:
 
 
 def init_tp(settings) -> tuple:
-    """Initialise torch.distributed from the torchrun env; returns (rank, world, control group)."""
-    import torch
+    """Initialise torch.distributed from the torchrun env; returns (rank, world, control group).
+
+    One bootstrap for the container, the bench and the tests alike: a gloo process group
+    carries the control traffic only (the seed, the RCCL unique id, the P2P IPC handles, the
+    CPU backend's call mirroring). The MI355X engine creates and owns the only RCCL
+    communicator (ncclCommInitRank inside the engine, its collectives on the engine stream and
+    in its hipGraphs) - a torch NCCL process group would be a second communicator on the same
+    GPUs that nothing uses."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1:
         return 0, 1, None
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", timeout=_LONG, device_id=torch.device("cuda", local))
-        ctrl = dist.new_group(backend="gloo", timeout=_LONG)
-    else:
-        dist.init_process_group("gloo", timeout=_LONG)
-        ctrl = None
+    dist.init_process_group("gloo", timeout=_LONG)
+    ctrl = None   # the default group is the gloo control group
     rank = dist.get_rank()
     if settings.seed is None:   # every rank must sample with the same seed
         obj = [int.from_bytes(os.urandom(4), "little") if rank == 0 else None]

@@ -69,7 +69,7 @@ class HipBackend:
             # a tensor_split given for a layer split would be silently ignored
             raise ValueError("tensor_split needs split_mode='row' (tensor parallelism); split_mode='layer' runs the "
                              "whole model on main_gpu")
-        comm = tp_comm or os.environ.get("LFK_TP_COMM", "auto")
+        comm = tp_comm or "auto"
         rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split, comm)
         if device is None:
             device = local if size > 1 else (main_gpu if split_mode in ("none", "layer") and main_gpu else local)

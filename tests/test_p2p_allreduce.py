@@ -20,7 +20,7 @@ def _inputs(rank, it, n=N):
     return np.random.default_rng(1000 * it + rank).standard_normal(n).astype(np.float32)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, uncached):
     try:
         import torch
         import torch.distributed as dist
@@ -31,7 +31,16 @@ def _worker(rank, world, port, q):
         from llama_fastapi_k8s_gpu_amd.parallel.comm import allgather_bytes
         from llama_fastapi_k8s_gpu_amd.runtime import load_hip
         hip = load_hip()
-        c = hip.P2PComm(rank, world, N, 0)
+        c = hip.P2PComm(rank, world, N, 0, uncached=uncached)
+        if uncached:
+            assert c.uncached, "hipDeviceMallocUncached refused"
+        # device memory freed and re-allocated between the region's setup and the first
+        # collective (the engine's MoE setup does this): the region is a whole allocation of its
+        # own (runtime/p2p.cpp checks it), so nothing carved out of the freed blocks aliases it
+        junk = [torch.empty(3 << 20, dtype=torch.uint8, device="cuda") for _ in range(4)]
+        del junk
+        torch.cuda.empty_cache()
+        junk2 = torch.full((5 << 20,), 7, dtype=torch.uint8, device="cuda")  # noqa: F841
         c.open(allgather_bytes(c.handle()))
         s = torch.cuda.current_stream()
         src = torch.empty(N, device="cuda")
@@ -84,7 +93,10 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(240)
-def test_p2p_allreduce_two_processes_one_gpu():
+@pytest.mark.parametrize("uncached", [True, False])
+def test_p2p_allreduce_two_processes_one_gpu(uncached):
+    """Both region types: hipDeviceMallocUncached (the engine's) and plain hipMalloc; device memory
+    is freed and re-allocated between the regions' setup and the handle exchange."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -92,7 +104,7 @@ def test_p2p_allreduce_two_processes_one_gpu():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + (os.getpid() % 1000)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port + (0 if uncached else 7), q, uncached)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=200) for _ in procs]
@@ -104,3 +116,39 @@ def test_p2p_allreduce_two_processes_one_gpu():
         assert err == 0, f"rank {rank}: device error word {err}"
         assert worst < 1e-5, (rank, worst)
     assert res[0][3] == res[1][3]   # bit-identical on both ranks
+
+
+def test_p2p_uncached_region_one_rank():
+    """One rank on an uncached region (no IPC import at all): the collective's own stores,
+    flags and system-scope loads, eager and graph-replayed."""
+    import torch
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    hip = load_hip()
+    c = hip.P2PComm(0, 1, N, 0, uncached=True)
+    if not c.uncached:
+        pytest.skip("hipDeviceMallocUncached refused on this device")
+    c.open([b"self"])
+    s = torch.cuda.current_stream()
+    for it in range(6):
+        n = [N, 37, 1000][it % 3]
+        x = torch.from_numpy(_inputs(0, 300 + it, n)).cuda()
+        y = torch.empty(n, device="cuda")
+        c.allreduce(x.data_ptr(), y.data_ptr(), n, s.cuda_stream)
+        z = torch.empty(n, device="cuda")
+        c.allgather(x.data_ptr(), z.data_ptr(), n, s.cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(y, x) and torch.equal(z, x)
+    x = torch.from_numpy(_inputs(0, 400, N)).cuda()
+    y = torch.zeros(N, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream()
+    with torch.cuda.stream(cs):
+        with torch.cuda.graph(g):
+            c.allreduce(x.data_ptr(), y.data_ptr(), N, torch.cuda.current_stream().cuda_stream)
+    for k in range(3):
+        x.add_(1.0)
+        y.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, x)
+    assert c.error() == 0

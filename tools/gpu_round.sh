@@ -15,6 +15,8 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in "$@"; do
   case $s in
+    rccl) step rccl 400 python -u -m pytest tests/test_rccl_gpu.py tests/test_serve_tp_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
+    p2pu) step p2pu 200 env LFK_P2P_UNCACHED=1 python -u -m pytest tests/test_p2p_allreduce.py -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ;;
     tp) step tp 460 python -u -m pytest tests/test_p2p_allreduce.py tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread -p no:cacheprovider ;;
     bmmt) step bmmt 400 python -u -m pytest tests/test_kernels_gpu.py -k "bmm or bprep" -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
@@ -28,6 +30,14 @@ for s in "$@"; do
           step absk1b 200 python tools/batch_bench.py --batches 6,8 --steps 64 ;;
     blocks) step blocks1 200 python tools/step_blocks.py --json gpurun_out/blocks_sk1.json
             step blocks0 200 env LFK_QKV_SK=0 python tools/step_blocks.py --json gpurun_out/blocks_sk0.json ;;
+    sksweep) for c in 8,8 4,6 4,8 2,3 16,6; do
+               step "sk_$c" 200 env LFK_QKV_SK_PARTS=${c%,*} LFK_QKV_SK_TPG=${c#*,} python tools/batch_bench.py --batches 6 --steps 64
+             done ;;
+    xfirst) step xf_blocks1 200 env LFK_WT_XFIRST=1 LFK_QKV_SK_PARTS=4 python tools/step_blocks.py --json gpurun_out/blocks_xf1.json
+            step xf_blocks0 200 env LFK_QKV_SK_PARTS=4 python tools/step_blocks.py --json gpurun_out/blocks_xf0.json
+            for x in 0 1 0 1; do step "xf_bench_$x" 200 env LFK_WT_XFIRST=$x LFK_QKV_SK_PARTS=4 python tools/batch_bench.py --batches 6 --steps 64; done ;;
+    p2pprobe) step p2pprobe0 120 python tools/p2p_probe.py
+              step p2pprobe1 120 python tools/p2p_probe.py --junk ;;
     stepprof) export TMPDIR=/tmp; step stepprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/sprof -o bstep --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
           python3 tools/step_kernels.py gpurun_out/sprof/bstep_kernel_trace.csv > gpurun_out/sprof_kernels.txt ;;
     samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;

@@ -50,14 +50,14 @@ def main():
     us = lambda t: float(t) / 100.0  # noqa: E731 (100 MHz)
     per = {}
     for k, name in enumerate(NAMES):
-        c = clk[k]
+        c = clk[k] if name == "attn" else clk[k].reshape(-1, 8)   # bmm stamps: 8 per block
         live = c[:, 0] > 0
         xcc_col = 15 if name == "attn" else 6
         c = c[live]
         if len(c) == 0:
             continue
         xcc = (c[:, xcc_col] & 0xF).astype(int)
-        ends = np.where(c[:, :15] > 0, c[:, :15], 0).max(axis=1) if name == "attn" else c[:, 4]
+        ends = np.where(c[:, :15] > 0, c[:, :15], 0).max(axis=1) if name == "attn" else c[:, 4].copy()
         ends = np.where(ends > 0, ends, c[:, :5].max(axis=1))
         life = ends - c[:, 0]
         d = {"blocks": int(len(c)), "life_us_p50_p90_max": [round(us(np.percentile(life, 50)), 2),
