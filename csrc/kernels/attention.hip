@@ -45,6 +45,12 @@ __device__ __forceinline__ float2 ld2_sc1(const float* p) {
 }
 
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+// c ? a : b per component (a ternary on the uint4 structs, or a conditional overwrite of a load's
+// registers, made the compiler keep the K / V load registers in a stack array or wait for every
+// outstanding load)
+__device__ __forceinline__ uint4 sel4(bool c, uint4 a, uint4 b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // Cross-lane helpers without the LDS crossbar: DPP within a row of 16 lanes,
@@ -138,11 +144,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   }
   // split-K Q|K|V (batched): q / k / v are RoPE'd unnormalised sums, this row's RMSNorm scale is
   // applied here (q is read from the raw sums)
-  float rs = 1.f;
-  if (a.qkv_raw) {
-    rs = rsqrtf(a.ss[a.batch > 0 ? blockIdx.z : 0] * a.inv_k + a.eps);
-    a.q = a.qkv_raw;
-  }
+  if (a.qkv_raw) a.q = a.qkv_raw;
   const int kvh = blockIdx.x, split = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kw = lane >> 2, sub = lane & 3;
@@ -168,9 +170,16 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     qv[j] = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
   }
   float2 nv = make_float2(0.f, 0.f);
-  if (a.qkv_raw && tid < HD) {  // the new key (tid < HD / 2) and value pairs
-    const int kv = tid / (HD / 2), pr = tid % (HD / 2);
-    nv = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
+  float ssv = 0.f;
+  if (a.qkv_raw) {
+    // the row's sum of squares as a VECTOR load beside q (a scalar one at the top was one more
+    // dependent round trip before any K / V load went out)
+    ssv = __hip_atomic_load(const_cast<float*>(a.ss + (a.batch > 0 ? blockIdx.z : 0)), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < HD) {  // the new key (tid < HD / 2) and value pairs
+      const int kv = tid / (HD / 2), pr = tid % (HD / 2);
+      nv = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
+    }
   }
   const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
   uint4 kr[NLD], vr[NLD];
@@ -178,6 +187,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   for (int i = 0; i < NLD; ++i) kr[i] = *reinterpret_cast<const uint4*>(a.k_cache + row + 8 * i);
 #pragma unroll
   for (int i = 0; i < NLD; ++i) vr[i] = *reinterpret_cast<const uint4*>(a.v_cache + row + 8 * i);
+  const float rs = a.qkv_raw ? rsqrtf(ssv * a.inv_k + a.eps) : 1.f;
   const float qscale = a.scale * rs;
 #pragma unroll
   for (int j = 0; j < QPT; ++j) {
@@ -192,22 +202,24 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   const int ns = (L + CH - 1) / CH;
   __syncthreads();  // qs, kvn
   LFK_STAMP(1);
+  // the new position (split-K Q|K|V): its cache rows are written here from the LDS copy (this
+  // launch's only reader of them is this lane; write-through stores), and its key / value slices
+  // replace the speculatively loaded stale rows where they are used - not by writing into the K / V
+  // load registers (a conditional overwrite of those made the wave wait for every load first)
   const bool newkey = a.qkv_raw && key == L - 1;
+  // block-uniform: only the block whose 64 keys hold the new position reads the LDS copies
+  const bool newblk = a.qkv_raw && start <= L - 1 && L - 1 < start + CH;
+  const uint4* kn = reinterpret_cast<const uint4*>(&kvn[0][sub * (DPL / 2)]);
+  const uint4* vn = reinterpret_cast<const uint4*>(&kvn[1][sub * (DPL / 2)]);
   if (newkey) {
-    // the new position: its cache rows are written here (this launch's only reader of them is
-    // this lane; write-through stores), and its key / value slices replace the speculatively
-    // loaded stale rows
-    const uint4* kn = reinterpret_cast<const uint4*>(&kvn[0][sub * (DPL / 2)]);
-    const uint4* vn = reinterpret_cast<const uint4*>(&kvn[1][sub * (DPL / 2)]);
     const auto rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.k_cache), 0, 0x7FFFFFFF, 0x00020000);
     const auto rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.v_cache), 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NLD; ++i) {
-      kr[i] = kn[i];
-      vr[i] = vn[i];
       const int off = (int)((row + 8 * i) * sizeof(__half));
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, kr[i]), rk, off, 0, 16);  // aux 16: sc1
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vr[i]), rv, off, 0, 16);
+      const uint4 kk = kn[i], vv = vn[i];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, kk), rk, off, 0, 16);  // aux 16: sc1
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, vv), rv, off, 0, 16);
     }
   }
   if (a.debug_stop == 2) {
@@ -221,10 +233,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   h2v kh[DPL / 2];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
-    kh[4 * i] = __builtin_bit_cast(h2v, kr[i].x);
-    kh[4 * i + 1] = __builtin_bit_cast(h2v, kr[i].y);
-    kh[4 * i + 2] = __builtin_bit_cast(h2v, kr[i].z);
-    kh[4 * i + 3] = __builtin_bit_cast(h2v, kr[i].w);
+    const uint4 k4 = newblk ? sel4(newkey, kn[i], kr[i]) : kr[i];
+    kh[4 * i] = __builtin_bit_cast(h2v, k4.x);
+    kh[4 * i + 1] = __builtin_bit_cast(h2v, k4.y);
+    kh[4 * i + 2] = __builtin_bit_cast(h2v, k4.z);
+    kh[4 * i + 3] = __builtin_bit_cast(h2v, k4.w);
   }
   float sc[G];
 #pragma unroll
@@ -257,7 +270,9 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
   }
   // this wave's V rows (the wave's own keys: a wave barrier, no block barrier)
 #pragma unroll
-  for (int i = 0; i < NLD; ++i) *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = vr[i];
+  for (int i = 0; i < NLD; ++i) {  // (the new position: its value in place of the stale cache row)
+    *reinterpret_cast<uint4*>(&vs[wave][kw][sub * DPL + 8 * i]) = newblk ? sel4(newkey, vn[i], vr[i]) : vr[i];
+  }
   LFK_STAMP(2);
   // ---- 2c. P.V over this wave's keys (LDS written by this wave only)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -403,16 +418,16 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
     }
     M = mb;
   }
-  // outputs through write-through stores (no dirty L2 lines for the end-of-kernel write-back the
-  // next launch waits for): f32 as sc1 words, the f16 Wo input as one 8-byte sc1 store per 4-group
-  // (the lanes of a group pass their values to its first lane)
+  // outputs: f32 (if asked for), and the f16 Wo input as one 8-byte store per 4-group (the lanes of
+  // a group pass their values to its first lane). (Write-through sc1 stores here and in the SwiGLU
+  // epilogue, against dirty lines at the kernel boundary, measured neutral.)
   float r[EPT];
 #pragma unroll
   for (int j = 0; j < EPT; ++j) r[j] = num[j] / den;
   const bool live = tid * EPT < G * HD;
   if (a.out && live) {
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) st_sc1(a.out + h * HD + d0 + j, r[j]);
+    for (int j = 0; j < EPT; ++j) a.out[h * HD + d0 + j] = r[j];
   }
   if (a.out_h) {
     static_assert(EPT == 1 || EPT == 2 || EPT % 4 == 0, "4-groups of the f16 output");
@@ -436,8 +451,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(AttnDecodeArgs a) {
         const h2v p1 = {(_Float16)g4[4 * k + 1], (_Float16)g4[4 * k + 3]};
         const unsigned long long w = ((unsigned long long)__builtin_bit_cast(unsigned, p1) << 32) |
                                      __builtin_bit_cast(unsigned, p0);
-        __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k), w, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k) = w;
       }
     }
   }

@@ -207,15 +207,6 @@ size_t t16_bytes(int type, int rows, int K) {
   return (size_t)((rows + 15) / 16) * (size_t)(K / 256) * (size_t)t16_step_bytes(type);
 }
 
-// 8-byte write-through store (global_store_dwordx2 sc1): the line leaves the XCD's L2 with the
-// store instead of staying dirty until the end-of-kernel write-back, which the next launch waits
-// for (the kernel boundaries after the SwiGLU and attention launches were 1.5-2 us longer than
-// after the atomic-only ones: tools/step_blocks.py)
-__device__ __forceinline__ void st8_wt(void* p, unsigned lo, unsigned hi) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), ((unsigned long long)hi << 32) | lo, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-
 __device__ __forceinline__ void copy16(uint8_t* d, const uint8_t* s, bool ok) {
   *reinterpret_cast<uint4*>(d) = ok ? *reinterpret_cast<const uint4*>(s) : make_uint4(0, 0, 0, 0);
 }
@@ -395,15 +386,9 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
 // round trip, like the f16 staging), then f16(x * w) goes to LDS in bprep's 4-group order and
 // each wave leaves its per-row partial sum of squares in rowss[b * NW + wave] (rows past B load
 // row B - 1 and are dropped: straight-line code, no predicated loads)
-struct NoOp {
-  __device__ void operator()() const {}
-};
-// `between` runs once the (first batch of) x loads are issued, before any of them is used: the
-// wave-owned kernels issue their first weight steps there (x first, a.x_first) - the x round
-// trip then no longer queues behind the weight bytes
-template <int NW, typename F = NoOp>
+template <int NW>
 __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                            int tid, int lane, int wave, F between = F()) {
+                                            int tid, int lane, int wave) {
   constexpr int kBlock = NW * 64;
   if (NW >= 8 && a.xf) {
     constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
@@ -416,7 +401,6 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
 #pragma unroll
       for (int j = 0; j < J; ++j) xv[J * b + j] = *reinterpret_cast<const float4*>(xr + 4 * (tid + j * kBlock));
     }
-    between();
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       float ss = 0.f;
@@ -444,7 +428,6 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
         const int b = i / nv, c = i - b * nv;
         v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
       }
-      if (i0 == 0) between();
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * kBlock + tid;
@@ -690,7 +673,7 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __
           const float rw = a.ew ? a.ew[(size_t)r16 * a.ew_ld + gt / a.tiles_per_expert] : 1.f;
           const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
           const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
-          st8_wt(a.h_out + (size_t)r16 * a.ldh_out + f0, as_u(p0), as_u(p1));
+          *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
         }
       } else if (col_ok && a.qkv_epi) {
         qkv_epilogue(a, sg, tile, n_out, acc, r16, kq);
@@ -797,9 +780,9 @@ void bmm_kernel(BmmArgs a, BmmArgs a2) {
 // f16(x * norm_w) in bmm's 4-group order, each row's sum of squares over the part added to
 // rowss[b] (LDS, zeroed by the caller). All loads of a batch go out before any use (one memory
 // round trip); kn % 256 == 0, so the 64 float4 of a wave lie in one row.
-template <int NW, typename F = NoOp>
+template <int NW>
 __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                                  int tid, int lane, F between = F()) {
+                                                  int tid, int lane) {
   constexpr int kBlock = NW * 64, U = 4;
   const int nv = kn >> 2, n = a.B * nv;
   for (int i0 = 0; i0 < n; i0 += U * kBlock) {
@@ -811,7 +794,6 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
       v[u] = *reinterpret_cast<const float4*>(a.xf + (size_t)b * a.ldxf + k0 + 4 * c);
       w[u] = *reinterpret_cast<const float4*>(a.norm_w + k0 + 4 * c);
     }
-    if (i0 == 0) between();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int iw = i0 + u * kBlock + (tid & ~63);  // the wave's first index (wave-uniform)
@@ -828,7 +810,10 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
   }
 }
 
-template <int QT, int PD>
+// SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
+// compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
+// per launch (registers and branches) when they were runtime ones
+template <int QT, int PD, bool SK>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   constexpr int NW = 8, R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -845,13 +830,13 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   const int bid = blockIdx.x;
   // segments (split-K Q|K|V): global tile g -> (segment, local tile)
   const int t1 = (a.n_out + 15) >> 4;
-  const int t2 = t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0);
-  const int t3 = t2 + (a.nseg > 2 ? (a.seg_rows[2] + 15) >> 4 : 0);
-  const int tiles = a.nseg == 1 ? t1 : a.nseg == 2 ? t2 : t3;
-  auto seg_of = [&](int g) { return g >= t1 ? (g >= t2 ? 2 : 1) : 0; };
+  const int t2 = SK ? t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0) : t1;
+  const int t3 = SK ? t2 + (a.nseg > 2 ? (a.seg_rows[2] + 15) >> 4 : 0) : t1;
+  const int tiles = !SK || a.nseg == 1 ? t1 : a.nseg == 2 ? t2 : t3;
+  auto seg_of = [&](int g) { return SK ? (g >= t1 ? (g >= t2 ? 2 : 1) : 0) : 0; };
   auto seg_first = [&](int sg) { return sg == 0 ? 0 : sg == 1 ? t1 : t2; };
   int t0, tn;
-  if (a.qkv_sk) {  // groups of a.tpg tiles inside one run (run B: from segment seg_split on)
+  if constexpr (SK) {  // groups of a.tpg tiles inside one run (run B: from segment seg_split on)
     const int ta = a.seg_split >= a.nseg ? tiles : a.seg_split == 1 ? t1 : t2;
     const int gl = run == 0 ? grp : grp - a.nb1;
     t0 = (run == 0 ? 0 : ta) + gl * a.tpg;
@@ -866,7 +851,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   auto tile_of = [&](int i) { return t0 + wave + i * NW; };
   auto tbase = [&](int i) {
     const int g = tile_of(i), sg = seg_of(g);
-    const uint8_t* base = sg == 0 ? a.w.base : sg == 1 ? a.seg_base[1] : a.seg_base[2];
+    const uint8_t* base = !SK || sg == 0 ? a.w.base : sg == 1 ? a.seg_base[1] : a.seg_base[2];
     return base + ((size_t)(g - seg_first(sg)) * steps + s0) * SB;
   };
   BRawT<QT> buf[R][2];
@@ -898,41 +883,36 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) rc[j] = a.qkv.rope[(size_t)pos * (hd >> 1) + ((row + 2 * j) % hd >> 1)];
   };
-  if (a.qkv_sk && tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
-  // the first PD steps of weights go out before the x staging round trip completes: ahead of the
-  // x loads, or (a.x_first) right behind them, so the x round trip does not queue behind them
-  auto issue_w = [&]() {
+  if (SK && tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
+  // the first PD steps of weights go out ahead of the x staging round trip (the x loads first
+  // instead, so that their round trip would not queue behind the weights: B = 6 step 2.25 -> 2.61 ms)
 #pragma unroll
-    for (int p = 0; p < PD; ++p)
-      if (p < N) load_next(buf[p]);
-    if (clk && tid == 0) clk[1] = wall_clock64();
-  };
-  if (!a.x_first) issue_w();
+  for (int p = 0; p < PD; ++p)
+    if (p < N) load_next(buf[p]);
+  if (clk && tid == 0) clk[1] = wall_clock64();
   // split-K Q|K|V: the row's position (its RoPE factors load after the staging, beside the
   // first tile's weights - a load issued ahead of the weights held their issue for a round trip)
-  if (a.qkv_sk) pos = a.qkv.pos[col_ok ? r16 : 0];
+  if constexpr (SK) pos = a.qkv.pos[col_ok ? r16 : 0];
   if (a.zero) {  // side job: zero the next consumer's accumulation rows
     float4* z = reinterpret_cast<float4*>(a.zero);
     for (int i = bid * 512 + tid; i < (a.zero_n >> 2); i += gridDim.x * 512) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (a.ss_out) lds_barrier(false);  // rowss zeroed
-  if (a.x_first) {
-    if (a.ss_out) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue_w);
-    else bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave, issue_w);
+  if (SK && a.ss_out) {
+    lds_barrier(false);  // rowss zeroed
+    stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
   } else {
-    if (a.ss_out) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
-    else bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+    bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
   }
   __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
-  if (a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
+  if (SK && a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
-  if (a.qkv_sk) {
+  if constexpr (SK) {
     pos = min(max(pos, 0), a.qkv.n_ctx - 1);
     rope_load(0);
   }
   float cs = 1.f;  // folded norm (one K part): this lane's column scale
-  if (a.xf && !a.ss_out) {
+  if (a.xf && !SK) {
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) t += rowss[(col_ok ? r16 : 0) * NW + w];
@@ -943,9 +923,9 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   int ci = 0, cstep = 0;  // compute cursor (step s0 + cstep of tile ci)
   auto finish = [&]() {   // tile ci is complete in acc + acc2: C[row 4kq + i][col r16]
     acc += acc2;
-    if (a.xf && !a.ss_out) acc *= cs;
+    if (a.xf && !SK) acc *= cs;
     const int gt = tile_of(ci);
-    if (a.qkv_sk) {
+    if constexpr (SK) {
       const int sg = seg_of(gt), kind = sg == 0 ? a.qkv.kind[0] : sg == 1 ? a.qkv.kind[1] : a.qkv.kind[2];
       const int n_out = sg == 0 ? a.n_out : sg == 1 ? a.seg_rows[1] : a.seg_rows[2];
       float* o = (sg == 0 ? a.out : sg == 1 ? a.seg_out[1] : a.seg_out[2]) + (size_t)r16 * a.ldo;
@@ -973,7 +953,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
         const int f0 = gt * 8 + 4 * kq;
         const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
         const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
-        st8_wt(a.h_out + (size_t)r16 * a.ldh_out + f0, as_u(p0), as_u(p1));
+        *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
       }
     } else if (col_ok) {
       float* o = a.out + (size_t)r16 * a.ldo;
@@ -1016,7 +996,15 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
 template <int QT, int PD>
 __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD>(*ka, 0);
+  wt_body<QT, PD, false>(*ka, 0);
+  (void)a;
+}
+
+// split-K Q|K|V of one weight type
+template <int QT, int PD>
+__global__ __launch_bounds__(512, 2) void bmm_sk_kernel(BmmArgs a) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  wt_body<QT, PD, true>(*ka, 0);
   (void)a;
 }
 
@@ -1026,8 +1014,8 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
 template <int QT, int QT2, int PD>
 __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD>(*ka, 1);
-  else wt_body<QT, PD>(*ka, 0);
+  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true>(*ka, 1);
+  else wt_body<QT, PD, true>(*ka, 0);
   (void)a;
 }
 
@@ -1255,7 +1243,8 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
     else tb += t;
   }
   const int steps = a.w.K / 256;
-  static const int parts_env = env_int("LFK_QKV_SK_PARTS", 8);
+  // 4 parts x 8-tile groups measured best at B = 6 (8 x 8: +3 %, 4 x 6 / 2 x 3: +1-4 %, 16 x 6: +15 %)
+  static const int parts_env = env_int("LFK_QKV_SK_PARTS", 4);
   static const int tpg_env = env_int("LFK_QKV_SK_TPG", 8);
   const int kparts = std::max(1, std::min(steps, parts_env));
   a.spp = (steps + kparts - 1) / kparts;
@@ -1266,7 +1255,7 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   const dim3 grid((ga + gb) * a.kparts);
   const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
   if constexpr (QT2 == 0) {
-    hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+    hipLaunchKernelGGL((bmm_sk_kernel<QT, 2>), grid, dim3(512), lds, s, a);
   } else {
     hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
   }
@@ -1312,10 +1301,8 @@ static void bmm_check(const BmmArgs& a) {
 
 void bmm(const BmmArgs& a0, hipStream_t s) {
   static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
-  static const bool xfirst = env_int("LFK_WT_XFIRST", 0) != 0;
   BmmArgs a = a0;
   a.fence_sync = fence;
-  a.x_first = xfirst;
   bmm_check(a);
   if (a.n_out <= 0) return;
   if (a.qkv_sk) {

@@ -143,7 +143,6 @@ struct BmmArgs {
   // side job of the split-K launches: zero [zero, zero + zero_n) floats (zero_n % 4 == 0)
   float* zero = nullptr;
   int zero_n = 0;
-  bool x_first = false;            // wave-owned kernels: x staging loads issued before the first weights
 };
 // split-K Q|K|V (BmmArgs::qkv_sk): false = unsupported shape / type mix (caller: one-part path)
 bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B);

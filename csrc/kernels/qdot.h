@@ -35,10 +35,10 @@ __device__ __forceinline__ float h2f(unsigned short h) {
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
 
-// 16-B non-temporal load (weights are streamed once per token: do not pollute L2/MALL)
 // the XCD (XCC) this wave runs on, for timeline stamps (per-XCD clocks; placement tools only)
 __device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg(20 | (0 << 6) | (15 << 11)); }
 
+// 16-B non-temporal load (weights are streamed once per token: do not pollute L2/MALL)
 __device__ __forceinline__ int4 ld_nt16(const void* p) {
   const i32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(p));
   return make_int4(v.x, v.y, v.z, v.w);

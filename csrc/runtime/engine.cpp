@@ -986,6 +986,19 @@ void Engine::bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int 
   }
 }
 
+// the down projection (split-K into the residual); with the split-K Q|K|V (`zero_qkv`) its blocks
+// also re-zero qkv_b_ / ss_b_ for the next layer (the attention, their only reader, has finished)
+void Engine::down_rows(const QMat& w, const __half* xh, int ldh, float* out, int B, hipStream_t s, bool zero_qkv,
+                       long long* dbg) {
+  const int d = hp_.n_embd;
+  BmmArgs a;
+  a.w = w; a.xh = xh; a.ldh = ldh; a.out = out; a.ldo = d; a.n_out = d; a.B = B; a.dbg_clk = dbg;
+  if (zero_qkv) {
+    a.zero = qkv_b_; a.zero_n = bmax_ * (nq_ + 2 * nkvd_) + 16;
+  }
+  bmm(a, s);
+}
+
 void Engine::bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero,
                         int zero_n, hipStream_t s, int swiglu_group) {
   BPrepArgs p;
@@ -1023,6 +1036,10 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   // Q|K|V split over K (the default at B <= 8): RoPE'd partial sums into qkv_b_, normalised and
   // appended to the caches by the attention
   const bool sk = qkv_sk_ && bmm_qkv_sk_supported(L.t_wq.type, L.t_wk.type, L.t_wv.type, d, B);
+  // FFN paths without the down projection's zero side job: a memset node re-zeroes qkv_b_ / ss_b_
+  auto zero_qkv = [&]() {
+    if (sk) HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * (bmax_ * (size_t)(nq_ + 2 * nkvd_) + 16), s));
+  };
   if (sk) {
     BmmArgs a;
     a.w = L.t_wq; a.n_out = L.t_wq.rows; a.out = qkv_b_; a.ldo = ncol; a.B = B;
@@ -1095,15 +1112,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   aa.dbg_clk = clk_of(l, 1);
   attn_decode(aa, s);
   tp_begin();
-  if (sk) {  // Wo also re-zeroes the split-K Q|K|V rows and sums of squares for the next layer
-    BmmArgs a;
-    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = acc; a.ldo = d; a.n_out = d; a.B = B;
-    a.zero = qkv_b_; a.zero_n = bmax_ * ncol + 16;
-    a.dbg_clk = clk_of(l, 2);
-    bmm(a, s);
-  } else {
-    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
-  }
+  bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
   tp_end();
   if (moe_b_ && fused) {
     // MoE: dense per-row expert weights (f32 router on the normed rows), then every expert's
@@ -1130,6 +1139,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
     dn.ew = ew_b_; dn.ew_ld = E; dn.steps_per_expert = F_l_ / 256;
     bmm(dn, s);
+    zero_qkv();
     tp_end();
     return;
   }
@@ -1148,7 +1158,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     a.dbg_clk = clk_of(l, 3);
     bmm(a, s);
     tp_begin();
-    bmm_rows(L.t_down, hh_b_, F_l_, acc, d, d, B, s, clk_of(l, 4));
+    down_rows(L.t_down, hh_b_, F_l_, acc, B, s, sk, clk_of(l, 4));
     tp_end();
     return;
   }
@@ -1157,12 +1167,13 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     bmm_rows(L.t_gu, xh_b_, d, gu_b_, 2 * F_l_, 2 * F_l_, B, s);
     bprep_rows(gu_b_, 2 * F_l_, true, nullptr, F_l_, B, nullptr, 0, s, /*swiglu_group=*/8);  // t_gu: SwiGLU copy
     tp_begin();
-    bmm_rows(L.t_down, xh_b_, F_l_, acc, d, d, B, s);
+    down_rows(L.t_down, xh_b_, F_l_, acc, B, s, sk);
     tp_end();
     return;
   }
   // MoE (or unsupported FFN types): the grouped-GEMM FFN of the prompt path over the B rows
   enqueue_rows_ffn(l, B, s);
+  zero_qkv();
 }
 
 // The device work of one batch step over B rows (slots / positions / tokens are read from

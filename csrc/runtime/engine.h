@@ -226,6 +226,8 @@ class Engine : public SlotBackend {
   void enqueue_batch_step(int B, hipStream_t s);
   void bmm_rows(const QMat& w, const __half* xh, int ldh, float* out, int ldo, int n_out, int B, hipStream_t s,
                 long long* dbg = nullptr);
+  void down_rows(const QMat& w, const __half* xh, int ldh, float* out, int B, hipStream_t s, bool zero_qkv,
+                 long long* dbg = nullptr);
   void bprep_rows(const float* x, int ldx, bool swiglu, const float* norm_w, int K, int B, float* zero, int zero_n,
                   hipStream_t s, int swiglu_group = 32);
   void setup_batch_mfma();

@@ -123,6 +123,10 @@ SPECS: Dict[str, ModelSpec] = {
     # layers 0 and 3 bump V/down to Q6_K): full-width kernels at test cost
     "pd-llama-g4": ModelSpec("pd-llama-g4", 4096, 4, 32, 8, 2048, 0, 500000.0, "bpe", "q4_k_m",
                              n_ctx_train=1024),
+    # d = 8192 (the 70B's width) in one layer: six rows no longer fit the one-part staging, so the
+    # batched step takes the prep (bprep) FFN path beside the split-K Q|K|V
+    "tiny-llama3-d8k": ModelSpec("tiny-llama3-d8k", 8192, 1, 64, 8, 512, 0, 500000.0, "bpe", "q4_k_m",
+                                 n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

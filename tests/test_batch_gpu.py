@@ -199,3 +199,31 @@ def test_pipelined_steps_equal_synchronous(models):
         assert eng.healthy, eng.last_error
         return first, out
     assert run(False) == run(True)
+
+
+def test_batch_step_six_rows_d8192(tmp_path):
+    """Six rows at d = 8192: the split-K Q|K|V beside the FFN path that does not stage a whole row
+    (its projections' inputs prepared by bprep), which must re-zero the split-K rows itself -
+    every row of three consecutive steps against the fp32 reference on its own sequence."""
+    from llama_fastapi_k8s_gpu_amd.gguf.reader import GGUFReader
+    from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = write_synthetic_gguf("tiny-llama3-d8k", str(tmp_path / "d8k.gguf"))
+    eng = load_hip().Engine(path, n_ctx=128, n_batch=64, device=0, use_graph=True, n_slots=7)
+    ref = ReferenceLlama(GGUFReader(path), n_ctx=128)
+    rng = np.random.default_rng(9)
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    slots = [6, 0, 1, 2, 4, 5]
+    seqs = {}
+    for s in slots:
+        prompt = [int(t) for t in rng.integers(3, 300, 4 + 3 * s)]
+        seqs[s] = prompt + [eng.slot_begin(s, prompt, 0, greedy)]
+    for step in range(3):
+        toks = eng.batch_step(slots)
+        logits = eng.batch_logits(len(slots))
+        for b, s in enumerate(slots):
+            want = ref.forward(seqs[s], 0).numpy()
+            assert rel_err(logits[b], want) < 5e-2, (step, s, rel_err(logits[b], want))
+            seqs[s].append(toks[b])
+    assert eng.healthy, eng.last_error

@@ -38,6 +38,7 @@ for s in "$@"; do
             for x in 0 1 0 1; do step "xf_bench_$x" 200 env LFK_WT_XFIRST=$x LFK_QKV_SK_PARTS=4 python tools/batch_bench.py --batches 6 --steps 64; done ;;
     p2pprobe) step p2pprobe0 120 python tools/p2p_probe.py
               step p2pprobe1 120 python tools/p2p_probe.py --junk ;;
+    abold) step abold 600 bash tools/gpu_ab_old.sh ;;
     stepprof) export TMPDIR=/tmp; step stepprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/sprof -o bstep --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
           python3 tools/step_kernels.py gpurun_out/sprof/bstep_kernel_trace.csv > gpurun_out/sprof_kernels.txt ;;
     samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
