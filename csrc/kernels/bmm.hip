@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <stdexcept>
 
+#include "attn_dev.h"
 #include "gemv_dev.h"
 
 namespace lfk {
@@ -386,6 +387,14 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
 // round trip, like the f16 staging), then f16(x * w) goes to LDS in bprep's 4-group order and
 // each wave leaves its per-row partial sum of squares in rowss[b * NW + wave] (rows past B load
 // row B - 1 and are dropped: straight-line code, no predicated loads)
+typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
+// 16-B load with sc1 (L1 bypassed, agent-coherent with sc1 producer stores: an in-flight hand-off)
+__device__ __forceinline__ uint4 ld16_sc1(const __half* base, size_t off_halves) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(base), 0, 0x7FFFFFFF, 0x00020000);
+  const v4u_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off_halves * sizeof(__half)), 0, 16);  // aux 16: sc1
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 template <int NW>
 __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
                                             int tid, int lane, int wave) {
@@ -426,7 +435,8 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
       for (int u = 0; u < U; ++u) {
         const int i = min(i0 + u * kBlock + tid, n - 1);
         const int b = i / nv, c = i - b * nv;
-        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
+        const size_t o = (size_t)b * a.ldh + k0 + 8 * c;
+        v[u] = a.wait ? ld16_sc1(a.xh, o) : *reinterpret_cast<const uint4*>(a.xh + o);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -475,14 +485,8 @@ __device__ __forceinline__ void qkv_epilogue(const BmmArgs& a, int sg, int tile,
 // Block barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global loads. __syncthreads() is a workgroup release/acquire, which makes every wave drain
 // its outstanding global loads (s_waitcnt vmcnt(0)) - at every tile boundary that emptied
-// the weight ring the loop keeps in flight across tiles. (`fence` = the plain barrier, A/B.)
-__device__ __forceinline__ void lds_barrier(bool fence) {
-  if (fence) {
-    __syncthreads();
-  } else {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-}
+// the weight ring the loop keeps in flight across tiles.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Items are (16-row tile, K part). A block serves ONE K part (block b: part b % kparts):
 // it stages that part of the B activation rows in LDS once (f16, row stride padded 16 B), then
@@ -656,7 +660,7 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __
     float* out = sg == 0 ? a.out : sg == 1 ? a.seg_out[1] : a.seg_out[2];
     // the 4 waves' partial tiles meet in LDS; wave 0 writes C[row 4kq + i][col r16]
     if (wave > 0) *reinterpret_cast<f4_t*>(red + ((wave - 1) * 64 + lane) * 4) = acc;
-    lds_barrier(a.fence_sync);
+    lds_barrier();
     if (wave == 0) {
 #pragma unroll
       for (int w = 0; w < NW - 1; ++w) acc += *reinterpret_cast<const f4_t*>(red + (w * 64 + lane) * 4);
@@ -690,7 +694,7 @@ __device__ __attribute__((always_inline)) inline void bmm_body(const BmmArgs* __
         }
       }
     }
-    lds_barrier(a.fence_sync);  // red is reused by the next tile
+    lds_barrier();  // red is reused by the next tile
     acc = f4_t{0.f, 0.f, 0.f, 0.f};
     acc2 = acc;
   };
@@ -813,9 +817,11 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
 // per launch (registers and branches) when they were runtime ones
-template <int QT, int PD, bool SK>
-__device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
-  constexpr int NW = 8, R = PD + 1;
+// (bid, nblk): the block's index and count in the launch's wave-owned grid (the fused attention +
+// Wo launch runs this body in planes of its grid past the attention's)
+template <int QT, int PD, bool SK, int NW = 8>
+__device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
+  constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* rowss = reinterpret_cast<float*>(smem);            // [8 rows][NW waves] folded norm
   __half* xs = reinterpret_cast<__half*>(smem + 256);
@@ -824,10 +830,9 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   const int K = a.w.K, steps = K >> 8;
   // block = (K part kp, tile group grp): parts > 1 add their partial tiles atomically (Wo /
   // down: 8 parts x 32 groups of 8 tiles = one block per CU for the 256-tile shapes)
-  const int kparts = a.kparts, kp = blockIdx.x % kparts, grp = blockIdx.x / kparts, G = gridDim.x / kparts;
+  const int kparts = a.kparts, kp = bid % kparts, grp = bid / kparts, G = nblk / kparts;
   const int s0 = kp * a.spp, ns = min(steps, s0 + a.spp) - s0;  // this part's steps [s0, s0 + ns)
   const int k0 = s0 * 256, kn = ns * 256, ldx = kn + 8;
-  const int bid = blockIdx.x;
   // segments (split-K Q|K|V): global tile g -> (segment, local tile)
   const int t1 = (a.n_out + 15) >> 4;
   const int t2 = SK ? t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0) : t1;
@@ -895,10 +900,28 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
   if constexpr (SK) pos = a.qkv.pos[col_ok ? r16 : 0];
   if (a.zero) {  // side job: zero the next consumer's accumulation rows
     float4* z = reinterpret_cast<float4*>(a.zero);
-    for (int i = bid * 512 + tid; i < (a.zero_n >> 2); i += gridDim.x * 512) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = bid * (NW * 64) + tid; i < (a.zero_n >> 2); i += nblk * (NW * 64)) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (!SK && a.wait) {
+    // in-flight producer (the batched attention beside this launch): its per-kv-head done
+    // counters, polled with sc1 loads by one lane; the block's weights are already in flight
+    if (tid == 0) {
+      const int h0 = k0 / a.wait_group, h1 = (k0 + kn - 1) / a.wait_group;
+      for (int h = h0; h <= h1; ++h) {
+        for (int spins = 0; __hip_atomic_load(const_cast<int*>(a.wait) + h, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) < a.wait_n; ++spins) {
+          if (spins > (1 << 22)) {
+            __hip_atomic_store(a.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    lds_barrier();  // the other waves load after the polling wave's match (no vmcnt drain)
   }
   if (SK && a.ss_out) {
-    lds_barrier(false);  // rowss zeroed
+    lds_barrier();  // rowss zeroed
     stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
   } else {
     bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
@@ -996,7 +1019,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run) {
 template <int QT, int PD>
 __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, false>(*ka, 0);
+  wt_body<QT, PD, false>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1004,7 +1027,7 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
 template <int QT, int PD>
 __global__ __launch_bounds__(512, 2) void bmm_sk_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, true>(*ka, 0);
+  wt_body<QT, PD, true>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1014,9 +1037,41 @@ __global__ __launch_bounds__(512, 2) void bmm_sk_kernel(BmmArgs a) {
 template <int QT, int QT2, int PD>
 __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true>(*ka, 1);
-  else wt_body<QT, PD, true>(*ka, 0);
+  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true>(*ka, 1, blockIdx.x, gridDim.x);
+  else wt_body<QT, PD, true>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
+}
+
+// ---------------------------------------------------------------- fused batched attention + Wo
+// One launch for a layer's batched attention AND its Wo projection: grid (kv heads, splits,
+// B + Wo planes). The planes z < B are the batched attention (attn_dev.h) with done counters:
+// each (row, kv head) output is stored sc1 and counted once. The planes past them are the
+// wave-owned split-K Wo with 4-wave blocks: every block issues its weights at once (the whole
+// K part of its 4 tiles fits the 2-step register ring at d = 4096), waits for the counters of
+// its K part's kv heads (sc1 poll) and stages their output with sc1 loads. The Wo stream then
+// overlaps the latency-bound attention and a kernel boundary per layer is gone (a graph branch
+// for the same overlap cost ~10 us per layer in cross-queue joins, r4 profile).
+// Blocks are dispatched in linear order in practice (not a guarantee): whatever the order, an
+// attention block can always become resident beside the waiting Wo blocks (LDS and waves: see
+// attn_wo), and every wait is bounded.
+struct AttnWoArgs {
+  AttnDecodeArgs att;
+  BmmArgs wo;
+  int n_wo = 0;  // Wo blocks (kparts x tile groups)
+};
+
+template <int QT, int HD, int G>
+__global__ __launch_bounds__(256) void attn_wo_kernel(AttnWoArgs p) {
+  const AttnWoArgs* k = (const AttnWoArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  if ((int)blockIdx.z < k->att.batch) {
+    attn_decode_body<HD, G, false>(k->att);
+    return;
+  }
+  const int per = gridDim.x * gridDim.y;
+  const int vb = ((int)blockIdx.z - k->att.batch) * per + blockIdx.y * gridDim.x + blockIdx.x;
+  if (vb >= k->n_wo) return;
+  wt_body<QT, 2, false, 4>(k->wo, 0, vb, k->n_wo);
+  (void)p;
 }
 
 // ---------------------------------------------------------------- activation prep
@@ -1117,102 +1172,67 @@ static int bmm_cus() {
   return cus;
 }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
-// weight steps in flight per wave (LFK_BMM_PD, tuning: 1 or 2; Q4_K only - the other types
-// need > 128 VGPRs for the third buffer)
-template <int QT>
-static int bmm_pd() {
-  static const int pd = env_int("LFK_BMM_PD", 1);
-  return QT == T_Q4_K ? pd : 1;
-}
-
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
   for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
   const int steps = a.w.K / 256;
-  // dense SwiGLU gate/up: wave-owned tiles (LFK_BMM_WT=0: the block-split kernel, A/B), PD
-  // steps of weights in flight per wave (LFK_BMM_WTPD: 1-3)
-  static const int wt_env = env_int("LFK_BMM_WT", 1);
-  static const int wtpd = std::min(3, std::max(1, env_int("LFK_BMM_WTPD", 2)));
-  // plain split-K projections (Wo, down): the same kernel over (K part, 8-tile group) blocks
-  // (LFK_BMM_WTK=0: the block-split kernel)
-  static const int wtk_env = env_int("LFK_BMM_WTK", 1);
-  const bool wt_sw = wt_env && a.swiglu_epi && !a.ew && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
+  // dense SwiGLU gate/up: wave-owned tiles, 2 steps of weights in flight per wave (3: same
+  // time, r3 sweep); plain split-K projections (Wo, down): the same kernel over (K part,
+  // 8-tile group) blocks
+  const bool wt_sw = a.swiglu_epi && !a.ew && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
                      a.B <= 8;
-  const bool wt_k = wtk_env && !a.swiglu_epi && !a.ew && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
+  const bool wt_k = !a.swiglu_epi && !a.ew && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
                     a.nseg == 1 && a.B <= 8;
   if (wt_sw || wt_k) {
     const int cus = bmm_cus();
     int kparts = 1;
     if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
+      // (8 parts for the 256-tile shapes; 4 / 16 measured 7 / 13 % slower steps, r3 sweep)
       kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
-      static const int parts_env = env_int("LFK_BMM_WTK_PARTS", 0);  // tuning: K parts (Wo / down)
-      if (parts_env > 0) kparts = std::max(1, std::min(steps, parts_env));
       // the staged slice (B rows x part) stays within the LDS
       while (kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
     }
     a.spp = (steps + kparts - 1) / kparts;
     a.kparts = kparts = (steps + a.spp - 1) / a.spp;
-    // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K group
-    // (LFK_BMM_WT_BPC=2, tuning: two blocks per CU - twice the weight bytes in flight per CU -
-    // where the LDS and the 4 waves / SIMD of the 8-wave block allow it)
-    static const int bpc = std::max(1, std::min(2, env_int("LFK_BMM_WT_BPC", 1)));
-    const int G = std::max(1, std::min(std::max(1, cus * bpc / kparts), wt_k ? (tiles + 7) / 8 : tiles));
+    // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K
+    // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
+    const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
     // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
+    // (an in-flight consumer of the attention shares the CUs with it: no pin)
     const size_t lds_need = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
-    const size_t lds = bpc > 1 && lds_need <= 78 * 1024 ? lds_need : std::max<size_t>(lds_need, 81 * 1024);
-    const dim3 grid(G * kparts);
-    if (wtpd == 1) hipLaunchKernelGGL((bmm_wt_kernel<QT, 1>), grid, dim3(512), lds, s, a);
-    else if (wtpd == 3) hipLaunchKernelGGL((bmm_wt_kernel<QT, 3>), grid, dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+    const size_t lds = a.wait ? lds_need : std::max<size_t>(lds_need, 81 * 1024);
+    hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
     return;
   }
   if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");
+  if (a.wait) throw std::runtime_error("bmm: the in-flight wait runs on the wave-owned split-K kernel only");
   if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
-    // one K part (the epilogue needs whole rows); 8-wave blocks, 2 per CU by LDS
-    static const int nw1_env = env_int("LFK_BMM_NW1", 8);  // tuning: 4, 8 or 16
-    // the folded norm needs 8 or 16 waves; 16-wave blocks only for Q4_K (the other types need
-    // more than 128 VGPRs, and a 1024-thread block must hold 4 waves per SIMD)
-    int nw1 = a.xf ? std::max(8, nw1_env) : nw1_env;
-    if (nw1 == 16 && QT != T_Q4_K) nw1 = 8;
+    // one K part (the epilogue needs whole rows); 8-wave blocks (the folded norm needs 8), 2 per
+    // CU by LDS (16-wave blocks staging x once per CU: 5 % slower steps, r2)
+    constexpr int nw1 = 8;
     a.spp = steps;
     a.kparts = 1;
     const size_t lds = bmm_lds(a.B, steps, nw1);
     // blocks per CU: LDS and the 16 waves a CU holds at this kernel's register count
     const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 16 / nw1));
     int nb = std::max(1, std::min(tiles, per_cu * bmm_cus()));
-    // Q|K|V (tuning, LFK_BMM_QKV_TPB): tiles per block - every block stages the whole x slice
-    // (B rows x K), so fewer blocks over more tiles each trade x staging for weight parallelism
-    static const int qkv_tpb = std::max(1, env_int("LFK_BMM_QKV_TPB", 1));
-    if (a.qkv_epi && qkv_tpb > 1) nb = std::max(1, std::min(nb, (tiles + qkv_tpb - 1) / qkv_tpb));
+    // one tile per Q|K|V block although every block stages the whole x slice: 2-4 tiles per
+    // block (fewer stagings, less weight parallelism) measured 1-8 % slower steps (r3 sweep)
     if (a.swiglu_epi) {  // every CU group gets the same number of blocks (the range split assumes it)
       const int G = std::max(1, std::min(bmm_cus(), tiles));
       nb = G * std::max(1, std::min(per_cu, tiles / G));
       a.tile_groups = G;
     }
-    if constexpr (QT == T_Q4_K) {
-      if (nw1 == 16) {
-        hipLaunchKernelGGL((bmm_kernel<QT, 16, 1>), dim3(nb), dim3(1024), lds, s, a, a);
-        return;
-      }
-    }
-    if (nw1 == 4) hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(nb), dim3(256), lds, s, a, a);
-    else if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 8, 2>), dim3(nb), dim3(512), lds, s, a, a);
-    else hipLaunchKernelGGL((bmm_kernel<QT, 8, 1>), dim3(nb), dim3(512), lds, s, a, a);
+    hipLaunchKernelGGL((bmm_kernel<QT, nw1, 1>), dim3(nb), dim3(nw1 * 64), lds, s, a, a);
     return;
   }
   // K part: the staged x slice stays <= 32 KB (B rows x part x 2 B); parts are split further
   // (more blocks, more-way atomics) only while there are fewer than ~4 blocks per CU
   const int bp = a.B <= 4 ? 4 : a.B <= 8 ? 8 : 16;
-  static const int xkb = env_int("LFK_BMM_XKB", 32);  // staged-x budget (tuning)
+  constexpr int xkb = 32;  // staged-x budget (KB)
   int spp = std::max(1, std::min(steps, 2 * xkb / bp));
-  static const int want_b = env_int("LFK_BMM_BLOCKS", 4);  // per CU (tuning)
-  const int want = want_b * bmm_cus();
+  const int want = 4 * bmm_cus();
   while (spp > 4 && (size_t)tiles * ((steps + spp - 1) / spp) < (size_t)want) spp = (spp + 1) / 2;
   // MoE down: every K part inside ONE expert - an unrouted expert's SwiGLU rows were never
   // written (its gate/up tiles are skipped), so its parts must be skipped whole, not mixed in
@@ -1223,17 +1243,15 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   a.kparts = kparts;
   // blocks per part: ~4 blocks per CU overall (each block loops over tiles, so its staged x
   // slice - as many bytes as a tile's weights at B = 8 - is amortised over several tiles)
-  static const int per_cu = env_int("LFK_BMM_GRID", 4);  // tuning
+  constexpr int per_cu = 4;
   // blocks past per_cu * CUs would start only when a first-round block retires (a whole
   // block lifetime of tail): the grid stays within one resident round
   const int bpk = std::max(1, std::min(tiles, (per_cu * bmm_cus()) / kparts));
   const size_t lds = bmm_lds(a.B, spp, 4);
-  if (bmm_pd<QT>() == 2) hipLaunchKernelGGL((bmm_kernel<QT, 4, 2>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
-  else hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
+  hipLaunchKernelGGL((bmm_kernel<QT, 4, 1>), dim3(bpk * kparts), dim3(256), lds, s, a, a);
 }
 
-// split-K Q|K|V: (K part, group of a.tpg tiles of one run) blocks, every wave one tile of the
-// part (tuning: LFK_QKV_SK_PARTS K parts, LFK_QKV_SK_TPG tiles per group)
+// split-K Q|K|V: (K part, group of a.tpg tiles of one run) blocks, every wave one tile of the part
 template <int QT, int QT2>
 static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   int ta = 0, tb = 0;
@@ -1244,12 +1262,10 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   }
   const int steps = a.w.K / 256;
   // 4 parts x 8-tile groups measured best at B = 6 (8 x 8: +3 %, 4 x 6 / 2 x 3: +1-4 %, 16 x 6: +15 %)
-  static const int parts_env = env_int("LFK_QKV_SK_PARTS", 4);
-  static const int tpg_env = env_int("LFK_QKV_SK_TPG", 8);
-  const int kparts = std::max(1, std::min(steps, parts_env));
+  const int kparts = std::max(1, std::min(steps, 4));
   a.spp = (steps + kparts - 1) / kparts;
   a.kparts = (steps + a.spp - 1) / a.spp;
-  a.tpg = std::max(1, tpg_env);
+  a.tpg = 8;
   const int ga = (ta + a.tpg - 1) / a.tpg, gb = (tb + a.tpg - 1) / a.tpg;
   a.nb1 = ga;
   const dim3 grid((ga + gb) * a.kparts);
@@ -1297,12 +1313,13 @@ static void bmm_check(const BmmArgs& a) {
   }
   if (a.ss_out && !(a.qkv_sk && a.xf)) throw std::runtime_error("bmm: ss_out needs the split-K Q|K|V norm");
   if (a.zero && (a.zero_n % 4 || reinterpret_cast<uintptr_t>(a.zero) % 16)) throw std::runtime_error("bmm: zero side job alignment");
+  if (a.wait && (a.wait_n < 1 || a.wait_group < 1 || !a.wait_err || a.xf || a.qkv_sk || a.swiglu_epi || a.ew || a.one_part ||
+                 a.store_out || a.nseg != 1 || a.B > 8))
+    throw std::runtime_error("bmm: in-flight wait arguments");
 }
 
 void bmm(const BmmArgs& a0, hipStream_t s) {
-  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
   BmmArgs a = a0;
-  a.fence_sync = fence;
   bmm_check(a);
   if (a.n_out <= 0) return;
   if (a.qkv_sk) {
@@ -1328,15 +1345,10 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
 }
 
 bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
-  static const int on = env_int("LFK_BMM_QKV2", 1);  // 0: one launch per run (A/B)
-  if (!on || !a0.qkv_epi || !b0.qkv_epi || a0.B != b0.B || a0.w.K != b0.w.K || a0.n_out <= 0 || b0.n_out <= 0)
+  if (!a0.qkv_epi || !b0.qkv_epi || a0.B != b0.B || a0.w.K != b0.w.K || a0.n_out <= 0 || b0.n_out <= 0)
     return false;
   if ((a0.xf == nullptr) != (b0.xf == nullptr)) return false;
-  static const int nw1_env = env_int("LFK_BMM_NW1", 8);
-  if (nw1_env != 8) return false;  // the one-part tuning knob picks other block shapes: separate launches
-  static const bool fence = env_int("LFK_BMM_SYNC", 0) != 0;
   BmmArgs a = a0, b = b0;
-  a.fence_sync = b.fence_sync = fence;
   bmm_check(a);
   bmm_check(b);
   auto tiles_of = [](const BmmArgs& x) {
@@ -1350,8 +1362,7 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
   const size_t lds = bmm_lds(a.B, steps, 8);
   const int per_cu = (int)std::max<size_t>(1, std::min<size_t>((160 * 1024) / lds, 2));
   const int ta = tiles_of(a), tb = tiles_of(b);
-  static const int qkv_tpb = std::max(1, env_int("LFK_BMM_QKV_TPB", 1));  // as in launch_bmm
-  const int cap = std::max(2, std::min(per_cu * bmm_cus(), (ta + tb + qkv_tpb - 1) / qkv_tpb));
+  const int cap = std::max(2, std::min(per_cu * bmm_cus(), ta + tb));
   // blocks in proportion to the runs' tiles, each run at least one block, within one resident round
   int na = std::min(ta, std::max(1, (int)((long long)cap * ta / (ta + tb))));
   int nbb = std::min(tb, std::max(1, cap - na));
@@ -1361,6 +1372,38 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
   if (ta_ == T_Q4_K && tb_ == T_Q6_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q6_K>), grid, blk, lds, s, a, b);
   else if (ta_ == T_Q4_K && tb_ == T_Q5_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q5_K>), grid, blk, lds, s, a, b);
   else return false;
+  return true;
+}
+
+bool attn_wo(const AttnDecodeArgs& aa, const BmmArgs& wo0, hipStream_t s) {
+  const int G = aa.n_kv_head > 0 ? aa.n_head / aa.n_kv_head : 0;
+  if (aa.head_dim != 128 || (G != 4 && G != 8) || aa.batch < 1 || aa.batch > 8 || !aa.done || !aa.out_h || aa.out ||
+      aa.pf[0] || wo0.w.type != T_Q4_K && wo0.w.type != T_Q6_K)
+    return false;
+  BmmArgs wo = wo0;
+  if (wo.B != aa.batch || !wo.wait || wo.wait != aa.done || wo.wait_n != aa.batch || wo.wait_group != G * aa.head_dim)
+    throw std::runtime_error("attn_wo: the Wo must wait for this attention's done counters");
+  bmm_check(wo);
+  const int tiles = (wo.n_out + 15) / 16, steps = wo.w.K / 256;
+  // K parts as the separate launch takes them (8 at d = 4096: one kv head of 4 query heads each)
+  int kparts = std::max(1, std::min(steps / 2, (bmm_cus() * 8 + tiles / 2) / std::max(1, tiles)));
+  wo.spp = (steps + kparts - 1) / kparts;
+  wo.kparts = kparts = (steps + wo.spp - 1) / wo.spp;
+  if (wo.spp > 2) return false;  // a wave's part must fit the 2-step register ring (issued before the wait)
+  AttnWoArgs p;
+  p.att = aa;
+  p.wo = wo;
+  p.n_wo = (tiles + 3) / 4 * kparts;  // 4-tile groups: one tile per wave
+  const int splits = (aa.n_ctx + 63) / 64, per = aa.n_kv_head * splits;
+  const dim3 grid(aa.n_kv_head, splits, aa.batch + (p.n_wo + per - 1) / per);
+  const size_t lds = 256 + (size_t)wo.B * (wo.spp * 256 + 8) * 2;
+  if (wo.w.type == T_Q4_K) {
+    if (G == 4) hipLaunchKernelGGL((attn_wo_kernel<T_Q4_K, 128, 4>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((attn_wo_kernel<T_Q4_K, 128, 8>), grid, dim3(256), lds, s, p);
+  } else {
+    if (G == 4) hipLaunchKernelGGL((attn_wo_kernel<T_Q6_K, 128, 4>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((attn_wo_kernel<T_Q6_K, 128, 8>), grid, dim3(256), lds, s, p);
+  }
   return true;
 }
 
@@ -1475,7 +1518,7 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   load_x(0);
   load_w(0, wa0, wa1);
   store_x(0);
-  lds_barrier(false);
+  lds_barrier();
   // nh is even (whole 256-k steps). The loads past the last half are clamped repeats and the
   // last stores go to the buffer nobody reads any more: no conditional around a load (a
   // load under a branch drains vmcnt at the join, and the conditional X slice went to scratch)
@@ -1485,13 +1528,13 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     load_x(i + 1);
     half(i, wa0, wa1);
     store_x((i + 1) & 1);
-    lds_barrier(false);
+    lds_barrier();
     // odd half: compute from B, load A
     load_w(min(i + 2, nh - 1), wa0, wa1);
     load_x(min(i + 2, nh - 1));
     half(i + 1, wb0, wb1);
     store_x(i & 1);
-    lds_barrier(false);
+    lds_barrier();
   }
   // ---- epilogue: acc[j][g][e] = (weight row 16 tile + 4 kq + e, token t0 + 16 g + r16)
 #pragma unroll
@@ -1546,15 +1589,13 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   // 2048 tokens: twice the fragment reuse once the grid is many rounds deep); the 4096- and
   // 1024-row projections on 4 x 64 - 4 blocks per CU - then split over K (partials by atomic
   // add) only while the grid does not cover the CUs, >= 2 steps (512 k) per part.
-  // LFK_T16_CFG="waves,tokens" pins one (tuning).
-  static const char* cfg_env = getenv("LFK_T16_CFG");
+  // a.cfg = waves * 1000 + tokens pins one (tools/gemm_bench.py --cfg).
   const int ntiles = (a.w.rows + 15) / 16, steps = a.w.K / 256, cus = bmm_cus();
   // grouped: size the shape and split for the expected rows, launch for the most
   const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
   int nw = 4, tm = 64;
-  int pin_nw = 0, pin_tm = 0;
-  if (cfg_env && sscanf(cfg_env, "%d,%d", &pin_nw, &pin_tm) == 2 &&
-      ((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && pin_tm == 64))) {
+  const int pin_nw = a.cfg / 1000, pin_tm = a.cfg % 1000;
+  if (((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && pin_tm == 64))) {
     nw = pin_nw;
     tm = pin_tm;
   } else if (EPI == GEMM_SWIGLU) {

@@ -218,9 +218,8 @@ static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
   }
   dim3 grid((a.w.rows + BNT - 1) / BNT, (a.T + BMT - 1) / BMT, split), block(2 * BNT);
   // 256-token or 256-row tiles are always double-buffered (110 KB of LDS, one block per CU)
-  static const int force_db = getenv("LFK_GEMM_DB") ? atoi(getenv("LFK_GEMM_DB")) : -1;
   constexpr bool big = BMT == 256 || BNT == 256;
-  const bool db = big || (force_db >= 0 ? force_db > 0 : tiles * split <= 512);
+  const bool db = big || tiles * split <= 512;
   if (a.seg_dev && split > 1 && epi != GEMM_STORE) throw std::runtime_error("gemm_dq: grouped split-K needs STORE");
 #define LFK_GEMM_LAUNCH(E)                                                                        \
   do {                                                                                             \
@@ -240,13 +239,11 @@ static void launch_gemm_t(const GemmArgs& a, int epi, hipStream_t s) {
 // 128-token tiles once a prompt chunk (or an expert's expected rows) exceeds 64 tokens;
 template <int QT>
 static void launch_gemm(const GemmArgs& a, int epi, hipStream_t s) {
-  static const int force = getenv("LFK_GEMM_BM") ? atoi(getenv("LFK_GEMM_BM")) : 0;
-  static const int force_bn = getenv("LFK_GEMM_BN") ? atoi(getenv("LFK_GEMM_BN")) : 0;
   const int rows = a.seg_dev ? (a.rows_hint > 0 ? a.rows_hint : a.T) : a.T;
-  const int bm = force ? force : (rows > 64 ? 128 : 64);
+  const int bm = rows > 64 ? 128 : 64;
   // 256-row tiles for the gate/up GEMM (measured: 124.6 -> 112.6 us at 256 tokens, 242 -> 239 at
   // 512); the split-K residual projections stay on 128-row tiles (Q6_K down is slower at 256)
-  const bool wide = force_bn ? force_bn == 256 : epi == GEMM_SWIGLU;
+  const bool wide = epi == GEMM_SWIGLU;
   if (bm >= 256) launch_gemm_t<QT, 256, 128>(a, epi, s);
   else if (bm >= 128) {
     if (wide) launch_gemm_t<QT, 128, 256>(a, epi, s);

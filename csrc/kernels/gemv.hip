@@ -192,11 +192,6 @@ static int pow2_floor(int v) {
 }
 static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
   const int LB = (qt == T_F32) ? 2 : ((qt == T_F16 || nchunks > 128) ? 4 : 8);
-  static const char* env = getenv("LFK_GEMV_CFG");  // "nr,u" override (tuning)
-  if (env && *env) {
-    GemvCfg c{4, 2};
-    if (sscanf(env, "%d,%d", &c.nr, &c.u) == 2 && c.nr >= min_nr && c.nr * c.u <= LB) return c;
-  }
   // measured on MI355X with weights streamed from HBM (tools/gemv_sweep.sh):
   //   K > 4096 (FFN down)         : one row per wave, 4 passes (Q6_K: 2) in flight
   //   >= 16384 rows (gate/up, head): 4 rows per wave, 1 pass
@@ -218,24 +213,11 @@ static GemvCfg pick_cfg(int qt, int rows, int nchunks, int min_nr) {
 // EARLY launches: 1024-thread blocks pinned to one per CU by their LDS request
 // (> half of the 160 KiB), so the grid is exactly one block per CU.
 static constexpr size_t kOnePerCuLds = 80 * 1024 + 256;
-// classes (bit mask, env LFK_GEMV_EARLY overrides the default)
+// classes: the SwiGLU gate/up, the long-K split-K (down) and the long-K Q|K|V, measured in-situ
+// (decode step) on MI355X; pinning the others, or loading x before the weights in the pinned
+// blocks, was slower (r2 sweeps)
 enum EarlyCls : int { EC_SWIGLU = 1, EC_SPLITK_LONG = 2, EC_SPLITK = 4, EC_STORE = 8, EC_QKV = 16, EC_QKV_LONG = 32 };
-static bool gemv_early(int cls) {
-  static const int mask = [] {
-    const char* e = getenv("LFK_GEMV_EARLY");
-    return e ? atoi(e) : (EC_SWIGLU | EC_SPLITK_LONG | EC_QKV_LONG);  // measured in-situ (decode step) on MI355X
-  }();
-  return (mask & cls) != 0;
-}
-// LFK_GEMV_PIN: same class mask; 1024-thread blocks pinned one per CU, x loaded
-// and quantised BEFORE the first weight loads (the classic order)
-static bool gemv_pin(int cls) {
-  static const int mask = [] {
-    const char* e = getenv("LFK_GEMV_PIN");
-    return e ? atoi(e) : 0;
-  }();
-  return (mask & cls) != 0;
-}
+static bool gemv_early(int cls) { return (cls & (EC_SWIGLU | EC_SPLITK_LONG | EC_QKV_LONG)) != 0; }
 static int early_cls(int epi, int K) {
   if (epi == EPI_SWIGLU) return EC_SWIGLU;
   if (epi == EPI_ADD) return K > 4096 ? EC_SPLITK_LONG : EC_SPLITK;
@@ -272,20 +254,14 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
     // K > 4096 (FFN down, 70B): 1024-thread blocks so the x prologue is one batch
     // of loads per thread (issued before the weights) and 16 waves share its LDS
     // copy; 16 waves per CU cap the registers at 128, hence NR*U <= 4 there
-    static const bool force1024 = getenv("LFK_GEMV_BLOCK") && atoi(getenv("LFK_GEMV_BLOCK")) == 1024;
     if constexpr (NR * U <= 4) {
       if (gemv_early(early_cls(EPI, a.w.K))) {
         if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, true>, lds, items, a, s);
         else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, false, false, true>, lds, items, a, s);
         return;
       }
-      if (gemv_pin(early_cls(EPI, a.w.K))) {
-        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, false>, lds, items, a, s);
-        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, false, false, false>, lds, items, a, s);
-        return;
-      }
     }
-    if (a.w.K > 4096 || (force1024 && NR * U <= 4)) {
+    if (a.w.K > 4096) {
       if constexpr (NR * U <= 4) {
         if (a.norm_w) {
           auto k = gemv_kernel<QT, EPI, NR, U, true, 1024>;
@@ -320,9 +296,6 @@ static void launch_gemv_tl(const GemvArgs& a, hipStream_t s) {
       if (gemv_early(early_cls(EPI, a.w.K))) {
         if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, true, false, true>, lds, items, a, s);
         else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, true, false, true>, lds, items, a, s);
-      } else if (gemv_pin(early_cls(EPI, a.w.K))) {
-        if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, true, false, false>, lds, items, a, s);
-        else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, true, false, false>, lds, items, a, s);
       } else if (a.w.K > 4096) {
         auto k = gemv_kernel<QT, EPI, NR, U, false, 1024, true>;
         hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
@@ -349,11 +322,6 @@ static void launch_gemv_splitk(const GemvArgs& a, hipStream_t s) {
     else launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true, true>, lds, items, a, s);
     return;
   }
-  if (gemv_pin(early_cls(EPI_ADD, a.w.K))) {
-    if (a.norm_w) launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true, false>, lds, items, a, s);
-    else launch_early(gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true, false>, lds, items, a, s);
-    return;
-  }
   if (a.w.K > 4096) {  // long rows: 1024-thread blocks, one-batch x prologue
     auto k = a.norm_w ? gemv_kernel<QT, EPI_ADD, 4, 1, true, 1024, false, true>
                       : gemv_kernel<QT, EPI_ADD, 4, 1, false, 1024, false, true>;
@@ -370,9 +338,7 @@ static void launch_gemv_splitk(const GemvArgs& a, hipStream_t s) {
 template <int QT, int EPI>
 static void launch_gemv(const GemvArgs& a, hipStream_t s) {
   if constexpr (EPI == EPI_ADD && (QT == T_Q4_K || QT == T_Q5_K || QT == T_Q6_K || QT == T_Q8_0)) {
-    static const char* sk = getenv("LFK_GEMV_SPLITK");  // "0" disables (A/B measurements)
-    const bool on = !(sk && sk[0] == '0');
-    if (on && !a.dbg_clk && a.w.K >= 4096 && !a.debug) return launch_gemv_splitk<QT>(a, s);
+    if (!a.dbg_clk && a.w.K >= 4096 && !a.debug) return launch_gemv_splitk<QT>(a, s);
   }
   if (a.dbg_clk) {
     if constexpr (QT == T_Q4_K || QT == T_Q6_K) return launch_gemv_tl<QT, EPI>(a, s);
@@ -676,8 +642,7 @@ __global__ __launch_bounds__(256) void gemv_moe_down_kernel(MoeDownArgs a) {
 }
 
 void gemv_moe_down(const MoeDownArgs& a, hipStream_t s) {
-  static const bool splitk = !(getenv("LFK_MOE_SPLITK") && getenv("LFK_MOE_SPLITK")[0] == '0');
-  if (splitk && moe_down_splitk(a, s)) return;
+  if (moe_down_splitk(a, s)) return;  // the split-K form where its types / shapes allow
   const int K = a.w.K;
   const size_t lds = (size_t)a.n_slots * (K + (K / 32) * 4) + 64;
   dim3 grid(grid_for((a.w.rows + 1) / 2)), block(256);

@@ -124,7 +124,6 @@ struct BmmArgs {
   // covers no expert with a routed row exit before loading a byte.
   const float* ew = nullptr;
   int ew_ld = 0, tiles_per_expert = 0, steps_per_expert = 0;
-  bool fence_sync = false;         // tile barriers as __syncthreads (drains the ring; A/B only)
   bool one_part = false;           // plain projection as one K part (8-wave blocks, no atomics)
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block wall_clock64 stamps [grid][8]
   int nb1 = 0;                     // bmm_qkv2: blocks of the first run; split-K Q|K|V: first group of run B
@@ -143,6 +142,13 @@ struct BmmArgs {
   // side job of the split-K launches: zero [zero, zero + zero_n) floats (zero_n % 4 == 0)
   float* zero = nullptr;
   int zero_n = 0;
+  // in-flight producer (the batched Wo beside the batched attention, wave-owned split-K kernel):
+  // a block of K part [k0, k0 + kn) issues its first weights, then waits until wait[h] >= wait_n
+  // for every h in [k0 / wait_group, (k0 + kn - 1) / wait_group] (the attention's per-kv-head
+  // done counters) and stages x with sc1 loads; a timed-out wait sets *wait_err (host-mapped)
+  const int* wait = nullptr;
+  int wait_n = 0, wait_group = 0;
+  int* wait_err = nullptr;
 };
 // split-K Q|K|V (BmmArgs::qkv_sk): false = unsupported shape / type mix (caller: one-part path)
 bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B);
@@ -267,6 +273,9 @@ struct AttnDecodeArgs {
   // batched: also write the output as the next projection's bmm input (f16, bmm k swizzle)
   __half* out_h = nullptr;
   size_t out_h_stride = 0;
+  // batched, with out_h: once a row's output of kv head h is written (sc1 stores), done[h] += 1
+  // (agent scope) - the Wo projection running beside this launch (BmmArgs::wait) polls it
+  int* done = nullptr;
   // batched, split-K Q|K|V (BmmArgs::qkv_sk): q / k / v of row b are the RoPE'd but unnormalised
   // sums qkv_raw[b * qkv_ld + ...] (q at 0, k at k_off, v at v_off), the row's RMSNorm scale is
   // rsqrt(ss[b] * inv_k + eps); the block holding the new position scales its k / v, writes them
@@ -283,6 +292,10 @@ struct AttnDecodeArgs {
   int* pf_sink = nullptr;
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
+// The batched attention and its Wo projection in ONE launch (bmm.hip): `wo` waits for the
+// attention's done counters (wo.wait == a.done). False: shape / weight type not covered - the
+// caller launches attn_decode + bmm instead.
+bool attn_wo(const AttnDecodeArgs& a, const BmmArgs& wo, hipStream_t s);
 size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim);
 
 // Prefill: causal attention of T queries at positions pos0.. over the cache.
@@ -342,6 +355,7 @@ struct GemmT16Args {
   // step inside each tile
   size_t tile_stride = 0;
   int step0 = 0;
+  int cfg = 0;                     // block shape pin (waves * 1000 + tokens; tuning tools), 0: the measured rule
 };
 void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s);
 

@@ -182,6 +182,7 @@ Engine::~Engine() {
     if (bev_[i]) hipEventDestroy(bev_[i]);
   }
   if (h_rmeta_) hipHostFree(h_rmeta_);
+  if (wo_err_h_) hipHostFree(wo_err_h_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -299,8 +300,7 @@ void Engine::alloc_buffers() {
   attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
-  if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = std::atoi(e);
-  if (const char* e = std::getenv("LFK_ATTN_TOUCH_GU_FRAC")) attn_touch_gu_frac_ = std::atof(e);
+  if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = e[0] != '0';  // A/B (test_engine_gpu)
   const int tp = opt_.tp_size;
   cand_words_ = sampler_cand_words(V_l_);
   cand_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_);
@@ -367,10 +367,6 @@ void Engine::alloc_buffers() {
 void Engine::setup_batch_mfma() {
   bg_ = bg_ffn_ = false;
   if (!bmax_ || opt_.layer_begin > 0) return;
-  const char* b1 = std::getenv("LFK_B1_GEMV");
-  b1_gemv_ = !(b1 && b1[0] == '0');
-  const char* e = std::getenv("LFK_BATCH_MFMA");
-  if (e && e[0] == '0') return;
   auto ok = [&](const QMat& m) { return m.base && bmm_supported(m.type, m.K); };
   auto kfit = [](int K) { return K % 128 == 0 && K <= 32768; };  // bprep's row shapes
   bool att = ok(output_) && kfit(hp_.n_embd) && kfit(nq_) && (V_pad_ % 4) == 0 && ((nq_ + 2 * nkvd_) % 4) == 0;
@@ -386,12 +382,9 @@ void Engine::setup_batch_mfma() {
     const Layer& L = layers_[l];
     moe = moe_router_fused_ok(L.router.type, hp_.n_expert, hp_.n_embd) && ok(L.gu_exps) && ok(L.down_exps);
   }
-  const char* bm = std::getenv("LFK_BATCH_MOE");
   bg_ = att;
   bg_ffn_ = att && ffn;
-  moe_b_ = att && moe && !(bm && bm[0] == '0');
-  const char* nf = std::getenv("LFK_BMM_NORM");
-  norm_fold_ = !(nf && nf[0] == '0');
+  moe_b_ = att && moe;
   const char* sk = std::getenv("LFK_QKV_SK");
   qkv_sk_ = !(sk && sk[0] == '0');
   if (const char* sc = std::getenv("LFK_STEP_CLK")) {
@@ -403,10 +396,19 @@ void Engine::setup_batch_mfma() {
   const int E = std::max(1, hp_.n_expert);
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
   {
-    const size_t n = (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16;  // + ss_b_
+    const size_t n = qkv_b_zero_n();  // + ss_b_ [16] + wo_done_ [64]
     qkv_b_ = (float*)dalloc(sizeof(float) * n);
     HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * n, stream_));
     ss_b_ = qkv_b_ + (size_t)bmax_ * (nq_ + 2 * nkvd_);
+    wo_done_ = reinterpret_cast<int*>(ss_b_ + 16);
+    if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
+    if (wo_fuse_ && nkv_l_ <= 64) {
+      HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
+      *wo_err_h_ = 0;
+      HIPCHK(hipHostGetDevicePointer((void**)&wo_err_, wo_err_h_, 0));
+    } else {
+      wo_fuse_ = false;
+    }
   }
   hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_) * (moe_b_ ? E : 1));
   if (moe_b_) ew_b_ = (float*)dalloc(sizeof(float) * bmax_ * E);
@@ -486,10 +488,11 @@ void Engine::step_clk_zero() {
 }
 
 void Engine::check_device_err() {
-  // the only bounded in-kernel wait left is the P2P all-reduce's (TP); a blocking read of an
-  // error word nothing else writes cost every step a synchronous copy
+  // the bounded in-kernel waits: the P2P all-reduce's (TP) and the batched Wo's (a host-mapped
+  // word: no copy); a blocking read of an error word nothing else writes cost every step a copy
   int e = 0;
   if (p2p_ && p2p_->ready()) e = p2p_->error();
+  if (!e && wo_err_h_ && __atomic_load_n(wo_err_h_, __ATOMIC_ACQUIRE)) e = 200;  // the batched Wo's wait
   if (e != 0) {
     healthy_ = false;
     last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
@@ -599,41 +602,10 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
-  if (attn_touch_ > 0 && nkv_l_ < 63) {  // weights into the memory-side cache under the attention
+  if (attn_touch_ && nkv_l_ < 63) {  // this layer's Wo into the memory-side cache under the attention
     aa.pf_sink = attn_cnt_ + 63;
-    if (attn_touch_ & 1) {                // this layer's Wo
-      aa.pf[0] = L.wo.base;
-      aa.pf_bytes[0] = qmat_bytes(L.wo);
-    }
-    if ((attn_touch_ & 2) && l + 1 < hp_.n_layer) {  // the next layer's QKV
-      const Layer& N = layers_[l + 1];
-      aa.pf[1] = N.wq.base; aa.pf_bytes[1] = qmat_bytes(N.wq);
-      aa.pf[2] = N.wk.base; aa.pf_bytes[2] = qmat_bytes(N.wk);
-      aa.pf[3] = N.wv.base; aa.pf_bytes[3] = qmat_bytes(N.wv);
-    }
-    if ((attn_touch_ & 4) && hp_.n_expert == 0 && L.w_gu.base) {
-      // the rows each CU's gate/up GEMV block streams first: the one-CU launch gives
-      // block b a contiguous item range, ~rows [b, b + 1) * rows / 256 in memory order
-      // Every touched byte stays inside the plane: rows need not divide by 256 (F = 8640 gives
-      // segR 68, and 255 * 68 > 2F), so the segment count is cut to the segments that start
-      // inside the plane and the head to what the LAST segment still holds.
-      const QMat& W = L.w_gu;
-      const size_t rows = (size_t)W.rows;
-      const size_t segR = (rows + 255) / 256;
-      const size_t nseg = std::min<size_t>(256, (rows + segR - 1) / segR);
-      const size_t last_rows = rows - (nseg - 1) * segR;
-      const double frac = std::min(1.0, std::max(0.0, attn_touch_gu_frac_));
-      const size_t head = std::min(last_rows, std::max<size_t>(1, (size_t)(segR * frac)));
-      aa.pf[4] = W.base + W.P.p0; aa.pf_nseg[4] = (int)nseg;
-      aa.pf_seg_stride[4] = segR * W.P.s0; aa.pf_bytes[4] = head * W.P.s0;
-      if (W.P.s1) {
-        aa.pf[5] = W.base + W.P.p1; aa.pf_nseg[5] = (int)nseg;
-        aa.pf_seg_stride[5] = segR * W.P.s1; aa.pf_bytes[5] = head * W.P.s1;
-      }
-      for (int k = 4; k < 6; ++k)  // (nseg-1)*stride + bytes <= plane bytes
-        if (aa.pf[k] && (nseg - 1) * aa.pf_seg_stride[k] + aa.pf_bytes[k] > rows * (k == 4 ? W.P.s0 : W.P.s1))
-          throw std::runtime_error("attention touch range exceeds the gate/up plane");
-    }
+    aa.pf[0] = L.wo.base;
+    aa.pf_bytes[0] = qmat_bytes(L.wo);
   }
   attn_decode(aa, s);
 
@@ -994,7 +966,7 @@ void Engine::down_rows(const QMat& w, const __half* xh, int ldh, float* out, int
   BmmArgs a;
   a.w = w; a.xh = xh; a.ldh = ldh; a.out = out; a.ldo = d; a.n_out = d; a.B = B; a.dbg_clk = dbg;
   if (zero_qkv) {
-    a.zero = qkv_b_; a.zero_n = bmax_ * (nq_ + 2 * nkvd_) + 16;
+    a.zero = qkv_b_; a.zero_n = (int)qkv_b_zero_n();
   }
   bmm(a, s);
 }
@@ -1032,13 +1004,13 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   // RoPE + KV append in the Q|K|V epilogue when the whole K fits one LDS-staged part
   const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
   // attention / FFN RMSNorm folded into the one-part projections' x staging (no prep launch)
-  const bool fnorm = fused && norm_fold_ && bmm_norm_fits(d, B);
+  const bool fnorm = fused && bmm_norm_fits(d, B);
   // Q|K|V split over K (the default at B <= 8): RoPE'd partial sums into qkv_b_, normalised and
   // appended to the caches by the attention
   const bool sk = qkv_sk_ && bmm_qkv_sk_supported(L.t_wq.type, L.t_wk.type, L.t_wv.type, d, B);
   // FFN paths without the down projection's zero side job: a memset node re-zeroes qkv_b_ / ss_b_
   auto zero_qkv = [&]() {
-    if (sk) HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * (bmax_ * (size_t)(nq_ + 2 * nkvd_) + 16), s));
+    if (sk) HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * qkv_b_zero_n(), s));
   };
   if (sk) {
     BmmArgs a;
@@ -1110,10 +1082,23 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
   }
   aa.dbg_clk = clk_of(l, 1);
-  attn_decode(aa, s);
-  tp_begin();
-  bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
-  tp_end();
+  // the attention and Wo in one launch (bmm.hip attn_wo): Wo's weights stream while the
+  // attention runs, each K part starting once its kv heads are done for every row
+  bool fused_wo = false;
+  if (sk && wo_fuse_ && !tp && B <= 8) {
+    aa.done = wo_done_;
+    BmmArgs a;
+    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = x_; a.ldo = d; a.n_out = d; a.B = B;
+    a.wait = wo_done_; a.wait_n = B; a.wait_group = (nh_l_ / nkv_l_) * hd; a.wait_err = wo_err_;
+    fused_wo = attn_wo(aa, a, s);
+    if (!fused_wo) aa.done = nullptr;
+  }
+  if (!fused_wo) {
+    attn_decode(aa, s);
+    tp_begin();
+    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
+    tp_end();
+  }
   if (moe_b_ && fused) {
     // MoE: dense per-row expert weights (f32 router on the normed rows), then every expert's
     // SwiGLU rows in ONE gate/up launch (epilogue scaled by the row's weight for that expert,
@@ -1552,7 +1537,7 @@ std::vector<int> Engine::batch_step_impl(const std::vector<int>& slots) {
 // Queue one batch step of `slots` and the copy of its tokens to the pinned h_dst (no sync).
 void Engine::enqueue_batch_launch(const std::vector<int>& slots, int* h_dst) {
   const int B = (int)slots.size();
-  if (B == 1 && b1_gemv_) {
+  if (B == 1) {
     // one active row: the single-row GEMV decode of that slot beats the batched projections
     launch_step(slots[0]);
     HIPCHK(hipMemcpyAsync(h_dst, state_ + (size_t)S_NSTATE * slots[0] + S_TOKEN, sizeof(int),

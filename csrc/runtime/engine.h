@@ -281,11 +281,9 @@ class Engine : public SlotBackend {
   // [64] per-kv-head split counters (last-arriver combine); word 63 is reserved as the
   // weight touch's pf_sink, which is why the touch needs nkv_l_ < 63
   int* attn_cnt_ = nullptr;
-  // LFK_ATTN_TOUCH: decode attention pre-touches weights into the memory-side cache:
-  // bit mask: 1 this layer's Wo, 2 the next layer's Wq/Wk/Wv, 4 the head of every CU's
-  // gate/up range (LFK_ATTN_TOUCH_GU_FRAC of it, clamped to (0, 1])
-  int attn_touch_ = 1;
-  double attn_touch_gu_frac_ = 0.3;
+  // decode attention pre-touches this layer's Wo into the memory-side cache (LFK_ATTN_TOUCH=0:
+  // off, A/B; touching the next Q|K|V or the gate/up heads too measured neutral, r2-r3)
+  bool attn_touch_ = true;
   size_t cand_words_ = 0;     // sampler candidate block of one row (sampler_cand_words(V_l))
   unsigned* cand_ = nullptr;  // [cand_words_] this rank's stage-1 block (single row)
   unsigned* cand_all_ = nullptr;   // [tp][cand_words_] gathered blocks (tp > 1)
@@ -333,22 +331,20 @@ class Engine : public SlotBackend {
   int last_batch_ = 0;
   // batch_step projections on the MFMA batched projection (bmm.hip: weights streamed once per
   // step for all rows) instead of the prefill GEMM: attention/head (bg_) and the dense FFN
-  // (bg_ffn_); LFK_BATCH_MFMA=0 keeps the GEMM path (A/B)
+  // (bg_ffn_); shapes bmm does not take keep the GEMM path
   bool bg_ = false, bg_ffn_ = false;
   bool prefill_t16_ = false;  // LFK_PREFILL_T16=0: the planar bf16 gemm_dq (A/B)
   // MoE FFN on the batched projections: the experts as one stacked SwiGLU matrix and one
   // K-concatenated down matrix (t_gu / t_down of each layer), routed by dense per-row expert
-  // weights ew_b_ [bmax][E] (bmm.hip, BmmArgs::ew); LFK_BATCH_MOE=0 keeps the grouped GEMM
+  // weights ew_b_ [bmax][E] (bmm.hip, BmmArgs::ew)
   bool moe_b_ = false;
   float* ew_b_ = nullptr;
   __half* xh_b_ = nullptr;    // [bmax][max(d, nq, F)] prepared f16 projection input
   QMat t_output_;             // tile16 copy of the output head
   float* gu_b_ = nullptr;     // [bmax][2 F_l] gate/up pre-activations (32-row interleaved)
   __half* hh_b_ = nullptr;    // [bmax][F_l] (MoE: [bmax][E F_l]) down input written by the SwiGLU epilogue
-  // RMSNorm folded into the one-part projections' staging (Q|K|V, gate/up: no prep launch;
-  // LFK_BMM_NORM=0 restores the prep launches); opt-in, measured neutral-to-slower: the final
-  // norm + one-part logits store for the head (LFK_BMM_HEAD1=1)
-  bool norm_fold_ = true;
+  // RMSNorm folded into the one-part projections' staging where the rows fit (Q|K|V, gate/up: no
+  // prep launch; the head as one part with the folded final norm measured neutral-to-slower)
   // Q|K|V as a split-K projection (bmm.hip BmmArgs::qkv_sk, B <= 8): RoPE'd partial sums added
   // into qkv_b_ [bmax][nq + 2 nkvd] (+ the rows' sums of squares ss_b_ [16]); the batched
   // attention normalises them and appends the new K / V, the Wo launch re-zeroes both
@@ -362,6 +358,15 @@ class Engine : public SlotBackend {
   }
   float* qkv_b_ = nullptr;
   float* ss_b_ = nullptr;
+  // the batched attention and Wo in one launch (split-K Q|K|V, no TP; bmm.hip attn_wo): Wo
+  // streams its weights while the attention runs and starts each K part once that part's kv
+  // heads are done for every row (wo_done_ [64] counters after ss_b_, zeroed with qkv_b_); a
+  // timed-out wait sets *wo_err_ (host-mapped). LFK_WO_FUSE=0: two launches (A/B).
+  bool wo_fuse_ = true;
+  int* wo_done_ = nullptr;
+  int* wo_err_h_ = nullptr;   // host view
+  int* wo_err_ = nullptr;     // device view
+  size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16 + 64; }
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   // a second instantiation of each, for the pipelined launches: consecutive in-flight steps
@@ -371,10 +376,9 @@ class Engine : public SlotBackend {
   int launch_par_ = 0;  // which instantiation enqueue_batch_launch uses (0: bgraph_, 1: bgraph2_)
   // single-row decode (GEMV path) of KV slot dslot_: enqueue_decode reads it while capturing;
   // one graph per slot (slot 0's is graph_exec_). batch_step over ONE row takes this path
-  // (LFK_B1_GEMV=0: the batched projections), the faster one at B = 1
+  // (the faster one at B = 1: 1.65 vs 2.18 ms)
   int dslot_ = 0;
   std::vector<hipGraphExec_t> sgraph_;
-  bool b1_gemv_ = true;
   bool last_b1_ = false;      // the last batch_step ran its one row on the single-row path
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr;

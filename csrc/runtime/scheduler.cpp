@@ -263,10 +263,14 @@ void BatchScheduler::loop() {
         // the next step feeds each row's newest token at position prompt + tokens - 1 + 1:
         // only while that stays inside the context (a row finishing on the context end must
         // not get a KV write past n_ctx from a step queued before its end was seen)
+        // (queued requests hold the next step back only when one of them could be admitted now:
+        // with every slot taken, pipelining stays on through the saturated stretch)
         bool more;
         {
           std::lock_guard<std::mutex> g(mu_);
-          more = pending_.empty() && !stop_;
+          bool free_slot = false;
+          for (int s = first_slot_; s < n_slots_ && !free_slot; ++s) free_slot = !slot_req_[s];
+          more = (pending_.empty() || !free_slot) && !stop_;
           for (size_t b = 0; more && b < row_req.size(); ++b) {
             const Req& r = *row_req[b];
             more = !r.done && !r.cancel && (int)(r.prompt.size() + r.tokens.size()) < eng_.n_ctx();

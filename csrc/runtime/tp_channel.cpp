@@ -26,8 +26,24 @@ struct alignas(64) TPChannel::Hdr {
   uint32_t cap;
   alignas(64) std::atomic<uint32_t> seq;          // commands published (futex word)
   alignas(64) std::atomic<uint32_t> ack[kMaxFollowers];  // last command each rank copied
+  std::atomic<int32_t> follower_pid[kMaxFollowers];      // set by attach(): the leader's liveness probe
   alignas(64) uint32_t len;                        // bytes of the current command
 };
+
+// a process that exited - or exited and is not yet reaped (a zombie) - is dead for the channel
+static bool pid_alive(int pid) {
+  if (pid <= 0) return true;  // not known (yet): nothing to probe
+  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  if (FILE* f = fopen(path, "r")) {
+    char state = 0;
+    const int n = fscanf(f, "%*d %*s %c", &state);
+    fclose(f);
+    if (n == 1 && (state == 'Z' || state == 'X')) return false;
+  }
+  return true;
+}
 
 static_assert(std::atomic<uint32_t>::is_always_lock_free, "futex word must be a plain 32-bit word");
 
@@ -55,6 +71,7 @@ std::unique_ptr<TPChannel> TPChannel::create(const std::string& name, int world,
   c->h_->len = 0;
   c->h_->seq.store(0);
   for (auto& a : c->h_->ack) a.store(0);
+  for (auto& p : c->h_->follower_pid) p.store(0);
   c->payload_ = static_cast<uint8_t*>(p) + sizeof(Hdr);
   std::atomic_thread_fence(std::memory_order_release);
   c->h_->magic = kMagic;
@@ -78,32 +95,22 @@ std::unique_ptr<TPChannel> TPChannel::attach(const std::string& name, int rank) 
   if (c->h_->magic != kMagic || rank >= c->h_->world) throw std::runtime_error("tp channel: segment not initialised");
   c->payload_ = static_cast<uint8_t*>(p) + sizeof(Hdr);
   c->last_ = c->h_->seq.load(std::memory_order_acquire);  // nothing before attach is ours
+  c->h_->follower_pid[rank].store((int32_t)getpid(), std::memory_order_relaxed);
   c->h_->ack[rank].store(c->last_, std::memory_order_release);
   return c;
 }
 
 TPChannel::~TPChannel() {
+  // rank 0 owns the segment; a follower outliving a dead leader removes it too (no /dev/shm leak)
+  const bool unlink = !name_.empty() && (rank_ == 0 || (h_ && !leader_alive()));
   if (h_) munmap(h_, bytes_);
   if (fd_ >= 0) close(fd_);
-  if (rank_ == 0 && !name_.empty()) shm_unlink(name_.c_str());
+  if (unlink) shm_unlink(name_.c_str());
 }
 
 int TPChannel::world() const { return h_->world; }
 
-bool TPChannel::leader_alive() const {
-  const int pid = h_->leader_pid;
-  if (kill(pid, 0) != 0 && errno == ESRCH) return false;
-  // an exited leader that its parent has not reaped yet is a zombie: dead for our purposes
-  char path[64];
-  snprintf(path, sizeof(path), "/proc/%d/stat", pid);
-  if (FILE* f = fopen(path, "r")) {
-    char state = 0;
-    const int n = fscanf(f, "%*d %*s %c", &state);
-    fclose(f);
-    if (n == 1 && (state == 'Z' || state == 'X')) return false;
-  }
-  return true;
-}
+bool TPChannel::leader_alive() const { return pid_alive(h_->leader_pid); }
 
 void TPChannel::publish(const TPMsg& m) {
   if (rank_ != 0) throw std::runtime_error("tp channel: only rank 0 publishes");
@@ -116,6 +123,10 @@ void TPChannel::publish(const TPMsg& m) {
     while (h_->ack[r].load(std::memory_order_acquire) != cur) {
       if (++spins < 2000) continue;
       std::this_thread::sleep_for(std::chrono::microseconds(20));
+      // a crashed follower fails the command at once (every ~50 ms a liveness probe) instead of
+      // holding the engine - and the scheduler thread behind it - for the full timeout
+      if (spins % 2500 == 0 && !pid_alive(h_->follower_pid[r].load(std::memory_order_relaxed)))
+        throw std::runtime_error("tp channel: follower rank " + std::to_string(r) + " exited");
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
         throw std::runtime_error("tp channel: follower rank " + std::to_string(r) + " stopped consuming commands");
     }

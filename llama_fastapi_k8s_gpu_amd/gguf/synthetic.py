@@ -127,6 +127,10 @@ SPECS: Dict[str, ModelSpec] = {
     # batched step takes the prep (bprep) FFN path beside the split-K Q|K|V
     "tiny-llama3-d8k": ModelSpec("tiny-llama3-d8k", 8192, 1, 64, 8, 512, 0, 500000.0, "bpe", "q4_k_m",
                                  n_ctx_train=1024),
+    # Llama-3-70B's layer shape in 2 layers (small vocabulary): the TP = 8 rehearsal's per-rank
+    # shapes are the 70B's own (1 KV head, 8 query heads, 3584 FFN features per rank)
+    "llama3-70b-2l": ModelSpec("llama3-70b-2l", 8192, 2, 64, 8, 28672, 0, 500000.0, "bpe", "q4_k_m",
+                               n_ctx_train=1024, size_class="70B"),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

@@ -101,6 +101,7 @@ class ReferenceLlama:
         self.torch = torch
         self.reader = reader
         self.device = device
+        self._router_trace = None
         self.hp = LlamaHParams.from_metadata(reader.metadata)
         hp = self.hp
         if not hp.n_vocab:
@@ -251,6 +252,8 @@ class ReferenceLlama:
         rw = L["ffn_gate_inp"] if path != "prefill" else self._bf16(L["ffn_gate_inp"])
         hr = self._normed_input(x, L["ffn_norm"], None) if path == "decode" else h
         logits = hr @ rw.T                                    # [T, E]
+        if self._router_trace is not None:
+            self._router_trace.append(logits.clone())
         probs = torch.softmax(logits, -1)
         w, ids = torch.topk(probs, self.hp.n_expert_used, dim=-1)
         w = w / w.sum(-1, keepdim=True)
@@ -289,16 +292,19 @@ class ReferenceLlama:
         return torch.einsum("htl,lhd->thd", torch.softmax(s, -1), V).reshape(T, -1)
 
     def forward(self, tokens, n_past: int, all_logits: bool = False, trace: Optional[List[Dict]] = None,
-                path: Optional[str] = None):
+                path: Optional[str] = None, router_trace: Optional[List] = None):
         """Evaluate ``tokens`` at positions n_past.. ; returns logits [T,V] or [V].
         ``trace`` (a list) receives per layer the last token's q / k / v (roped), the attention
         output, x after the attention residual, the SwiGLU output and x after the FFN residual.
-        ``path``: None (exact fp32) or the engine path whose rounding to reproduce (class doc)."""
+        ``path``: None (exact fp32) or the engine path whose rounding to reproduce (class doc).
+        ``router_trace`` (a list, MoE, path None / decode / prefill) receives per layer the router
+        logits [T, E] - the TP tests judge an expert flip by their top-k margin."""
         torch = self.torch
         hp = self.hp
         if path not in (None, "decode", "prefill", "prefill16", "batch"):
             raise ValueError(f"unknown path {path!r}")
         T = len(tokens)
+        self._router_trace = router_trace
         pos = torch.arange(n_past, n_past + T)
         x = self.tok_embd[torch.as_tensor(list(tokens))]
         wk = self._wkind(path)

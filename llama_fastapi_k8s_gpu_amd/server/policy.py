@@ -84,13 +84,18 @@ def exact_token_trim(messages: List[Dict[str, str]], n_tokens: Callable[[List[Di
     token count reaches n_ctx fails the request (reference api.py:35-46 -> 500). Drop
     the oldest message after indices 0 and 1 (the reference's drop order) while the
     templated prompt's real token count is >= ``limit``; if two messages still do not
-    fit, shorten the last message's text from its start (its newest words survive).
+    fit, shorten the longest non-system message from its start (its newest words survive):
+    the persona (system) prompt is never cut - with no other message left to shorten the
+    prompt cannot fit and ValueError is raised.
     ``n_tokens(messages)`` = token count of the chat-templated prompt."""
     while n_tokens(messages) >= limit and len(messages) > 2:
         messages.pop(2)
     if n_tokens(messages) < limit or not messages:
         return messages
-    last = messages[-1]
+    cand = [i for i, m in enumerate(messages) if m.get("role") != "system"]
+    if not cand:
+        raise ValueError(f"prompt does not fit the context window of {limit} tokens")
+    last = messages[max(cand, key=lambda i: len(messages[i]["content"]))]
     text = last["content"]
     lo, hi = 0, len(text)           # smallest cut so the prompt fits: binary search on the prefix dropped
     while lo < hi:

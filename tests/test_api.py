@@ -239,3 +239,10 @@ def test_exact_token_trim_shortens_last_message():
     assert count(out) == 59 and out[1]["content"].endswith("b" * 49)
     with pytest.raises(ValueError):
         exact_token_trim([{"role": "system", "content": "s" * 80}, {"role": "user", "content": "u"}], count, 60)
+    # the reference's order puts the persona at index 1: with [ctx0, system] left, the context
+    # message is shortened, never the system prompt
+    msgs = [{"role": "user", "content": "c" * 40 + "d" * 40}, {"role": "system", "content": "p" * 30}]
+    out = exact_token_trim(msgs, count, 60)
+    assert out[1]["content"] == "p" * 30 and out[0]["content"] == "d" * 29 and count(out) == 59
+    with pytest.raises(ValueError):   # only the system prompt left: a clear error, not a cut persona
+        exact_token_trim([{"role": "system", "content": "p" * 80}], count, 60)

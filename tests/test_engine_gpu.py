@@ -125,15 +125,12 @@ def test_deep_model_no_drift(tmp_path):
 
 @pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m", "tiny-q8-oddff"])
 def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
-    """The decode attention's weight-touch plane (LFK_ATTN_TOUCH bits: 1 Wo, 2 next QKV, 4 gate/up heads)
-    only reads weights: decode logits match the untouched launch up to the fp32 order of the
-    split-K atomics."""
+    """The decode attention's weight-touch plane (LFK_ATTN_TOUCH: this layer's Wo) only reads
+    weights: decode logits match the untouched launch up to the fp32 order of the split-K atomics."""
     path = models[spec]
     toks = [int(t) for t in np.random.default_rng(3).integers(0, 1000, 24)]
     logits = []
-    # tiny-q8-oddff: 2F = 1152 gate/up rows, not a multiple of 256 (segments clamp to the plane)
-    monkeypatch.setenv("LFK_ATTN_TOUCH_GU_FRAC", "1.5")   # clamped to 1
-    for mode in ("0", "1", "7"):
+    for mode in ("0", "1"):
         monkeypatch.setenv("LFK_ATTN_TOUCH", mode)
         eng = _engine(path)
         eng.eval_logits(toks[:20], 0)

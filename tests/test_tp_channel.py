@@ -90,10 +90,37 @@ def test_follower_detects_dead_leader():
     assert q.get(timeout=60) == "leader gone"
     lp.join(timeout=10)
     fp.join(timeout=10)
-    try:
-        os.unlink("/dev/shm/" + name)
-    except FileNotFoundError:
-        pass
+    # the orphaned follower removed the dead leader's segment when its channel closed
+    assert not os.path.exists("/dev/shm/" + name)
+
+
+def _attach_then_exit(name, q):
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    c = load_cpu().TPChannel.attach(name, 1)   # noqa: F841 (kept open until the process dies)
+    q.put("attached")
+    q.close()
+    q.join_thread()   # the message is out before the process dies
+    os._exit(0)   # a follower that crashes without consuming anything
+
+
+def test_leader_detects_dead_follower():
+    """A follower that died fails the leader's next publish within a fraction of a second
+    (its pid is probed while the leader waits for the mailbox), not after the 600 s timeout."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_cpu
+    cpu = load_cpu()
+    name = _name("deadf")
+    lead = cpu.TPChannel.create(name, 2, 64)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    fp = ctx.Process(target=_attach_then_exit, args=(name, q))
+    fp.start()
+    assert q.get(timeout=60) == "attached"
+    fp.join(timeout=30)
+    lead.publish(b"one")           # the mailbox was empty: nothing to wait for
+    t0 = time.time()
+    with pytest.raises(Exception, match="exited"):
+        lead.publish(b"two")       # waits for the dead follower's copy of "one"
+    assert time.time() - t0 < 10
 
 
 def test_channel_rejects_bad_use():

@@ -8,13 +8,22 @@ sampling (candidate all-gather), rank 0 driving and rank 1 replaying its command
 over the native control channel (csrc/runtime/tp_channel.h).
 
 Checked against the same model at TP=1 in the same process and against the exact fp32
-model: prefill and graph-replayed decode logits (TP within 1e-2 of TP=1 - the activation
-quantum of the q8 / bf16 paths, whose rounding the all-reduce's summation order can flip
-- and no further from the exact model than TP=1), greedy generations (identical, or
-diverging only at a near-tie of the exact model), seeded sampling (identical draws until
-rounding noise moves a probability boundary), continuous batching under TP (rows of one
-batched step), cooperative cancel (the followers stop at rank 0's step), and one
-``/response`` through the FastAPI app on rank 0.
+model:
+  * prefill logits within 5e-3 of TP=1 (the all-reduce's fp32 summation order can flip a bf16
+    / f16 activation rounding, nothing more); graph-replayed decode logits within 1e-2 of TP=1
+    and no further from the exact fp32 model than TP=1 is (+2e-3): the decode steps read the
+    K/V the prefill wrote, whose f16 / bf16 roundings (0.1-0.4 % ulps) the sharded summation
+    flips (measured 0.3-0.55 % vs TP=1, r4) - a wrong shard moves the logits by tens of %;
+    MoE: the same, except where the exact model's router puts two experts within rounding
+    noise of the top-k boundary somewhere in the sequence (an expert flip moves the logits
+    far more than any rounding);
+  * greedy generations identical, or diverging only at a near-tie of the exact model's
+    logits (MoE: or of its router, anywhere in the prefix up to the divergence);
+  * continuous batching under TP: every row's text identical to TP=1, or its divergence
+    justified the same way;
+  * seeded sampling (identical draws until rounding noise moves a probability boundary),
+    cooperative cancel (the followers stop at rank 0's step), and one ``/response`` through
+    the FastAPI app on rank 0.
 """
 import os
 
@@ -54,6 +63,7 @@ def _exercise(llm, with_app):
         res = list(ex.map(lambda i: llm.create_completion([1, 5 + i, 9, 12 + i, 30 + 2 * i], max_tokens=12,
                                                           temperature=0.0), range(3)))
     out["batched"] = [x["choices"][0]["text"] for x in res]
+    out["batched_tokens"] = [llm.tokenize(t.encode(), add_bos=False, special=True) for t in out["batched"]]
     out["batched_n"] = [x["usage"]["completion_tokens"] for x in res]
     # an after-the-batch single-sequence request still works (slot 0 path)
     out["greedy2"] = eng.generate(toks[:9], 0, 8, {"temperature": 0.0}, [], None, None)["tokens"]
@@ -139,6 +149,8 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
         x_pre = exact.forward(toks[:39], 0).numpy()
         x_dec = [exact.forward([toks[39 + i]], 39 + i).numpy() for i in range(4)]
 
+        moe = "mixtral" in spec
+
         def near_tie(prompt, a, b, k):
             """Tokens a (TP) and b (TP=1) at step k of a greedy run from `prompt`: both are
             argmax candidates of the exact model within the engines' activation-rounding noise."""
@@ -146,36 +158,55 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
             lg = m.forward(list(prompt) + list(b[:k]), 0).numpy()
             return abs(lg[a[k]] - lg[b[k]]) <= 2e-2 * np.abs(lg).max()
 
-        moe = "mixtral" in spec
+        def router_tie(seq):
+            """MoE: somewhere in `seq` (every token, every layer) the exact router's k-th and
+            (k+1)-th expert logits lie within rounding noise of each other - an expert flip."""
+            if not moe:
+                return False
+            m = ReferenceLlama(GGUFReader(path), n_ctx=256)
+            tr = []
+            m.forward(list(seq), 0, router_trace=tr)
+            k = m.hp.n_expert_used
+            for lg in tr:
+                srt = np.sort(lg.numpy(), -1)[:, ::-1]
+                gap = srt[:, k - 1] - srt[:, k]
+                if np.any(gap <= 2e-2 * np.abs(srt).max(-1)):
+                    return True
+            return False
 
         def greedy_ok(prompt, a, b):
             k = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), None)
-            # MoE: a near-tie in the ROUTER (top-2 of 4 experts) flips an expert, which moves
-            # the logits far more than the rounding noise (both engines sit ~0.2 from the exact
-            # model on such steps); past the first token only the teacher-forced logits compare
-            return k is None or near_tie(prompt, a, b, k) or (moe and k >= 1)
+            if k is None:
+                return len(a) == len(b)
+            return near_tie(prompt, a, b, k) or router_tie(list(prompt) + list(b[:k + 1]))
         e_tp = [_rel(got["prefill"], x_pre)] + [_rel(g, x) for g, x in zip(got["decode"], x_dec)]
         e_1 = [_rel(ref["prefill"], x_pre)] + [_rel(r, x) for r, x in zip(ref["decode"], x_dec)]
+        d_tp1 = [_rel(got["prefill"], ref["prefill"])] + [_rel(a_, b_) for a_, b_ in zip(got["decode"], ref["decode"])]
+        seqs = [toks[:39]] + [toks[:40 + i] for i in range(4)]
+        # an expert flip (MoE router near-tie in the sequence) excuses a logits difference
+        tol = [5e-3] + [1e-2] * 4   # prefill, decode steps
+        logits_ok = all(d <= tl and t <= o + 2e-3 or router_tie(q)
+                        for d, tl, t, o, q in zip(d_tp1, tol, e_tp, e_1, seqs))
         sd = next((i for i, (x, y) in enumerate(zip(got["sampled"], ref["sampled"])) if x != y), None)
+        prompts = [[1, 5 + i, 9, 12 + i, 30 + 2 * i] for i in range(3)]
+        batched_ok = got["batched_n"] == ref["batched_n"] and all(
+            tg == tr_ or greedy_ok(p, a, b) for p, tg, tr_, a, b in
+            zip(prompts, got["batched"], ref["batched"], got["batched_tokens"], ref["batched_tokens"]))
         checks = {
-            # q8 (decode GEMV) / bf16 (prefill GEMM) activations: the all-reduce's fp32 summation
-            # order can flip a rounding, so TP and TP=1 agree to the activation quantum, and TP is
-            # as close to the exact fp32 model as TP=1 is
-            "logits_vs_tp1": max([_rel(got["prefill"], ref["prefill"])] +
-                                 [_rel(a_, b_) for a_, b_ in zip(got["decode"], ref["decode"])]) <= 1e-2,
-            "logits_vs_exact": all(t <= o + 5e-3 for t, o in zip(e_tp, e_1)),
+            "logits": logits_ok,
             "greedy": greedy_ok(toks[:20], got["greedy"], ref["greedy"]),
             "greedy2": greedy_ok(toks[:9], got["greedy2"], ref["greedy2"]),
             # seeded sampling: identical draws until the rounding noise moves a probability boundary
             "sampled": (sd is None or sd >= 4) and len(got["sampled"]) == len(ref["sampled"]),
             "cancel": got["cancel"][0] == "cancelled" and got["cancel"][1] < 200,
-            "batched": got["batched_n"] == ref["batched_n"] and
-                       sum(x == y for x, y in zip(got["batched"], ref["batched"])) >= 2,
+            "batched": batched_ok,
             "healthy": got["healthy"],
         }
         if "http" in got:
             checks["http"] = got["http"] == (200, True) and got["health"] == 2
-        report.append((spec, {"err_tp": [round(v, 5) for v in e_tp], "err_tp1": [round(v, 5) for v in e_1],
+        report.append((spec, {"vs_tp1": [round(v, 5) for v in d_tp1],
+                              "err_tp": [round(v, 5) for v in e_tp], "err_tp1": [round(v, 5) for v in e_1],
+                              "batched_same": [a == b for a, b in zip(got["batched"], ref["batched"])],
                               "sampled_diff_at": sd, "cancel": got["cancel"]},
                        [k for k, ok in checks.items() if not ok]))
         bad += [(spec, k) for k, ok in checks.items() if not ok]

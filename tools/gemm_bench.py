@@ -24,12 +24,17 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--eager", action="store_true")
     ap.add_argument("--t16", action="store_true", help="the tile16 prefill GEMM (gemm_t16, f16 X)")
+    ap.add_argument("--cfg", default="", help="gemm_t16 block shape 'waves,tokens' (8,128 / 8,64 / 4,64)")
     args = ap.parse_args()
     from llama_fastapi_k8s_gpu_amd.runtime import load_hip
     hip = load_hip()
     s = torch.cuda.current_stream().cuda_stream
     d, F, T = 4096, 14336, args.T
-    res = {"T": T, "kernel": "gemm_t16" if args.t16 else "gemm_dq"}
+    res = {"T": T, "kernel": "gemm_t16" if args.t16 else "gemm_dq", "cfg": args.cfg}
+    cfg = 0
+    if args.cfg:
+        nw, tm = (int(v) for v in args.cfg.split(","))
+        cfg = nw * 1000 + tm
     for name, t, R, K, epi in [
         ("gateup_q4k_swiglu", Q4_K, 2 * F, d, SWIGLU),
         ("down_q4k_add", Q4_K, d, F, ADD),
@@ -50,7 +55,7 @@ def main():
 
         def fn():
             if args.t16:
-                hip.gemm_t16(tw.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), R, ob.data_ptr(), R // 2, epi, s)
+                hip.gemm_t16(tw.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), R, ob.data_ptr(), R // 2, epi, s, cfg=cfg)
             else:
                 hip.gemm(w.data_ptr(), t, R, K, x.data_ptr(), T, out.data_ptr(), ob.data_ptr(), R, epi, s)
 

@@ -1,8 +1,15 @@
 #!/bin/bash
-# One GPU session: kernel numerics, engine tests, smoke, raw decode timing.
-# Test failures (exit 1) do not stop the session; a crash/abort/timeout does.
+# The one GPU-session driver: `gpurun -- bash tools/gpu_round.sh <target> [<target> ...]`.
+# Every step runs under its own time limit; a test failure (exit 1) does not stop the session,
+# a crash / abort / timeout does. Logs land in gpurun_out/<step>.log.
+#   tests:    gputests kern eng batch tp tp8 rccl p2pu qkvsk bmmt t16t samp opsgpu smoke
+#   benches:  bench bench20 serial benchtp2 benchdp2 bstep decode decode70 mixtral
+#   profiles: stepprof decprof prefprof bmmpmc t16pmc blocks attntl bmmtl p2plat
+#   A/B:      abold (the tree vs ab_old/, alternating), abprof (kernel tables, tree vs ab_old/)
+#   final:    every GPU test + smoke + headline bench + step / decode kernel traces
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+export TMPDIR=/tmp
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 to=$2; shift 2
   echo "=== $name" >&2
@@ -13,71 +20,85 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after rc=$rc" >&2; exit $rc; fi
   return 0
 }
+PYT="python -u -m pytest -x -v --timeout-method thread -p no:cacheprovider"
+prof() {  # prof <name> <timeout> <python args...>: rocprofv3 kernel trace + per-kernel summary
+  local name=$1 to=$2; shift 2
+  step "$name" "$to" rocprofv3 --kernel-trace --stats -d "gpurun_out/$name" -o k --output-format csv -- python3 "$@"
+}
+pmc() {  # pmc <name> <python args...>: one counter pass per run (8 SQ / 4 TCC / 2 GRBM slots)
+  local name=$1; shift
+  step "${name}A" 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d "gpurun_out/${name}A" -o pmc --output-format csv -- python3 "$@"
+  step "${name}B" 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES \
+    SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD -d "gpurun_out/${name}B" -o pmc --output-format csv -- python3 "$@"
+  python3 tools/pmc_summary.py "gpurun_out/${name}A" "gpurun_out/${name}B" > "gpurun_out/${name}_summary.json" || true
+}
 for s in "$@"; do
   case $s in
-    rccl) step rccl 400 python -u -m pytest tests/test_rccl_gpu.py tests/test_serve_tp_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    p2pu) step p2pu 200 env LFK_P2P_UNCACHED=1 python -u -m pytest tests/test_p2p_allreduce.py -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ;;
-    tp) step tp 460 python -u -m pytest tests/test_p2p_allreduce.py tests/test_tp_gpu.py -x -v --timeout 420 --timeout-method thread -p no:cacheprovider ;;
-    bmmt) step bmmt 400 python -u -m pytest tests/test_kernels_gpu.py -k "bmm or bprep" -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
-    attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
-    attntl1) step attntl1 200 python tools/attn_timeline.py --rows 1 --L 700 ;;
-    bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
-    qkvsk) step qkvsk 300 python -u -m pytest tests/test_kernels_gpu.py -k "qkv_splitk or attn_decode or bmm_rows" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    absk) step absk0 200 env LFK_QKV_SK=0 python tools/batch_bench.py --batches 6,8 --steps 64
-          step absk1 200 python tools/batch_bench.py --batches 6,8 --steps 64
-          step absk0b 200 env LFK_QKV_SK=0 python tools/batch_bench.py --batches 6,8 --steps 64
-          step absk1b 200 python tools/batch_bench.py --batches 6,8 --steps 64 ;;
-    blocks) step blocks1 200 python tools/step_blocks.py --json gpurun_out/blocks_sk1.json
-            step blocks0 200 env LFK_QKV_SK=0 python tools/step_blocks.py --json gpurun_out/blocks_sk0.json ;;
-    sksweep) for c in 8,8 4,6 4,8 2,3 16,6; do
-               step "sk_$c" 200 env LFK_QKV_SK_PARTS=${c%,*} LFK_QKV_SK_TPG=${c#*,} python tools/batch_bench.py --batches 6 --steps 64
-             done ;;
-    xfirst) step xf_blocks1 200 env LFK_WT_XFIRST=1 LFK_QKV_SK_PARTS=4 python tools/step_blocks.py --json gpurun_out/blocks_xf1.json
-            step xf_blocks0 200 env LFK_QKV_SK_PARTS=4 python tools/step_blocks.py --json gpurun_out/blocks_xf0.json
-            for x in 0 1 0 1; do step "xf_bench_$x" 200 env LFK_WT_XFIRST=$x LFK_QKV_SK_PARTS=4 python tools/batch_bench.py --batches 6 --steps 64; done ;;
-    p2pprobe) step p2pprobe0 120 python tools/p2p_probe.py
-              step p2pprobe1 120 python tools/p2p_probe.py --junk ;;
-    abold) step abold 600 bash tools/gpu_ab_old.sh ;;
-    stepprof) export TMPDIR=/tmp; step stepprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/sprof -o bstep --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
-          python3 tools/step_kernels.py gpurun_out/sprof/bstep_kernel_trace.csv > gpurun_out/sprof_kernels.txt ;;
-    samp) step samp 300 python -u -m pytest tests/test_kernels_gpu.py -k sampler -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    kern) step kern 900 python -m pytest tests/test_kernels_gpu.py -q -p no:cacheprovider ;;
-    eng) step eng 900 python -m pytest tests/test_engine_gpu.py -q -p no:cacheprovider ;;
-    gputests) step gputests 1000 python -u -m pytest tests -m gpu -q --timeout 420 --timeout-method thread -p no:cacheprovider ;;
+    # ---- tests
+    gputests) step gputests 1000 $PYT tests -m gpu --timeout 420 ;;
+    kern) step kern 900 $PYT tests/test_kernels_gpu.py --timeout 120 ;;
+    eng) step eng 900 $PYT tests/test_engine_gpu.py --timeout 300 ;;
+    batch) step batch 600 $PYT tests/test_batch_gpu.py tests/test_batch_serving_gpu.py --timeout 300 ;;
+    tp) step tp 900 $PYT tests/test_p2p_allreduce.py tests/test_tp_gpu.py --timeout 600 ;;
+    tp8) step tp8 900 $PYT tests/test_tp8_gpu.py --timeout 850 -s ;;
+    rccl) step rccl 400 $PYT tests/test_rccl_gpu.py tests/test_serve_tp_gpu.py --timeout 300 ;;
+    p2pu) step p2pu 200 $PYT tests/test_p2p_allreduce.py --timeout 150 ;;
+    qkvsk) step qkvsk 300 $PYT tests/test_kernels_gpu.py -k "qkv_splitk or attn_decode or bmm_rows" --timeout 120 ;;
+    bmmt) step bmmt 400 $PYT tests/test_kernels_gpu.py -k "bmm or bprep" --timeout 120 ;;
+    t16t) step t16t 400 $PYT tests/test_kernels_gpu.py -k "t16 or rmsnorm_f16 or attn_prefill" --timeout 120 ;;
+    samp) step samp 300 $PYT tests/test_kernels_gpu.py -k sampler --timeout 120 ;;
+    opsgpu) step opsgpu 600 $PYT tests/test_ops_gpu.py --timeout 120 ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
-    decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
-    micro) step micro 300 python tools/launch_microbench.py ;;
-    gemvb) step gemvb 300 python tools/gemv_bench.py --debug ;;
-    sweep) step sweep 900 bash tools/gemv_sweep.sh ;;
-    timeline) step timeline 300 python tools/gemv_timeline.py ;;
-    sampb) step sampb 300 python tools/sampler_bench.py ;;
-    variants) step variants 900 bash tools/gemv_variants.sh ;;
-    profgemv) export TMPDIR=/tmp; step profgemv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profgemv -o gemv \
-            --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 ;;
-    gvpmc) export TMPDIR=/tmp; step gvpmc 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d gpurun_out/gvpmc -o pmc --output-format csv -- python3 tools/gemv_bench.py --eager --reps 20 --only q4k ;;
-    opsgpu) step opsgpu 600 python -m pytest tests/test_ops_gpu.py -q -p no:cacheprovider ;;
-    gemmb) step gemmb 300 bash -c 'python tools/gemm_bench.py --T 512 && python tools/gemm_bench.py --T 2048' ;;
-    gemmt) step gemmt 300 bash -c 'for T in 384 512 2048 2304; do python tools/gemm_bench.py --T $T && python tools/gemm_bench.py --T $T --t16 || exit 1; done; for c in 8,128 8,64 4,64; do LFK_T16_CFG=$c python tools/gemm_bench.py --T 512 --t16 || exit 1; done' ;;
-    gemmt2) step gemmt2 300 bash -c 'for T in 2304 2400 1536; do python tools/gemm_bench.py --T $T --t16 && LFK_T16_CFG=8,128 python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
-    gemmt4) step gemmt4 300 bash -c 'for T in 384 512 1024 2304; do python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
-    gemmt3) step gemmt3 400 bash -c 'for T in 384 1024 1536 2304; do for c in 8,128 8,64 4,64; do echo cfg=$c; LFK_T16_CFG=$c python tools/gemm_bench.py --T $T --t16 || exit 1; done; done' ;;
-    t16t) step t16t 400 python -u -m pytest tests/test_kernels_gpu.py -k "t16 or rmsnorm_f16 or attn_prefill" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider ;;
-    gemmpmc) export TMPDIR=/tmp; step gemmpmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
-            -d gpurun_out/gemmpmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup
-            step gemmpmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
-            -d gpurun_out/gemmpmcB -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --only gateup ;;
-    t16pmc) export TMPDIR=/tmp; step t16pmcA 90 timeout -s KILL 80 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
-            -d gpurun_out/t16pmcA -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --T 512 --t16
-            step t16pmcB 90 timeout -s KILL 80 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VMEM_RD \
-            -d gpurun_out/t16pmcB -o pmc --output-format csv -- python3 tools/gemm_bench.py --eager --reps 5 --T 512 --t16
-            step prefprof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/prefprof -o pre --output-format csv -- python3 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
+    # ---- benches
     bench) step bench 900 python bench.py --steps 3 --warmup 1 ;;
     bench20) step bench20 900 python bench.py --steps 20 --warmup 2 ;;
-    benchtp2) LFK_BENCH_DEVICE=0 step benchtp2 900 python bench.py --gpus 2 --steps 12 --warmup 2 ;;
-    benchdp2) LFK_BENCH_DEVICE=0 step benchdp2 900 python bench.py --gpus 2 --parallel dp --steps 12 --warmup 2 ;;
-    batch) step batch 600 python -u -m pytest tests/test_batch_gpu.py tests/test_batch_serving_gpu.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
-    prof) export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o decode \
-            --output-format csv -- python3 tools/decode_bench.py --steps 64 --no-graph ;;
+    serial) step serial 900 python bench.py --steps 10 --warmup 1 --clients 1 --max-batch 1 ;;
+    benchtp2) step benchtp2 900 env LFK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 12 --warmup 2 ;;
+    benchdp2) step benchdp2 900 env LFK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --parallel dp --steps 4 --warmup 1 ;;
+    bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
+    decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
+    decode70) step decode70 900 python tools/decode_bench.py --model llama3-70b-q4_k_m --gen 128 ;;
+    mixtral) step mixtral 900 python bench.py --model mixtral-8x7b-q4_k_m --steps 6 --warmup 1 ;;
+    # ---- profiles
+    stepprof) prof stepprof 300 tools/batch_bench.py --batches 6 --steps 32
+              python3 tools/step_kernels.py gpurun_out/stepprof/k_kernel_trace.csv > gpurun_out/stepprof_kernels.txt
+              python3 tools/step_slots.py gpurun_out/stepprof/k_kernel_trace.csv >> gpurun_out/stepprof_kernels.txt ;;
+    decprof) prof decprof 300 tools/decode_bench.py --steps 64 --no-graph ;;
+    prefprof) prof prefprof 300 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
+    bmmpmc) pmc bmmpmc tools/batch_bench.py --batches 6 --steps 4 ;;
+    t16pmc) pmc t16pmc tools/gemm_bench.py --eager --reps 5 --T 512 --t16 ;;
+    blocks) step blocks 200 python tools/step_blocks.py --json gpurun_out/blocks.json ;;
+    attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
+    bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
+    gemmt) step gemmt 400 bash -c 'for T in 384 512 1024 2304; do python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
+    p2plat) step p2plat 300 python tools/p2p_latency.py --ranks 2,4,8 --json gpurun_out/p2p_latency.json ;;
+    # ---- same-box A/B against the older build staged in ab_old/ (drop ./ab_old from .gpurunignore)
+    abold) for r in 1 2; do
+             step "abo_new_$r" 200 python tools/batch_bench.py --batches 1,6,8
+             step "abo_old_$r" 200 python ab_old/tools/batch_bench.py --batches 1,6,8
+           done ;;
+    abprof) for v in new old; do
+              bb=tools/batch_bench.py; [ $v = old ] && bb=ab_old/tools/batch_bench.py
+              prof "abp_$v" 240 $bb --batches 6 --steps 32
+              python3 tools/step_kernels.py "gpurun_out/abp_$v/k_kernel_trace.csv" > "gpurun_out/abp_$v.txt"
+              python3 tools/step_slots.py "gpurun_out/abp_$v/k_kernel_trace.csv" >> "gpurun_out/abp_$v.txt"
+            done ;;
+    # ---- same-box A/B of an env switch of the tree's build: AB_ENV="LFK_X=0" (alternating runs,
+    #      then a kernel table of each)
+    abenv) for r in 1 2; do
+             step "abe_on_$r" 200 python tools/batch_bench.py --batches 1,6,8 --steps 64
+             step "abe_off_$r" 200 env $AB_ENV python tools/batch_bench.py --batches 1,6,8 --steps 64
+           done
+           prof abe_on_prof 240 tools/batch_bench.py --batches 6 --steps 32
+           python3 tools/step_slots.py gpurun_out/abe_on_prof/k_kernel_trace.csv > gpurun_out/abe_on_slots.txt
+           step abe_off_prof 240 env $AB_ENV rocprofv3 --kernel-trace --stats -d gpurun_out/abe_off_prof -o k \
+             --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
+           python3 tools/step_slots.py gpurun_out/abe_off_prof/k_kernel_trace.csv > gpurun_out/abe_off_slots.txt ;;
+    # ---- round-end check of the committed tree
+    final) bash "$0" gputests smoke bench20 serial stepprof decprof || exit $? ;;
+    *) echo "unknown target $s" >&2; exit 2 ;;
   esac
 done
