@@ -15,7 +15,7 @@ GPUs: ``--gpus N`` runs N ranks, one process per GPU. Without ``WORLD_SIZE`` in 
 environment and N > 1, bench.py starts ``torch.distributed.run`` itself (before anything
 touches a GPU) and exits with its status; under a launcher, ``WORLD_SIZE`` must equal N.
 
-Parallelism (``--parallel``, default ``auto`` = ``tp`` for N > 1):
+Parallelism (``--parallel``, default ``auto`` = ``dp``):
   * ``tp``: ONE model row-split over the N GPUs (BASELINE configs "8B tensor_split across
     2 MI355X", "70B across 8"): heads / FFN / vocabulary sharded, two all-reduces per
     layer (one-shot P2P kernel over xGMI for decode messages, RCCL for prefill), rank 0
@@ -23,7 +23,10 @@ Parallelism (``--parallel``, default ``auto`` = ``tp`` for N > 1):
     natively. Strong scaling: value = the job's output tokens/s.
   * ``dp``: every GPU an independent replica with its own request stream (the reference's
     deployment model: replicas behind one Service, reference helm/values.yaml:17). Weak
-    scaling; value = sum over ranks.
+    scaling; value = sum over ranks. The default: a Q4_K_M 8B (5 GB) or 70B (40 GB) fits one
+    MI355X's 288 GB many times over, and a decode step sharded N ways pays two all-reduces per
+    layer for 1/N of a weight stream that takes ~1.7 ms whole - replicas are the throughput
+    configuration; ``tp`` is the latency / memory configuration and stays selectable.
 
 Load: ``--clients C`` concurrent clients (default 6 = the reference pod's admission
 capacity, 1 in flight + MAX_QUEUE_SIZE 5, reference api.py:19,113) post the K timed
@@ -132,7 +135,7 @@ def main() -> int:
         raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    parallel = args.parallel if args.parallel != "auto" else ("tp" if world > 1 else "dp")
+    parallel = args.parallel if args.parallel != "auto" else "dp"
     # Rehearsal mode: LFK_BENCH_DEVICE=<d> puts every rank on GPU d (a one-GPU box running the
     # N-rank flow); RCCL refuses two ranks on one device, so TP collectives take the P2P kernel
     # for every message (comm=ipc) and the bench's own reductions go over gloo.

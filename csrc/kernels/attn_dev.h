@@ -147,8 +147,6 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
   __shared__ float wm[4][G], wl[4][G];
   __shared__ __attribute__((aligned(16))) float wo[4][G][HD];
   __shared__ int last;
-  // single split with a done counter (BmmArgs::wait consumer): the f16 output staged for 8-B sc1 stores
-  __shared__ __attribute__((aligned(16))) __half res[G * HD];
   __shared__ __attribute__((aligned(16))) h2v kvn[2][HD / 2];  // split-K Q|K|V: the new key / value (f16)
 
   // ---- 1. loads: q (and the split-K new key / value) first, then the K / V rows
@@ -331,15 +329,13 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
     }
     if (ns == 1) {
       const int o = (kvh * G + g) * HD + d;
-      if (a.out) {
+      if (a.out && a.done) {
+        st2_sc1(a.out + o, acc0 / l, acc1 / l);  // an in-flight consumer reads it (attn_wo1)
+      } else if (a.out) {
         a.out[o] = acc0 / l;
         a.out[o + 1] = acc1 / l;
       }
-      if (a.out_h && a.done) {
-        const int ol = g * HD + d;  // kv-head-local (4-groups stay whole)
-        res[swz4(ol)] = __float2half(acc0 / l);
-        res[swz4(ol + 1)] = __float2half(acc1 / l);
-      } else if (a.out_h) {
+      if (a.out_h) {
         a.out_h[swz4(o)] = __float2half(acc0 / l);
         a.out_h[swz4(o + 1)] = __float2half(acc1 / l);
       }
@@ -350,14 +346,7 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
     }
   }
   LFK_STAMP(4);
-  if (ns == 1 && a.done && a.out_h) {
-    // the kv head's G x HD outputs as 8-B sc1 stores, then one agent-scope add for the consumer
-    __syncthreads();
-    for (int i = tid; i < G * HD / 4; i += 256) {
-      const unsigned long long w = *reinterpret_cast<const unsigned long long*>(&res[4 * i]);
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.out_h + kvh * G * HD + 4 * i), w, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
+  if (ns == 1 && a.done) {  // (single row) the f32 output went out sc1 above: one add for the block
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(a.done + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -434,8 +423,18 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
   for (int j = 0; j < EPT; ++j) r[j] = num[j] / den;
   const bool live = tid * EPT < G * HD;
   if (a.out && live) {
+    if (a.done) {  // an in-flight consumer reads it (attn_wo1): sc1
+      if constexpr (EPT % 2 == 0) {
 #pragma unroll
-    for (int j = 0; j < EPT; ++j) a.out[h * HD + d0 + j] = r[j];
+        for (int j = 0; j < EPT; j += 2) st2_sc1(a.out + h * HD + d0 + j, r[j], r[j + 1]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) st_sc1(a.out + h * HD + d0 + j, r[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < EPT; ++j) a.out[h * HD + d0 + j] = r[j];
+    }
   }
   if (a.out_h) {
     static_assert(EPT == 1 || EPT == 2 || EPT % 4 == 0, "4-groups of the f16 output");
@@ -459,18 +458,14 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
         const h2v p1 = {(_Float16)g4[4 * k + 1], (_Float16)g4[4 * k + 3]};
         const unsigned long long w = ((unsigned long long)__builtin_bit_cast(unsigned, p1) << 32) |
                                      __builtin_bit_cast(unsigned, p0);
-        if (a.done)  // an in-flight consumer reads it: sc1 (write-through, agent scope)
-          __hip_atomic_store(reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k), w, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else
-          *reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k) = w;
+        *reinterpret_cast<unsigned long long*>(a.out_h + o0 + 4 * k) = w;
       }
     }
-    if (a.done) {  // every storing wave drained, then one add for the whole block (Guideline 16, R1)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) __hip_atomic_fetch_add(a.done + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  }
+  if (a.done) {  // every storing wave drained, then one add for the whole block (Guideline 16, R1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(a.done + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if constexpr (TL) { if (threadIdx.x == 0) tl[9] = wall_clock64(); }
 #undef LFK_STAMP

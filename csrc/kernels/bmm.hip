@@ -29,7 +29,6 @@
 #include <algorithm>
 #include <stdexcept>
 
-#include "attn_dev.h"
 #include "gemv_dev.h"
 
 namespace lfk {
@@ -387,14 +386,6 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
 // round trip, like the f16 staging), then f16(x * w) goes to LDS in bprep's 4-group order and
 // each wave leaves its per-row partial sum of squares in rowss[b * NW + wave] (rows past B load
 // row B - 1 and are dropped: straight-line code, no predicated loads)
-typedef unsigned v4u_t __attribute__((ext_vector_type(4)));
-// 16-B load with sc1 (L1 bypassed, agent-coherent with sc1 producer stores: an in-flight hand-off)
-__device__ __forceinline__ uint4 ld16_sc1(const __half* base, size_t off_halves) {
-  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(base), 0, 0x7FFFFFFF, 0x00020000);
-  const v4u_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(off_halves * sizeof(__half)), 0, 16);  // aux 16: sc1
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-
 template <int NW>
 __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
                                             int tid, int lane, int wave) {
@@ -435,8 +426,7 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
       for (int u = 0; u < U; ++u) {
         const int i = min(i0 + u * kBlock + tid, n - 1);
         const int b = i / nv, c = i - b * nv;
-        const size_t o = (size_t)b * a.ldh + k0 + 8 * c;
-        v[u] = a.wait ? ld16_sc1(a.xh, o) : *reinterpret_cast<const uint4*>(a.xh + o);
+        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -902,24 +892,6 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     float4* z = reinterpret_cast<float4*>(a.zero);
     for (int i = bid * (NW * 64) + tid; i < (a.zero_n >> 2); i += nblk * (NW * 64)) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  if (!SK && a.wait) {
-    // in-flight producer (the batched attention beside this launch): its per-kv-head done
-    // counters, polled with sc1 loads by one lane; the block's weights are already in flight
-    if (tid == 0) {
-      const int h0 = k0 / a.wait_group, h1 = (k0 + kn - 1) / a.wait_group;
-      for (int h = h0; h <= h1; ++h) {
-        for (int spins = 0; __hip_atomic_load(const_cast<int*>(a.wait) + h, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) < a.wait_n; ++spins) {
-          if (spins > (1 << 22)) {
-            __hip_atomic_store(a.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-    }
-    lds_barrier();  // the other waves load after the polling wave's match (no vmcnt drain)
-  }
   if (SK && a.ss_out) {
     lds_barrier();  // rowss zeroed
     stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
@@ -1040,38 +1012,6 @@ __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true>(*ka, 1, blockIdx.x, gridDim.x);
   else wt_body<QT, PD, true>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
-}
-
-// ---------------------------------------------------------------- fused batched attention + Wo
-// One launch for a layer's batched attention AND its Wo projection: grid (kv heads, splits,
-// B + Wo planes). The planes z < B are the batched attention (attn_dev.h) with done counters:
-// each (row, kv head) output is stored sc1 and counted once. The planes past them are the
-// wave-owned split-K Wo with 4-wave blocks: every block issues its weights at once (the whole
-// K part of its 4 tiles fits the 2-step register ring at d = 4096), waits for the counters of
-// its K part's kv heads (sc1 poll) and stages their output with sc1 loads. The Wo stream then
-// overlaps the latency-bound attention and a kernel boundary per layer is gone (a graph branch
-// for the same overlap cost ~10 us per layer in cross-queue joins, r4 profile).
-// Blocks are dispatched in linear order in practice (not a guarantee): whatever the order, an
-// attention block can always become resident beside the waiting Wo blocks (LDS and waves: see
-// attn_wo), and every wait is bounded.
-struct AttnWoArgs {
-  AttnDecodeArgs att;
-  BmmArgs wo;
-  int n_wo = 0;  // Wo blocks (kparts x tile groups)
-};
-
-template <int QT, int HD, int G>
-__global__ __launch_bounds__(256) void attn_wo_kernel(AttnWoArgs p) {
-  const AttnWoArgs* k = (const AttnWoArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  if ((int)blockIdx.z < k->att.batch) {
-    attn_decode_body<HD, G, false>(k->att);
-    return;
-  }
-  const int per = gridDim.x * gridDim.y;
-  const int vb = ((int)blockIdx.z - k->att.batch) * per + blockIdx.y * gridDim.x + blockIdx.x;
-  if (vb >= k->n_wo) return;
-  wt_body<QT, 2, false, 4>(k->wo, 0, vb, k->n_wo);
-  (void)p;
 }
 
 // ---------------------------------------------------------------- activation prep
@@ -1199,14 +1139,11 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
     const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
     // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
-    // (an in-flight consumer of the attention shares the CUs with it: no pin)
-    const size_t lds_need = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
-    const size_t lds = a.wait ? lds_need : std::max<size_t>(lds_need, 81 * 1024);
+    const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
     hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
     return;
   }
   if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");
-  if (a.wait) throw std::runtime_error("bmm: the in-flight wait runs on the wave-owned split-K kernel only");
   if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
     // one K part (the epilogue needs whole rows); 8-wave blocks (the folded norm needs 8), 2 per
     // CU by LDS (16-wave blocks staging x once per CU: 5 % slower steps, r2)
@@ -1313,9 +1250,6 @@ static void bmm_check(const BmmArgs& a) {
   }
   if (a.ss_out && !(a.qkv_sk && a.xf)) throw std::runtime_error("bmm: ss_out needs the split-K Q|K|V norm");
   if (a.zero && (a.zero_n % 4 || reinterpret_cast<uintptr_t>(a.zero) % 16)) throw std::runtime_error("bmm: zero side job alignment");
-  if (a.wait && (a.wait_n < 1 || a.wait_group < 1 || !a.wait_err || a.xf || a.qkv_sk || a.swiglu_epi || a.ew || a.one_part ||
-                 a.store_out || a.nseg != 1 || a.B > 8))
-    throw std::runtime_error("bmm: in-flight wait arguments");
 }
 
 void bmm(const BmmArgs& a0, hipStream_t s) {
@@ -1372,38 +1306,6 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
   if (ta_ == T_Q4_K && tb_ == T_Q6_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q6_K>), grid, blk, lds, s, a, b);
   else if (ta_ == T_Q4_K && tb_ == T_Q5_K) hipLaunchKernelGGL((bmm_kernel<T_Q4_K, 8, 1, T_Q5_K>), grid, blk, lds, s, a, b);
   else return false;
-  return true;
-}
-
-bool attn_wo(const AttnDecodeArgs& aa, const BmmArgs& wo0, hipStream_t s) {
-  const int G = aa.n_kv_head > 0 ? aa.n_head / aa.n_kv_head : 0;
-  if (aa.head_dim != 128 || (G != 4 && G != 8) || aa.batch < 1 || aa.batch > 8 || !aa.done || !aa.out_h || aa.out ||
-      aa.pf[0] || wo0.w.type != T_Q4_K && wo0.w.type != T_Q6_K)
-    return false;
-  BmmArgs wo = wo0;
-  if (wo.B != aa.batch || !wo.wait || wo.wait != aa.done || wo.wait_n != aa.batch || wo.wait_group != G * aa.head_dim)
-    throw std::runtime_error("attn_wo: the Wo must wait for this attention's done counters");
-  bmm_check(wo);
-  const int tiles = (wo.n_out + 15) / 16, steps = wo.w.K / 256;
-  // K parts as the separate launch takes them (8 at d = 4096: one kv head of 4 query heads each)
-  int kparts = std::max(1, std::min(steps / 2, (bmm_cus() * 8 + tiles / 2) / std::max(1, tiles)));
-  wo.spp = (steps + kparts - 1) / kparts;
-  wo.kparts = kparts = (steps + wo.spp - 1) / wo.spp;
-  if (wo.spp > 2) return false;  // a wave's part must fit the 2-step register ring (issued before the wait)
-  AttnWoArgs p;
-  p.att = aa;
-  p.wo = wo;
-  p.n_wo = (tiles + 3) / 4 * kparts;  // 4-tile groups: one tile per wave
-  const int splits = (aa.n_ctx + 63) / 64, per = aa.n_kv_head * splits;
-  const dim3 grid(aa.n_kv_head, splits, aa.batch + (p.n_wo + per - 1) / per);
-  const size_t lds = 256 + (size_t)wo.B * (wo.spp * 256 + 8) * 2;
-  if (wo.w.type == T_Q4_K) {
-    if (G == 4) hipLaunchKernelGGL((attn_wo_kernel<T_Q4_K, 128, 4>), grid, dim3(256), lds, s, p);
-    else hipLaunchKernelGGL((attn_wo_kernel<T_Q4_K, 128, 8>), grid, dim3(256), lds, s, p);
-  } else {
-    if (G == 4) hipLaunchKernelGGL((attn_wo_kernel<T_Q6_K, 128, 4>), grid, dim3(256), lds, s, p);
-    else hipLaunchKernelGGL((attn_wo_kernel<T_Q6_K, 128, 8>), grid, dim3(256), lds, s, p);
-  }
   return true;
 }
 

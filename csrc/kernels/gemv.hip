@@ -17,6 +17,7 @@
 #include <map>
 #include <mutex>
 
+#include "attn_dev.h"
 #include "gemv_dev.h"
 
 namespace lfk {
@@ -34,15 +35,19 @@ namespace lfk {
 // after the x loads and BEFORE the prologue waits for x, so the weight stream
 // starts at block entry; with one block per CU no other block's weight stream
 // sits in front of this CU's x loads (in-order returns per CU).
+// WAIT (SPLITK, not EARLY; attn_wo1): the first item's weights go out first, then the block waits
+// for the in-flight producer of x (GemvArgs::wait) and loads x with sc1 loads.
+// (bid, nblk): the block's index and count in the GEMV's grid (a plane of attn_wo1's grid).
 template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false,
-          bool EARLY = false>
-__global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
+          bool EARLY = false, bool WAIT = false>
+__device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, const int nblk) {
+  static_assert(!WAIT || (SPLITK && !EARLY && !TL), "the in-flight wait is a split-K, non-EARLY form");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // TL: per-block timeline (wall_clock64 ticks, microbenchmarks only):
   // [entry, prologue done, first item done, exit, items done by wave 0]
   long long* tl = nullptr;
   if constexpr (TL) {
-    tl = a.dbg_clk + (size_t)blockIdx.x * 5;
+    tl = a.dbg_clk + (size_t)bid * 5;
     if (threadIdx.x == 0) tl[0] = wall_clock64();
   }
   int n_done = 0;
@@ -62,25 +67,46 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   // per block left the last quarter of the CUs with half the items of the rest).
   int item, stride, item_end;
   if constexpr (EARLY) {
-    const int per = (total + (int)gridDim.x - 1) / (int)gridDim.x;
-    const int b0 = min(total, (int)blockIdx.x * per);
+    const int per = (total + nblk - 1) / nblk;
+    const int b0 = min(total, bid * per);
     item = b0 + wave;
     stride = WPB;
     item_end = min(total, b0 + per);
   } else {
-    item = blockIdx.x * WPB + wave;
-    stride = gridDim.x * WPB;
+    item = bid * WPB + wave;
+    stride = nblk * WPB;
     item_end = total;
   }
   RowPtr R[NR];
   int slot = 0, f0 = 0;
   WStream<QT, NR, U> ws;
-  XPrologue<NORM, BLOCK> xp;
+  XPrologue<NORM, BLOCK, WAIT> xp;
+  int kp = 0;
+  if constexpr (WAIT) {
+    // the weights stream while the producer (the attention planes of this launch) finishes
+    if (item < total) {
+      item_rows<EPI, NR>(a, item / kparts, groups, R, slot, f0);
+      kp = item % kparts;
+      ws.load(R, kp * 64 * U, nchunks, lane);
+    }
+    if (threadIdx.x == 0) {
+      for (int h = 0; h < a.wait_cnt; ++h) {
+        for (int spins = 0; __hip_atomic_load(const_cast<int*>(a.wait) + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                            a.wait_n; ++spins) {
+          if (spins > (1 << 22)) {
+            __hip_atomic_store(a.wait_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    asm volatile("s_barrier" ::: "memory");  // the other waves load x after the poll matched
+  }
   // The x prologue runs BEFORE the first weight loads: measured on MI355X, a
   // prologue whose L2 reads queue behind a saturated weight stream (its own CU's
   // or its neighbours') costs more than the latency its prefetch would hide.
   if (a.debug != 1) xp.load(a.x, a.norm_w, K);
-  int kp = 0;
   if constexpr (EARLY) {  // unconditional (clamped) so no control-flow join sits between these loads and finish()
     const int it0 = min(item, total - 1);
     item_rows<EPI, NR>(a, SPLITK ? it0 / kparts : it0, groups, R, slot, f0);
@@ -88,7 +114,7 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
     ws.load(R, kp * 64 * U, nchunks, lane);
   }
   const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
-  if constexpr (!EARLY) {
+  if constexpr (!EARLY && !WAIT) {
     if (item < total) {
       item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0);
       if constexpr (SPLITK) kp = item % kparts;
@@ -134,6 +160,73 @@ __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   if constexpr (TL) {
     if (threadIdx.x == 0) { tl[3] = wall_clock64(); tl[4] = n_done; }
   }
+}
+
+template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false,
+          bool EARLY = false>
+__global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
+  // the body reads the arguments through the kernarg segment pointer (a reference to the by-value
+  // parameter would make the compiler copy it to scratch)
+  const GemvArgs* ka = (const GemvArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  gemv_body<QT, EPI, NR, U, NORM, BLOCK, TL, SPLITK, EARLY>(*ka, blockIdx.x, gridDim.x);
+  (void)a;
+}
+
+// ---------------------------------------------------------------- fused decode attention + Wo
+// One launch for the single-row decode's attention AND its Wo projection: grid (kv heads,
+// splits, 1 + Wo planes). Plane 0 is the attention (attn_dev.h) with done counters (each kv
+// head's output stored sc1, counted once); the planes past it are the split-K Wo GEMV (4 rows x
+// 64 chunks per wave item, atomics into the residual) whose blocks issue their first item's
+// weights at once, wait for every kv head's counter and quantise x from sc1 loads. Wo's weight
+// stream overlaps the latency-bound attention, and the launch replaces two (4 per layer).
+struct AttnWo1Args {
+  AttnDecodeArgs att;
+  GemvArgs wo;
+  int n_wo = 0;  // Wo blocks
+};
+
+template <int QT, int HD, int G>
+__global__ __launch_bounds__(256) void attn_wo1_kernel(AttnWo1Args p) {
+  const AttnWo1Args* k = (const AttnWo1Args*)__builtin_amdgcn_kernarg_segment_ptr();
+  if (blockIdx.z == 0) {
+    attn_decode_body<HD, G, false>(k->att);
+    return;
+  }
+  const int per = gridDim.x * gridDim.y;
+  const int vb = ((int)blockIdx.z - 1) * per + blockIdx.y * gridDim.x + blockIdx.x;
+  if (vb >= k->n_wo) return;
+  gemv_body<QT, EPI_ADD, 4, 1, false, 256, false, true, false, true>(k->wo, vb, k->n_wo);
+  (void)p;
+}
+
+bool attn_wo1(const AttnDecodeArgs& aa, const GemvArgs& wo, hipStream_t s) {
+  const int G = aa.n_kv_head > 0 ? aa.n_head / aa.n_kv_head : 0;
+  if (aa.head_dim != 128 || (G != 4 && G != 8) || aa.batch != 0 || !aa.done || !aa.out || aa.out_h || aa.qkv_raw ||
+      (wo.w.type != T_Q4_K && wo.w.type != T_Q6_K) || wo.norm_w || wo.n_slots != 1 || wo.expert_ids || wo.resid ||
+      wo.debug || wo.dbg_clk || wo.w.K % 2048)
+    return false;
+  for (int r = 0; r < AttnDecodeArgs::kTouchRanges; ++r)
+    if (aa.pf[r]) return false;
+  if (!wo.wait || wo.wait != aa.done || wo.wait_cnt != aa.n_kv_head || wo.wait_n != 1 || !wo.wait_err ||
+      wo.x != aa.out)
+    throw std::runtime_error("attn_wo1: the Wo must wait for this attention's done counters");
+  AttnWo1Args p;
+  p.att = aa;
+  p.wo = wo;
+  // one 4-row x 64-chunk item per wave: every weight of Wo is in flight before the wait
+  const int items = (wo.n_out + 3) / 4 * (wo.w.K / 2048);
+  p.n_wo = (items + 3) / 4;
+  const int splits = (aa.n_ctx + 63) / 64, per = aa.n_kv_head * splits;
+  const dim3 grid(aa.n_kv_head, splits, 1 + (p.n_wo + per - 1) / per);
+  const size_t lds = wo.w.K + (wo.w.K / 32) * 4 + 128;
+  if (wo.w.type == T_Q4_K) {
+    if (G == 4) hipLaunchKernelGGL((attn_wo1_kernel<T_Q4_K, 128, 4>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((attn_wo1_kernel<T_Q4_K, 128, 8>), grid, dim3(256), lds, s, p);
+  } else {
+    if (G == 4) hipLaunchKernelGGL((attn_wo1_kernel<T_Q6_K, 128, 4>), grid, dim3(256), lds, s, p);
+    else hipLaunchKernelGGL((attn_wo1_kernel<T_Q6_K, 128, 8>), grid, dim3(256), lds, s, p);
+  }
+  return true;
 }
 
 QMat make_qmat(const void* base, int type, int rows, int K, size_t expert_stride) {

@@ -19,7 +19,15 @@ static constexpr int kMaxBlocks = 1024;  // 256 CUs x 4
 // RMSNorm's 1/rms is a scalar, so q8(x * w) equals q8(x * w / rms) up to the
 // block scale: the kernel multiplies its final dot products by the returned
 // scale instead of making a second pass over x.
-template <bool NORM, int BLOCK = 256>
+typedef unsigned xp_v4u __attribute__((ext_vector_type(4)));
+// 16-B load with sc1 (L1 bypassed; agent-coherent with sc1 producer stores of the same launch)
+__device__ __forceinline__ float4 ld16f_sc1(const float* base, int i) {
+  const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7FFFFFFF, 0x00020000);
+  const xp_v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, i * (int)sizeof(float), 0, 16);  // aux 16: sc1
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+template <bool NORM, int BLOCK = 256, bool SC1 = false>
 struct XPrologue {
   static constexpr int NB = 4;
   static constexpr int SHIFT = (BLOCK == 1024) ? 12 : (BLOCK == 512 ? 11 : 10);  // log2(BLOCK * 4 floats per slot)
@@ -29,7 +37,8 @@ struct XPrologue {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int i = ((j0 + b) << SHIFT) + tid * 4;
-      v[b] = i < K ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (SC1) v[b] = i < K ? ld16f_sc1(x, i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      else v[b] = i < K ? *reinterpret_cast<const float4*>(x + i) : make_float4(0.f, 0.f, 0.f, 0.f);
       if constexpr (NORM) w[b] = i < K ? *reinterpret_cast<const float4*>(nw + i) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }

@@ -57,6 +57,12 @@ struct GemvArgs {
   const float* resid = nullptr;    // EPI_STORE: out = acc + resid (TP rank 0 residual)
   int debug = 0;                   // microbenchmarks only: 1 = skip the x prologue, 2 = prologue only, 3 = weights after it
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block timeline [grid][5] (instrumented build)
+  // in-flight producer (the decode attention of the same launch, attn_wo1): a block issues its
+  // first item's weights, waits until wait[0 .. wait_cnt) >= wait_n (sc1 poll) and loads x with
+  // sc1 loads; a timed-out wait sets *wait_err (host-mapped)
+  const int* wait = nullptr;
+  int wait_cnt = 0, wait_n = 0;
+  int* wait_err = nullptr;
 };
 void gemv(const GemvArgs& a, int epi, hipStream_t s);
 
@@ -142,13 +148,6 @@ struct BmmArgs {
   // side job of the split-K launches: zero [zero, zero + zero_n) floats (zero_n % 4 == 0)
   float* zero = nullptr;
   int zero_n = 0;
-  // in-flight producer (the batched Wo beside the batched attention, wave-owned split-K kernel):
-  // a block of K part [k0, k0 + kn) issues its first weights, then waits until wait[h] >= wait_n
-  // for every h in [k0 / wait_group, (k0 + kn - 1) / wait_group] (the attention's per-kv-head
-  // done counters) and stages x with sc1 loads; a timed-out wait sets *wait_err (host-mapped)
-  const int* wait = nullptr;
-  int wait_n = 0, wait_group = 0;
-  int* wait_err = nullptr;
 };
 // split-K Q|K|V (BmmArgs::qkv_sk): false = unsupported shape / type mix (caller: one-part path)
 bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B);
@@ -224,7 +223,9 @@ void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hip
 
 // ---------------------------------------------------------------- tensor-parallel collectives
 // One-shot push all-reduce / all-gather over peer memory (p2p_allreduce.hip). Rank p's
-// receive region: data [2 slots][world][max_n] f32, then flags [2][world][kP2PMaxBlocks] i32.
+// receive region: data [2 slots][world][max_n + kP2PMaxBlocks] 8-byte granules {f32 value,
+// u32 epoch} (max_n elements + one heartbeat per block; the `data` pointers address the region
+// as floats, two per granule), then an unused flag area.
 // Every launch runs exactly kP2PMaxBlocks blocks (the slot-reuse argument needs it).
 static constexpr int kP2PMaxRanks = 8;
 static constexpr int kP2PMaxBlocks = 64;
@@ -273,8 +274,8 @@ struct AttnDecodeArgs {
   // batched: also write the output as the next projection's bmm input (f16, bmm k swizzle)
   __half* out_h = nullptr;
   size_t out_h_stride = 0;
-  // batched, with out_h: once a row's output of kv head h is written (sc1 stores), done[h] += 1
-  // (agent scope) - the Wo projection running beside this launch (BmmArgs::wait) polls it
+  // single row (attn_wo1): once kv head h's output is written (sc1 stores), done[h] += 1 (agent
+  // scope) - the Wo GEMV planes of the same launch (GemvArgs::wait) poll it
   int* done = nullptr;
   // batched, split-K Q|K|V (BmmArgs::qkv_sk): q / k / v of row b are the RoPE'd but unnormalised
   // sums qkv_raw[b * qkv_ld + ...] (q at 0, k at k_off, v at v_off), the row's RMSNorm scale is
@@ -292,10 +293,10 @@ struct AttnDecodeArgs {
   int* pf_sink = nullptr;
 };
 void attn_decode(const AttnDecodeArgs& a, hipStream_t s);
-// The batched attention and its Wo projection in ONE launch (bmm.hip): `wo` waits for the
-// attention's done counters (wo.wait == a.done). False: shape / weight type not covered - the
-// caller launches attn_decode + bmm instead.
-bool attn_wo(const AttnDecodeArgs& a, const BmmArgs& wo, hipStream_t s);
+// The single-row decode attention and its Wo GEMV (split-K into the residual) in ONE launch
+// (gemv.hip): `wo` waits for the attention's done counters (wo.wait == a.done, one per kv head).
+// False: shape / weight type not covered.
+bool attn_wo1(const AttnDecodeArgs& a, const GemvArgs& wo, hipStream_t s);
 size_t attn_decode_workspace_floats(int n_ctx, int n_head, int head_dim);
 
 // Prefill: causal attention of T queries at positions pos0.. over the cache.
@@ -369,7 +370,9 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 
 // ---------------------------------------------------------------- elementwise / misc
 // x[t][:] = dequant(token_embd[tokens[t]][:])
-void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s);
+// (side job: zero [zero, zero + zero_n) ints)
+void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s, int* zero = nullptr,
+                int zero_n = 0);
 // y_bf16[t] = rmsnorm(x[t]) * w
 // zero (optional): also zero rows [T][zero_ld] f32 (the next split-K GEMM's output)
 // f16sw: write y as f16 in bmm's 4-group k order instead (gemm_t16's input; same 2-byte rows)

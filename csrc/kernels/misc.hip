@@ -24,13 +24,15 @@ __device__ void embed_body(const QMat& e, const int* tokens, int T, float* x) {
   }
 }
 
-__global__ __launch_bounds__(128) void embed_kernel(QMat e, const int* tokens, int T, float* x) {
+// side job: zero [zero, zero + zero_n) ints (the decode step's done counters, attn_wo1)
+__global__ __launch_bounds__(128) void embed_kernel(QMat e, const int* tokens, int T, float* x, int* zero, int zero_n) {
+  for (int i = blockIdx.x * 128 + threadIdx.x; i < zero_n; i += gridDim.x * 128) zero[i] = 0;
   LFK_DISPATCH_TYPE(e.type, embed_body<QT>(e, tokens, T, x));
 }
 
-void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s) {
+void embed_rows(const QMat& emb, const int* tokens, int T, float* x, hipStream_t s, int* zero, int zero_n) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(128), 0, s, emb, tokens, T, x);
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(128), 0, s, emb, tokens, T, x, zero, zero ? zero_n : 0);
 }
 
 template <bool F16SW>

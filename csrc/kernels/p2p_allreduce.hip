@@ -2,106 +2,110 @@
 // §5.8): the two per-layer all-reduces of a row-parallel decode step carry 16-32 KiB
 // per row, where a ring all-reduce is latency-bound (2(N-1) dependent steps). Here
 // every rank WRITES its buffer straight into every peer's receive slot over its
-// point-to-point xGMI link (7 links used at once on an 8-GPU node), raises one flag
-// per (rank, block) in each peer, then waits for the N flags in its OWN memory and
+// point-to-point xGMI link (7 links used at once on an 8-GPU node) as 8-byte granules
+// {value, epoch}, and reads its OWN slots until every granule carries this launch's epoch:
 //   * all-reduce: sums the N slots locally in fixed rank order - every rank computes
 //     bit-identical results (the TP ranks must stay in lock-step), or
 //   * all-gather: copies slot p to dst[p * n ...] (the sampler's candidate blocks,
 //     logit shards for the test hooks).
+// The data carries its own readiness (the LL form of a hand-off, MI355X_MICROARCH "granule"):
+// no release fence behind the payload, no flag store, no flag poll before the payload reads -
+// one memory round trip per element instead of store -> fence -> flag -> poll -> load (the
+// round-3 form measured ~10 us per 2-rank collective on one GPU).
 //
 // Receive regions are exported/imported once with hipIpc* handles (one process per
 // GPU, or several processes on one GPU in the IPC-only test mode); the kernel is
 // graph-capturable: the epoch lives in device memory and advances on every launch.
 //
 // Slot reuse needs no second barrier because EVERY launch uses the same fixed grid
-// (kP2PMaxBlocks blocks, whatever n is): all blocks share one epoch sequence, slot
-// parity alternates per launch, and a rank writes parity e&1 again at epoch e+2 only
-// after it saw every peer's flags of epoch e+1 - raised by a peer's launch e+1, which
-// started after that peer's launch e (and its reads of the slot) completed (stream
-// order). A per-launch block count would break this: blocks of different launches
-// would advance different epochs and alias slot ranges.
+// (kP2PMaxBlocks blocks, whatever n is) and a block's chunk is fixed per n: all blocks
+// advance one epoch sequence, slot parity alternates per launch, and rank R's block b writes
+// parity e&1 again at epoch e+2 only after it received every peer's block-b granules of epoch
+// e+1 - written by that peer's launch e+1, which started after the peer's launch e (and its
+// block b's reads of parity e&1) completed (stream order). That needs every block to receive at
+// least one granule from every peer in every launch, whatever n is: each block also exchanges
+// one heartbeat granule of its own (index max_n + b of the slot). A granule of an older epoch is
+// never taken for a newer one: the tag is the full 32-bit epoch.
 //
-// Memory model (why a peer's bytes are never read stale, across xGMI or on one GPU):
-//   * the receive region is allocated hipDeviceMallocUncached (runtime/p2p.cpp): no L2 /
-//     L1 of the owning GPU or of a writing peer keeps a line of it, so every store lands in
-//     the owner's HBM and every load reads HBM - there is no previous-epoch line to hit;
-//   * payload stores are plain (vectorised) stores into the peer's region, ordered before
-//     the flag stores by a system-scope release fence + block barrier (the fence waits for
-//     the stores to be acknowledged by the peer's memory);
-//   * the reader polls its LOCAL flags with system-scope acquire loads and reads the slots
-//     with system-scope loads; on a cacheable fallback region (hipMalloc, if the uncached
-//     allocation is refused) the system scope still bypasses the non-coherent caches.
-// Slot reuse (a rank overwriting a slot a slower peer still reads) is excluded by the epoch
-// argument above.
-// Every wait is bounded: a timeout sets *err and the launch completes (the engine
-// then reports itself unhealthy) instead of hanging.
+// Memory model: the region is hipDeviceMallocUncached (runtime/p2p.cpp), so no L2 of either
+// side keeps a line of it; each granule is one naturally aligned 8-byte system-scope atomic
+// store (untorn: value and tag arrive together) and is read with 8-byte system-scope atomic
+// loads. On a cacheable fallback region (hipMalloc, if the uncached allocation is refused) the
+// system scope still bypasses the non-coherent caches.
+// Every wait is bounded: a timeout sets *err and the launch completes (the engine then reports
+// itself unhealthy) instead of hanging.
 #include "kernels.h"
 
 namespace lfk {
 
 static constexpr int kP2PSpin = 1 << 22;
 
-__device__ __forceinline__ float ld_sys(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+typedef unsigned long long u64_t;
 
 __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
-  __shared__ int s_ep, s_ok;
+  __shared__ unsigned s_ep;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int W = a.world, R = a.rank;
-  const int chunk = ((a.n + kP2PMaxBlocks - 1) / kP2PMaxBlocks + 3) & ~3;
+  const int chunk = (a.n + kP2PMaxBlocks - 1) / kP2PMaxBlocks;
   const int i0 = min(a.n, b * chunk), i1 = min(a.n, i0 + chunk);
   if (tid == 0) {
     const int e = a.epochs[b] + 1;  // block-private word: plain access
     a.epochs[b] = e;
-    s_ep = e;
-    s_ok = 1;
+    s_ep = (unsigned)e;
   }
   __syncthreads();
-  const int ep = s_ep, slot = ep & 1;
-  const size_t FB = kP2PMaxBlocks;
+  const unsigned ep = s_ep;
+  const int slot = ep & 1;
+  const size_t M = (size_t)a.max_n + kP2PMaxBlocks;  // granules per (slot, rank): data + heartbeats
+  const int hb = a.max_n + b;                          // this block's heartbeat granule
+  const int nb = i1 - i0 + 1;                           // the chunk + the heartbeat
   // 1. push this rank's chunk into slot [slot][R] of every rank (self included)
-  const bool vec = ((reinterpret_cast<uintptr_t>(a.src) & 15) == 0) && (a.max_n % 4 == 0);
-  const int v0 = i0, v1 = vec ? i0 + ((i1 - i0) & ~3) : i0;
-  for (int p = 0; p < W; ++p) {
-    float* dst = a.peers.data[p] + ((size_t)slot * W + R) * a.max_n;
-    for (int i = v0 + 4 * tid; i < v1; i += 4 * blockDim.x)
-      *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(a.src + i);
-    for (int i = v1 + tid; i < i1; i += blockDim.x) dst[i] = a.src[i];
+  for (int j = tid; j < nb; j += blockDim.x) {
+    const int i = j < nb - 1 ? i0 + j : hb;
+    const u64_t g = ((u64_t)ep << 32) | (j < nb - 1 ? __float_as_uint(a.src[i]) : 0u);
+#pragma unroll
+    for (int p = 0; p < kP2PMaxRanks; ++p)
+      if (p < W)
+        __hip_atomic_store(reinterpret_cast<u64_t*>(a.peers.data[p]) + ((size_t)slot * W + R) * M + i, g,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this thread's stores before the barrier
-  __syncthreads();
-  // 2. one flag per (slot, rank, block) in every rank
-  if (tid < W)
-    __hip_atomic_store(a.peers.flags[tid] + ((size_t)slot * W + R) * FB + b, ep, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  // 3. wait for every rank's flag in this rank's own region
-  if (tid < W) {
-    const int* f = a.peers.flags[R] + ((size_t)slot * W + tid) * FB + b;
-    for (int spins = 0; __hip_atomic_load(const_cast<int*>(f), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < ep;
-         ++spins) {
-      if (spins > kP2PSpin) {
-        __hip_atomic_store(a.err, 100 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_ok = 0;
-        break;
+  // 2. this rank's slots: every rank's granule of element i, re-read until it carries this epoch
+  const u64_t* mine = reinterpret_cast<const u64_t*>(a.peers.data[R]) + (size_t)slot * W * M;
+  for (int j = tid; j < nb; j += blockDim.x) {
+    const int i = j < nb - 1 ? i0 + j : hb;
+    float v[kP2PMaxRanks];
+    unsigned pending = (1u << W) - 1;
+    for (int spins = 0; pending; ++spins) {
+#pragma unroll
+      for (int p = 0; p < kP2PMaxRanks; ++p) {
+        if (p < W && (pending >> p & 1)) {
+          const u64_t g = __hip_atomic_load(const_cast<u64_t*>(mine + (size_t)p * M + i), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((unsigned)(g >> 32) == ep) {
+            v[p] = __uint_as_float((unsigned)g);
+            pending &= ~(1u << p);
+          }
+        }
       }
-      __builtin_amdgcn_s_sleep(2);
+      if (!pending) break;
+      if (spins > kP2PSpin) {
+        __hip_atomic_store(a.err, 100 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
-  }
-  __syncthreads();
-  if (!s_ok) return;
-  const float* mine = a.peers.data[R] + (size_t)slot * W * a.max_n;
-  if (a.gather) {
-    // 4a. rank p's chunk -> dst[p * n + i]
-    for (int p = 0; p < W; ++p)
-      for (int i = i0 + tid; i < i1; i += blockDim.x) a.dst[(size_t)p * a.n + i] = ld_sys(mine + (size_t)p * a.max_n + i);
-    return;
-  }
-  // 4b. sum the W slots in rank order (bit-identical on every rank)
-  for (int i = i0 + tid; i < i1; i += blockDim.x) {
-    float v = 0.f;
-    for (int p = 0; p < W; ++p) v += ld_sys(mine + (size_t)p * a.max_n + i);
-    a.dst[i] = v;
+    if (j == nb - 1) continue;  // the heartbeat: received, nothing to write
+    if (a.gather) {
+#pragma unroll
+      for (int p = 0; p < kP2PMaxRanks; ++p)
+        if (p < W) a.dst[(size_t)p * a.n + i] = v[p];
+    } else {
+      float sum = 0.f;  // rank order: bit-identical on every rank
+#pragma unroll
+      for (int p = 0; p < kP2PMaxRanks; ++p)
+        if (p < W) sum += v[p];
+      a.dst[i] = sum;
+    }
   }
 }
 

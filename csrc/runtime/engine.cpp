@@ -160,8 +160,11 @@ Engine::~Engine() {
   } catch (...) {
   }
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
+  if (graph_exec2_) hipGraphExecDestroy(graph_exec2_);
   for (size_t i = 1; i < sgraph_.size(); ++i)
     if (sgraph_[i]) hipGraphExecDestroy(sgraph_[i]);
+  for (size_t i = 1; i < sgraph2_.size(); ++i)
+    if (sgraph2_[i]) hipGraphExecDestroy(sgraph2_[i]);
   for (hipGraphExec_t g : bgraph_)
     if (g) hipGraphExecDestroy(g);
   for (hipGraphExec_t g : bgraph2_)
@@ -301,6 +304,18 @@ void Engine::alloc_buffers() {
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = e[0] != '0';  // A/B (test_engine_gpu)
+  // single-row decode: attention + Wo in one launch (attn_wo1); per-layer done counters, zeroed
+  // by every decode step's embedding launch
+  if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
+  if (wo_fuse_ && nkv_l_ <= 64) {
+    HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
+    *wo_err_h_ = 0;
+    HIPCHK(hipHostGetDevicePointer((void**)&wo_err_, wo_err_h_, 0));
+    dec_done_ = (int*)dalloc(sizeof(int) * 64 * hp_.n_layer);
+    HIPCHK(hipMemset(dec_done_, 0, sizeof(int) * 64 * hp_.n_layer));
+  } else {
+    wo_fuse_ = false;
+  }
   const int tp = opt_.tp_size;
   cand_words_ = sampler_cand_words(V_l_);
   cand_ = (unsigned*)dalloc(sizeof(unsigned) * cand_words_);
@@ -396,19 +411,10 @@ void Engine::setup_batch_mfma() {
   const int E = std::max(1, hp_.n_expert);
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
   {
-    const size_t n = qkv_b_zero_n();  // + ss_b_ [16] + wo_done_ [64]
+    const size_t n = qkv_b_zero_n();  // + ss_b_ [16]
     qkv_b_ = (float*)dalloc(sizeof(float) * n);
     HIPCHK(hipMemsetAsync(qkv_b_, 0, sizeof(float) * n, stream_));
     ss_b_ = qkv_b_ + (size_t)bmax_ * (nq_ + 2 * nkvd_);
-    wo_done_ = reinterpret_cast<int*>(ss_b_ + 16);
-    if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
-    if (wo_fuse_ && nkv_l_ <= 64) {
-      HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
-      *wo_err_h_ = 0;
-      HIPCHK(hipHostGetDevicePointer((void**)&wo_err_, wo_err_h_, 0));
-    } else {
-      wo_fuse_ = false;
-    }
   }
   hh_b_ = (__half*)dalloc(2ull * bmax_ * std::max(1, F_l_) * (moe_b_ ? E : 1));
   if (moe_b_) ew_b_ = (float*)dalloc(sizeof(float) * bmax_ * E);
@@ -602,16 +608,31 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.n_ctx = opt_.n_ctx; aa.n_head = nh_l_; aa.n_kv_head = nkv_l_; aa.head_dim = hd;
   aa.scale = 1.f / std::sqrt((float)hd);
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
-  if (attn_touch_ && nkv_l_ < 63) {  // this layer's Wo into the memory-side cache under the attention
-    aa.pf_sink = attn_cnt_ + 63;
-    aa.pf[0] = L.wo.base;
-    aa.pf_bytes[0] = qmat_bytes(L.wo);
-  }
-  attn_decode(aa, s);
-
   GemvArgs o;
   o.w = L.wo; o.x = attn_; o.n_out = d;
-  if (!tp) {
+  // attention + Wo in one launch: Wo's weights stream while the attention runs
+  bool fused = false;
+  if (!tp && wo_fuse_) {
+    aa.done = dec_done_ + 64 * l;
+    o.out = x_;
+    o.wait = aa.done; o.wait_cnt = nkv_l_; o.wait_n = 1; o.wait_err = wo_err_;
+    fused = attn_wo1(aa, o, s);
+    if (!fused) {
+      aa.done = nullptr;
+      o.wait = nullptr; o.wait_cnt = 0; o.wait_n = 0; o.wait_err = nullptr;
+    }
+  }
+  if (!fused) {
+    if (attn_touch_ && nkv_l_ < 63) {  // this layer's Wo into the memory-side cache under the attention
+      aa.pf_sink = attn_cnt_ + 63;
+      aa.pf[0] = L.wo.base;
+      aa.pf_bytes[0] = qmat_bytes(L.wo);
+    }
+    attn_decode(aa, s);
+  }
+
+  if (fused) {
+  } else if (!tp) {
     o.out = x_;
     gemv(o, EPI_ADD, s);
   } else {
@@ -680,7 +701,8 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int
 }
 
 void Engine::enqueue_decode(hipStream_t s) {
-  embed_rows(tok_embd_, state_ + (size_t)S_NSTATE * dslot_ + S_TOKEN, 1, x_, s);
+  // (the embedding launch also zeroes the layers' attention -> Wo done counters)
+  embed_rows(tok_embd_, state_ + (size_t)S_NSTATE * dslot_ + S_TOKEN, 1, x_, s, dec_done_, 64 * hp_.n_layer);
   for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
   enqueue_head(x_, 1, s, dslot_);
 }
@@ -875,6 +897,9 @@ void Engine::enqueue_rows_ffn(int l, int T, hipStream_t s, bool t16) {
   }
 }
 
+// (two instantiations of every one-row graph: pipelined one-row steps alternate them as the
+// batched ones do - an instance relaunched while its previous launch is still queued can be held
+// back until that launch completes; launch_par_ picks the flight's instance)
 void Engine::launch_step(int slot) {
   dslot_ = slot;
   if (opt_.use_graph) {
@@ -884,20 +909,25 @@ void Engine::launch_step(int slot) {
         enqueue_decode(stream_);
         HIPCHK(hipStreamEndCapture(stream_, &graph_));
         HIPCHK(hipGraphInstantiate(&graph_exec_, graph_, nullptr, nullptr, 0));
+        HIPCHK(hipGraphInstantiate(&graph_exec2_, graph_, nullptr, nullptr, 0));
       }
-      HIPCHK(hipGraphLaunch(graph_exec_, stream_));
+      HIPCHK(hipGraphLaunch(launch_par_ ? graph_exec2_ : graph_exec_, stream_));
     } else {
-      if ((int)sgraph_.size() <= slot) sgraph_.resize(slot + 1, nullptr);
+      if ((int)sgraph_.size() <= slot) {
+        sgraph_.resize(slot + 1, nullptr);
+        sgraph2_.resize(slot + 1, nullptr);
+      }
       if (!sgraph_[slot]) {
         hipGraph_t g = nullptr;
         HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
         enqueue_decode(stream_);
         HIPCHK(hipStreamEndCapture(stream_, &g));
-        const hipError_t e = hipGraphInstantiate(&sgraph_[slot], g, nullptr, nullptr, 0);
+        hipError_t e = hipGraphInstantiate(&sgraph_[slot], g, nullptr, nullptr, 0);
+        if (e == hipSuccess) e = hipGraphInstantiate(&sgraph2_[slot], g, nullptr, nullptr, 0);
         hipGraphDestroy(g);
         HIPCHK(e);
       }
-      HIPCHK(hipGraphLaunch(sgraph_[slot], stream_));
+      HIPCHK(hipGraphLaunch(launch_par_ ? sgraph2_[slot] : sgraph_[slot], stream_));
     }
   } else {
     enqueue_decode(stream_);
@@ -1082,23 +1112,14 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
   }
   aa.dbg_clk = clk_of(l, 1);
-  // the attention and Wo in one launch (bmm.hip attn_wo): Wo's weights stream while the
-  // attention runs, each K part starting once its kv heads are done for every row
-  bool fused_wo = false;
-  if (sk && wo_fuse_ && !tp && B <= 8) {
-    aa.done = wo_done_;
-    BmmArgs a;
-    a.w = L.t_wo; a.xh = xh_b_; a.ldh = nq_; a.out = x_; a.ldo = d; a.n_out = d; a.B = B;
-    a.wait = wo_done_; a.wait_n = B; a.wait_group = (nh_l_ / nkv_l_) * hd; a.wait_err = wo_err_;
-    fused_wo = attn_wo(aa, a, s);
-    if (!fused_wo) aa.done = nullptr;
-  }
-  if (!fused_wo) {
-    attn_decode(aa, s);
-    tp_begin();
-    bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
-    tp_end();
-  }
+  // (the batched Wo stays its own launch: in one launch with the attention - Wo planes streaming
+  // their weights meanwhile and starting on done counters - the B = 6 step measured 2.42 vs 2.34
+  // ms, r4: the in-launch hand-off costs what the boundary did and the weight stream slowed the
+  // attention's K / V loads)
+  attn_decode(aa, s);
+  tp_begin();
+  bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
+  tp_end();
   if (moe_b_ && fused) {
     // MoE: dense per-row expert weights (f32 router on the normed rows), then every expert's
     // SwiGLU rows in ONE gate/up launch (epilogue scaled by the row's weight for that expert,
@@ -1198,6 +1219,8 @@ enum TPOp : int32_t {
   TPO_BATCH_LOGITS,
   TPO_BENCH_DECODE,
   TPO_SLOTS_BEGIN,  // slots_begin(): n, slots, n_keep, then n x (prompt, sampling)
+  TPO_BATCH_LAUNCH,   // batch_launch(): slots (pipelined steps: queued, not waited for)
+  TPO_BATCH_COLLECT,  // batch_collect(): the oldest step in flight
 };
 
 static void put_sp(TPMsg& m, const SamplingOpts& sp) {
@@ -1303,6 +1326,8 @@ void Engine::follow() {
           break;
         }
         case TPO_BATCH_STEP: batch_step_impl(m.get_vec<int>()); break;
+        case TPO_BATCH_LAUNCH: batch_launch_impl(m.get_vec<int>()); break;
+        case TPO_BATCH_COLLECT: batch_collect_impl(); break;
         case TPO_EVAL_LOGITS: {
           const int pos0 = m.get<int>();
           eval_logits_impl(m.get_vec<int>(), pos0);
@@ -1476,11 +1501,24 @@ void Engine::check_batch_rows(const std::vector<int>& slots) const {
   }
 }
 
+// Pipelined steps under TP: rank 0 publishes every launch and collect, the followers replay them in
+// the same order (their step k + 1 queued behind step k, the collectives pairing up as in
+// synchronous steps); a follower's collect only waits for its own step.
 void Engine::batch_launch(const std::vector<int>& slots) {
   ExecGuard guard(this);
-  if (!can_pipeline()) throw std::runtime_error("batch_launch: not available on this engine (TP)");
+  if (!can_pipeline()) throw std::runtime_error("batch_launch: not available on this engine");
   if (fl_n_ >= 2) throw std::runtime_error("batch_launch: two steps already in flight");
   check_batch_rows(slots);
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_BATCH_LAUNCH); m.put_vec(slots);
+    mirror(m);
+  }
+  batch_launch_impl(slots);
+}
+
+void Engine::batch_launch_impl(const std::vector<int>& slots) {
+  if (fl_n_ >= 2) throw std::runtime_error("batch_launch: two steps already in flight");
   const int B = (int)slots.size();
   // a changed row -> slot map is rewritten in pinned memory: no copy of it may still be queued
   const bool remap = B != bslots_n_ || std::memcmp(h_bslots_, slots.data(), sizeof(int) * B) != 0;
@@ -1500,6 +1538,16 @@ void Engine::batch_launch(const std::vector<int>& slots) {
 
 std::vector<int> Engine::batch_collect() {
   ExecGuard guard(this);
+  if (fl_n_ <= 0) throw std::runtime_error("batch_collect: no step in flight");
+  if (leader()) {
+    TPMsg m;
+    m.put<int32_t>(TPO_BATCH_COLLECT);
+    mirror(m);
+  }
+  return batch_collect_impl();
+}
+
+std::vector<int> Engine::batch_collect_impl() {
   if (fl_n_ <= 0) throw std::runtime_error("batch_collect: no step in flight");
   const int i = fl_head_;
   fl_head_ ^= 1;

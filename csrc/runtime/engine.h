@@ -144,9 +144,9 @@ class Engine : public SlotBackend {
   std::vector<int> batch_step(const std::vector<int>& slots) override;
   // Pipelined batch_step (the scheduler's decode loop, slots.h): without it the host turnaround
   // between steps - stream-sync wake-up, token hand-off, graph launch - left the GPU idle
-  // ~60-80 us per 2.3 ms step. Single-GPU engines only (TP followers replay the leader's
-  // synchronous commands).
-  bool can_pipeline() const override { return opt_.tp_size == 1 && bmax_ > 0; }
+  // ~60-80 us per 2.3 ms step. Under TP rank 0 publishes each launch and collect and the
+  // followers replay them in order (their steps queue the same way).
+  bool can_pipeline() const override { return bmax_ > 0; }
   void batch_launch(const std::vector<int>& slots) override;
   std::vector<int> batch_collect() override;
   std::vector<float> batch_logits(int B);  // test hook: logits [B][n_vocab] of the last batch_step
@@ -327,6 +327,8 @@ class Engine : public SlotBackend {
   int fl_head_ = 0, fl_n_ = 0;
   void check_batch_rows(const std::vector<int>& slots) const;
   void enqueue_batch_launch(const std::vector<int>& slots, int* h_dst);
+  void batch_launch_impl(const std::vector<int>& slots);
+  std::vector<int> batch_collect_impl();
   int bslots_n_ = -1;         // rows of the row -> slot map last uploaded to bslots_
   int last_batch_ = 0;
   // batch_step projections on the MFMA batched projection (bmm.hip: weights streamed once per
@@ -358,15 +360,14 @@ class Engine : public SlotBackend {
   }
   float* qkv_b_ = nullptr;
   float* ss_b_ = nullptr;
-  // the batched attention and Wo in one launch (split-K Q|K|V, no TP; bmm.hip attn_wo): Wo
-  // streams its weights while the attention runs and starts each K part once that part's kv
-  // heads are done for every row (wo_done_ [64] counters after ss_b_, zeroed with qkv_b_); a
-  // timed-out wait sets *wo_err_ (host-mapped). LFK_WO_FUSE=0: two launches (A/B).
+  // the single-row decode's attention and Wo in one launch (no TP; gemv.hip attn_wo1): Wo
+  // streams its weights while the attention runs and starts once every kv head is done
+  // (dec_done_); a timed-out wait sets *wo_err_ (host-mapped). LFK_WO_FUSE=0: two launches (A/B).
   bool wo_fuse_ = true;
-  int* wo_done_ = nullptr;
   int* wo_err_h_ = nullptr;   // host view
   int* wo_err_ = nullptr;     // device view
-  size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16 + 64; }
+  int* dec_done_ = nullptr;   // single-row decode: [n_layer][64] done counters (attn_wo1)
+  size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16; }
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
   // a second instantiation of each, for the pipelined launches: consecutive in-flight steps
@@ -378,10 +379,10 @@ class Engine : public SlotBackend {
   // one graph per slot (slot 0's is graph_exec_). batch_step over ONE row takes this path
   // (the faster one at B = 1: 1.65 vs 2.18 ms)
   int dslot_ = 0;
-  std::vector<hipGraphExec_t> sgraph_;
+  std::vector<hipGraphExec_t> sgraph_, sgraph2_;  // (second instances: pipelined one-row steps)
   bool last_b1_ = false;      // the last batch_step ran its one row on the single-row path
   hipGraph_t graph_ = nullptr;
-  hipGraphExec_t graph_exec_ = nullptr;
+  hipGraphExec_t graph_exec_ = nullptr, graph_exec2_ = nullptr;
   static constexpr int kDepth = 2;
   hipEvent_t step_ev_[kDepth] = {};
 };

@@ -14,7 +14,8 @@ P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached)
   if (world < 1 || world > kP2PMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("p2p: bad rank/world");
   if (max_n <= 0) throw std::runtime_error("p2p: bad max_n");
   p2pchk(hipSetDevice(device_), "hipSetDevice");
-  data_bytes_ = sizeof(float) * 2 * (size_t)world * max_n_;
+  // {value, epoch} granules: max_n data + kP2PMaxBlocks heartbeats per (slot, rank)
+  data_bytes_ = sizeof(unsigned long long) * 2 * (size_t)world * (max_n_ + kP2PMaxBlocks);
   data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
   region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
   // A whole, 2 MiB-granular allocation of its own, UNCACHED (hipDeviceMallocUncached): peers

@@ -171,8 +171,8 @@ class ReferenceLlama:
     def _rms(self, x, w):
         return x * self.torch.rsqrt((x * x).mean(-1, keepdim=True) + self.hp.rms_eps) * w
 
-    def _normed_input(self, x, w, path):
-        """The normalised projection input the path feeds its matmul."""
+    def _normed_input(self, x, w, path, attn: bool = False):
+        """The normalised projection input the path feeds its matmul (``attn``: the Q|K|V input)."""
         torch = self.torch
         rs = torch.rsqrt((x * x).mean(-1, keepdim=True) + self.hp.rms_eps)
         if path == "decode":
@@ -182,9 +182,9 @@ class ReferenceLlama:
         if path == "prefill16":
             return self._f16(x * rs * w)
         if path == "batch":
-            # d = 4096 (B <= 8): the norm folded into the projection's x staging applies 1/rms
-            # to the f32 result; otherwise bmm's prep kernel stages f16(x / rms * w)
-            return self._f16(x * w) * rs if x.shape[-1] == 4096 else self._f16(x * rs * w)
+            # the split-K Q|K|V (any d) and, at d = 4096, the one-part gate/up stage f16(x * w) and
+            # apply 1/rms to the f32 result; otherwise bmm's prep kernel stages f16(x / rms * w)
+            return self._f16(x * w) * rs if attn or x.shape[-1] == 4096 else self._f16(x * rs * w)
         return x * rs * w
 
     def _plain_input(self, h, path):
@@ -309,7 +309,7 @@ class ReferenceLlama:
         x = self.tok_embd[torch.as_tensor(list(tokens))]
         wk = self._wkind(path)
         for li, L in enumerate(self.layers):
-            h = self._normed_input(x, L["attn_norm"], path)
+            h = self._normed_input(x, L["attn_norm"], path, attn=True)
             q = (h @ self._weight("attn_q", L, wk).T).view(T, hp.n_head, hp.head_dim)
             k = (h @ self._weight("attn_k", L, wk).T).view(T, hp.n_head_kv, hp.head_dim)
             v = (h @ self._weight("attn_v", L, wk).T).view(T, hp.n_head_kv, hp.head_dim)

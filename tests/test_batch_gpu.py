@@ -201,6 +201,44 @@ def test_pipelined_steps_equal_synchronous(models):
     assert run(False) == run(True)
 
 
+@pytest.mark.parametrize("joint", [False, True])
+def test_slot_begin_while_steps_in_flight(models, joint):
+    """The scheduler admits a request (slot_begin / slots_begin) while a pipelined step is still
+    queued - into a slot whose row that very step is computing (its request just ended): the
+    admission's state upload and prefill are ordered behind the in-flight step on the engine
+    stream, so the new request's first token and every later step equal a run that collected
+    the step first."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-llama3-q4_k_m"]
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    rng = np.random.default_rng(12)
+    prompts = {s: [int(t) for t in rng.integers(3, 300, n)] for s, n in ((1, 9), (2, 14), (3, 11))}
+    newp = [int(t) for t in rng.integers(3, 300, 17)]
+
+    def run(overlap):
+        eng = load_hip().Engine(path, n_ctx=256, n_batch=64, device=0, use_graph=True, n_slots=4)
+        for s, p in prompts.items():
+            eng.slot_begin(s, p, 0, greedy)
+        out = []
+        eng.batch_launch([1, 2, 3])
+        eng.batch_launch([1, 2, 3])
+        out.append(list(eng.batch_collect()))
+
+        def admit():
+            return eng.slots_begin([3], [newp], [0], [greedy])[0] if joint else eng.slot_begin(3, newp, 0, greedy)
+        if overlap:
+            first = admit()                              # step 2 still queued
+            out.append(list(eng.batch_collect())[:2])    # slot 3's token of that step is dropped
+        else:
+            out.append(list(eng.batch_collect())[:2])
+            first = admit()
+        for _ in range(4):
+            out.append(list(eng.batch_step([1, 2, 3])))
+        assert eng.healthy, eng.last_error
+        return first, out
+    assert run(True) == run(False)
+
+
 def test_batch_step_six_rows_d8192(tmp_path):
     """Six rows at d = 8192: the split-K Q|K|V beside the FFN path that does not stage a whole row
     (its projections' inputs prepared by bprep), which must re-zero the split-K rows itself -

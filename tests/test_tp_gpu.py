@@ -65,6 +65,14 @@ def _exercise(llm, with_app):
     out["batched"] = [x["choices"][0]["text"] for x in res]
     out["batched_tokens"] = [llm.tokenize(t.encode(), add_bos=False, special=True) for t in out["batched"]]
     out["batched_n"] = [x["usage"]["completion_tokens"] for x in res]
+    # pipelined steps (the scheduler's mode): step k + 1 queued before step k is collected - under
+    # TP the followers replay the launches and collects in the same order
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    pf = [eng.slot_begin(1, toks[:6], 0, greedy), eng.slot_begin(2, toks[3:12], 0, greedy)]
+    eng.batch_launch([1, 2])
+    eng.batch_launch([1, 2])
+    pf += list(eng.batch_collect()) + list(eng.batch_collect()) + list(eng.batch_step([1, 2]))
+    out["pipelined"] = pf
     # an after-the-batch single-sequence request still works (slot 0 path)
     out["greedy2"] = eng.generate(toks[:9], 0, 8, {"temperature": 0.0}, [], None, None)["tokens"]
     if with_app:
@@ -200,6 +208,7 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
             "sampled": (sd is None or sd >= 4) and len(got["sampled"]) == len(ref["sampled"]),
             "cancel": got["cancel"][0] == "cancelled" and got["cancel"][1] < 200,
             "batched": batched_ok,
+            "pipelined": got["pipelined"] == ref["pipelined"],
             "healthy": got["healthy"],
         }
         if "http" in got:

@@ -55,7 +55,7 @@ for s in "$@"; do
     bench20) step bench20 900 python bench.py --steps 20 --warmup 2 ;;
     serial) step serial 900 python bench.py --steps 10 --warmup 1 --clients 1 --max-batch 1 ;;
     benchtp2) step benchtp2 900 env LFK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 12 --warmup 2 ;;
+                --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --parallel tp --steps 6 --warmup 1 ;;
     benchdp2) step benchdp2 900 env LFK_BENCH_DEVICE=0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --parallel dp --steps 4 --warmup 1 ;;
     bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
@@ -66,7 +66,8 @@ for s in "$@"; do
     stepprof) prof stepprof 300 tools/batch_bench.py --batches 6 --steps 32
               python3 tools/step_kernels.py gpurun_out/stepprof/k_kernel_trace.csv > gpurun_out/stepprof_kernels.txt
               python3 tools/step_slots.py gpurun_out/stepprof/k_kernel_trace.csv >> gpurun_out/stepprof_kernels.txt ;;
-    decprof) prof decprof 300 tools/decode_bench.py --steps 64 --no-graph ;;
+    decprof) prof decprof 300 tools/decode_bench.py --steps 64 --no-graph
+             python3 tools/prof_summary.py gpurun_out/decprof/k_kernel_stats.csv > gpurun_out/decprof_summary.md ;;
     prefprof) prof prefprof 300 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
     bmmpmc) pmc bmmpmc tools/batch_bench.py --batches 6 --steps 4 ;;
     t16pmc) pmc t16pmc tools/gemm_bench.py --eager --reps 5 --T 512 --t16 ;;

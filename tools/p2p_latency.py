@@ -21,6 +21,9 @@ SIZES = [4096, 8192, 6 * 4096, 6 * 8192]
 
 def _worker(rank, world, port, reps, q):
     try:
+        # one hardware queue per process: 8 processes x the default 4 queues oversubscribe the
+        # scheduler, which then time-slices the queues (~10 ms per collective measured, r4)
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
         import torch
         import torch.distributed as dist
         os.environ["MASTER_ADDR"] = "127.0.0.1"
