@@ -35,10 +35,13 @@
 // Every wait is bounded: a timeout sets *err and the launch completes (the engine then reports
 // itself unhealthy) instead of hanging.
 #include "kernels.h"
+#include "qdot.h"
 
 namespace lfk {
 
-static constexpr int kP2PSpin = 1 << 22;
+// bounded waits, in wall_clock64 ticks (100 MHz): 20 s - ranks time-sliced on one GPU (the IPC
+// rehearsal) can legitimately wait long for a peer's queue to run
+static constexpr long long kP2PWaitTicks = 2000000000LL;
 
 typedef unsigned long long u64_t;
 
@@ -58,23 +61,49 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
   const int slot = ep & 1;
   const size_t M = (size_t)a.max_n + kP2PMaxBlocks;  // granules per (slot, rank): data + heartbeats
   const int hb = a.max_n + b;                          // this block's heartbeat granule
-  const int nb = i1 - i0 + 1;                           // the chunk + the heartbeat
-  // 1. push this rank's chunk into slot [slot][R] of every rank (self included)
-  for (int j = tid; j < nb; j += blockDim.x) {
-    const int i = j < nb - 1 ? i0 + j : hb;
-    const u64_t g = ((u64_t)ep << 32) | (j < nb - 1 ? __float_as_uint(a.src[i]) : 0u);
+  // 1. push this rank's chunk into slot [slot][R] of every rank (self included), then the block's
+  //    heartbeat (last, so that a peer seeing it mostly finds the data there too)
+  for (int i = i0 + tid; i < i1; i += blockDim.x) {
+    const u64_t g = ((u64_t)ep << 32) | __float_as_uint(a.src[i]);
 #pragma unroll
     for (int p = 0; p < kP2PMaxRanks; ++p)
       if (p < W)
         __hip_atomic_store(reinterpret_cast<u64_t*>(a.peers.data[p]) + ((size_t)slot * W + R) * M + i, g,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // 2. this rank's slots: every rank's granule of element i, re-read until it carries this epoch
+  __syncthreads();
+  if (tid < W)
+    __hip_atomic_store(reinterpret_cast<u64_t*>(a.peers.data[tid]) + ((size_t)slot * W + R) * M + hb, (u64_t)ep << 32,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // 2. the block's heartbeats first - W lanes poll (sleeping between polls) while the rest of the
+  //    block waits at the barrier, so a late peer costs polling traffic of W lanes per block, not
+  //    of every lane (8 ranks sharing one GPU in the IPC rehearsal starved each other's queues)
   const u64_t* mine = reinterpret_cast<const u64_t*>(a.peers.data[R]) + (size_t)slot * W * M;
-  for (int j = tid; j < nb; j += blockDim.x) {
-    const int i = j < nb - 1 ? i0 + j : hb;
+  __shared__ int s_ok;
+  if (tid == 0) s_ok = 1;
+  __syncthreads();
+  if (tid < W) {
+    const long long t0 = wall_clock64();
+    for (int spins = 0;; ++spins) {
+      const u64_t g = __hip_atomic_load(const_cast<u64_t*>(mine + (size_t)tid * M + hb), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
+      if ((unsigned)(g >> 32) == ep) break;
+      if ((spins & 255) == 255 && wall_clock64() - t0 > kP2PWaitTicks) {
+        __hip_atomic_store(a.err, 100 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  // 3. every rank's granule of each element, re-read (rarely) until it carries this epoch: the
+  //    peer's data stores were issued before its heartbeat but may land after it
+  for (int i = i0 + tid; i < i1; i += blockDim.x) {
     float v[kP2PMaxRanks];
     unsigned pending = (1u << W) - 1;
+    const long long t0 = wall_clock64();
     for (int spins = 0; pending; ++spins) {
 #pragma unroll
       for (int p = 0; p < kP2PMaxRanks; ++p) {
@@ -88,13 +117,12 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
         }
       }
       if (!pending) break;
-      if (spins > kP2PSpin) {
+      if ((spins & 255) == 255 && wall_clock64() - t0 > kP2PWaitTicks) {
         __hip_atomic_store(a.err, 100 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (j == nb - 1) continue;  // the heartbeat: received, nothing to write
     if (a.gather) {
 #pragma unroll
       for (int p = 0; p < kP2PMaxRanks; ++p)

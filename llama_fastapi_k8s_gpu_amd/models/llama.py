@@ -275,7 +275,7 @@ class ReferenceLlama:
         Lk = n_past + T
         K = self.k_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)   # [Lk, H, D]
         V = self.v_cache[li, :Lk].repeat_interleave(hp.gqa, dim=1)
-        mask = torch.arange(Lk)[None, :] > pos[:, None]
+        mask = torch.arange(Lk, device=pos.device)[None, :] > pos[:, None]
         if path in ("prefill", "prefill16"):
             l2e = 1.4426950408889634
             s = torch.einsum("thd,lhd->htl", self._f16(q * (scale * l2e)), K)
@@ -305,8 +305,8 @@ class ReferenceLlama:
             raise ValueError(f"unknown path {path!r}")
         T = len(tokens)
         self._router_trace = router_trace
-        pos = torch.arange(n_past, n_past + T)
-        x = self.tok_embd[torch.as_tensor(list(tokens))]
+        pos = torch.arange(n_past, n_past + T, device=self.device)
+        x = self.tok_embd[torch.as_tensor(list(tokens), device=self.device)]
         wk = self._wkind(path)
         for li, L in enumerate(self.layers):
             h = self._normed_input(x, L["attn_norm"], path, attn=True)

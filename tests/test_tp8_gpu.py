@@ -48,6 +48,9 @@ def _exercise(llm):
 
 def _worker(rank, world, port, path, q):
     try:
+        # one hardware queue per process: eight processes x the default four oversubscribe the
+        # queue scheduler, which then time-slices them (tools/p2p_latency.py, r4)
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world), LOCAL_RANK="0")
         import torch.distributed as dist

@@ -19,7 +19,7 @@ import sys
 SIZES = [4096, 8192, 6 * 4096, 6 * 8192]
 
 
-def _worker(rank, world, port, reps, q):
+def _worker(rank, world, port, reps, q, stress=0):
     try:
         # one hardware queue per process: 8 processes x the default 4 queues oversubscribe the
         # scheduler, which then time-slices the queues (~10 ms per collective measured, r4)
@@ -37,6 +37,25 @@ def _worker(rank, world, port, reps, q):
         c = hip.P2PComm(rank, world, max(SIZES), 0)
         c.open(allgather_bytes(c.handle()))
         out = {}
+        if stress:
+            # mixed sizes back to back, eager, no host barrier between launches: checked sums
+            s = torch.cuda.current_stream().cuda_stream
+            bad = 0
+            for it in range(stress):
+                n = [SIZES[-1], 37, 1000 + it % 97, 4096][it % 4]
+                x = torch.full((n,), float(rank + 1), device="cuda")
+                y = torch.empty(n * (world if it % 5 == 0 else 1), device="cuda")
+                (c.allgather if it % 5 == 0 else c.allreduce)(x.data_ptr(), y.data_ptr(), n, s)
+                if it % 25 == 0:
+                    torch.cuda.synchronize()
+                    want = float(world * (world + 1) // 2)
+                    bad += int(it % 5 != 0 and not bool((y == want).all()))
+            torch.cuda.synchronize()
+            out["stress_bad"] = bad
+            q.put((rank, out, c.error(), None))
+            dist.barrier()
+            dist.destroy_process_group()
+            return
         for op in ("allreduce", "allgather"):
             for n in SIZES:
                 src = torch.randn(n, device="cuda")
@@ -73,6 +92,7 @@ def main():
     ap.add_argument("--ranks", default="2,4,8")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--json", default="")
+    ap.add_argument("--stress", type=int, default=0, help="instead: this many mixed-size eager collectives, checked")
     args = ap.parse_args()
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -81,7 +101,7 @@ def main():
     for i, world in enumerate(int(r) for r in args.ranks.split(",")):
         q = ctx.Queue()
         port = 29800 + (os.getpid() % 500) + 11 * i
-        procs = [ctx.Process(target=_worker, args=(r, world, port, args.reps, q)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, args.reps, q, args.stress)) for r in range(world)]
         for p in procs:
             p.start()
         got = [q.get(timeout=300) for _ in procs]
