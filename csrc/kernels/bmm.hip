@@ -809,7 +809,7 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
 // per launch (registers and branches) when they were runtime ones
 // (bid, nblk): the block's index and count in the launch's wave-owned grid (the fused attention +
 // Wo launch runs this body in planes of its grid past the attention's)
-template <int QT, int PD, bool SK, int NW = 8>
+template <int QT, int PD, bool SK, int NW = 8, bool MOE = false>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
   constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -823,6 +823,21 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   const int kparts = a.kparts, kp = bid % kparts, grp = bid / kparts, G = nblk / kparts;
   const int s0 = kp * a.spp, ns = min(steps, s0 + a.spp) - s0;  // this part's steps [s0, s0 + ns)
   const int k0 = s0 * 256, kn = ns * 256, ldx = kn + 8;
+  if (MOE && !SK && a.ew && a.steps_per_expert > 0) {
+    // MoE down: the part of an unrouted expert adds nothing (and its SwiGLU rows were never
+    // written - its gate/up tiles were skipped): the whole block leaves, before any barrier
+    const int e = s0 / a.steps_per_expert;
+    bool any = false;
+    for (int b = 0; b < a.B; ++b) any = any || a.ew[(size_t)b * a.ew_ld + e] != 0.f;
+    if (!any) {
+      if (a.zero) {  // (its share of the zero side job still gets done)
+        float4* z = reinterpret_cast<float4*>(a.zero);
+        for (int i = bid * (NW * 64) + threadIdx.x; i < (a.zero_n >> 2); i += nblk * (NW * 64))
+          z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      return;
+    }
+  }
   // segments (split-K Q|K|V): global tile g -> (segment, local tile)
   const int t1 = (a.n_out + 15) >> 4;
   const int t2 = SK ? t1 + (a.nseg > 1 ? (a.seg_rows[1] + 15) >> 4 : 0) : t1;
@@ -836,14 +851,34 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     const int gl = run == 0 ? grp : grp - a.nb1;
     t0 = (run == 0 ? 0 : ta) + gl * a.tpg;
     tn = max(0, min(a.tpg, (run == 0 ? ta : tiles) - t0));
-  } else {
-    t0 = grp * (tiles / G) + min(grp, tiles % G);
-    tn = tiles / G + (grp < tiles % G ? 1 : 0);
+  }
+  // MoE gate/up (the experts stacked as one SwiGLU matrix, routing weights a.ew [B][E]): only the
+  // experts some row is routed to are computed - the even split runs over their tiles alone
+  // ("active" index space: expert rank * tpe + local tile; E <= 64, one bit per expert)
+  const bool moe_sw = MOE && !SK && a.swiglu_epi && a.ew;  // (a separate instantiation)
+  const int tpe = moe_sw ? a.tiles_per_expert : 1;
+  unsigned long long act = ~0ull;
+  if (moe_sw) {
+    bool any = false;
+    if (lane < tiles / tpe)
+      for (int b = 0; b < a.B; ++b) any = any || a.ew[(size_t)b * a.ew_ld + lane] != 0.f;
+    act = __ballot(any);
+  }
+  if constexpr (!SK) {
+    const int ta = moe_sw ? (int)__popcll(act) * tpe : tiles;
+    t0 = grp * (ta / G) + min(grp, ta % G);
+    tn = ta / G + (grp < ta % G ? 1 : 0);
   }
   const int nt = wave < tn ? (tn - 1 - wave) / NW + 1 : 0;  // this wave's tiles (wave-uniform)
   const int N = nt * ns;                                    // ... as one sequence of steps
   const int SB = t16_step_bytes(QT);
-  auto tile_of = [&](int i) { return t0 + wave + i * NW; };
+  auto tile_of = [&](int i) {
+    const int ai = t0 + wave + i * NW;
+    if (!moe_sw) return ai;
+    unsigned long long m = act;  // the (ai / tpe)-th routed expert: drop the lower set bits
+    for (int r = ai / tpe; r > 0; --r) m &= m - 1;
+    return (int)__builtin_ctzll(m) * tpe + ai % tpe;
+  };
   auto tbase = [&](int i) {
     const int g = tile_of(i), sg = seg_of(g);
     const uint8_t* base = !SK || sg == 0 ? a.w.base : sg == 1 ? a.seg_base[1] : a.seg_base[2];
@@ -946,8 +981,10 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
       for (int i = 0; i < 4; ++i) up[i] = __shfl_xor(acc[i], 32);
       if (col_ok && lane < 32) {
         const int f0 = gt * 8 + 4 * kq;
-        const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0]), (_Float16)(silu(acc[2]) * up[2])};
-        const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1]), (_Float16)(silu(acc[3]) * up[3])};
+        // MoE: the row's routing weight of this tile's expert (0: not routed there)
+        const float rw = moe_sw ? a.ew[(size_t)r16 * a.ew_ld + gt / tpe] : 1.f;
+        const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
+        const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
         *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
       }
     } else if (col_ok) {
@@ -988,10 +1025,10 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
 
 // (the body reads its arguments through the kernarg segment pointer: a reference to the by-value
 // parameter made the compiler copy the whole block to scratch, as in bmm_kernel)
-template <int QT, int PD>
+template <int QT, int PD, bool MOE = false>
 __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, false>(*ka, 0, blockIdx.x, gridDim.x);
+  wt_body<QT, PD, false, 8, MOE>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1120,9 +1157,9 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   // dense SwiGLU gate/up: wave-owned tiles, 2 steps of weights in flight per wave (3: same
   // time, r3 sweep); plain split-K projections (Wo, down): the same kernel over (K part,
   // 8-tile group) blocks
-  const bool wt_sw = a.swiglu_epi && !a.ew && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
+  const bool wt_sw = a.swiglu_epi && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
                      a.B <= 8;
-  const bool wt_k = !a.swiglu_epi && !a.ew && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
+  const bool wt_k = !a.swiglu_epi && (!a.ew || a.steps_per_expert > 0) && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
                     a.nseg == 1 && a.B <= 8;
   if (wt_sw || wt_k) {
     const int cus = bmm_cus();
@@ -1130,8 +1167,17 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
       // (8 parts for the 256-tile shapes; 4 / 16 measured 7 / 13 % slower steps, r3 sweep)
       kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
+      if (a.ew) {
+        // MoE down (K = the experts' F concatenated): every part inside one expert, the parts of
+        // an unrouted expert skipped whole; parts per expert: the count nearest the dense rule
+        // whose staged slice fits the LDS and divides the expert's steps
+        const int spe = a.steps_per_expert, E = steps / spe;
+        int ppe = std::max(1, (kparts + E / 2) / E);
+        while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + 8) * 2 > 150 * 1024)) ++ppe;
+        kparts = E * ppe;
+      }
       // the staged slice (B rows x part) stays within the LDS
-      while (kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
+      while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
     }
     a.spp = (steps + kparts - 1) / kparts;
     a.kparts = kparts = (steps + a.spp - 1) / a.spp;
@@ -1140,7 +1186,8 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
     // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
     const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
-    hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
+    if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(G * kparts), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
     return;
   }
   if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");

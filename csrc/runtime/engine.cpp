@@ -1144,8 +1144,10 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     dn.w = L.t_down; dn.xh = hh_b_; dn.ldh = E * F_l_;
     dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
     dn.ew = ew_b_; dn.ew_ld = E; dn.steps_per_expert = F_l_ / 256;
+    if (sk) {  // (the wave-owned down re-zeroes the split-K Q|K|V rows as a side job)
+      dn.zero = qkv_b_; dn.zero_n = (int)qkv_b_zero_n();
+    }
     bmm(dn, s);
-    zero_qkv();
     tp_end();
     return;
   }

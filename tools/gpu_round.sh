@@ -60,8 +60,20 @@ for s in "$@"; do
                 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --parallel dp --steps 4 --warmup 1 ;;
     bstep) step bstep 300 python tools/batch_bench.py --batches 1,6,8 --steps 48 ;;
     decode) step decode 600 python tools/decode_bench.py --gen 400 ;;
-    decode70) step decode70 900 python tools/decode_bench.py --model llama3-70b-q4_k_m --gen 128 ;;
-    mixtral) step mixtral 900 python bench.py --model mixtral-8x7b-q4_k_m --steps 6 --warmup 1 ;;
+    decode70) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
+              step decode70 900 python tools/decode_bench.py --model llama3-70b-q4_k_m --steps 64 ;;
+    mixtral) step genmx 900 python tools/gen_model.py mixtral-8x7b-q4_k_m
+             step mixdec 600 python tools/decode_bench.py --model mixtral-8x7b-q4_k_m --steps 64
+             step mixtral 900 python bench.py --model mixtral-8x7b-q4_k_m --steps 2 --warmup 1 ;;
+    mixprof) export TMPDIR=/tmp; step genmx 900 python tools/gen_model.py mixtral-8x7b-q4_k_m
+             prof mixprof 300 tools/decode_bench.py --model mixtral-8x7b-q4_k_m --steps 32 --no-graph
+             python3 tools/prof_summary.py gpurun_out/mixprof/k_kernel_stats.csv > gpurun_out/mixprof_summary.md
+             prof mixbprof 300 tools/batch_bench.py --model mixtral-8x7b-q4_k_m --batches 6 --steps 16
+             python3 tools/step_kernels.py gpurun_out/mixbprof/k_kernel_trace.csv > gpurun_out/mixbprof_kernels.txt ;;
+    tp8bench70) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
+                step tp8bench70 1100 env LFK_BENCH_DEVICE=0 GPU_MAX_HW_QUEUES=1 python -m torch.distributed.run --nnodes=1 \
+                  --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --parallel tp \
+                  --model llama3-70b-q4_k_m --steps 1 --warmup 0 --serial-steps 1 ;;
     # ---- profiles
     stepprof) prof stepprof 300 tools/batch_bench.py --batches 6 --steps 32
               python3 tools/step_kernels.py gpurun_out/stepprof/k_kernel_trace.csv > gpurun_out/stepprof_kernels.txt
