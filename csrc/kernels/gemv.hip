@@ -201,7 +201,9 @@ __global__ __launch_bounds__(256) void attn_wo1_kernel(AttnWo1Args p) {
 
 bool attn_wo1(const AttnDecodeArgs& aa, const GemvArgs& wo, hipStream_t s) {
   const int G = aa.n_kv_head > 0 ? aa.n_head / aa.n_kv_head : 0;
-  if (aa.head_dim != 128 || (G != 4 && G != 8) || aa.batch != 0 || !aa.done || !aa.out || aa.out_h || aa.qkv_raw ||
+  // (G = 8, the 70B: the one launch measured 9.88 vs 9.74 ms per token for two, r4 - the G = 8
+  // attention body's registers (168) leave the Wo planes 2-3 waves per SIMD: not taken)
+  if (aa.head_dim != 128 || G != 4 || aa.batch != 0 || !aa.done || !aa.out || aa.out_h || aa.qkv_raw ||
       (wo.w.type != T_Q4_K && wo.w.type != T_Q6_K) || wo.norm_w || wo.n_slots != 1 || wo.expert_ids || wo.resid ||
       wo.debug || wo.dbg_clk || wo.w.K % 2048)
     return false;
@@ -213,19 +215,17 @@ bool attn_wo1(const AttnDecodeArgs& aa, const GemvArgs& wo, hipStream_t s) {
   AttnWo1Args p;
   p.att = aa;
   p.wo = wo;
-  // one 4-row x 64-chunk item per wave: every weight of Wo is in flight before the wait
+  // 4-row x 64-chunk items, grid-strided over at most 512 blocks (2 per CU): at d = 4096 one item
+  // per wave - every weight of Wo in flight before the wait; at d = 8192 (70B) 4 per wave, the
+  // x prologue (each block quantises all of x) amortised as the separate GEMV's grid cap does
+  // (one item per wave there cost 2048 prologues: 29.7 vs ~15 us per layer, r4 profile)
   const int items = (wo.n_out + 3) / 4 * (wo.w.K / 2048);
-  p.n_wo = (items + 3) / 4;
+  p.n_wo = std::min((items + 3) / 4, 512);
   const int splits = (aa.n_ctx + 63) / 64, per = aa.n_kv_head * splits;
   const dim3 grid(aa.n_kv_head, splits, 1 + (p.n_wo + per - 1) / per);
   const size_t lds = wo.w.K + (wo.w.K / 32) * 4 + 128;
-  if (wo.w.type == T_Q4_K) {
-    if (G == 4) hipLaunchKernelGGL((attn_wo1_kernel<T_Q4_K, 128, 4>), grid, dim3(256), lds, s, p);
-    else hipLaunchKernelGGL((attn_wo1_kernel<T_Q4_K, 128, 8>), grid, dim3(256), lds, s, p);
-  } else {
-    if (G == 4) hipLaunchKernelGGL((attn_wo1_kernel<T_Q6_K, 128, 4>), grid, dim3(256), lds, s, p);
-    else hipLaunchKernelGGL((attn_wo1_kernel<T_Q6_K, 128, 8>), grid, dim3(256), lds, s, p);
-  }
+  if (wo.w.type == T_Q4_K) hipLaunchKernelGGL((attn_wo1_kernel<T_Q4_K, 128, 4>), grid, dim3(256), lds, s, p);
+  else hipLaunchKernelGGL((attn_wo1_kernel<T_Q6_K, 128, 4>), grid, dim3(256), lds, s, p);
   return true;
 }
 

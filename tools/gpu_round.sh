@@ -73,11 +73,14 @@ for s in "$@"; do
     tp8bench70) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
                 step tp8bench70 1100 env LFK_BENCH_DEVICE=0 GPU_MAX_HW_QUEUES=1 python -m torch.distributed.run --nnodes=1 \
                   --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 8 --parallel tp \
-                  --model llama3-70b-q4_k_m --steps 1 --warmup 0 --serial-steps 1 ;;
+                  --model llama3-70b-q4_k_m --steps 1 --warmup 0 --serial-steps 1 --clients ${TP8_CLIENTS:-6} ;;
     # ---- profiles
     stepprof) prof stepprof 300 tools/batch_bench.py --batches 6 --steps 32
               python3 tools/step_kernels.py gpurun_out/stepprof/k_kernel_trace.csv > gpurun_out/stepprof_kernels.txt
               python3 tools/step_slots.py gpurun_out/stepprof/k_kernel_trace.csv >> gpurun_out/stepprof_kernels.txt ;;
+    dec70prof) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
+               prof dec70prof 400 tools/decode_bench.py --model llama3-70b-q4_k_m --steps 16 --no-graph
+               python3 tools/prof_summary.py gpurun_out/dec70prof/k_kernel_stats.csv > gpurun_out/dec70prof_summary.md ;;
     decprof) prof decprof 300 tools/decode_bench.py --steps 64 --no-graph
              python3 tools/prof_summary.py gpurun_out/decprof/k_kernel_stats.csv > gpurun_out/decprof_summary.md ;;
     prefprof) prof prefprof 300 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
