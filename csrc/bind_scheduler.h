@@ -75,6 +75,7 @@ void bind_scheduler(pybind11::module_& m) {
              d["admitted"] = s.admitted;
              d["reused_tokens"] = s.reused_tokens;
              d["joint_admissions"] = s.joint_admissions;
+             d["chunked_admissions"] = s.chunked_admissions;
              d["active"] = s.active;
              d["pending"] = s.pending;
              d["slots"] = s.slots;

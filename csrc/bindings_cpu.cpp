@@ -61,6 +61,30 @@ class FakeSlotEngine : public SlotBackend {
     cur_[slot] = next_token(kv, vocab_);
     return cur_[slot];
   }
+  // chunked admission: the prompt enters the slot's KV part by part (a reused prefix first)
+  int prefill_part_tokens() const override { return chunk_; }
+  int slot_begin_part(int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n,
+                      const SamplingOpts&) override {
+    std::lock_guard<std::mutex> g(mu_);
+    if (slot < 0 || slot >= n_slots_) throw std::runtime_error("fake: slot out of range");
+    std::vector<int>& kv = kv_[slot];
+    if (n_done == n_keep) {  // first part: the reused prefix must be resident
+      if (n_keep > (int)kv.size()) throw std::runtime_error("fake: reused prefix is not resident");
+      for (int i = 0; i < n_keep; ++i)
+        if (kv[i] != prompt[i]) throw std::runtime_error("fake: reused prefix differs");
+      kv.resize(n_keep);
+    }
+    if ((int)kv.size() != n_done) throw std::runtime_error("fake: prompt part out of order");
+    const int end = std::min((int)prompt.size(), n_done + n);
+    kv.insert(kv.end(), prompt.begin() + n_done, prompt.begin() + end);
+    prefilled_ += end - n_done;
+    ++parts_;
+    if (end < (int)prompt.size()) return -1;
+    cur_[slot] = next_token(kv, vocab_);
+    return cur_[slot];
+  }
+  void set_prefill_chunk(int n) { chunk_ = n; }
+  long long parts() { std::lock_guard<std::mutex> g(mu_); return parts_; }
   std::vector<int> batch_step(const std::vector<int>& slots) override {
     if (step_us_ > 0) std::this_thread::sleep_for(std::chrono::microseconds(step_us_));
     std::lock_guard<std::mutex> g(mu_);
@@ -105,7 +129,8 @@ class FakeSlotEngine : public SlotBackend {
   std::mutex mu_;
   std::vector<std::vector<int>> kv_;
   std::vector<int> cur_;
-  long long prefilled_ = 0, steps_ = 0, fail_at_ = 0;
+  long long prefilled_ = 0, steps_ = 0, fail_at_ = 0, parts_ = 0;
+  int chunk_ = 0;
   int max_rows_ = 0;
   bool pipeline_ = false;
   std::deque<std::vector<int>> queued_;
@@ -227,7 +252,9 @@ PYBIND11_MODULE(_cpu, m) {
       .def_property_readonly("steps", &FakeSlotEngine::steps)
       .def_property_readonly("max_rows", &FakeSlotEngine::max_rows)
       .def("fail_at", &FakeSlotEngine::fail_at)
-      .def("set_pipeline", &FakeSlotEngine::set_pipeline);
+      .def("set_pipeline", &FakeSlotEngine::set_pipeline)
+      .def("set_prefill_chunk", &FakeSlotEngine::set_prefill_chunk)
+      .def_property_readonly("parts", &FakeSlotEngine::parts);
   bind_scheduler<FakeSlotEngine>(m);
 
   // the tensor-parallel control channel (runtime/tp_channel.h), for host-side tests of its

@@ -125,6 +125,13 @@ PYBIND11_MODULE(_hip, m) {
              py::gil_scoped_release nogil;
              return e.slot_begin(slot, prompt, n_keep, o);
            })
+      .def("slot_begin_part",
+           [](Engine& e, int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n, py::dict sp) {
+             const SamplingOpts o = sampling_opts(sp);
+             py::gil_scoped_release nogil;
+             return e.slot_begin_part(slot, prompt, n_keep, n_done, n, o);
+           })
+      .def_property_readonly("prefill_part_tokens", &Engine::prefill_part_tokens)
       .def("slots_begin",
            [](Engine& e, const std::vector<int>& slots, const std::vector<std::vector<int>>& prompts,
               const std::vector<int>& n_keep, py::list sps) {

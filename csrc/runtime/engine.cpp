@@ -304,6 +304,12 @@ void Engine::alloc_buffers() {
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = e[0] != '0';  // A/B (test_engine_gpu)
+  if (hp_.n_expert > 0) {  // the split router's partials and per-row counters
+    const int rows = std::max(opt_.n_slots, 1);  // a batch step routes at most one row per slot
+    router_ws_ = (float*)dalloc(sizeof(float) * moe_router_ws_floats(rows, hp_.n_embd));
+    router_cnt_ = (int*)dalloc(sizeof(int) * rows);
+    HIPCHK(hipMemset(router_cnt_, 0, sizeof(int) * rows));
+  }
   // single-row decode: attention + Wo in one launch (attn_wo1); per-layer done counters, zeroed
   // by every decode step's embedding launch
   if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
@@ -645,7 +651,7 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   if (hp_.n_expert > 0) {
     if (moe_router_fused_ok(L.router.type, hp_.n_expert, d)) {  // one launch: norm + f32 router + top-k
       moe_router_fused(x_, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, hp_.n_expert,
-                       hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, s);
+                       hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, router_ws_, router_cnt_, s);
     } else {
       GemvArgs ra;
       ra.w = L.router; ra.x = x_; ra.norm_w = L.ffn_norm; ra.eps = hp_.rms_eps;
@@ -1127,7 +1133,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     // experts skipped): two weight streams per layer instead of a GEMM pair per expert
     const int E = hp_.n_expert;
     moe_router_rows(x_, d, B, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, E,
-                    hp_.n_expert_used, ew_b_, E, s);
+                    hp_.n_expert_used, ew_b_, E, router_ws_, router_cnt_, s);
     BmmArgs a;
     if (fnorm) {
       a.xf = x_; a.ldxf = d; a.norm_w = L.ffn_norm; a.eps = hp_.rms_eps;
@@ -1390,6 +1396,33 @@ int Engine::slot_begin(int slot, const std::vector<int>& prompt, int n_keep, con
     mirror(m);
   }
   return slot_begin_impl(slot, prompt, n_keep, sp);
+}
+
+int Engine::slot_begin_part(int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n,
+                            const SamplingOpts& sp) {
+  ExecGuard guard(this);
+  if (!bmax_ || tp_on_) throw std::runtime_error("slot_begin_part: batching engines on one GPU only");
+  if (slot < 0 || slot >= opt_.n_slots) throw std::runtime_error("slot_begin_part: slot out of range");
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  if (n_done < n_keep || n_done >= n_prompt || n < 1) throw std::runtime_error("slot_begin_part: bad part");
+  if (n_done == n_keep) {
+    (void)make_sparams(sp);
+    begin_slot_state(slot, prompt, sp);
+  }
+  const int end = std::min(n_prompt, n_done + n);
+  for (int pos = n_done; pos < end;) {
+    const int T = std::min(opt_.n_batch, end - pos);
+    prefill_chunk(slot, prompt.data() + pos, T, pos, pos + T == n_prompt);
+    pos += T;
+  }
+  if (end < n_prompt) return -1;
+  int tok = 0;
+  HIPCHK(hipMemcpy(&tok, state_ + (size_t)S_NSTATE * slot + S_TOKEN, sizeof(int), hipMemcpyDeviceToHost));
+  check_device_err();
+  return tok;
 }
 
 int Engine::slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) {

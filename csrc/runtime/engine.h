@@ -131,6 +131,11 @@ class Engine : public SlotBackend {
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
   int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
+  // chunked admission (scheduler): parts of min(n_batch, 256) tokens between decode steps of
+  // the other rows; single-GPU engines (under TP admission stays whole)
+  int prefill_part_tokens() const override { return bmax_ > 0 && !tp_on_ ? std::min(opt_.n_batch, 256) : 0; }
+  int slot_begin_part(int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n,
+                      const SamplingOpts& sp) override;
   // Admission of several requests in ONE prefill: the prompts' rows are packed into shared
   // chunks of up to n_batch rows (per-row KV slot / position for RoPE and the KV append,
   // one attention launch per prompt piece), so every weight is streamed once per chunk for
@@ -367,6 +372,8 @@ class Engine : public SlotBackend {
   int* wo_err_h_ = nullptr;   // host view
   int* wo_err_ = nullptr;     // device view
   int* dec_done_ = nullptr;   // single-row decode: [n_layer][64] done counters (attn_wo1)
+  float* router_ws_ = nullptr;  // MoE: the split router's partials (moe.hip)
+  int* router_cnt_ = nullptr;   // MoE: its per-row arrival counters (each launch leaves them at 0)
   size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16; }
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count

@@ -160,6 +160,7 @@ void BatchScheduler::loop() {
     std::vector<std::shared_ptr<Req>> req;
   };
   std::deque<Flight> flights;  // pipelined steps queued on the engine, oldest first
+  std::deque<std::shared_ptr<Req>> prefilling;  // chunked admissions in progress, oldest first
   while (true) {
     cv_work_.wait(lk, [&] {
       if (stop_ || !pending_.empty() || !flights.empty()) return true;
@@ -176,6 +177,9 @@ void BatchScheduler::loop() {
     {
       std::vector<std::shared_ptr<Req>> adm;
       std::vector<int> a_slot, a_keep;
+      const int chunk = eng_.prefill_part_tokens();
+      bool decoding = false;
+      for (int s = first_slot_; s < n_slots_; ++s) decoding = decoding || (slot_req_[s] && slot_req_[s]->n_done < 0);
       while (!pending_.empty()) {
         std::shared_ptr<Req> r = pending_.front();
         if (r->cancel) {
@@ -191,9 +195,18 @@ void BatchScheduler::loop() {
         slot_req_[slot] = r;
         slot_used_[slot] = ++tick_;
         r->t_start = sched_now();
+        const int keep = std::min(lcp, (int)r->prompt.size() - 1);
+        // chunked admission: a prompt longer than one chunk, while rows are decoding, is
+        // prefilled in parts between their steps (below) instead of stalling them for all of it
+        if (chunk > 0 && decoding && (int)r->prompt.size() - keep > chunk) {
+          r->n_keep = keep;
+          r->n_done = keep;
+          prefilling.push_back(r);
+          continue;
+        }
         adm.push_back(r);
         a_slot.push_back(slot);
-        a_keep.push_back(std::min(lcp, (int)r->prompt.size() - 1));
+        a_keep.push_back(keep);
       }
       if (!adm.empty()) {
         std::vector<std::vector<int>> prompts;
@@ -232,6 +245,48 @@ void BatchScheduler::loop() {
         cv_out_.notify_all();  // the first tokens reach their waiters now, not after the next step
       }
     }
+    // 2b. one part of the oldest chunked admission (a part is one prefill pass; the rows
+    //     that decode get their next step right after it)
+    if (!prefilling.empty()) {
+      std::shared_ptr<Req> r = prefilling.front();
+      if (r->cancel || r->done) {
+        prefilling.pop_front();
+      } else {
+        const int n = eng_.prefill_part_tokens();
+        const int done = r->n_done;
+        const int slot = r->slot, keep = r->n_keep;
+        std::vector<int> prompt = r->prompt;
+        SamplingOpts sp = r->sp;
+        std::string err;
+        int tok = -1;
+        lk.unlock();
+        try {
+          tok = eng_.slot_begin_part(slot, prompt, keep, done, n, sp);
+        } catch (const std::exception& e) {
+          err = e.what();
+        }
+        lk.lock();
+        if (!err.empty()) {
+          prefilling.pop_front();
+          slot_hist_[slot].clear();
+          r->error = err;
+          finish(*r, "error");
+        } else if (tok < 0) {
+          r->n_done = std::min((int)prompt.size(), done + n);
+        } else {
+          prefilling.pop_front();
+          r->n_done = -1;
+          r->t_first = sched_now();
+          ++st_.admitted;
+          ++st_.chunked_admissions;
+          st_.reused_tokens += keep;
+          r->n_prefilled = (int)prompt.size() - keep;
+          slot_hist_[slot] = prompt;
+          push_token(*r, tok);
+          cv_out_.notify_all();
+        }
+      }
+    }
     // 3. one decode step over every active row. Pipelined (engines that can): the step of
     //    the current rows is queued and, while nothing waits for admission and the rows are
     //    those of the step already in flight, the NEXT step is queued too before the host
@@ -241,7 +296,7 @@ void BatchScheduler::loop() {
     rows.clear();
     row_req.clear();
     for (int s = first_slot_; s < n_slots_; ++s)
-      if (slot_req_[s]) {
+      if (slot_req_[s] && slot_req_[s]->n_done < 0) {  // (a slot still prefilling has no row yet)
         rows.push_back(s);
         row_req.push_back(slot_req_[s]);
       }

@@ -51,6 +51,7 @@ struct SchedStats {
   long long admitted = 0;
   long long reused_tokens = 0;  // prompt tokens served from a slot's resident KV prefix
   long long joint_admissions = 0;  // admissions that prefilled several prompts in one pass
+  long long chunked_admissions = 0;  // prompts prefilled in parts between decode steps
   int active = 0, pending = 0, slots = 0;
 };
 
@@ -83,6 +84,8 @@ class BatchScheduler {
     std::vector<int> tokens;
     int slot = -1;
     int n_prefilled = 0;
+    int n_keep = 0;
+    int n_done = -1;   // chunked admission: prompt tokens prefilled so far (-1: not prefilling)
     bool cancel = false, done = false;
     std::string finish, error;
     double t_submit = 0, t_start = 0, t_first = 0, t_done = 0;

@@ -42,6 +42,17 @@ class SlotBackend {
   // from the tokens its predecessor sampled on the device, so the scheduler can queue step
   // k + 1 before it has handled step k's tokens. At most two steps in flight.
   virtual bool can_pipeline() const { return false; }
+  // Chunked admission (optional; prefill_part_tokens() > 0 enables it): slot_begin in parts, so a
+  // long prompt arriving while other rows decode does not stall them for its whole prefill.
+  // slot_begin_part prefills prompt[n_done, n_done + n) into `slot` (the first call, with
+  // n_done == n_keep, also sets the slot's state) and returns the first token once the prompt
+  // is complete, -1 before. Decode steps of OTHER slots may run between the parts.
+  virtual int prefill_part_tokens() const { return 0; }
+  virtual int slot_begin_part(int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n,
+                              const SamplingOpts& sp) {
+    (void)n_done; (void)n;
+    return slot_begin(slot, prompt, n_keep, sp);
+  }
   virtual void batch_launch(const std::vector<int>& slots) { (void)slots; }
   virtual std::vector<int> batch_collect() { return {}; }
 };

@@ -239,6 +239,40 @@ def test_slot_begin_while_steps_in_flight(models, joint):
     assert run(True) == run(False)
 
 
+def test_chunked_admission_equals_whole(models):
+    """slot_begin_part (the scheduler's chunked admission: prompt parts between other rows'
+    decode steps) gives the same first token and the same following batched rows as slot_begin,
+    with a batch step of another slot between every two parts and a reused prefix."""
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-llama3-q4_k_m"]
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    rng = np.random.default_rng(21)
+    other = [int(t) for t in rng.integers(3, 300, 10)]
+    base = [int(t) for t in rng.integers(3, 300, 12)]
+    long_p = base + [int(t) for t in rng.integers(3, 300, 75)]
+
+    def run(chunked):
+        eng = load_hip().Engine(path, n_ctx=256, n_batch=32, device=0, use_graph=True, n_slots=4)
+        assert eng.prefill_part_tokens > 0
+        eng.slot_begin(1, other, 0, greedy)
+        eng.slot_begin(2, base, 0, greedy)              # slot 2 holds `base`: reused below
+        out = []
+        if chunked:
+            done, first = len(base), -1
+            while first < 0:
+                first = eng.slot_begin_part(2, long_p, len(base), done, 20, greedy)
+                done = min(len(long_p), done + 20)
+                out.append(list(eng.batch_step([1])))   # the other row decodes in between
+        else:
+            first = eng.slot_begin(2, long_p, len(base), greedy)
+            for _ in range(4):                          # (20-token parts of 75: 4 parts)
+                out.append(list(eng.batch_step([1])))
+        out += [list(eng.batch_step([1, 2])) for _ in range(3)]
+        assert eng.healthy, eng.last_error
+        return first, out
+    assert run(True) == run(False)
+
+
 def test_batch_step_six_rows_d8192(tmp_path):
     """Six rows at d = 8192: the split-K Q|K|V beside the FFN path that does not stage a whole row
     (its projections' inputs prepared by bprep), which must re-zero the split-K rows itself -

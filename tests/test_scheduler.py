@@ -179,3 +179,52 @@ def test_requests_queued_together_are_admitted_together():
     st = sched.stats()
     assert st["joint_admissions"] >= 1 and st["admitted"] == 4
     sched.shutdown()
+
+
+def test_long_prompt_admitted_in_parts_between_decode_steps():
+    """Chunked admission: a prompt longer than the engine's prefill chunk that arrives while
+    rows decode is prefilled part by part between their steps (the rows keep stepping while it
+    loads), and its tokens - like the decoding rows' - equal the sequential runs; a prompt
+    arriving on an idle engine is admitted whole; a reused prefix is not prefilled again."""
+    eng, sched = make(n_slots=4, max_batch=3, n_ctx=256, step_us=1000)
+    eng.set_prefill_chunk(16)
+    first_p = [3, 1, 4, 1, 5]
+    first = sched.submit(first_p, 60, {}, [])
+    time.sleep(0.02)                       # `first` is decoding now
+    steps0 = eng.steps
+    long_p = list(range(100, 170))         # 70 tokens: 5 parts of 16
+    rid = sched.submit(long_p, 8, {}, [])
+    toks, r = run(sched, rid)
+    assert toks == sequential(long_p, 8, 256) and r["n_prefilled"] == len(long_p)
+    assert eng.parts >= 5
+    assert eng.steps - steps0 >= 4         # the decoding row stepped while the prompt loaded
+    ftoks, _ = run(sched, first)
+    assert ftoks == sequential(first_p, 60, 256)
+    st = sched.stats()
+    assert st["chunked_admissions"] == 1 and st["admitted"] == 2
+    # the follow-up turn on the now idle engine reuses the long prompt's resident prefix
+    p2 = long_p + toks[:-1] + [toks[-1], 9, 9]
+    t2, r2 = run(sched, sched.submit(p2, 4, {}, []))
+    assert t2 == sequential(p2, 4, 256)
+    assert r2["n_prefilled"] == len(p2) - (len(long_p) + len(toks) - 1)
+    sched.shutdown()
+
+
+def test_cancel_while_prefilling_in_parts():
+    eng, sched = make(n_slots=4, max_batch=3, n_ctx=512, step_us=2000)
+    eng.set_prefill_chunk(8)
+    first = sched.submit([1, 2], 200, {}, [])
+    time.sleep(0.02)
+    rid = sched.submit(list(range(10, 300)), 5, {}, [])   # 37 parts
+    time.sleep(0.01)
+    sched.cancel(rid)
+    r = sched.wait(rid, 0, 5000)
+    while not r["done"]:
+        r = sched.wait(rid, 0, 5000)
+    assert r["finish"] == "cancelled"
+    # the slot is free again: another long request is admitted and completes
+    p = list(range(400, 440))
+    toks, _ = run(sched, sched.submit(p, 6, {}, []))
+    assert toks == sequential(p, 6, 512)
+    sched.cancel(first)
+    sched.shutdown()
