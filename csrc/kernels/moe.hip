@@ -115,85 +115,57 @@ void moe_scatter_add(float* acc, const float* y, const int* pos, const float* gw
 
 // ------------------------------------------------------------------ decode: fused router
 // logits = W_r (F32 [E][d]) . (RMSNorm(x) * w_norm), softmax over E, top-k, renormalise.
-// Split over d: grid (d / 256 slices, rows), one wave per block, each lane one float4 of x, of
-// w_norm and of the E router rows - every load of the launch in flight at once; each block
-// leaves its partial dots and sum of squares (sc1 stores) and adds to the row's counter, and the
-// last-arriving block of the row sums the partials in slice order (deterministic), then softmax
-// + top-k. (One 1024-thread block per row read the whole 144 KB of x + router rows through one
-// CU: 7.5 us per layer, r4 Mixtral profile.) The router stays in f32 end to end.
+// One block of 1024 threads: replaces the router GEMV launch + the routing launch
+// (two kernel boundaries per MoE layer). The router stays in f32 end to end.
 static constexpr int kRouterMaxE = 16;
-static constexpr int kRouterSlice = 256;  // floats of d per block
 
-__device__ __forceinline__ void st_sc1f(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1f(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// (batched rows: row b = blockIdx.y routes x + b * ldx and writes the dense weight row
+// (batched rows: block b routes row b - x + b * ldx - and writes the dense weight row
 // wd + b * ld_dense instead of ids / wout)
 template <int EM>
-__global__ __launch_bounds__(64) void moe_router_fused_kernel(const float* __restrict__ x, const float* __restrict__ nw,
-                                                              float eps, const float* __restrict__ W, int d, int E,
-                                                              int k, float* logits, int* ids, float* wout, int ldx,
-                                                              float* wd, int ld_dense, float* ws, int* cnt) {
-  const int j = blockIdx.x, NB = gridDim.x, b = blockIdx.y, lane = threadIdx.x;
-  x += (size_t)b * ldx;
-  const int i = (j * 64 + lane) * 4;
+__global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __restrict__ x, const float* __restrict__ nw,
+                                                                float eps, const float* __restrict__ W, int d, int E,
+                                                                int k, float* logits, int* ids, float* wout, int ldx,
+                                                                float* wd, int ld_dense) {
+  __shared__ float red[16][EM + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  x += (size_t)blockIdx.x * ldx;
   float ss = 0.f, acc[EM];
 #pragma unroll
   for (int e = 0; e < EM; ++e) acc[e] = 0.f;
-  if (i < d) {
+  for (int i = tid * 4; i < d; i += 4096) {
     const float4 xv = *reinterpret_cast<const float4*>(x + i);
     const float4 wv = *reinterpret_cast<const float4*>(nw + i);
-    // every row load unconditional (clamped row, result masked): a load under a runtime
-    // `e < E` branch makes hipcc drain vmcnt per row (E dependent round trips)
+    ss += xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
+    const float4 n = make_float4(xv.x * wv.x, xv.y * wv.y, xv.z * wv.z, xv.w * wv.w);
+    // every row load unconditional (clamped row, result masked): a load under a
+    // runtime `e < E` branch makes hipcc drain vmcnt per row (E dependent round trips)
     float4 r[EM];
 #pragma unroll
     for (int e = 0; e < EM; ++e) r[e] = *reinterpret_cast<const float4*>(W + (size_t)min(e, E - 1) * d + i);
-    ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
-    const float4 n = make_float4(xv.x * wv.x, xv.y * wv.y, xv.z * wv.z, xv.w * wv.w);
 #pragma unroll
-    for (int e = 0; e < EM; ++e) acc[e] = e < E ? n.x * r[e].x + n.y * r[e].y + n.z * r[e].z + n.w * r[e].w : 0.f;
+    for (int e = 0; e < EM; ++e)
+      acc[e] += e < E ? n.x * r[e].x + n.y * r[e].y + n.z * r[e].z + n.w * r[e].w : 0.f;
   }
   ss = wave_sum_fast(ss);
 #pragma unroll
-  for (int e = 0; e < EM; ++e) acc[e] = wave_sum_fast(acc[e]);
-  float* part = ws + ((size_t)b * NB + j) * (EM + 1);
-  int last = 1;
-  if (NB > 1) {
-    if (lane == 0) {
+  for (int e = 0; e < EM; ++e) acc[e] = e < E ? wave_sum_fast(acc[e]) : 0.f;
+  if (lane == 0) {
+    red[wave][EM] = ss;
 #pragma unroll
-      for (int e = 0; e < EM; ++e) st_sc1f(part + e, acc[e]);
-      st_sc1f(part + EM, ss);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial is out before the add
-    if (lane == 0) {
-      const int prev = __hip_atomic_fetch_add(cnt + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == NB - 1;
-      if (last) __hip_atomic_store(cnt + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last = __shfl(last, 0);
-    if (!last) return;
-    // the row's partials in slice order: lane e < E its expert, every lane the sum of squares
-    float tot = 0.f, sum = 0.f;
-    const float* p0 = ws + (size_t)b * NB * (EM + 1);
-    for (int jj = 0; jj < NB; ++jj) {
-      tot += ld_sc1f(p0 + (size_t)jj * (EM + 1) + EM);
-      if (lane < E) sum += ld_sc1f(p0 + (size_t)jj * (EM + 1) + lane);
-    }
-    ss = tot;
-#pragma unroll
-    for (int e = 0; e < EM; ++e) acc[e] = __shfl(sum, e);
+    for (int e = 0; e < EM; ++e) red[wave][e] = acc[e];
   }
-  const float sc = rsqrtf(ss / (float)d + eps);
+  __syncthreads();
+  if (wave != 0) return;
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) tot += red[w][EM];
+  const float sc = rsqrtf(tot / (float)d + eps);
   float v = -INFINITY;
   if (lane < E) {
-    float a = 0.f;
+    float sum = 0.f;
 #pragma unroll
-    for (int e = 0; e < EM; ++e) a = lane == e ? acc[e] : a;
-    v = a * sc;
+    for (int w = 0; w < 16; ++w) sum += red[w][lane];
+    v = sum * sc;
     if (logits) logits[lane] = v;
   }
   // softmax + top-k (lowest index on ties) + renormalise: as moe_route_kernel
@@ -202,7 +174,7 @@ __global__ __launch_bounds__(64) void moe_router_fused_kernel(const float* __res
   p /= wave_sum(p);
   float taken = lane < E ? p : -1.f, sel_sum = 0.f, my_w = 0.f;
   int my_id = 0;
-  for (int jj = 0; jj < k; ++jj) {
+  for (int j = 0; j < k; ++j) {
     float best = taken;
     int bi = lane;
     for (int o = 32; o > 0; o >>= 1) {
@@ -210,17 +182,17 @@ __global__ __launch_bounds__(64) void moe_router_fused_kernel(const float* __res
       const int oi = __shfl_xor(bi, o);
       if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     }
-    if (lane == jj) { my_id = bi; my_w = best; }
+    if (lane == j) { my_id = bi; my_w = best; }
     sel_sum += best;
     if (lane == bi) taken = -1.f;
   }
   if (wd) {
     // dense row: lane e < E finds its own weight among the k picks (lanes 0..k-1 hold them)
-    float* row = wd + (size_t)b * ld_dense;
+    float* row = wd + (size_t)blockIdx.x * ld_dense;
     float mine = 0.f;
-    for (int jj = 0; jj < k; ++jj) {
-      const int id = __shfl(my_id, jj);
-      const float w = __shfl(my_w, jj);
+    for (int j = 0; j < k; ++j) {
+      const int id = __shfl(my_id, j);
+      const float w = __shfl(my_w, j);
       if (id == lane) mine = w / sel_sum;
     }
     if (lane < E) row[lane] = mine;
@@ -236,32 +208,26 @@ bool moe_router_fused_ok(int router_type, int E, int d) {
   return router_type == T_F32 && E <= kRouterMaxE && E >= 1 && d % 4 == 0;
 }
 
-size_t moe_router_ws_floats(int rows, int d) {
-  return (size_t)std::max(rows, 1) * ((d + kRouterSlice - 1) / kRouterSlice) * (kRouterMaxE + 1);
-}
-
-static void launch_router(const float* x, int ldx, int B, const float* nw, float eps, const float* W, int d, int E, int k,
-                          float* logits, int* ids, float* w, float* wd, int ld, float* ws, int* cnt, hipStream_t s) {
-  if (!ws || !cnt) throw std::runtime_error("moe router: workspace missing");
-  const dim3 grid((d + kRouterSlice - 1) / kRouterSlice, B);
-  if (E <= 8)  // rows padded to EM are loaded (clamped) and masked: size EM to the expert count
-    hipLaunchKernelGGL(moe_router_fused_kernel<8>, grid, dim3(64), 0, s, x, nw, eps, W, d, E, k, logits, ids, w, ldx,
-                       wd, ld, ws, cnt);
-  else
-    hipLaunchKernelGGL(moe_router_fused_kernel<16>, grid, dim3(64), 0, s, x, nw, eps, W, d, E, k, logits, ids, w, ldx,
-                       wd, ld, ws, cnt);
-}
-
 void moe_router_fused(const float* x, const float* nw, float eps, const float* W, int d, int E, int k, float* logits,
-                      int* ids, float* w, float* ws, int* cnt, hipStream_t s) {
+                      int* ids, float* w, hipStream_t s) {
   if (E > kRouterMaxE || k > E || d % 4) throw std::runtime_error("moe_router_fused: unsupported shape");
-  launch_router(x, 0, 1, nw, eps, W, d, E, k, logits, ids, w, nullptr, 0, ws, cnt, s);
+  if (E <= 8)  // rows padded to EM are loaded (clamped) and masked: size EM to the expert count
+    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w,
+                       0, nullptr, 0);
+  else
+    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(1), dim3(1024), 0, s, x, nw, eps, W, d, E, k, logits, ids, w,
+                       0, nullptr, 0);
 }
 
 void moe_router_rows(const float* x, int ldx, int B, const float* nw, float eps, const float* W, int d, int E, int k,
-                     float* wd, int ld, float* ws, int* cnt, hipStream_t s) {
+                     float* wd, int ld, hipStream_t s) {
   if (E > kRouterMaxE || k > E || d % 4 || B < 1 || ld < E || ldx % 4) throw std::runtime_error("moe_router_rows: unsupported shape");
-  launch_router(x, ldx, B, nw, eps, W, d, E, k, nullptr, nullptr, nullptr, wd, ld, ws, cnt, s);
+  if (E <= 8)
+    hipLaunchKernelGGL(moe_router_fused_kernel<8>, dim3(B), dim3(1024), 0, s, x, nw, eps, W, d, E, k, nullptr, nullptr,
+                       nullptr, ldx, wd, ld);
+  else
+    hipLaunchKernelGGL(moe_router_fused_kernel<16>, dim3(B), dim3(1024), 0, s, x, nw, eps, W, d, E, k, nullptr, nullptr,
+                       nullptr, ldx, wd, ld);
 }
 
 // ------------------------------------------------------------------ decode: grouped down, split-K

@@ -304,12 +304,6 @@ void Engine::alloc_buffers() {
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
   if (const char* e = std::getenv("LFK_ATTN_TOUCH")) attn_touch_ = e[0] != '0';  // A/B (test_engine_gpu)
-  if (hp_.n_expert > 0) {  // the split router's partials and per-row counters
-    const int rows = std::max(opt_.n_slots, 1);  // a batch step routes at most one row per slot
-    router_ws_ = (float*)dalloc(sizeof(float) * moe_router_ws_floats(rows, hp_.n_embd));
-    router_cnt_ = (int*)dalloc(sizeof(int) * rows);
-    HIPCHK(hipMemset(router_cnt_, 0, sizeof(int) * rows));
-  }
   // single-row decode: attention + Wo in one launch (attn_wo1); per-layer done counters, zeroed
   // by every decode step's embedding launch
   if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
@@ -651,7 +645,7 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   if (hp_.n_expert > 0) {
     if (moe_router_fused_ok(L.router.type, hp_.n_expert, d)) {  // one launch: norm + f32 router + top-k
       moe_router_fused(x_, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, hp_.n_expert,
-                       hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, router_ws_, router_cnt_, s);
+                       hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, s);
     } else {
       GemvArgs ra;
       ra.w = L.router; ra.x = x_; ra.norm_w = L.ffn_norm; ra.eps = hp_.rms_eps;
@@ -1133,7 +1127,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     // experts skipped): two weight streams per layer instead of a GEMM pair per expert
     const int E = hp_.n_expert;
     moe_router_rows(x_, d, B, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, E,
-                    hp_.n_expert_used, ew_b_, E, router_ws_, router_cnt_, s);
+                    hp_.n_expert_used, ew_b_, E, s);
     BmmArgs a;
     if (fnorm) {
       a.xf = x_; a.ldxf = d; a.norm_w = L.ffn_norm; a.eps = hp_.rms_eps;

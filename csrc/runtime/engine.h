@@ -372,8 +372,6 @@ class Engine : public SlotBackend {
   int* wo_err_h_ = nullptr;   // host view
   int* wo_err_ = nullptr;     // device view
   int* dec_done_ = nullptr;   // single-row decode: [n_layer][64] done counters (attn_wo1)
-  float* router_ws_ = nullptr;  // MoE: the split router's partials (moe.hip)
-  int* router_cnt_ = nullptr;   // MoE: its per-row arrival counters (each launch leaves them at 0)
   size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16; }
 
   std::vector<hipGraphExec_t> bgraph_;  // captured batch steps, one per row count
