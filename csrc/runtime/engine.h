@@ -131,9 +131,13 @@ class Engine : public SlotBackend {
   // Prefill prompt[n_keep:] into `slot` (positions [0, n_keep) of the slot are reused),
   // set the slot's sampling state and sample its first token (synchronous).
   int slot_begin(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp) override;
-  // chunked admission (scheduler): parts of min(n_batch, 256) tokens between decode steps of
-  // the other rows; single-GPU engines (under TP admission stays whole)
-  int prefill_part_tokens() const override { return bmax_ > 0 && !tp_on_ ? std::min(opt_.n_batch, 256) : 0; }
+  // chunked admission (scheduler): parts of 1024 tokens between decode steps of the other rows;
+  // single-GPU engines (under TP admission stays whole). Parts of 256 hurt the 6-client bench
+  // (decode 438 -> 418 tok/s per request, p50 1.51 -> 1.57 s): its ~390-token prompts arriving
+  // a few ms apart lost the joint admission (one weight pass for all of them) to 2-part
+  // admissions each; 1024-token parts leave prompts below that whole and bound the stall a
+  // long-context prompt imposes on the decoding rows to ~20 ms per part (8B).
+  int prefill_part_tokens() const override { return bmax_ > 0 && !tp_on_ ? 1024 : 0; }
   int slot_begin_part(int slot, const std::vector<int>& prompt, int n_keep, int n_done, int n,
                       const SamplingOpts& sp) override;
   // Admission of several requests in ONE prefill: the prompts' rows are packed into shared
