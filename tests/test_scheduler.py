@@ -190,7 +190,8 @@ def test_long_prompt_admitted_in_parts_between_decode_steps():
     eng.set_prefill_chunk(16)
     first_p = [3, 1, 4, 1, 5]
     first = sched.submit(first_p, 60, {}, [])
-    time.sleep(0.02)                       # `first` is decoding now
+    got = sched.wait(first, 0, 5000)       # `first` is decoding now (its first token is out)
+    assert got["tokens"] and not got["done"]
     steps0 = eng.steps
     long_p = list(range(100, 170))         # 70 tokens: 5 parts of 16
     rid = sched.submit(long_p, 8, {}, [])
@@ -214,7 +215,7 @@ def test_cancel_while_prefilling_in_parts():
     eng, sched = make(n_slots=4, max_batch=3, n_ctx=512, step_us=2000)
     eng.set_prefill_chunk(8)
     first = sched.submit([1, 2], 200, {}, [])
-    time.sleep(0.02)
+    assert sched.wait(first, 0, 5000)["tokens"]           # decoding
     rid = sched.submit(list(range(10, 300)), 5, {}, [])   # 37 parts
     time.sleep(0.01)
     sched.cancel(rid)
