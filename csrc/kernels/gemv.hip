@@ -35,6 +35,55 @@ namespace lfk {
 // after the x loads and BEFORE the prologue waits for x, so the weight stream
 // starts at block entry; with one block per CU no other block's weight stream
 // sits in front of this CU's x loads (in-order returns per CU).
+// TP epilogue all-reduce of one output row (GemvArgs::tp_*): this rank's partial goes to every
+// rank as a {value, epoch} granule, then the row's granules of every rank are read back from this
+// rank's own area until they carry this launch's epoch and summed in rank order (bit-identical
+// ranks). The epoch is per ROW (every launch writes every row exactly once on every rank, whatever
+// the item shape of the launch), so a granule of an older launch is never taken for a newer one;
+// a rank rewrites parity e & 1 of a row at epoch e + 2 only after it received every peer's
+// granule of that row at e + 1, i.e. after the peer's launch e (its reads of parity e & 1) ended.
+__device__ __forceinline__ void tp_store_row(const GemvArgs& a, int row, float v) {
+  typedef unsigned long long u64;
+  const int W = a.tp_world, R = a.tp_rank;
+  const unsigned e = (unsigned)(a.tp_epochs[row] + 1);
+  a.tp_epochs[row] = (int)e;  // lane-private word
+  const size_t par = e & 1;
+  const u64 g = ((u64)e << 32) | __float_as_uint(v);
+#pragma unroll
+  for (int p = 0; p < kP2PMaxRanks; ++p)
+    if (p < W)
+      __hip_atomic_store(reinterpret_cast<u64*>(a.tp_peers.data[p]) + (par * W + R) * a.tp_stride + a.tp_off + row, g,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const u64* mine = reinterpret_cast<const u64*>(a.tp_peers.data[R]) + par * W * a.tp_stride + a.tp_off + row;
+  float val[kP2PMaxRanks];
+  unsigned pending = (1u << W) - 1;
+  const long long t0 = wall_clock64();
+  for (int spins = 0; pending; ++spins) {
+#pragma unroll
+    for (int p = 0; p < kP2PMaxRanks; ++p) {
+      if (p < W && (pending >> p & 1)) {
+        const u64 x = __hip_atomic_load(const_cast<u64*>(mine + (size_t)p * a.tp_stride), __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((unsigned)(x >> 32) == e) {
+          val[p] = __uint_as_float((unsigned)x);
+          pending &= ~(1u << p);
+        }
+      }
+    }
+    if (!pending) break;
+    if ((spins & 255) == 255 && wall_clock64() - t0 > 2000000000LL) {  // 20 s (100 MHz clock)
+      __hip_atomic_store(a.tp_err, 300 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int p = 0; p < kP2PMaxRanks; ++p)
+    if (p < W) sum += val[p];
+  a.out[row] = (a.resid ? a.resid[row] : 0.f) + sum;
+}
+
 // WAIT (SPLITK, not EARLY; attn_wo1): the first item's weights go out first, then the block waits
 // for the in-flight producer of x (GemvArgs::wait) and loads x with sc1 loads.
 // (bid, nblk): the block's index and count in the GEMV's grid (a plane of attn_wo1's grid).
@@ -145,6 +194,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
     if constexpr (EPI == EPI_SWIGLU) {
       const float u = __shfl(v, (lane + NF) & 63);      // up row NF + r sits in lane NF + r
       if (lane < NF && cf + lane < a.n_out) a.out[(size_t)cs * a.out_slot_stride + cf + lane] = silu(v) * u;
+    } else if (EPI == EPI_STORE && !SPLITK && a.tp_world > 0) {
+      if (lane < NF && cf + lane < a.n_out) tp_store_row(a, cf + lane, v);
     } else if (lane < NF && cf + lane < a.n_out) {
       float* o = a.out + (size_t)cs * a.out_slot_stride + cf + lane;
       if constexpr (EPI == EPI_STORE) *o = a.resid ? v + a.resid[cf + lane] : v;
@@ -266,10 +317,10 @@ static int resident_blocks(F kern, size_t lds, int block = 256) {
   return r;
 }
 template <typename F>
-static dim3 gemv_grid(F kern, size_t lds, int items, int block = 256) {
+static dim3 gemv_grid(F kern, size_t lds, int items, int block = 256, int div = 1) {
   const int wpb = block / 64;
   const int want = std::max(1, (items + wpb - 1) / wpb);
-  return dim3(std::min(want, resident_blocks(kern, lds, block)));
+  return dim3(std::min(want, std::max(1, resident_blocks(kern, lds, block) / std::max(1, div))));
 }
 
 // (rows per item, passes per load group) for a weight type and shape.
@@ -358,20 +409,20 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
       if constexpr (NR * U <= 4) {
         if (a.norm_w) {
           auto k = gemv_kernel<QT, EPI, NR, U, true, 1024>;
-          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024, a.grid_div), dim3(1024), lds, s, a);
         } else {
           auto k = gemv_kernel<QT, EPI, NR, U, false, 1024>;
-          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024), dim3(1024), lds, s, a);
+          hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 1024, a.grid_div), dim3(1024), lds, s, a);
         }
       } else {
         throw std::runtime_error("gemv: K > 4096 needs rows*passes <= 4");
       }
     } else if (a.norm_w) {
       auto k = gemv_kernel<QT, EPI, NR, U, true, 256>;
-      hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+      hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 256, a.grid_div), dim3(256), lds, s, a);
     } else {
       auto k = gemv_kernel<QT, EPI, NR, U, false, 256>;
-      hipLaunchKernelGGL(k, gemv_grid(k, lds, items), dim3(256), lds, s, a);
+      hipLaunchKernelGGL(k, gemv_grid(k, lds, items, 256, a.grid_div), dim3(256), lds, s, a);
     }
   }
 }

@@ -44,6 +44,14 @@ enum GemvEpi : int {
   EPI_SWIGLU = 2,  // out[f] = silu(acc_gate)*acc_up ; W = gate/up interleaved in 32-row groups
 };
 
+// peer receive regions of the tensor-parallel collectives (p2p_allreduce.hip, runtime/p2p.cpp)
+static constexpr int kP2PMaxRanks = 8;
+static constexpr int kP2PMaxBlocks = 64;
+struct P2PPeers {
+  float* data[kP2PMaxRanks] = {};
+  int* flags[kP2PMaxRanks] = {};
+};
+
 struct GemvArgs {
   QMat w;
   const float* x = nullptr;       // [K] f32 activation
@@ -63,6 +71,18 @@ struct GemvArgs {
   const int* wait = nullptr;
   int wait_cnt = 0, wait_n = 0;
   int* wait_err = nullptr;
+  // tensor-parallel all-reduce in the epilogue (EPI_STORE, the row-parallel Wo / down of a TP
+  // decode step): each item's rows go to every rank as {value, epoch} granules (the fused area
+  // of the P2P regions: tp_peers, granule tp_off + row of slot (parity, rank), tp_stride per
+  // slot), the item waits for its rows from every rank and writes out[row] = resid[row] + the
+  // rank-order sum. tp_epochs: one word per item (local, zero-initialised).
+  P2PPeers tp_peers;
+  int tp_world = 0, tp_rank = 0, tp_stride = 0, tp_off = 0;
+  int* tp_epochs = nullptr;
+  int* tp_err = nullptr;
+  // grid cap: 1/grid_div of the resident blocks (TP ranks sharing one GPU: every rank's grid of
+  // a waiting epilogue must be resident at once)
+  int grid_div = 1;
 };
 void gemv(const GemvArgs& a, int epi, hipStream_t s);
 
@@ -229,17 +249,12 @@ void moe_route(const float* logits, int n_expert, int k, int* ids, float* w, hip
 // u32 epoch} (max_n elements + one heartbeat per block; the `data` pointers address the region
 // as floats, two per granule), then an unused flag area.
 // Every launch runs exactly kP2PMaxBlocks blocks (the slot-reuse argument needs it).
-static constexpr int kP2PMaxRanks = 8;
-static constexpr int kP2PMaxBlocks = 64;
-struct P2PPeers {
-  float* data[kP2PMaxRanks] = {};
-  int* flags[kP2PMaxRanks] = {};
-};
 struct P2PArgs {
   P2PPeers peers;                  // every rank's region as mapped in THIS process (own one included)
   const float* src = nullptr;      // [n] this rank's buffer
   float* dst = nullptr;            // all-reduce: [n] the sum; all-gather: [world][n]
   int n = 0, max_n = 0, rank = 0, world = 1;
+  int stride = 0;                  // granules per (slot, rank): max_n + kP2PMaxBlocks (+ the fused area)
   int gather = 0;                  // 0: all-reduce (sum), 1: all-gather
   int* epochs = nullptr;           // [kP2PMaxBlocks] local, zero-initialised, advanced per launch
   int* err = nullptr;              // set on a timed-out wait

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
   __syncthreads();
   const unsigned ep = s_ep;
   const int slot = ep & 1;
-  const size_t M = (size_t)a.max_n + kP2PMaxBlocks;  // granules per (slot, rank): data + heartbeats
+  const size_t M = (size_t)a.stride;                   // granules per (slot, rank): data + heartbeats (+ fused)
   const int hb = a.max_n + b;                          // this block's heartbeat granule
   // 1. push this rank's chunk into slot [slot][R] of every rank (self included), then the block's
   //    heartbeat (last, so that a peer seeing it mostly finds the data there too)
@@ -141,6 +141,7 @@ void p2p_collective(const P2PArgs& a, hipStream_t s) {
   if (a.world < 1 || a.world > kP2PMaxRanks) throw std::runtime_error("p2p: world must be 1..8");
   if (a.n <= 0) return;
   if (a.n > a.max_n) throw std::runtime_error("p2p: message larger than the slot");
+  if (a.stride < a.max_n + kP2PMaxBlocks) throw std::runtime_error("p2p: slot stride");
   hipLaunchKernelGGL(p2p_collective_kernel, dim3(kP2PMaxBlocks), dim3(256), 0, s, a);
 }
 

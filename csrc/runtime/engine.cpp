@@ -522,7 +522,8 @@ void Engine::build_rope() {
 std::string Engine::p2p_handle() {
   if (opt_.tp_size < 2) throw std::runtime_error("p2p: tensor parallelism is off");
   if (opt_.comm == "rccl") throw std::runtime_error("p2p: comm=rccl has no P2P path");
-  if (!p2p_) p2p_ = std::make_unique<P2PComm>(opt_.tp_rank, opt_.tp_size, p2p_max_n_, opt_.device);
+  // (+ the fused area of d granules: the decode GEMVs' epilogue all-reduce, tp_epilogue())
+  if (!p2p_) p2p_ = std::make_unique<P2PComm>(opt_.tp_rank, opt_.tp_size, p2p_max_n_, opt_.device, true, hp_.n_embd);
   return p2p_->handle();
 }
 
@@ -535,6 +536,20 @@ void Engine::p2p_open(const std::vector<std::string>& handles) {
 // Decode-sized messages (a step's hidden rows, the sampler's candidate blocks) take the
 // one-shot P2P path when the peers are open; prefill-sized ones (T x d) go to RCCL's
 // ring/tree algorithms - or, with comm=ipc (no RCCL), to the P2P kernel as well.
+// Decode GEMVs under TP: the row-parallel all-reduce in the epilogue (GemvArgs::tp_*) when the
+// P2P regions carry the fused area (one launch per projection instead of two, no tmp_ copy)
+bool Engine::tp_epilogue(GemvArgs& g) const {
+  if (!p2p_ || !p2p_->ready() || p2p_->fused_n() < hp_.n_embd || g.n_out > p2p_->fused_n()) return false;
+  g.tp_peers = p2p_->peers();
+  g.tp_world = p2p_->world(); g.tp_rank = p2p_->rank();
+  g.tp_stride = p2p_->stride(); g.tp_off = p2p_->fused_offset();
+  g.tp_epochs = p2p_->fused_epochs(); g.tp_err = p2p_->err_word();
+  // ranks sharing this GPU (the one-GPU rehearsal): each rank's grid a 1/world share of the
+  // resident blocks, or one rank's waiting epilogue waves could hold every CU its peers need
+  if (p2p_->shared_device()) g.grid_div = p2p_->world();
+  return true;
+}
+
 void Engine::allreduce_into(const float* send, float* recv, size_t n, hipStream_t s) {
   if (p2p_ && p2p_->ready() && n <= (size_t)p2p_->max_n()) {
     p2p_->allreduce(send, recv, (int)n, s);
@@ -610,6 +625,7 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   aa.part = attn_part_; aa.counters = attn_cnt_; aa.out = attn_;
   GemvArgs o;
   o.w = L.wo; o.x = attn_; o.n_out = d;
+  const bool tpe = tp && tp_epilogue(o);  // the all-reduce in the GEMV epilogue (no collective launch)
   // attention + Wo in one launch: Wo's weights stream while the attention runs
   bool fused = false;
   if (!tp && wo_fuse_) {
@@ -635,6 +651,9 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   } else if (!tp) {
     o.out = x_;
     gemv(o, EPI_ADD, s);
+  } else if (tpe) {
+    o.out = x_; o.resid = x_;  // x += sum over ranks of the partial rows
+    gemv(o, EPI_STORE, s);
   } else {
     o.out = tmp_;
     o.resid = opt_.tp_rank == 0 ? x_ : nullptr;
@@ -679,6 +698,9 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
     if (!tp) {
       dn.out = x_;
       gemv(dn, EPI_ADD, s);
+    } else if (tp_epilogue(dn)) {
+      dn.out = x_; dn.resid = x_;
+      gemv(dn, EPI_STORE, s);
     } else {
       dn.out = tmp_;
       dn.resid = opt_.tp_rank == 0 ? x_ : nullptr;

@@ -195,6 +195,7 @@ class Engine : public SlotBackend {
   void build_rope();
 
   void allreduce_into(const float* send, float* recv, size_t n, hipStream_t s);
+  bool tp_epilogue(GemvArgs& g) const;
   void allgather_into(const float* send, float* recv, size_t n, hipStream_t s);  // recv [tp][n]
   // the sampler over this rank's logits rows (vocabulary shard under TP): stage 1, the
   // candidate all-gather, stage 2 (single row: slot; batched: the bslots_ rows)

@@ -1,5 +1,6 @@
 #include "p2p.h"
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 
@@ -9,13 +10,14 @@ static void p2pchk(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("p2p: ") + what + ": " + hipGetErrorString(e));
 }
 
-P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached)
-    : rank_(rank), world_(world), max_n_((max_n + 3) & ~3), device_(device), uncached_(uncached) {
+P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached, int fused_n)
+    : rank_(rank), world_(world), max_n_((max_n + 3) & ~3), device_(device), fused_n_(std::max(0, fused_n)),
+      uncached_(uncached) {
   if (world < 1 || world > kP2PMaxRanks || rank < 0 || rank >= world) throw std::runtime_error("p2p: bad rank/world");
   if (max_n <= 0) throw std::runtime_error("p2p: bad max_n");
   p2pchk(hipSetDevice(device_), "hipSetDevice");
-  // {value, epoch} granules: max_n data + kP2PMaxBlocks heartbeats per (slot, rank)
-  data_bytes_ = sizeof(unsigned long long) * 2 * (size_t)world * (max_n_ + kP2PMaxBlocks);
+  // {value, epoch} granules: max_n data + kP2PMaxBlocks heartbeats (+ the fused area) per (slot, rank)
+  data_bytes_ = sizeof(unsigned long long) * 2 * (size_t)world * (max_n_ + kP2PMaxBlocks + fused_n_);
   data_bytes_ = (data_bytes_ + 255) & ~(size_t)255;
   region_bytes_ = data_bytes_ + sizeof(int) * 2 * (size_t)world * kP2PMaxBlocks;
   // A whole, 2 MiB-granular allocation of its own, UNCACHED (hipDeviceMallocUncached): peers
@@ -44,6 +46,10 @@ P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached)
   p2pchk(hipMemset(region_, 0, region_bytes_), "hipMemset region");
   p2pchk(hipMalloc((void**)&epochs_, sizeof(int) * kP2PMaxBlocks), "hipMalloc epochs");
   p2pchk(hipMemset(epochs_, 0, sizeof(int) * kP2PMaxBlocks), "hipMemset epochs");
+  if (fused_n_ > 0) {  // per-item epochs of the fused area (an item = one GEMV wave item, >= 1 row)
+    p2pchk(hipMalloc((void**)&fused_epochs_, sizeof(int) * fused_n_), "hipMalloc fused epochs");
+    p2pchk(hipMemset(fused_epochs_, 0, sizeof(int) * fused_n_), "hipMemset fused epochs");
+  }
   p2pchk(hipMalloc((void**)&err_, sizeof(int) * 4), "hipMalloc err");
   p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "hipMemset err");
   p2pchk(hipDeviceSynchronize(), "sync");
@@ -54,13 +60,16 @@ P2PComm::~P2PComm() {
     if (p) (void)hipIpcCloseMemHandle(p);
   if (region_) (void)hipFree(region_);
   if (epochs_) (void)hipFree(epochs_);
+  if (fused_epochs_) (void)hipFree(fused_epochs_);
   if (err_) (void)hipFree(err_);
 }
 
 std::string P2PComm::handle() const {
   hipIpcMemHandle_t h;
   p2pchk(hipIpcGetMemHandle(&h, region_), "hipIpcGetMemHandle");
-  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+  // + this rank's device index: peers on the same device (the one-GPU IPC rehearsal) are told apart
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h)) +
+         std::string(reinterpret_cast<const char*>(&device_), sizeof(int));
 }
 
 void P2PComm::open(const std::vector<std::string>& handles) {
@@ -71,7 +80,10 @@ void P2PComm::open(const std::vector<std::string>& handles) {
     if (p == rank_) {
       base = static_cast<char*>(region_);
     } else {
-      if (handles[p].size() != sizeof(hipIpcMemHandle_t)) throw std::runtime_error("p2p: bad handle size");
+      if (handles[p].size() != sizeof(hipIpcMemHandle_t) + sizeof(int)) throw std::runtime_error("p2p: bad handle size");
+      int pdev = -1;
+      std::memcpy(&pdev, handles[p].data() + sizeof(hipIpcMemHandle_t), sizeof(int));
+      shared_device_ = shared_device_ || pdev == device_;
       hipIpcMemHandle_t h;
       std::memcpy(&h, handles[p].data(), sizeof(h));
       void* ptr = nullptr;
@@ -97,6 +109,7 @@ void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_
   P2PArgs a;
   a.peers = peers_;
   a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_; a.gather = gather;
+  a.stride = stride();
   a.epochs = epochs_; a.err = err_;
   p2p_collective(a, s);
 }

@@ -15,7 +15,9 @@ namespace lfk {
 
 class P2PComm {
  public:
-  P2PComm(int rank, int world, int max_n, int device, bool uncached = true);
+  // fused_n > 0: a further area of fused_n granules per (slot, rank) past the collective's, for
+  // the GEMV epilogue all-reduce (gemv.hip, GemvArgs::tp_*), with its own per-item epochs
+  P2PComm(int rank, int world, int max_n, int device, bool uncached = true, int fused_n = 0);
   ~P2PComm();
   P2PComm(const P2PComm&) = delete;
   P2PComm& operator=(const P2PComm&) = delete;
@@ -31,9 +33,20 @@ class P2PComm {
   // diagnostics: per rank (mapped pointer, allocation base, allocation size) as seen here
   std::vector<std::vector<unsigned long long>> mappings() const;
   void reset_error();
+  // the fused area: granule stride per (slot, rank), its offset, per-item epochs, peers
+  int stride() const { return max_n_ + kP2PMaxBlocks + fused_n_; }
+  int fused_offset() const { return max_n_ + kP2PMaxBlocks; }
+  int fused_n() const { return fused_n_; }
+  int* fused_epochs() const { return fused_epochs_; }
+  int* err_word() const { return err_; }
+  const P2PPeers& peers() const { return peers_; }
+  int rank() const { return rank_; }
+  bool shared_device() const { return shared_device_; }  // some peer is on this rank's GPU (rehearsal)
+  int world() const { return world_; }
 
  private:
-  int rank_, world_, max_n_, device_;
+  int rank_, world_, max_n_, device_, fused_n_ = 0;
+  int* fused_epochs_ = nullptr;
   size_t data_bytes_ = 0, region_bytes_ = 0;
   void* region_ = nullptr;
   std::vector<void*> imported_;
@@ -41,6 +54,7 @@ class P2PComm {
   int* err_ = nullptr;
   P2PPeers peers_;
   bool ready_ = false;
+  bool shared_device_ = false;
   bool uncached_ = false;
   void launch(const float* src, float* dst, int n, int gather, hipStream_t s);
 };

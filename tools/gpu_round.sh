@@ -41,7 +41,7 @@ for s in "$@"; do
     eng) step eng 900 $PYT tests/test_engine_gpu.py --timeout 300 ;;
     batch) step batch 600 $PYT tests/test_batch_gpu.py tests/test_batch_serving_gpu.py --timeout 300 ;;
     tp) step tp 900 $PYT tests/test_p2p_allreduce.py tests/test_tp_gpu.py --timeout 600 ;;
-    tp8) step tp8 900 $PYT tests/test_tp8_gpu.py --timeout 850 -s ;;
+    tp8) step tp8 170 $PYT tests/test_tp8_gpu.py --timeout 160 -s ;;
     rccl) step rccl 400 $PYT tests/test_rccl_gpu.py tests/test_serve_tp_gpu.py --timeout 300 ;;
     p2pu) step p2pu 200 $PYT tests/test_p2p_allreduce.py --timeout 150 ;;
     qkvsk) step qkvsk 300 $PYT tests/test_kernels_gpu.py -k "qkv_splitk or attn_decode or bmm_rows" --timeout 120 ;;
