@@ -38,9 +38,10 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
                        int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split,
-                       int n_slots, const std::string& comm) {
+                       int n_slots, const std::string& comm, int layer_end) {
              EngineOptions o;
              o.layer_begin = layer_begin;
+             o.layer_end = layer_end;
              o.n_slots = n_slots;
              o.n_ctx = n_ctx;
              o.n_batch = n_batch;
@@ -57,7 +58,8 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("path"), py::arg("n_ctx") = 1024, py::arg("n_batch") = 512, py::arg("device") = 0,
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
            py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0,
-           py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1, py::arg("comm") = "auto")
+           py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1, py::arg("comm") = "auto",
+           py::arg("layer_end") = -1)
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
@@ -106,6 +108,30 @@ PYBIND11_MODULE(_hip, m) {
              return py::array_t<float>(v.size(), v.data());
            })
       .def_property_readonly("layer_begin", &Engine::layer_begin)
+      .def_property_readonly("layer_end", &Engine::layer_end)
+      .def_property_readonly("has_head", &Engine::has_head)
+      .def("eval_stage",
+           [](Engine& e, py::object x, std::vector<int> tokens, int pos0) {
+             std::vector<float> v;
+             int T = (int)tokens.size();
+             if (!x.is_none()) {
+               auto a = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(x);
+               if (!a || a.ndim() != 2 || a.shape(1) != e.hparams().n_embd)
+                 throw std::runtime_error("eval_stage: x must be [T, n_embd]");
+               T = (int)a.shape(0);
+               const float* ptr = a.data();
+               py::gil_scoped_release nogil;
+               v = e.eval_stage(ptr, nullptr, T, pos0);
+             } else {
+               py::gil_scoped_release nogil;
+               v = e.eval_stage(nullptr, tokens.data(), T, pos0);
+             }
+             const bool hidden = !e.has_head();
+             py::array_t<float> out(v.size(), v.data());
+             if (hidden) out.resize({(py::ssize_t)T, (py::ssize_t)e.hparams().n_embd});
+             return out;
+           },
+           py::arg("x"), py::arg("tokens") = std::vector<int>{}, py::arg("pos0") = 0)
       .def("decode_logits",
            [](Engine& e, int token, int pos) {
              std::vector<float> v;

@@ -133,7 +133,10 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   if (opt_.layer_begin > 0 && tp > 1) throw std::runtime_error("partial offload cannot be combined with split_mode=row");
   if (opt_.n_ctx <= 0) opt_.n_ctx = hp_.n_ctx_train;
   if (opt_.n_slots < 1) throw std::runtime_error("n_slots must be >= 1");
-  if (opt_.n_slots > 1 && opt_.layer_begin > 0)
+  layer_end_ = opt_.layer_end < 0 ? hp_.n_layer : opt_.layer_end;
+  if (layer_end_ <= opt_.layer_begin || layer_end_ > hp_.n_layer) throw std::runtime_error("bad layer_end");
+  if (layer_end_ < hp_.n_layer && tp > 1) throw std::runtime_error("a layer split cannot be combined with split_mode=row");
+  if (opt_.n_slots > 1 && (opt_.layer_begin > 0 || layer_end_ < hp_.n_layer))
     throw std::runtime_error("KV slots (batched decode) need the GPU to hold every layer");
   // comm=rccl at tp_size 1: the tensor-parallel code paths over a ONE-rank RCCL communicator
   // (every collective a copy) - how a one-GPU box runs the RCCL branch inside captured graphs
@@ -251,11 +254,13 @@ void Engine::load(const GGUFFile& f) {
   const int r = opt_.tp_rank;
   const int d = hp_.n_embd, hd = hp_.head_dim;
   tok_embd_ = upload_matrix(f, "token_embd.weight", 0, hp_.n_vocab, 0, d);
-  out_norm_ = upload_f32(f, "output_norm.weight");
-  const std::string out_name = f.find("output.weight") ? "output.weight" : "token_embd.weight";
-  output_ = upload_matrix(f, out_name, (size_t)r * V_l_, V_l_, 0, d);
+  if (has_head()) {  // (a layer-split stage before the last holds no head)
+    out_norm_ = upload_f32(f, "output_norm.weight");
+    const std::string out_name = f.find("output.weight") ? "output.weight" : "token_embd.weight";
+    output_ = upload_matrix(f, out_name, (size_t)r * V_l_, V_l_, 0, d);
+  }
   layers_.resize(hp_.n_layer);
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) {
+  for (int l = opt_.layer_begin; l < layer_end_; ++l) {
     const std::string p = "blk." + std::to_string(l) + ".";
     Layer& L = layers_[l];
     L.attn_norm = upload_f32(f, p + "attn_norm.weight");
@@ -381,7 +386,7 @@ void Engine::alloc_buffers() {
 
 void Engine::setup_batch_mfma() {
   bg_ = bg_ffn_ = false;
-  if (!bmax_ || opt_.layer_begin > 0) return;
+  if (!bmax_ || opt_.layer_begin > 0 || !has_head()) return;
   auto ok = [&](const QMat& m) { return m.base && bmm_supported(m.type, m.K); };
   auto kfit = [](int K) { return K % 128 == 0 && K <= 32768; };  // bprep's row shapes
   bool att = ok(output_) && kfit(hp_.n_embd) && kfit(nq_) && (V_pad_ % 4) == 0 && ((nq_ + 2 * nkvd_) % 4) == 0;
@@ -725,13 +730,13 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int
 void Engine::enqueue_decode(hipStream_t s) {
   // (the embedding launch also zeroes the layers' attention -> Wo done counters)
   embed_rows(tok_embd_, state_ + (size_t)S_NSTATE * dslot_ + S_TOKEN, 1, x_, s, dec_done_, 64 * hp_.n_layer);
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_layer_decode(l, s);
+  for (int l = opt_.layer_begin; l < layer_end_; ++l) enqueue_layer_decode(l, s);
   enqueue_head(x_, 1, s, dslot_);
 }
 
 void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
   if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
-  for (int l = opt_.layer_begin; l < hp_.n_layer; ++l) enqueue_rows_layer(l, T, pos0, false, s);
+  for (int l = opt_.layer_begin; l < layer_end_; ++l) enqueue_rows_layer(l, T, pos0, false, s);
 }
 
 void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_t s) {
@@ -1729,6 +1734,7 @@ std::vector<float> Engine::batch_logits_impl(int B) {
 GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new, const SamplingOpts& sp,
                         const std::vector<int>& stop_ids, const std::function<bool()>& poll,
                         const std::function<void(int)>& on_token) {
+  if (!has_head()) throw std::runtime_error("generate: this layer-split stage holds no head (eval_stage)");
   ExecGuard guard(this);
   GenOut out;
   const int n_prompt = (int)prompt.size();
@@ -1818,6 +1824,7 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
 }
 
 std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0) {
+  if (!has_head()) throw std::runtime_error("eval_logits: this layer-split stage holds no head (eval_stage)");
   ExecGuard guard(this);
   const int T = (int)tokens.size();
   if (T <= 0 || T > opt_.n_batch || pos0 < 0 || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_logits: bad size");
@@ -1859,6 +1866,30 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
   return out;
 }
 
+std::vector<float> Engine::eval_stage(const float* x, const int* tokens, int T, int pos0) {
+  if (has_head()) {
+    if (x) return eval_hidden(x, T, pos0);
+    return eval_logits(std::vector<int>(tokens, tokens + T), pos0);
+  }
+  ExecGuard guard(this);
+  if (tp_on_) throw std::runtime_error("eval_stage: not available with tensor parallelism");
+  if (T <= 0 || T > opt_.n_batch || pos0 < 0 || pos0 + T > opt_.n_ctx) throw std::runtime_error("eval_stage: bad size");
+  if (x) {
+    HIPCHK(hipMemcpyAsync(x_, x, sizeof(float) * T * hp_.n_embd, hipMemcpyHostToDevice, stream_));
+  } else {
+    if (opt_.layer_begin > 0) throw std::runtime_error("eval_stage: token input needs the first stage");
+    for (int i = 0; i < T; ++i)
+      if (tokens[i] < 0 || tokens[i] >= hp_.n_vocab) throw std::runtime_error("eval_stage: token out of range");
+    std::memcpy(h_tokens_, tokens, sizeof(int) * T);
+    HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
+  }
+  enqueue_prefill(T, pos0, stream_, /*embed=*/x == nullptr);
+  std::vector<float> out((size_t)T * hp_.n_embd);
+  HIPCHK(hipMemcpyAsync(out.data(), x_, sizeof(float) * out.size(), hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return out;
+}
+
 void Engine::kv_transfer(void* buf, int n, bool load) {
   ExecGuard guard(this);
   if (tp_on_)
@@ -1880,6 +1911,7 @@ void Engine::kv_transfer(void* buf, int n, bool load) {
 }
 
 std::vector<float> Engine::decode_logits(int token, int pos) {
+  if (!has_head()) throw std::runtime_error("decode_logits: this layer-split stage holds no head (eval_stage)");
   ExecGuard guard(this);
   if (pos < 0 || pos >= opt_.n_ctx) throw std::runtime_error("decode_logits: pos out of range");
   if (leader()) {

@@ -47,6 +47,8 @@ struct EngineOptions {
   std::string comm = "auto";
   std::vector<float> tensor_split;  // per-rank weights (empty = even); see shard.h
   int layer_begin = 0;  // hybrid placement: layers [0, layer_begin) run on the CPU backend
+  int layer_end = -1;   // layer split: this engine runs layers [layer_begin, layer_end) (-1: n_layer);
+                        // the output norm and head are loaded only by the stage ending at n_layer
   // KV slots (continuous batching): slot 0 serves generate() / the graph decode path, slots
   // [0, n_slots) can decode together through batch_step() (also under tensor parallelism)
   int n_slots = 1;
@@ -97,6 +99,10 @@ class Engine : public SlotBackend {
   void kv_transfer(void* buf, int n, bool load);
   // hybrid placement: hidden states [T][d] of layer `layer_begin` in, last-row logits out
   std::vector<float> eval_hidden(const float* x, int T, int pos0);
+  // layer split (runtime/layer_split_backend.py): tokens (x == nullptr, first stage) or hidden
+  // states [T][d] in; the hidden states after layer_end - 1 out ([T][d]), or the last row's logits
+  // when this stage holds the head
+  std::vector<float> eval_stage(const float* x, const int* tokens, int T, int pos0);
   void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing
 
   const HParams& hparams() const { return hp_; }
@@ -119,6 +125,8 @@ class Engine : public SlotBackend {
   std::string last_error() const { return last_error_; }
   int n_ctx() const override { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
+  int layer_end() const { return layer_end_; }
+  bool has_head() const { return layer_end_ == hp_.n_layer; }
   int device() const { return opt_.device; }
 
   // ---- continuous batching over KV slots (EngineOptions::n_slots > 1, one rank, all layers)
@@ -363,6 +371,7 @@ class Engine : public SlotBackend {
   // (LFK_QKV_SK=0: the one-part Q|K|V with the RoPE / KV-append epilogue, A/B)
   bool qkv_sk_ = true;
   bool tp_on_ = false;        // the tensor-parallel code paths (tp_size > 1, or comm=rccl at one rank)
+  int layer_end_ = 0;         // layers [opt_.layer_begin, layer_end_) live here
   long long* step_clk_ = nullptr;
   int step_clk_layer_ = -1;
   long long* clk_of(int l, int k) const {

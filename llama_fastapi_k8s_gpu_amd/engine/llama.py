@@ -37,7 +37,13 @@ from .tokenizer import tokenizer_from_metadata
 logger = logging.getLogger(__name__)
 
 
-def _select_backend(reader, hp: LlamaHParams, n_gpu_layers: int, backend: Optional[str]) -> str:
+def _layer_split(split_mode: str, tensor_split) -> bool:
+    """upstream's multi-GPU layer placement: split_mode LAYER with weights on >1 GPUs"""
+    return split_mode == "layer" and bool(tensor_split) and sum(1 for v in tensor_split if float(v) > 0) > 1
+
+
+def _select_backend(reader, hp: LlamaHParams, n_gpu_layers: int, backend: Optional[str],
+                    split_mode: str = "layer", tensor_split=None) -> str:
     if backend:
         return backend
     env = os.environ.get("LLAMA_BACKEND")
@@ -51,7 +57,9 @@ def _select_backend(reader, hp: LlamaHParams, n_gpu_layers: int, backend: Option
     try:
         from ..runtime import load_hip
         if load_hip().device_count() > 0:
-            return "hip" if n_gpu >= hp.n_layer else "hybrid"
+            if n_gpu < hp.n_layer:
+                return "hybrid"
+            return "layer" if _layer_split(split_mode, tensor_split) else "hip"
     except Exception:
         pass
     logger.warning("no GPU visible: n_gpu_layers=%d falls back to the CPU backend", n_gpu_layers)
@@ -87,7 +95,7 @@ class Llama:
         bos = self.tokenizer.tokens[self.tokenizer.bos_id] if self.tokenizer.bos_id >= 0 else ""
         eos = self.tokenizer.tokens[self.tokenizer.eos_id] if self.tokenizer.eos_id >= 0 else ""
         self.chat_format, self._formatter = get_formatter(self.metadata, chat_format, bos, eos)
-        kind = _select_backend(reader, self.hparams, n_gpu_layers, backend)
+        kind = _select_backend(reader, self.hparams, n_gpu_layers, backend, split_mode, tensor_split)
         self.backend_name = kind
         if kind == "reference":
             self._backend = ReferenceBackend(reader, self._n_ctx)
@@ -99,6 +107,11 @@ class Llama:
             from ..runtime.hybrid_backend import HybridBackend
             self._backend = HybridBackend(model_path, self.hparams, n_gpu_layers=n_gpu_layers, n_ctx=self._n_ctx,
                                           main_gpu=main_gpu, n_threads=n_threads, n_batch=n_batch)
+        elif kind == "layer":
+            from ..runtime.layer_split_backend import LayerSplitBackend
+            self._backend = LayerSplitBackend(model_path, self.hparams, tensor_split=tensor_split or [1.0],
+                                              n_ctx=self._n_ctx, n_batch=n_batch,
+                                              layer_devices=kwargs.get("layer_devices"))
         elif kind == "hip":
             from ..runtime.hip_backend import HipBackend
             self._backend = HipBackend(model_path, self.hparams, n_ctx=self._n_ctx, n_gpu_layers=n_gpu_layers,

@@ -17,8 +17,9 @@ api.py:24-28) mapped onto one process per GPU:
     csrc/runtime/shard.h). Rank 0 drives; ranks 1..N-1 run ``follow()``, which
     replays rank 0's engine commands natively (csrc/runtime/tp_channel.h), so
     continuous batching and cooperative cancel work unchanged under TP.
-  * ``split_mode="none"/"layer"`` in one process: the model runs on
-    ``main_gpu`` (one GPU holds any BASELINE model: 288 GB HBM).
+  * ``split_mode="none"``, or ``"layer"`` without a multi-GPU ``tensor_split``: the model
+    runs on ``main_gpu`` (one GPU holds any BASELINE model: 288 GB HBM). A layer split
+    over several GPUs is runtime/layer_split_backend.py (contiguous layer ranges per GPU).
   * ``max_batch=M > 1``: continuous batching (under TP the scheduler runs on rank 0). The engine gets M + 1 KV
     slots; a native scheduler thread (csrc/runtime/scheduler.cpp) decodes every
     admitted request as one row of a batched step (one weight stream per step
@@ -64,11 +65,10 @@ class HipBackend:
             raise ValueError(f"n_gpu_layers={n_gpu_layers} < n_layer={hparams.n_layer}: partial offload runs on "
                              "the hybrid backend (backend='hybrid')")
         if split_mode == "layer" and tensor_split and sum(1 for v in tensor_split if float(v) > 0) > 1:
-            # upstream's layer split places contiguous layer ranges by tensor_split; one MI355X
-            # holds any supported model (288 GB), so layers are not split across GPUs here -
-            # a tensor_split given for a layer split would be silently ignored
-            raise ValueError("tensor_split needs split_mode='row' (tensor parallelism); split_mode='layer' runs the "
-                             "whole model on main_gpu")
+            # upstream's layer split (contiguous layer ranges by tensor_split) is its own backend:
+            # the Llama facade routes it to runtime/layer_split_backend.py
+            raise ValueError("split_mode='layer' with a multi-GPU tensor_split runs on the layer-split backend "
+                             "(backend='layer')")
         comm = tp_comm or "auto"
         rank, size, local, nccl_id, ts = _tp_setup(split_mode, tensor_split, comm)
         if device is None:
