@@ -111,7 +111,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("layer_end", &Engine::layer_end)
       .def_property_readonly("has_head", &Engine::has_head)
       .def("eval_stage",
-           [](Engine& e, py::object x, std::vector<int> tokens, int pos0) {
+           [](Engine& e, py::object x, std::vector<int> tokens, int pos0, bool to_host) {
              std::vector<float> v;
              int T = (int)tokens.size();
              if (!x.is_none()) {
@@ -121,17 +121,26 @@ PYBIND11_MODULE(_hip, m) {
                T = (int)a.shape(0);
                const float* ptr = a.data();
                py::gil_scoped_release nogil;
-               v = e.eval_stage(ptr, nullptr, T, pos0);
+               v = e.eval_stage(ptr, nullptr, T, pos0, to_host);
              } else {
                py::gil_scoped_release nogil;
-               v = e.eval_stage(nullptr, tokens.data(), T, pos0);
+               v = e.eval_stage(nullptr, tokens.data(), T, pos0, to_host);
              }
-             const bool hidden = !e.has_head();
+             const bool hidden = !e.has_head() && to_host;
              py::array_t<float> out(v.size(), v.data());
              if (hidden) out.resize({(py::ssize_t)T, (py::ssize_t)e.hparams().n_embd});
              return out;
            },
-           py::arg("x"), py::arg("tokens") = std::vector<int>{}, py::arg("pos0") = 0)
+           py::arg("x"), py::arg("tokens") = std::vector<int>{}, py::arg("pos0") = 0, py::arg("to_host") = true)
+      .def("eval_stage_peer",
+           [](Engine& e, const Engine& prev, int T, int pos0) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.eval_stage_peer(prev, T, pos0);
+             }
+             return py::array_t<float>(v.size(), v.data());
+           })
       .def("decode_logits",
            [](Engine& e, int token, int pos) {
              std::vector<float> v;

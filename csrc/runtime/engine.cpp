@@ -1866,7 +1866,7 @@ std::vector<float> Engine::eval_hidden(const float* x, int T, int pos0) {
   return out;
 }
 
-std::vector<float> Engine::eval_stage(const float* x, const int* tokens, int T, int pos0) {
+std::vector<float> Engine::eval_stage(const float* x, const int* tokens, int T, int pos0, bool to_host) {
   if (has_head()) {
     if (x) return eval_hidden(x, T, pos0);
     return eval_logits(std::vector<int>(tokens, tokens + T), pos0);
@@ -1884,8 +1884,28 @@ std::vector<float> Engine::eval_stage(const float* x, const int* tokens, int T, 
     HIPCHK(hipMemcpyAsync(tokens_, h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, stream_));
   }
   enqueue_prefill(T, pos0, stream_, /*embed=*/x == nullptr);
-  std::vector<float> out((size_t)T * hp_.n_embd);
-  HIPCHK(hipMemcpyAsync(out.data(), x_, sizeof(float) * out.size(), hipMemcpyDeviceToHost, stream_));
+  std::vector<float> out(to_host ? (size_t)T * hp_.n_embd : 0);  // (else the next stage copies x_ peer to peer)
+  if (to_host) HIPCHK(hipMemcpyAsync(out.data(), x_, sizeof(float) * out.size(), hipMemcpyDeviceToHost, stream_));
+  HIPCHK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+std::vector<float> Engine::eval_stage_peer(const Engine& prev, int T, int pos0) {
+  ExecGuard guard(this);
+  if (tp_on_) throw std::runtime_error("eval_stage_peer: not available with tensor parallelism");
+  if (prev.hp_.n_embd != hp_.n_embd || prev.layer_end_ != opt_.layer_begin)
+    throw std::runtime_error("eval_stage_peer: prev must be the stage that ends where this one begins");
+  if (T <= 0 || T > opt_.n_batch || T > prev.opt_.n_batch || pos0 < 0 || pos0 + T > opt_.n_ctx)
+    throw std::runtime_error("eval_stage_peer: bad size");
+  // (prev's eval synchronised its stream before returning: its x_ rows are final)
+  HIPCHK(hipMemcpyPeerAsync(x_, opt_.device, prev.x_, prev.opt_.device, sizeof(float) * T * hp_.n_embd, stream_));
+  enqueue_prefill(T, pos0, stream_, /*embed=*/false);
+  std::vector<float> out;
+  if (has_head()) {
+    enqueue_head(x_ + (size_t)(T - 1) * hp_.n_embd, 0, stream_);
+    out.resize(hp_.n_vocab);
+    HIPCHK(hipMemcpyAsync(out.data(), logits_, sizeof(float) * hp_.n_vocab, hipMemcpyDeviceToHost, stream_));
+  }
   HIPCHK(hipStreamSynchronize(stream_));
   return out;
 }

@@ -102,7 +102,11 @@ class Engine : public SlotBackend {
   // layer split (runtime/layer_split_backend.py): tokens (x == nullptr, first stage) or hidden
   // states [T][d] in; the hidden states after layer_end - 1 out ([T][d]), or the last row's logits
   // when this stage holds the head
-  std::vector<float> eval_stage(const float* x, const int* tokens, int T, int pos0);
+  std::vector<float> eval_stage(const float* x, const int* tokens, int T, int pos0, bool to_host = true);
+  // the same, with the hidden states taken device to device from the previous stage's engine
+  // (its last eval_stage / eval_stage_peer output, T rows; hipMemcpyPeerAsync across GPUs): no
+  // host round trip between stages. Returns the last row's logits at the head stage, else nothing
+  std::vector<float> eval_stage_peer(const Engine& prev, int T, int pos0);
   void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing
 
   const HParams& hparams() const { return hp_; }

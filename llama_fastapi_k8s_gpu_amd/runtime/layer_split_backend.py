@@ -7,8 +7,8 @@ in those proportions. The same placement here: one MI355X engine per stage, stag
 on device ``i`` holding layers ``[begin_i, end_i)`` and its part of the KV cache; the
 first stage gathers the embedding, the last holds the output norm and head. A token's
 hidden states (``n_embd`` floats per row) pass from stage to stage once per prompt chunk
-or decoded token; sampling is the host C++ chain (bit-identical uniforms, as the hybrid
-backend). One MI355X holds every BASELINE model (288 GB), so this is a capacity and
+or decoded token (device to device, ``hipMemcpyPeerAsync``); sampling is the host C++
+chain (bit-identical uniforms, as the hybrid backend). One MI355X holds every BASELINE model (288 GB), so this is a capacity and
 compatibility placement, not a speed-up: a single decode still walks every layer in
 order. Tensor parallelism (``split_mode="row"``) is the multi-GPU speed path.
 
@@ -101,8 +101,16 @@ class LayerSplitBackend:
         """Tokens into every stage's KV cache (chunks of at most n_batch) -> last raw logits."""
         tokens = [int(t) for t in tokens]
         logits = None
+        # HIP stages hand the hidden states over device to device (hipMemcpyPeerAsync into the
+        # next stage's activation buffer); other stage objects through the host
+        peer = len(self.stages) > 1 and all(hasattr(s, "eval_stage_peer") for s in self.stages)
         for p in range(0, len(tokens), self.n_batch):
             chunk, at = tokens[p:p + self.n_batch], int(pos0 + p)
+            if peer:
+                self.stages[0].eval_stage(None, chunk, at, False)
+                for prev, st in zip(self.stages, self.stages[1:]):
+                    logits = st.eval_stage_peer(prev, len(chunk), at)
+                continue
             h = self.stages[0].eval_stage(None, chunk, at)
             for st in self.stages[1:]:
                 h = st.eval_stage(h, [], at)

@@ -38,6 +38,10 @@ def test_layer_split_matches_whole_model(path):
     whole.eval_logits(toks[:32], 0)
     ref = whole.eval_logits(toks[32:], 32)
     assert rel_err(got, ref) < 1e-4, rel_err(got, ref)
+    # the host hand-off (eval_stage with hidden states in / out) gives the same logits
+    h0 = be.stages[0].eval_stage(None, toks[32:], 32)
+    h1 = be.stages[1].eval_stage(h0, [], 32)
+    assert rel_err(be.stages[2].eval_stage(h1, [], 32), ref) < 1e-4
     # a stage without the head returns hidden states [T, d]; it refuses the logits entry points
     h = be.stages[0].eval_stage(None, toks[:5], 0)
     assert h.shape == (5, split.hparams.n_embd) and np.isfinite(h).all()
