@@ -98,7 +98,8 @@ def _worker(rank, world, port, path, q):
 @pytest.mark.timeout(900)
 def test_tensor_parallel_eight_ranks_70b_width(tmp_path):
     import torch
-    if not torch.cuda.is_available():
+    # (device_count does not initialise HIP in this process: no queues held beside the ranks')
+    if torch.cuda.device_count() < 1:
         pytest.skip("no GPU")
     import torch.multiprocessing as mp
 
