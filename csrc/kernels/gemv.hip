@@ -19,6 +19,7 @@
 
 #include "attn_dev.h"
 #include "gemv_dev.h"
+#include "moe_route_dev.h"
 
 namespace lfk {
 
@@ -87,10 +88,12 @@ __device__ __forceinline__ void tp_store_row(const GemvArgs& a, int row, float v
 // WAIT (SPLITK, not EARLY; attn_wo1): the first item's weights go out first, then the block waits
 // for the in-flight producer of x (GemvArgs::wait) and loads x with sc1 loads.
 // (bid, nblk): the block's index and count in the GEMV's grid (a plane of attn_wo1's grid).
+// ROUTE (EARLY SwiGLU, BLOCK = 1024, K = 4096, NORM): the block routes the token itself (GemvArgs::route_w)
 template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false,
-          bool EARLY = false, bool WAIT = false>
+          bool EARLY = false, bool WAIT = false, bool ROUTE = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, const int nblk) {
   static_assert(!WAIT || (SPLITK && !EARLY && !TL), "the in-flight wait is a split-K, non-EARLY form");
+  static_assert(!ROUTE || (EARLY && !SPLITK && NORM && BLOCK == 1024 && EPI == EPI_SWIGLU), "routed form");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // TL: per-block timeline (wall_clock64 ticks, microbenchmarks only):
   // [entry, prologue done, first item done, exit, items done by wave 0]
@@ -134,7 +137,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
   if constexpr (WAIT) {
     // the weights stream while the producer (the attention planes of this launch) finishes
     if (item < total) {
-      item_rows<EPI, NR>(a, item / kparts, groups, R, slot, f0);
+      item_rows<EPI, NR>(a, item / kparts, groups, R, slot, f0, a.expert_ids);
       kp = item % kparts;
       ws.load(R, kp * 64 * U, nchunks, lane);
     }
@@ -155,17 +158,59 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
   // The x prologue runs BEFORE the first weight loads: measured on MI355X, a
   // prologue whose L2 reads queue behind a saturated weight stream (its own CU's
   // or its neighbours') costs more than the latency its prefetch would hide.
-  if (a.debug != 1) xp.load(a.x, a.norm_w, K);
+  if (a.debug != 1 || ROUTE) xp.load(a.x, a.norm_w, K);
+  const int* ids = a.expert_ids;
+  if constexpr (ROUTE) {
+    // the router, exactly as moe_router_fused_kernel sums it: thread t's float4 at k = 4t
+    // (K == 4 * BLOCK), wave sums, waves in order (moe_route_dev.h)
+    constexpr int EM = 8, NWV = BLOCK / 64;
+    __shared__ float rred[NWV][EM + 1];
+    __shared__ int rids[EM];
+    const int E = a.route_E, i4 = threadIdx.x * 4;
+    float4 rw[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) rw[e] = *reinterpret_cast<const float4*>(a.route_w + (size_t)min(e, E - 1) * K + i4);
+    const float4 xv = xp.v[0], wv = xp.w[0];
+    float ss = xv.x * xv.x + xv.y * xv.y + xv.z * xv.z + xv.w * xv.w;
+    const float4 n = make_float4(xv.x * wv.x, xv.y * wv.y, xv.z * wv.z, xv.w * wv.w);
+    float racc[EM];
+#pragma unroll
+    for (int e = 0; e < EM; ++e) racc[e] = e < E ? n.x * rw[e].x + n.y * rw[e].y + n.z * rw[e].z + n.w * rw[e].w : 0.f;
+    ss = wave_sum_fast(ss);
+#pragma unroll
+    for (int e = 0; e < EM; ++e) racc[e] = e < E ? wave_sum_fast(racc[e]) : 0.f;
+    if (lane == 0) {
+      rred[wave][EM] = ss;
+#pragma unroll
+      for (int e = 0; e < EM; ++e) rred[wave][e] = racc[e];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      int my_id;
+      float my_w, sel_sum, v;
+      moe_route_finish<EM, NWV>(rred, E, a.route_k, K, a.eps, lane, my_id, my_w, sel_sum, v);
+      if (lane < a.route_k) rids[lane] = my_id;
+      if (bid == 0) {  // the picks for the down projection (the next launch)
+        if (a.route_logits && lane < E) a.route_logits[lane] = v;
+        if (lane < a.route_k) {
+          a.route_ids[lane] = my_id;
+          a.route_wts[lane] = my_w / sel_sum;
+        }
+      }
+    }
+    __syncthreads();
+    ids = rids;
+  }
   if constexpr (EARLY) {  // unconditional (clamped) so no control-flow join sits between these loads and finish()
     const int it0 = min(item, total - 1);
-    item_rows<EPI, NR>(a, SPLITK ? it0 / kparts : it0, groups, R, slot, f0);
+    item_rows<EPI, NR>(a, SPLITK ? it0 / kparts : it0, groups, R, slot, f0, ids);
     if constexpr (SPLITK) kp = it0 % kparts;
     ws.load(R, kp * 64 * U, nchunks, lane);
   }
   const float xs = a.debug != 1 ? xp.finish(a.x, a.norm_w, a.eps, K, xq, xd, red) : 1.f;
   if constexpr (!EARLY && !WAIT) {
     if (item < total) {
-      item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0);
+      item_rows<EPI, NR>(a, SPLITK ? item / kparts : item, groups, R, slot, f0, ids);
       if constexpr (SPLITK) kp = item % kparts;
       ws.load(R, kp * 64 * U, nchunks, lane);
     }
@@ -184,7 +229,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
     const int cs = slot, cf = f0;
     const int next = item + stride;
     if (next < item_end) {
-      item_rows<EPI, NR>(a, SPLITK ? next / kparts : next, groups, R, slot, f0);
+      item_rows<EPI, NR>(a, SPLITK ? next / kparts : next, groups, R, slot, f0, ids);
       if constexpr (SPLITK) kp = next % kparts;
       ws.load(R, kp * 64 * U, nchunks, lane);
     }
@@ -214,12 +259,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
 }
 
 template <int QT, int EPI, int NR, int U, bool NORM, int BLOCK, bool TL = false, bool SPLITK = false,
-          bool EARLY = false>
+          bool EARLY = false, bool ROUTE = false>
 __global__ __launch_bounds__(BLOCK) void gemv_kernel(GemvArgs a) {
   // the body reads the arguments through the kernarg segment pointer (a reference to the by-value
   // parameter would make the compiler copy it to scratch)
   const GemvArgs* ka = (const GemvArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  gemv_body<QT, EPI, NR, U, NORM, BLOCK, TL, SPLITK, EARLY>(*ka, blockIdx.x, gridDim.x);
+  gemv_body<QT, EPI, NR, U, NORM, BLOCK, TL, SPLITK, EARLY, false, ROUTE>(*ka, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -400,11 +445,22 @@ static void launch_gemv_cfg(const GemvArgs& a, hipStream_t s) {
     // copy; 16 waves per CU cap the registers at 128, hence NR*U <= 4 there
     if constexpr (NR * U <= 4) {
       if (gemv_early(early_cls(EPI, a.w.K))) {
+        if constexpr (EPI == EPI_SWIGLU) {
+          if (a.route_w) {
+            if (!a.norm_w || a.w.K != 4096 || a.route_E < 1 || a.route_E > 8 || a.route_k < 1 || a.route_k > a.route_E ||
+                a.route_k != a.n_slots || !a.route_ids || !a.route_wts || !a.w.expert_stride)
+              throw std::runtime_error("gemv: routed SwiGLU needs K = 4096, norm, E <= 8, k = n_slots, outputs");
+            launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, true, true>, lds, items, a, s);
+            return;
+          }
+        }
+        if (a.route_w) throw std::runtime_error("gemv: routing is a SwiGLU form");
         if (a.norm_w) launch_early(gemv_kernel<QT, EPI, NR, U, true, 1024, false, false, true>, lds, items, a, s);
         else launch_early(gemv_kernel<QT, EPI, NR, U, false, 1024, false, false, true>, lds, items, a, s);
         return;
       }
     }
+    if (a.route_w) throw std::runtime_error("gemv: routing needs the one-block-per-CU SwiGLU form");
     if (a.w.K > 4096) {
       if constexpr (NR * U <= 4) {
         if (a.norm_w) {

@@ -178,13 +178,15 @@ __device__ __forceinline__ float reduce_rows(float (&acc)[NR], int lane) {
   }
 }
 
+// ids: the slots' expert indices (a.expert_ids, or the routed GEMV's LDS copy)
 template <int EPI, int NR>
-__device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups, RowPtr (&R)[NR], int& slot, int& f0) {
+__device__ __forceinline__ void item_rows(const GemvArgs& a, int it, int groups, RowPtr (&R)[NR], int& slot, int& f0,
+                                          const int* ids) {
   constexpr int NF = (EPI == EPI_SWIGLU) ? NR / 2 : NR;
   slot = it / groups;
   f0 = (it - slot * groups) * NF;
   const uint8_t* base = a.w.base;
-  if (a.expert_ids) base += (size_t)a.expert_ids[slot] * a.w.expert_stride;
+  if (ids) base += (size_t)ids[slot] * a.w.expert_stride;
 #pragma unroll
   for (int r = 0; r < NF; ++r) {
     if constexpr (EPI == EPI_SWIGLU) {

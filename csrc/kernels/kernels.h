@@ -62,6 +62,15 @@ struct GemvArgs {
   int n_slots = 1;                 // MoE: experts used per token
   const int* expert_ids = nullptr; // [n_slots] expert index per slot (device)
   int out_slot_stride = 0;
+  // routed SwiGLU (the single-row MoE gate/up, K = 4 x 1024): every block computes the f32 router
+  // itself - RMSNorm'd x . route_w^T, softmax, top-k - in place of reading expert_ids (one launch
+  // and one dependent boundary less per MoE layer); block 0 writes the picks for the down
+  // projection (route_ids / route_wts) and the logits (route_logits, optional)
+  const float* route_w = nullptr;  // [route_E][K] f32 router
+  int route_E = 0, route_k = 0;
+  int* route_ids = nullptr;
+  float* route_wts = nullptr;
+  float* route_logits = nullptr;
   const float* resid = nullptr;    // EPI_STORE: out = acc + resid (TP rank 0 residual)
   int debug = 0;                   // microbenchmarks only: 1 = skip the x prologue, 2 = prologue only, 3 = weights after it
   long long* dbg_clk = nullptr;    // microbenchmarks only: per-block timeline [grid][5] (instrumented build)

@@ -11,6 +11,7 @@
 #include <algorithm>
 
 #include "gemv_dev.h"
+#include "moe_route_dev.h"
 
 namespace lfk {
 
@@ -156,36 +157,12 @@ __global__ __launch_bounds__(1024) void moe_router_fused_kernel(const float* __r
   }
   __syncthreads();
   if (wave != 0) return;
-  float tot = 0.f;
-#pragma unroll
-  for (int w = 0; w < 16; ++w) tot += red[w][EM];
-  const float sc = rsqrtf(tot / (float)d + eps);
-  float v = -INFINITY;
-  if (lane < E) {
-    float sum = 0.f;
-#pragma unroll
-    for (int w = 0; w < 16; ++w) sum += red[w][lane];
-    v = sum * sc;
-    if (logits) logits[lane] = v;
-  }
-  // softmax + top-k (lowest index on ties) + renormalise: as moe_route_kernel
-  const float m = wave_max(v);
-  float p = lane < E ? __expf(v - m) : 0.f;
-  p /= wave_sum(p);
-  float taken = lane < E ? p : -1.f, sel_sum = 0.f, my_w = 0.f;
-  int my_id = 0;
-  for (int j = 0; j < k; ++j) {
-    float best = taken;
-    int bi = lane;
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    if (lane == j) { my_id = bi; my_w = best; }
-    sel_sum += best;
-    if (lane == bi) taken = -1.f;
-  }
+  // softmax + top-k (lowest index on ties) + renormalise (moe_route_dev.h, shared with the
+  // routed SwiGLU GEMV)
+  int my_id;
+  float my_w, sel_sum, v;
+  moe_route_finish<EM, 16>(red, E, k, d, eps, lane, my_id, my_w, sel_sum, v);
+  if (logits && lane < E) logits[lane] = v;
   if (wd) {
     // dense row: lane e < E finds its own weight among the k picks (lanes 0..k-1 hold them)
     float* row = wd + (size_t)blockIdx.x * ld_dense;

@@ -312,6 +312,7 @@ void Engine::alloc_buffers() {
   // single-row decode: attention + Wo in one launch (attn_wo1); per-layer done counters, zeroed
   // by every decode step's embedding launch
   if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
+  if (const char* e = std::getenv("LFK_MOE_ROUTE_FUSE")) moe_route_fuse_ = e[0] != '0';  // A/B (test_engine_gpu)
   if (wo_fuse_ && nkv_l_ <= 64) {
     HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
     *wo_err_h_ = 0;
@@ -667,7 +668,13 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   }
 
   if (hp_.n_expert > 0) {
-    if (moe_router_fused_ok(L.router.type, hp_.n_expert, d)) {  // one launch: norm + f32 router + top-k
+    // the router inside the gate/up GEMV's blocks (each block routes the token itself, block 0
+    // writes the picks for the down projection): one launch and one dependent boundary less
+    const bool route_in_gu = moe_route_fuse_ && moe_router_fused_ok(L.router.type, hp_.n_expert, d) &&
+                             hp_.n_expert <= 8 && d == 4096;
+    if (route_in_gu) {
+      // (routing happens in the gate/up launch below)
+    } else if (moe_router_fused_ok(L.router.type, hp_.n_expert, d)) {  // one launch: norm + f32 router + top-k
       moe_router_fused(x_, L.ffn_norm, hp_.rms_eps, reinterpret_cast<const float*>(L.router.base), d, hp_.n_expert,
                        hp_.n_expert_used, router_logits_, moe_ids_, moe_w_, s);
     } else {
@@ -680,6 +687,11 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
     GemvArgs g;
     g.w = L.gu_exps; g.x = x_; g.norm_w = L.ffn_norm; g.eps = hp_.rms_eps;
     g.out = hf_; g.n_out = F_l_; g.n_slots = hp_.n_expert_used; g.expert_ids = moe_ids_; g.out_slot_stride = F_l_;
+    if (route_in_gu) {
+      g.route_w = reinterpret_cast<const float*>(L.router.base);
+      g.route_E = hp_.n_expert; g.route_k = hp_.n_expert_used;
+      g.route_ids = moe_ids_; g.route_wts = moe_w_; g.route_logits = router_logits_;
+    }
     gemv(g, EPI_SWIGLU, s);
     MoeDownArgs md;
     md.w = L.down_exps; md.h = hf_; md.expert_ids = moe_ids_; md.expert_w = moe_w_; md.n_slots = hp_.n_expert_used;

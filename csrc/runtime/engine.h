@@ -387,6 +387,7 @@ class Engine : public SlotBackend {
   // streams its weights while the attention runs and starts once every kv head is done
   // (dec_done_); a timed-out wait sets *wo_err_ (host-mapped). LFK_WO_FUSE=0: two launches (A/B).
   bool wo_fuse_ = true;
+  bool moe_route_fuse_ = true;  // single-row MoE: the router inside the gate/up GEMV (LFK_MOE_ROUTE_FUSE A/B)
   int* wo_err_h_ = nullptr;   // host view
   int* wo_err_ = nullptr;     // device view
   int* dec_done_ = nullptr;   // single-row decode: [n_layer][64] done counters (attn_wo1)

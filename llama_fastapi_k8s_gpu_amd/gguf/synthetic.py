@@ -131,6 +131,10 @@ SPECS: Dict[str, ModelSpec] = {
     # shapes are the 70B's own (1 KV head, 8 query heads, 3584 FFN features per rank)
     "llama3-70b-2l": ModelSpec("llama3-70b-2l", 8192, 2, 64, 8, 28672, 0, 500000.0, "bpe", "q4_k_m",
                                n_ctx_train=1024, size_class="70B"),
+    # Mixtral's width (d = 4096, 8 experts, top-2) in one layer: the single-row decode routes
+    # inside the gate/up GEMV at this width (csrc/kernels/gemv.hip, GemvArgs::route_w)
+    "tiny-mixtral-d4k": ModelSpec("tiny-mixtral-d4k", 4096, 1, 32, 8, 512, 0, 1e6, "spm", "q4_k_m",
+                                  n_expert=8, n_expert_used=2, n_ctx_train=1024),
     "tiny-llama3-f32": ModelSpec("tiny-llama3-f32", 128, 2, 2, 1, 256, 0, 500000.0, "bpe", "f32",
                                  n_ctx_train=512),
 }

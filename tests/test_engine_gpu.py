@@ -141,6 +141,34 @@ def test_attention_weight_touch_is_transparent(models, spec, monkeypatch):
             assert rel_err(a, b) < 1e-2, (spec, rel_err(a, b))
 
 
+def test_moe_routing_inside_gate_up_matches_router_launch(tmp_path, monkeypatch):
+    """Single-row MoE decode at Mixtral's width (d = 4096, 8 experts, top-2): every block of the
+    gate/up GEMV routes the token itself (LFK_MOE_ROUTE_FUSE=1, the default) instead of a router
+    launch before it. The routing is summed in the router kernel's order (bit-identical picks),
+    so the logits match the two-launch form up to the split-K atomics' fp32 order (which flips
+    q8 roundings of the next activations: ~1e-2, as test_attention_weight_touch_is_transparent),
+    eager and graph, and stay within the fp32 decode emulation's tolerance."""
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    path = write_synthetic_gguf("tiny-mixtral-d4k", str(tmp_path / "mx4k.gguf"), seed=6)
+    toks = [int(t) for t in np.random.default_rng(8).integers(3, 1000, 28)]
+    out = {}
+    for mode, graph in (("0", False), ("1", False), ("1", True)):
+        monkeypatch.setenv("LFK_MOE_ROUTE_FUSE", mode)
+        eng = _engine(path, graph=graph)
+        eng.eval_logits(toks[:20], 0)
+        out[(mode, graph)] = [eng.decode_logits(toks[i], i) for i in range(20, 26)]
+        assert eng.healthy
+        del eng
+    for key in (("1", False), ("1", True)):
+        for a, b in zip(out[("0", False)], out[key]):
+            assert rel_err(b, a) < 1e-2, (key, rel_err(b, a))
+    emu = ReferenceLlama(GGUFReader(path), n_ctx=256)
+    emu.forward(toks[:20], 0, path="prefill")
+    for j, i in enumerate(range(20, 26)):
+        e = rel_err(out[("1", True)][j], emu.forward([toks[i]], i, path="decode").numpy())
+        assert e < 1.5e-2, ("decode", i, e)
+
+
 def test_moe_grouped_prefill_chunked(models):
     """Grouped expert prefill (device-side routing, per-expert row counts) is independent of
     how the prompt is chunked: n_batch 16 (3 chunks, partial last) == n_batch 128 (one chunk)."""
