@@ -546,6 +546,10 @@ void Engine::p2p_open(const std::vector<std::string>& handles) {
 // P2P regions carry the fused area (one launch per projection instead of two, no tmp_ copy)
 bool Engine::tp_epilogue(GemvArgs& g) const {
   if (!p2p_ || !p2p_->ready() || p2p_->fused_n() < hp_.n_embd || g.n_out > p2p_->fused_n()) return false;
+  // more than two ranks on ONE GPU (the eight-rank rehearsal): a waiting epilogue needs every
+  // peer's GEMV resident at once, and eight single-queue processes are not reliably co-scheduled
+  // (runs of 15 s to > 170 s, r4) - the separate collective kernel's short waits are
+  if (p2p_->shared_device() && p2p_->world() > 2) return false;
   g.tp_peers = p2p_->peers();
   g.tp_world = p2p_->world(); g.tp_rank = p2p_->rank();
   g.tp_stride = p2p_->stride(); g.tp_off = p2p_->fused_offset();

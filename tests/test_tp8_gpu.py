@@ -13,7 +13,8 @@ logits within 2e-2 of TP = 1 and no further from the exact model than TP = 1 is 
 decode steps read the K/V the bf16 / f16 prefill wrote, and eight-way sharded sums over
 8192-wide rows flip more of those roundings than test_tp_gpu.py's two-way ones (measured
 1.1-1.4 % vs TP = 1, r4); greedy generations identical or diverging at a near-tie of the TP = 1
-logits, two rows of continuous batching identical, every rank healthy.
+logits, two rows of continuous batching identical or diverging at a near-tie of the exact model,
+every rank healthy.
 """
 import os
 
@@ -42,6 +43,7 @@ def _exercise(llm):
         res = list(ex.map(lambda i: llm.create_completion([1, 7 + i, 11, 19 + i], max_tokens=8, temperature=0.0),
                           range(2)))
     out["batched"] = [x["choices"][0]["text"] for x in res]
+    out["batched_tokens"] = [llm.tokenize(t.encode(), add_bos=False, special=True) for t in out["batched"]]
     out["healthy"] = bool(llm.health()["ok"])
     return out
 
@@ -85,7 +87,18 @@ def _worker(rank, world, port, path, q):
             with torch.no_grad():
                 exact = [ex.forward(allt[:24], 0).cpu().numpy()]
                 exact += [ex.forward([allt[24 + i]], 24 + i).cpu().numpy() for i in range(3)]
+                # a batched row whose greedy text differs: the exact model's margin between the two
+                # engines' tokens at the first difference (near-tie judgement, as test_tp_gpu.py)
+                bties = []
+                for i, (ta, tb) in enumerate(zip(got["batched_tokens"], ref["batched_tokens"])):
+                    j = next((n for n, (x, y) in enumerate(zip(ta, tb)) if x != y), None)
+                    if got["batched"][i] == ref["batched"][i] or j is None:
+                        bties.append(None)
+                        continue
+                    lg = ex.forward([1, 7 + i, 11, 19 + i] + list(tb[:j]), 0).cpu().numpy()
+                    bties.append(float(abs(lg[ta[j]] - lg[tb[j]]) / np.abs(lg).max()))
             del ex
+            got["batched_ties"] = bties
             result = (got, ref, k, tie, exact)
         dist.barrier()
         q.put((rank, result, None))
@@ -129,10 +142,14 @@ def test_tensor_parallel_eight_ranks_70b_width(tmp_path):
     e_1 = [_rel(a, x) for a, x in zip([ref["prefill"]] + ref["decode"], exact)]
     report = {"vs_tp1": [round(v, 5) for v in d], "err_tp": [round(v, 5) for v in e_tp],
               "err_tp1": [round(v, 5) for v in e_1], "greedy_diverge_at": k, "tie": tie,
-              "batched_same": [a == b for a, b in zip(got["batched"], ref["batched"])]}
+              "batched_same": [a == b for a, b in zip(got["batched"], ref["batched"])],
+              "batched_ties": got["batched_ties"]}
     print("TP8 report:", report)
     assert d[0] <= 5e-3 and max(d[1:]) <= 2e-2, report
     assert all(t <= o + 5e-3 for t, o in zip(e_tp, e_1)), report
     assert k is None or tie <= 2e-2, report
-    assert got["batched"] == ref["batched"], report
+    # continuous batching under TP = 8: every row's text equal, or diverging at a near-tie of the
+    # exact model (eight-way sharded sums move the batched rows' logits ~1 %, measured r4)
+    assert all(a == b or (t is not None and t <= 2e-2)
+               for a, b, t in zip(got["batched"], ref["batched"], got["batched_ties"])), report
     assert got["healthy"], report
