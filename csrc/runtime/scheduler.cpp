@@ -201,6 +201,9 @@ void BatchScheduler::loop() {
         if (chunk > 0 && decoding && (int)r->prompt.size() - keep > chunk) {
           r->n_keep = keep;
           r->n_done = keep;
+          // the parts overwrite the slot's KV from `keep` on: only that prefix of the previous
+          // occupant's history stays valid, whether or not this request completes its prefill
+          if ((int)slot_hist_[slot].size() > keep) slot_hist_[slot].resize(keep);
           prefilling.push_back(r);
           continue;
         }

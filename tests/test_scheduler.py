@@ -229,3 +229,31 @@ def test_cancel_while_prefilling_in_parts():
     assert toks == sequential(p, 6, 512)
     sched.cancel(first)
     sched.shutdown()
+
+
+def test_cancelled_part_admission_does_not_leave_a_stale_prefix():
+    """A chunked admission overwrites its slot's KV from the reused prefix on. Cancelled
+    mid-prefill, the slot must not still advertise the previous occupant's history: a later
+    prompt extending that history may reuse only the prefix both requests shared (the fake
+    engine raises 'reused prefix differs' otherwise)."""
+    eng, sched = make(n_slots=3, max_batch=2, n_ctx=512, step_us=2000)
+    eng.set_prefill_chunk(8)
+    p = list(range(50, 90))
+    ta, _ = run(sched, sched.submit(p, 3, {}, []))         # idle engine: admitted whole, slot s
+    first = sched.submit([1, 2], 400, {}, [])              # decodes in the other slot
+    assert sched.wait(first, 0, 5000)["tokens"]
+    q = p[:10] + list(range(600, 890))                     # shares 10 tokens with p: slot s, keep 10
+    rid = sched.submit(q, 5, {}, [])
+    time.sleep(0.01)
+    sched.cancel(rid)
+    r = sched.wait(rid, 0, 5000)
+    while not r["done"]:
+        r = sched.wait(rid, 0, 5000)
+    assert r["finish"] == "cancelled"
+    sched.release(rid)
+    p2 = p + ta[:-1] + [ta[-1], 7, 7]                      # the follow-up turn of the first request
+    t2, r2 = run(sched, sched.submit(p2, 4, {}, []))
+    assert r2["finish"] == "length", r2.get("error")
+    assert t2 == sequential(p2, 4, 512)
+    sched.cancel(first)
+    sched.shutdown()
