@@ -253,7 +253,9 @@ float* Engine::upload_f32(const GGUFFile& f, const std::string& name) {
 void Engine::load(const GGUFFile& f) {
   const int r = opt_.tp_rank;
   const int d = hp_.n_embd, hd = hp_.head_dim;
-  tok_embd_ = upload_matrix(f, "token_embd.weight", 0, hp_.n_vocab, 0, d);
+  // only the stage that starts at layer 0 gathers embeddings (a hybrid / layer-split stage past
+  // it takes hidden states in)
+  if (opt_.layer_begin == 0) tok_embd_ = upload_matrix(f, "token_embd.weight", 0, hp_.n_vocab, 0, d);
   if (has_head()) {  // (a layer-split stage before the last holds no head)
     out_norm_ = upload_f32(f, "output_norm.weight");
     const std::string out_name = f.find("output.weight") ? "output.weight" : "token_embd.weight";
@@ -297,7 +299,8 @@ void Engine::alloc_buffers() {
   logits_ = (float*)dalloc(sizeof(float) * V_pad_);
   logits_l_ = (float*)dalloc(sizeof(float) * V_l_);
   HIPCHK(hipMemset(logits_l_, 0, sizeof(float) * V_l_));
-  const size_t kv = (size_t)hp_.n_layer * nkv_l_ * opt_.n_ctx * hd;
+  // KV of this engine's layers only (a layer-split / hybrid stage holds its range's part)
+  const size_t kv = (size_t)(layer_end_ - opt_.layer_begin) * nkv_l_ * opt_.n_ctx * hd;
   const int NS = opt_.n_slots;
   slot_stride_ = kv;
   kc_ = (__half*)dalloc(kv * 2 * NS);
@@ -621,8 +624,8 @@ void Engine::enqueue_layer_decode(int l, hipStream_t s) {
   qa.wq = L.wq; qa.wk = L.wk; qa.wv = L.wv;
   qa.x = x_; qa.norm_w = L.attn_norm; qa.eps = hp_.rms_eps;
   qa.q_out = q_;
-  qa.k_cache = kc_ + slot_stride_ * dslot_ + kv_layer * l;
-  qa.v_cache = vc_ + slot_stride_ * dslot_ + kv_layer * l;
+  qa.k_cache = kc_ + slot_stride_ * dslot_ + kv_layer * (l - opt_.layer_begin);
+  qa.v_cache = vc_ + slot_stride_ * dslot_ + kv_layer * (l - opt_.layer_begin);
   qa.n_ctx = opt_.n_ctx; qa.head_dim = hd;
   qa.pos = st + S_POS;
   qa.rope = rope_;
@@ -745,12 +748,14 @@ void Engine::enqueue_head(const float* xrow, int advance_pos, hipStream_t s, int
 
 void Engine::enqueue_decode(hipStream_t s) {
   // (the embedding launch also zeroes the layers' attention -> Wo done counters)
+  if (!tok_embd_.base) throw std::runtime_error("decode: this stage starts past layer 0 (hidden states in)");
   embed_rows(tok_embd_, state_ + (size_t)S_NSTATE * dslot_ + S_TOKEN, 1, x_, s, dec_done_, 64 * hp_.n_layer);
   for (int l = opt_.layer_begin; l < layer_end_; ++l) enqueue_layer_decode(l, s);
   enqueue_head(x_, 1, s, dslot_);
 }
 
 void Engine::enqueue_prefill(int T, int pos0, hipStream_t s, bool embed) {
+  if (embed && !tok_embd_.base) throw std::runtime_error("prefill: this stage starts past layer 0 (hidden states in)");
   if (embed) embed_rows(tok_embd_, tokens_, T, x_, s);
   for (int l = opt_.layer_begin; l < layer_end_; ++l) enqueue_rows_layer(l, T, pos0, false, s);
 }
@@ -781,8 +786,8 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       g.w = L.wv; g.out = qkv_ + nq_ + nkvd_; gemm_dq(g, GEMM_STORE, s);
     }
     if (!batched && segs_) {  // packed prompts: per-row slot / position, attention per piece
-      __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; + slot * slot_stride_
-      __half* vcl = vc_ + kv_layer * l;
+      __half* kcl = kc_ + kv_layer * (l - opt_.layer_begin);  // slot 0's layer l; + slot * slot_stride_
+      __half* vcl = vc_ + kv_layer * (l - opt_.layer_begin);
       rope_kv_prefill(qkv_, T, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, rpos_, rslots_, slot_stride_);
       for (const PrefillSeg& g : *segs_) {
         AttnPrefillArgs pa;
@@ -796,8 +801,8 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
         attn_prefill(pa, s);
       }
     } else if (!batched) {
-      __half* kcl = kc_ + slot_stride_ * kv_slot_ + kv_layer * l;
-      __half* vcl = vc_ + slot_stride_ * kv_slot_ + kv_layer * l;
+      __half* kcl = kc_ + slot_stride_ * kv_slot_ + kv_layer * (l - opt_.layer_begin);
+      __half* vcl = vc_ + slot_stride_ * kv_slot_ + kv_layer * (l - opt_.layer_begin);
       rope_kv_prefill(qkv_, T, pos0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s);
       AttnPrefillArgs pa;
       pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.T = T; pa.pos0 = pos0; pa.n_ctx = opt_.n_ctx;
@@ -807,8 +812,8 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       pa.out_stride = nq_;
       attn_prefill(pa, s);
     } else {  // T decode rows, each of its own KV slot and position
-      __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
-      __half* vcl = vc_ + kv_layer * l;
+      __half* kcl = kc_ + kv_layer * (l - opt_.layer_begin);  // slot 0's layer l; the kernels add slot * slot_stride_
+      __half* vcl = vc_ + kv_layer * (l - opt_.layer_begin);
       rope_kv_prefill(qkv_, T, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, bpos_, bslots_, slot_stride_);
       AttnDecodeArgs aa;
       aa.q = q_; aa.k_cache = kcl; aa.v_cache = vcl; aa.pos = bpos_;
@@ -1072,8 +1077,8 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     if (tp) allreduce_into(tmp_, x_, (size_t)B * d, s);
   };
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
-  __half* kcl = kc_ + kv_layer * l;  // slot 0's layer l; the kernels add slot * slot_stride_
-  __half* vcl = vc_ + kv_layer * l;
+  __half* kcl = kc_ + kv_layer * (l - opt_.layer_begin);  // slot 0's layer l; the kernels add slot * slot_stride_
+  __half* vcl = vc_ + kv_layer * (l - opt_.layer_begin);
   // RoPE + KV append in the Q|K|V epilogue when the whole K fits one LDS-staged part
   const bool fused = B <= kBmmMaxRows && bmm_qkv_fits(d, B);
   // attention / FFN RMSNorm folded into the one-part projections' x staging (no prep launch)
@@ -1933,7 +1938,7 @@ void Engine::kv_transfer(void* buf, int n, bool load) {
   if (n < 0 || n > opt_.n_ctx) throw std::runtime_error("kv_transfer: n out of range");
   if (n == 0) return;
   const size_t row = (size_t)n * hp_.head_dim * 2, pitch = (size_t)opt_.n_ctx * hp_.head_dim * 2;
-  const size_t rows = (size_t)hp_.n_layer * nkv_l_;
+  const size_t rows = (size_t)(layer_end_ - opt_.layer_begin) * nkv_l_;
   char* b = static_cast<char*>(buf);
   for (int which = 0; which < 2; ++which) {
     char* cache = reinterpret_cast<char*>(which == 0 ? kc_ : vc_);

@@ -95,7 +95,7 @@ class Engine : public SlotBackend {
   static constexpr int kStepClkBlocks = 8192;
   std::vector<long long> step_clk();
   void step_clk_zero();
-  size_t kv_state_bytes(int n) const { return 2ull * hp_.n_layer * nkv_l_ * (size_t)n * hp_.head_dim * 2; }
+  size_t kv_state_bytes(int n) const { return 2ull * (layer_end_ - opt_.layer_begin) * nkv_l_ * (size_t)n * hp_.head_dim * 2; }
   void kv_transfer(void* buf, int n, bool load);
   // hybrid placement: hidden states [T][d] of layer `layer_begin` in, last-row logits out
   std::vector<float> eval_hidden(const float* x, int T, int pos0);

@@ -109,6 +109,11 @@ class Llama:
                                           main_gpu=main_gpu, n_threads=n_threads, n_batch=n_batch)
         elif kind == "layer":
             from ..runtime.layer_split_backend import LayerSplitBackend
+            if int(kwargs.get("max_batch", 1) or 1) > 1:
+                raise ValueError("split_mode='layer' across GPUs runs one generation at a time: max_batch > 1 "
+                                 "needs split_mode='row' (tensor parallelism) or a single GPU")
+            if main_gpu != 0:
+                logger.warning("split_mode='layer': main_gpu=%d is ignored (stage i runs on device i)", main_gpu)
             self._backend = LayerSplitBackend(model_path, self.hparams, tensor_split=tensor_split or [1.0],
                                               n_ctx=self._n_ctx, n_batch=n_batch,
                                               layer_devices=kwargs.get("layer_devices"))

@@ -12,9 +12,12 @@ chain (bit-identical uniforms, as the hybrid backend). One MI355X holds every BA
 compatibility placement, not a speed-up: a single decode still walks every layer in
 order. Tensor parallelism (``split_mode="row"``) is the multi-GPU speed path.
 
-Layer assignment follows llama.cpp: with ``tensor_split`` normalised to cumulative
-fractions ``c_0 < c_1 < ... = 1``, layer ``l`` goes to the first device ``i`` with
-``l / n_layer < c_i``.
+Layer assignment follows llama.cpp's full-offload rule: with ``tensor_split`` normalised to
+cumulative fractions ``c_0 < c_1 < ... = 1``, layer ``l`` goes to the first device ``i`` with
+``l / (n_layer + 1) < c_i`` - the divisor counts the output layer as one more offloaded layer,
+which lands on the last device. (The reference ships no llama.cpp source, so this parity is
+from the upstream rule as recalled, pinned by tests/test_layer_split.py, not checked against a
+file.)
 """
 from __future__ import annotations
 
@@ -41,7 +44,7 @@ def layer_ranges(n_layer: int, tensor_split: Sequence[float]) -> List[Tuple[int,
     cum[-1] = 1.0 + 1e-9  # (rounding: the last device with weight takes the remainder)
     dev_of = []
     for layer in range(n_layer):
-        f = layer / n_layer
+        f = layer / (n_layer + 1)   # the output layer counts as layer n_layer
         dev_of.append(next(i for i, c in enumerate(cum) if f < c and w[i] > 0))
     out: List[Tuple[int, int, int]] = []
     for layer, dv in enumerate(dev_of):

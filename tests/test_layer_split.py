@@ -12,12 +12,14 @@ from llama_fastapi_k8s_gpu_amd.runtime.layer_split_backend import LayerSplitBack
 
 
 @pytest.mark.parametrize("n_layer,ts,want", [
-    (32, [1, 1], [(0, 0, 16), (1, 16, 32)]),
-    (32, [3, 1], [(0, 0, 24), (1, 24, 32)]),
-    (80, [1] * 8, [(i, 10 * i, 10 * i + 10) for i in range(8)]),
-    (4, [1, 0, 1], [(0, 0, 2), (2, 2, 4)]),          # a zero entry: that GPU gets no layer
-    (3, [1, 1, 1, 1], [(0, 0, 1), (1, 1, 2), (2, 2, 3)]),  # more GPUs than layers
-    (5, [2, 1], [(0, 0, 4), (1, 4, 5)]),             # l / n_layer < 2/3 -> device 0 for l = 0..3
+    # l / (n_layer + 1) < c_i (the output layer counts as one more): 2 x 32 -> 17 + 15 (+ head)
+    (32, [1, 1], [(0, 0, 17), (1, 17, 32)]),
+    (32, [3, 1], [(0, 0, 25), (1, 25, 32)]),         # l / 33 < 0.75 -> l <= 24
+    (80, [1] * 8, [(i, b, e) for i, (b, e) in enumerate(
+        [(0, 11), (11, 21), (21, 31), (31, 41), (41, 51), (51, 61), (61, 71), (71, 80)])]),
+    (4, [1, 0, 1], [(0, 0, 3), (2, 3, 4)]),          # a zero entry: that GPU gets no layer
+    (3, [1, 1, 1, 1], [(0, 0, 1), (1, 1, 2), (2, 2, 3)]),  # more GPUs than layers (l / 4 < 1/4, 2/4, 3/4)
+    (5, [2, 1], [(0, 0, 4), (1, 4, 5)]),             # l / 6 < 2/3 -> device 0 for l = 0..3
 ])
 def test_layer_ranges_follow_llama_cpp(n_layer, ts, want):
     got = layer_ranges(n_layer, ts)
@@ -61,13 +63,13 @@ def _backend(ts, n_batch=4, V=50, n_layer=6):
 
 def test_stage_chain_order_and_chunks():
     be, log = _backend([1, 2], n_batch=4)
-    assert [(s.b, s.e, s.device) for s in be.stages] == [(0, 2, 0), (2, 6, 1)]
+    assert [(s.b, s.e, s.device) for s in be.stages] == [(0, 3, 0), (3, 6, 1)]
     logits = be.eval_logits([5, 6, 7, 8, 9, 10], 3)
     # two prompt chunks (4 + 2 tokens) at positions 3 and 7, each through stage 0 then stage 1
-    assert log == [(0, 3, 4), (2, 3, 4), (0, 7, 2), (2, 7, 2)]
+    assert log == [(0, 3, 4), (3, 3, 4), (0, 7, 2), (3, 7, 2)]
     assert int(np.argmax(logits)) == (10 + 6) % 50       # token 10 plus 6 layers
     h = be.health()
-    assert h["ok"] and h["backend"] == "layer" and h["stages"] == [[0, 0, 2], [1, 2, 6]]
+    assert h["ok"] and h["backend"] == "layer" and h["stages"] == [[0, 0, 3], [1, 3, 6]]
     assert be.device_memory() == {"hip:0": 100, "hip:1": 100}
 
 

@@ -1,5 +1,6 @@
 """split_mode=LAYER across stages (runtime/layer_split_backend.py) on the GPU: three HIP engines
-over layer ranges [0, 1), [1, 2), [2, 4) of a 4-layer model, rehearsed on device 0 (one GPU box;
+over layer ranges [0, 2), [2, 3), [3, 4) of a 4-layer model (tensor_split 1:1:2, llama.cpp's
+l / (n_layer + 1) rule), rehearsed on device 0 (one GPU box;
 on a node each stage sits on its own GPU), against the whole model in one engine. The stages run
 the same kernels on the same fp32 hidden states, so the prompt logits agree to rounding of the
 identical path (tight), and greedy generation matches the single engine's eval path token by
@@ -30,8 +31,11 @@ def test_layer_split_matches_whole_model(path):
     split = Llama(path, split_mode="layer", tensor_split=[1, 1, 2], layer_devices=[0, 0, 0], **kw)
     be = split._backend
     assert split.backend_name == "layer"
-    assert [(s.layer_begin, s.layer_end, s.has_head) for s in be.stages] == [(0, 1, False), (1, 2, False), (2, 4, True)]
+    assert [(s.layer_begin, s.layer_end, s.has_head) for s in be.stages] == [(0, 2, False), (2, 3, False), (3, 4, True)]
     whole = load_hip().Engine(path, n_ctx=128, n_batch=32, device=0, use_graph=False)
+    # each stage holds the KV of its own layers only, and only the first one the embedding
+    assert [s.kv_state_bytes(10) for s in be.stages] == [whole.kv_state_bytes(10) * n // 4 for n in (2, 1, 1)]
+    assert be.stages[1].device_bytes < be.stages[0].device_bytes
     toks = [int(t) for t in np.random.default_rng(4).integers(3, 400, 40)]
     # a 40-token prompt: chunks of 32 + 8 tokens through all three stages
     got = be.eval_logits(toks, 0)
