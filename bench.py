@@ -15,7 +15,8 @@ GPUs: ``--gpus N`` runs N ranks, one process per GPU. Without ``WORLD_SIZE`` in 
 environment and N > 1, bench.py starts ``torch.distributed.run`` itself (before anything
 touches a GPU) and exits with its status; under a launcher, ``WORLD_SIZE`` must equal N.
 
-Parallelism (``--parallel``, default ``auto`` = ``dp``):
+Parallelism (``--parallel``, default ``auto`` = ``dp``; the JSON records both the requested and
+the resolved mode):
   * ``tp``: ONE model row-split over the N GPUs (BASELINE configs "8B tensor_split across
     2 MI355X", "70B across 8"): heads / FFN / vocabulary sharded, two all-reduces per
     layer (one-shot P2P kernel over xGMI for decode messages, RCCL for prefill), rank 0
@@ -27,6 +28,15 @@ Parallelism (``--parallel``, default ``auto`` = ``dp``):
     MI355X's 288 GB many times over, and a decode step sharded N ways pays two all-reduces per
     layer for 1/N of a weight stream that takes ~1.7 ms whole - replicas are the throughput
     configuration; ``tp`` is the latency / memory configuration and stays selectable.
+
+TP pass (``--tp-pass``, default ``auto`` = on when N > 1): after the data-parallel headline is
+measured, every rank frees its engine and rank 0 runs ONE tensor-parallel pass over the same N
+GPUs in a fresh ``torch.distributed.run`` child (its own process group; the DP ranks wait at a
+gloo barrier and touch no GPU meanwhile), bounded by ``--tp-timeout`` seconds. Its result -
+tokens/s at C clients, p50, the serial rate, and which comm path each TP message takes with the
+rank count RCCL reports (``Engine.comm_info``) - goes into ``config.tp`` (BASELINE's "8B across 2
+MI355X, RCCL all-reduce" at N = 2; ``--tp-model llama3-70b-q4_k_m`` for "70B across 8"). A failed
+or timed-out pass is recorded there with its error and never touches the DP headline.
 
 Load: ``--clients C`` concurrent clients (default 6 = the reference pod's admission
 capacity, 1 in flight + MAX_QUEUE_SIZE 5, reference api.py:19,113) post the K timed
@@ -44,12 +54,15 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import datetime
 import json
 import os
+import signal
 import socket
 import statistics
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -105,6 +118,65 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+# torchrun's per-rank environment: a TP-pass child must start a launcher of its own without it
+_LAUNCHER_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                  "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+
+
+def tp_pass_cmd(args, world: int, json_out: str) -> list:
+    """The TP child: this script under its own torch.distributed.run, --parallel tp over `world` GPUs."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+            "--gpus", str(world), "--parallel", "tp", "--model", args.tp_model or args.model,
+            "--steps", str(args.tp_steps), "--warmup", "1", "--serial-steps", "1", "--tp-pass", "off",
+            "--clients", str(args.clients), "--max-batch", str(args.max_batch), "--n-ctx", str(args.n_ctx),
+            "--model-dir", args.model_dir, "--json-out", json_out]
+
+
+def run_tp_pass(cmd: list, json_out: str, timeout_s: float, heartbeat_s: float = 60.0) -> dict:
+    """Run the TP child (its own session, launcher variables dropped) for at most `timeout_s`;
+    returns its result block, or {"ok": False, "error": ...} - it never raises."""
+    t0 = time.time()
+    log_path = json_out + ".log"
+    env = {k: v for k, v in os.environ.items() if k not in _LAUNCHER_VARS and not k.startswith("TORCHELASTIC_")}
+    try:
+        with open(log_path, "w") as log:
+            proc = subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+            next_beat = t0 + heartbeat_s
+            while proc.poll() is None:
+                now = time.time()
+                if now - t0 > timeout_s:
+                    try:
+                        os.killpg(proc.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    proc.wait()
+                    raise TimeoutError(f"TP pass timed out after {timeout_s:.0f} s")
+                if now >= next_beat:
+                    print(f"[bench] tp pass running ({now - t0:.0f} s)", file=sys.stderr, flush=True)
+                    next_beat += heartbeat_s
+                time.sleep(0.5)
+        if proc.returncode != 0:
+            raise RuntimeError(f"TP pass exited with status {proc.returncode}")
+        with open(json_out) as f:
+            res = json.load(f)
+    except Exception as e:
+        tail = ""
+        try:
+            with open(log_path, errors="replace") as f:
+                tail = f.read()[-2000:]
+        except OSError:
+            pass
+        return {"ok": False, "error": f"{type(e).__name__}: {e}", "wall_s": round(time.time() - t0, 1),
+                "log": log_path, "log_tail": tail}
+    cfg = res.get("config", {})
+    return {"ok": True, "model": cfg.get("model"), "parallelism": cfg.get("parallelism"), "scaling": "strong",
+            "value": res.get("value"), "unit": res.get("unit"), "ms_per_step": res.get("ms_per_step"),
+            "p50_response_ms": cfg.get("p50_response_ms"), "requests": cfg.get("requests"),
+            "avg_output_tokens": cfg.get("avg_output_tokens"), "serial": cfg.get("serial"),
+            "comm": cfg.get("comm"), "wall_s": round(time.time() - t0, 1)}
+
+
 def _launch_ranks(n: int) -> int:
     """Start n ranks of this script under torch.distributed.run (no GPU touched here)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -126,6 +198,12 @@ def main() -> int:
                     help="requests of the one-client serial run after the timed run (-1: max(2, steps // 4))")
     ap.add_argument("--model-dir", default=os.environ.get("SYNTH_MODEL_DIR", os.path.join(
         os.environ.get("TMPDIR", "/tmp"), "llama_amd_models")))
+    ap.add_argument("--tp-pass", choices=["auto", "on", "off"], default="auto",
+                    help="N > 1: a tensor-parallel pass over the same GPUs after the DP headline (config.tp)")
+    ap.add_argument("--tp-model", default="", help="model of the TP pass (default: --model)")
+    ap.add_argument("--tp-steps", type=int, default=2, help="timed rounds of the TP pass")
+    ap.add_argument("--tp-timeout", type=float, default=480.0, help="wall bound of the TP pass (s)")
+    ap.add_argument("--json-out", default="", help="also write rank 0's JSON result to this file")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -144,9 +222,11 @@ def main() -> int:
 
     import torch
     import torch.distributed as dist
+    tp_pass = world > 1 and parallel == "dp" and args.tp_pass != "off"
     if world > 1:
-        # control plane only (barriers, object broadcasts): the engine runs its own collectives
-        dist.init_process_group("gloo")
+        # control plane only (barriers, object broadcasts): the engine runs its own collectives.
+        # (the DP ranks wait out rank 0's TP pass at a barrier: the timeout covers it)
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=1800 + args.tp_timeout))
 
     def barrier():
         if world > 1:
@@ -187,6 +267,7 @@ def main() -> int:
         dist.destroy_process_group()
         return 0
 
+    comm = llm._backend.engine.comm_info() if tp and hasattr(getattr(llm, "_backend", None), "engine") else None
     eng = CountingEngine(llm)
     settings = Settings()
     settings.timeout_seconds = BENCH_TIMEOUT_S  # measure latency, do not 408 long generations in the bench
@@ -238,6 +319,7 @@ def main() -> int:
 
     elapsed, n0, n1, serial_s = asyncio.run(run())
     llm.close()   # TP: publishes STOP, the followers' follow() returns
+    del app, eng.llm
     toks = sum(eng.completion_tokens[n0:n1])
     ptoks = sum(eng.prompt_tokens[n0:n1])
     s_toks = sum(eng.completion_tokens[n1:])
@@ -260,7 +342,9 @@ def main() -> int:
         model_label = ("Llama-3-8B Q4_K_M" if args.model == "llama3-8b-q4_k_m"
                        else f"{_spec.name} {_spec.quant.upper()}" if _spec is not None else args.model)
         res = {
-            "metric": METRIC, "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+            # BASELINE.json's metric string names the headline model; another --model names itself
+            "metric": METRIC if args.model == "llama3-8b-q4_k_m" else METRIC.replace("Llama-3-8B Q4_K_M", model_label),
+            "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "strong" if tp else "weak",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
@@ -270,6 +354,7 @@ def main() -> int:
             "config": {"model": model_label,
                        "global_batch": (1 if tp else world) * min(args.clients, max_batch),
                        "seq_len": args.n_ctx, "parallelism": f"{'tp' if tp else 'dp'}{world}",
+                       "parallel_requested": args.parallel,
                        "clients_per_group": args.clients, "max_batch": max_batch,
                        "p50_response_ms": round(p50, 1),
                        "decode_tokens_per_s_per_request": round(toks / dec, 1) if dec > 0 else None,
@@ -285,6 +370,23 @@ def main() -> int:
                                            "max_queue_size": settings.max_queue_size,
                                            "production": {"timeout_seconds": 25.0, "max_queue_size": 5}}},
         }
+        if comm is not None:
+            res["config"]["comm"] = comm
+    # the TP pass: every rank's engine is gone (its memory with it); rank 0 runs the child while
+    # the others wait at the barrier below
+    del llm
+    import gc
+    gc.collect()
+    if tp_pass:
+        dist.barrier()
+        if rank == 0:
+            print(f"[bench] tp pass: tp{world} over {args.tp_model or args.model}", file=sys.stderr, flush=True)
+            out = os.path.join(tempfile.gettempdir(), f"lfk_bench_tp{world}_{os.getpid()}.json")
+            res["config"]["tp"] = run_tp_pass(tp_pass_cmd(args, world, out), out, args.tp_timeout)
+    if rank == 0:
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                json.dump(res, f)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier()

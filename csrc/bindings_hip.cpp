@@ -239,6 +239,11 @@ PYBIND11_MODULE(_hip, m) {
              e.bench_decode(n, pos0, &ms);
              return ms;
            })
+      .def("comm_info", [](Engine& e) {
+        py::dict d;
+        for (auto& kv : e.comm_info()) d[py::str(kv.first)] = kv.second;
+        return d;
+      })
       .def_property_readonly("device_bytes", &Engine::device_bytes)
       .def_property_readonly("healthy", &Engine::healthy)
       .def("p2p_handle", [](Engine& e) { return py::bytes(e.p2p_handle()); })
@@ -311,6 +316,28 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out"), py::arg("n_out"), py::arg("epi"), py::arg("stream"), py::arg("n_slots") = 1,
      py::arg("ids") = 0, py::arg("expert_stride") = 0, py::arg("slot_stride") = 0, py::arg("resid") = 0,
      py::arg("debug") = 0, py::arg("dbg_clk") = 0);
+
+  // the row-parallel decode GEMV with its epilogue all-reduce (GemvArgs::tp_*) for ONE rank of a
+  // group whose regions the caller laid out (tests/test_tp_epilogue_gpu.py: a single process
+  // pre-writes the peers' granules and fault words, so any world size runs on one GPU)
+  m.def("gemv_tp", [](uintptr_t w, int type, int rows, int K, uintptr_t x, uintptr_t out, int n_out, uintptr_t resid,
+                      const std::vector<uintptr_t>& data, const std::vector<uintptr_t>& fault, int rank, int stride,
+                      int off, uintptr_t epochs, uintptr_t err, uintptr_t stream) {
+    const int W = (int)data.size();
+    if (W < 1 || W > kP2PMaxRanks || (int)fault.size() != W || rank < 0 || rank >= W || stride < n_out + off)
+      throw std::runtime_error("gemv_tp: bad group layout");
+    GemvArgs a;
+    a.w = make_qmat(P<void>(w), type, rows, K, 0);
+    a.x = P<float>(x); a.out = P<float>(out); a.n_out = n_out; a.resid = P<float>(resid);
+    for (int p = 0; p < W; ++p) {
+      a.tp_peers.data[p] = P<float>(data[p]);
+      a.tp_peers.fault[p] = P<int>(fault[p]);
+    }
+    a.tp_world = W; a.tp_rank = rank; a.tp_stride = stride; a.tp_off = off;
+    a.tp_epochs = P<int>(epochs); a.tp_err = P<int>(err);
+    gemv(a, EPI_STORE, S(stream));
+    hip_ok("gemv_tp");
+  });
 
   m.def("bprep", [](uintptr_t x, int ldx, bool swiglu, uintptr_t norm, float eps, int K, int B, uintptr_t xh, int ldh,
                     uintptr_t stream, uintptr_t zero, int zero_n, int swiglu_group) {

@@ -72,9 +72,13 @@ __device__ __forceinline__ void tp_store_row(const GemvArgs& a, int row, float v
       }
     }
     if (!pending) break;
-    if ((spins & 255) == 255 && wall_clock64() - t0 > 2000000000LL) {  // 20 s (100 MHz clock)
-      __hip_atomic_store(a.tp_err, 300 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
+    if ((spins & 255) == 255) {
+      if (wall_clock64() - t0 > 2000000000LL) {  // 20 s (100 MHz clock)
+        __hip_atomic_store(a.tp_err, 300 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        p2p_raise(a.tp_peers, W, R, 300 + __builtin_ctz(pending));  // poison the group
+        return;
+      }
+      if (p2p_poisoned(a.tp_peers, W, R)) return;  // another rank failed: stop waiting
     }
     __builtin_amdgcn_s_sleep(1);
   }

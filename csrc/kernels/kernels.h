@@ -47,10 +47,29 @@ enum GemvEpi : int {
 // peer receive regions of the tensor-parallel collectives (p2p_allreduce.hip, runtime/p2p.cpp)
 static constexpr int kP2PMaxRanks = 8;
 static constexpr int kP2PMaxBlocks = 64;
+// fault[p][r]: rank r's fault code as stored in rank p's region (0 = none). A rank whose wait
+// times out stores its code into EVERY rank's region, and every wait polls its own region's words
+// between spins: the first fault poisons the group - no rank sits out its own 20 s bound, and
+// every rank's host (the leader's included) sees who failed (P2PComm::fault_report)
 struct P2PPeers {
   float* data[kP2PMaxRanks] = {};
-  int* flags[kP2PMaxRanks] = {};
+  int* fault[kP2PMaxRanks] = {};
 };
+
+#ifdef __HIPCC__
+__device__ __forceinline__ void p2p_raise(const P2PPeers& pe, int W, int R, int code) {
+#pragma unroll
+  for (int p = 0; p < kP2PMaxRanks; ++p)
+    if (p < W) __hip_atomic_store(pe.fault[p] + R, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool p2p_poisoned(const P2PPeers& pe, int W, int R) {
+  int any = 0;
+#pragma unroll
+  for (int p = 0; p < kP2PMaxRanks; ++p)
+    if (p < W) any |= __hip_atomic_load(pe.fault[R] + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return any != 0;
+}
+#endif
 
 struct GemvArgs {
   QMat w;

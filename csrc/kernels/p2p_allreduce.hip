@@ -32,8 +32,11 @@
 // store (untorn: value and tag arrive together) and is read with 8-byte system-scope atomic
 // loads. On a cacheable fallback region (hipMalloc, if the uncached allocation is refused) the
 // system scope still bypasses the non-coherent caches.
-// Every wait is bounded: a timeout sets *err and the launch completes (the engine then reports
-// itself unhealthy) instead of hanging.
+// Every wait is bounded: a timeout sets *err, stores the rank's fault code into every rank's
+// region (P2PPeers::fault) and the launch completes instead of hanging; every wait also polls
+// the fault words between spins, so one rank's fault ends every rank's waits at once. A faulted
+// group is poisoned: its outputs are stale from then on, every rank's engine reports the fault
+// (check_device_err) and the leader refuses further steps.
 #include "kernels.h"
 #include "qdot.h"
 
@@ -88,10 +91,17 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
       const u64_t g = __hip_atomic_load(const_cast<u64_t*>(mine + (size_t)tid * M + hb), __ATOMIC_RELAXED,
                                         __HIP_MEMORY_SCOPE_SYSTEM);
       if ((unsigned)(g >> 32) == ep) break;
-      if ((spins & 255) == 255 && wall_clock64() - t0 > kP2PWaitTicks) {
-        __hip_atomic_store(a.err, 100 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        s_ok = 0;
-        break;
+      if ((spins & 255) == 255) {
+        if (wall_clock64() - t0 > kP2PWaitTicks) {
+          __hip_atomic_store(a.err, 100 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          p2p_raise(a.peers, W, R, 100 + tid);  // poison the group: every rank's waits end
+          s_ok = 0;
+          break;
+        }
+        if (p2p_poisoned(a.peers, W, R)) {  // some rank already failed: the group is dead
+          s_ok = 0;
+          break;
+        }
       }
       __builtin_amdgcn_s_sleep(2);
     }
@@ -117,9 +127,13 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
         }
       }
       if (!pending) break;
-      if ((spins & 255) == 255 && wall_clock64() - t0 > kP2PWaitTicks) {
-        __hip_atomic_store(a.err, 100 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return;
+      if ((spins & 255) == 255) {
+        if (wall_clock64() - t0 > kP2PWaitTicks) {
+          __hip_atomic_store(a.err, 100 + __builtin_ctz(pending), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          p2p_raise(a.peers, W, R, 100 + __builtin_ctz(pending));
+          return;
+        }
+        if (p2p_poisoned(a.peers, W, R)) return;
       }
       __builtin_amdgcn_s_sleep(1);
     }

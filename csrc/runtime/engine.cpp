@@ -502,12 +502,26 @@ void Engine::step_clk_zero() {
   HIPCHK(hipMemset(step_clk_, 0, sizeof(long long) * 5 * kStepClkBlocks * 16));
 }
 
+std::string Engine::group_fault() const {
+  if (!leader() || !tp_ctl_ || tp_stopped_) return "";
+  return tp_ctl_->fault_report();
+}
+
 void Engine::check_device_err() {
   // the bounded in-kernel waits: the P2P all-reduce's (TP) and the batched Wo's (a host-mapped
-  // word: no copy); a blocking read of an error word nothing else writes cost every step a copy
+  // word: no copy); a blocking read of an error word nothing else writes cost every step a copy.
+  // Under TP a timed-out wait on ANY rank stores that rank's code into every rank's region, and a
+  // follower's host failure lands in the control channel: either poisons the group here
   int e = 0;
-  if (p2p_ && p2p_->ready()) e = p2p_->error();
-  if (!e && wo_err_h_ && __atomic_load_n(wo_err_h_, __ATOMIC_ACQUIRE)) e = 200;  // the batched Wo's wait
+  std::string group;
+  if (p2p_ && p2p_->ready()) group = p2p_->fault_report();
+  if (group.empty()) group = group_fault();
+  if (!group.empty()) {
+    healthy_ = false;
+    last_error_ = "tensor-parallel group fault: " + group;
+    throw std::runtime_error(last_error_);
+  }
+  if (wo_err_h_ && __atomic_load_n(wo_err_h_, __ATOMIC_ACQUIRE)) e = 200;  // the batched Wo's wait
   if (e != 0) {
     healthy_ = false;
     last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
@@ -561,6 +575,36 @@ bool Engine::tp_epilogue(GemvArgs& g) const {
   // resident blocks, or one rank's waiting epilogue waves could hold every CU its peers need
   if (p2p_->shared_device()) g.grid_div = p2p_->world();
   return true;
+}
+
+std::vector<std::pair<std::string, std::string>> Engine::comm_info() const {
+  std::vector<std::pair<std::string, std::string>> o;
+  auto put = [&](const char* k, const std::string& v) { o.emplace_back(k, v); };
+  put("tp_size", std::to_string(opt_.tp_size));
+  put("comm", opt_.comm);
+  int nccl_ranks = 0;
+  if (comm_ && ncclCommCount(static_cast<ncclComm_t>(comm_), &nccl_ranks) != ncclSuccess) nccl_ranks = -1;
+  put("rccl_comm_ranks", std::to_string(nccl_ranks));
+  const bool p2p = p2p_ && p2p_->ready();
+  put("p2p_ready", p2p ? "1" : "0");
+  if (p2p) {
+    put("p2p_shared_device", p2p_->shared_device() ? "1" : "0");
+    put("p2p_uncached_region", p2p_->uncached() ? "1" : "0");
+    put("p2p_max_floats", std::to_string(p2p_->max_n()));
+  }
+  GemvArgs probe;
+  probe.n_out = hp_.n_embd;
+  const bool epi = tp_on_ && tp_epilogue(probe);
+  const std::string coll = p2p ? "p2p one-shot collective kernel" : comm_ ? "rccl all-reduce" : "none";
+  put("decode_row_parallel_allreduce", !tp_on_ ? "none (tp=1)" : epi ? "gemv epilogue granules (no collective launch)" : coll);
+  const size_t brow = (size_t)std::max(bmax_, 1) * hp_.n_embd;
+  put("batched_row_parallel_allreduce",
+      !tp_on_ ? "none (tp=1)" : p2p && brow <= (size_t)p2p_->max_n() ? "p2p one-shot collective kernel" : comm_ ? "rccl all-reduce" : "none");
+  const size_t pre = (size_t)opt_.n_batch * hp_.n_embd;
+  put("prefill_allreduce",
+      !tp_on_ ? "none (tp=1)" : p2p && pre <= (size_t)p2p_->max_n() ? "p2p one-shot collective kernel" : comm_ ? "rccl all-reduce" : "none");
+  put("sampler_candidate_gather", !tp_on_ ? "none (tp=1)" : p2p ? "p2p all-gather" : comm_ ? "rccl all-gather" : "none");
+  return o;
 }
 
 void Engine::allreduce_into(const float* send, float* recv, size_t n, hipStream_t s) {
@@ -1295,6 +1339,15 @@ void Engine::mirror(const TPMsg& m) {
   if (opt_.tp_rank != 0) throw std::runtime_error("tensor parallelism: follower ranks only run follow()");
   if (!tp_ctl_) throw std::runtime_error("tensor parallelism: the control channel is not open (tp_ctl_create)");
   if (tp_stopped_) throw std::runtime_error("tensor parallelism: the group was stopped");
+  // a poisoned group (a rank's wait timed out, a follower failed or exited) runs no further step:
+  // its ranks' states have diverged, so every later result would be computed from stale data
+  if (!healthy_) throw std::runtime_error("tensor parallelism: the group is poisoned (" + last_error_ + ")");
+  const std::string f = group_fault();
+  if (!f.empty()) {
+    healthy_ = false;
+    last_error_ = "tensor-parallel group fault: " + f;
+    throw std::runtime_error(last_error_);
+  }
   tp_ctl_->publish(m);
 }
 
@@ -1310,6 +1363,17 @@ void Engine::tp_ctl_create(const std::string& name) {
 void Engine::tp_ctl_attach(const std::string& name) {
   if (opt_.tp_size < 2 || opt_.tp_rank == 0) throw std::runtime_error("tp_ctl_attach: follower ranks only");
   tp_ctl_ = TPChannel::attach(name, opt_.tp_rank);
+  // test hook: LFK_TP_FAULT=<rank>:<n>[:dev] - follower <rank> fails its n-th command, as a host
+  // failure (reported over the channel), or with ":dev" as a device-side fault word (what a
+  // timed-out collective wait stores) while it goes on replaying (tests/test_tp_fault_gpu.py)
+  if (const char* e = std::getenv("LFK_TP_FAULT")) {
+    int rk = -1, n = 0;
+    char kind[8] = {0};
+    if (std::sscanf(e, "%d:%d:%7s", &rk, &n, kind) >= 2 && rk == opt_.tp_rank && n > 0) {
+      fault_after_ = n;
+      fault_dev_ = std::strcmp(kind, "dev") == 0;
+    }
+  }
 }
 
 void Engine::tp_stop() {
@@ -1322,8 +1386,9 @@ void Engine::tp_stop() {
 }
 
 // Follower ranks: replay rank 0's commands until TPO_STOP. A failing command marks this
-// rank unhealthy (rank 0's next collective then times out and reports it) and the loop
-// goes on, so a later STOP still ends it.
+// rank unhealthy and publishes the failure (channel word + every rank's region fault word), so
+// rank 0 fails the request in flight and refuses further steps; the loop goes on, so a later
+// STOP still ends it.
 void Engine::follow() {
   if (!tp_ctl_ || opt_.tp_rank == 0) throw std::runtime_error("follow: attach a follower rank first");
   TPMsg m;
@@ -1339,6 +1404,10 @@ void Engine::follow() {
       return;
     }
     try {
+      if (fault_after_ > 0 && --fault_after_ == 0) {
+        if (!fault_dev_) throw std::runtime_error("injected follower fault (LFK_TP_FAULT)");
+        if (p2p_ && p2p_->ready()) p2p_->raise_fault(300 + opt_.tp_rank);  // as a timed-out epilogue wait
+      }
       switch (op) {
         case TPO_SLOT_STATE: {
           const int slot = m.get<int>();
@@ -1400,6 +1469,14 @@ void Engine::follow() {
       healthy_ = false;
       last_error_ = std::string("follower rank ") + std::to_string(opt_.tp_rank) + ": " + e.what();
       fprintf(stderr, "[lfk] %s\n", last_error_.c_str());
+      // rank 0 must learn of it (its next command or collect fails, /health turns false) and the
+      // other ranks' kernels must stop waiting for this one: the channel word and the region's
+      try {
+        tp_ctl_->report_fault(e.what());
+        // (a group already poisoned keeps the code of the rank that failed first)
+        if (p2p_ && p2p_->ready() && p2p_->fault_report().empty()) p2p_->raise_fault(1000 + opt_.tp_rank);
+      } catch (...) {
+      }
     }
   }
 }

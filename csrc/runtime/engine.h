@@ -118,6 +118,9 @@ class Engine : public SlotBackend {
   std::string p2p_handle();
   void p2p_open(const std::vector<std::string>& handles);
   bool p2p_ready() const { return p2p_ && p2p_->ready(); }
+  // which path each tensor-parallel message takes, and the communicator as RCCL reports it
+  // (bench.py's TP pass records it): key -> value strings
+  std::vector<std::pair<std::string, std::string>> comm_info() const;
   // tensor parallelism: the host control channel (tp_channel.h). Rank 0 creates it, the
   // followers attach and then sit in follow() replaying rank 0's commands until tp_stop().
   void tp_ctl_create(const std::string& name);
@@ -125,8 +128,9 @@ class Engine : public SlotBackend {
   void follow();
   void tp_stop();
   bool tp_ctl_open() const { return tp_ctl_ != nullptr; }
-  bool healthy() const { return healthy_; }
-  std::string last_error() const { return last_error_; }
+  // (a TP leader also reports its followers' published failures and exits: TPChannel::fault_report)
+  bool healthy() const { return healthy_ && group_fault().empty(); }
+  std::string last_error() const { return healthy_ ? group_fault() : last_error_; }
   int n_ctx() const override { return opt_.n_ctx; }
   int layer_begin() const { return opt_.layer_begin; }
   int layer_end() const { return layer_end_; }
@@ -215,6 +219,9 @@ class Engine : public SlotBackend {
   void gather_logits_rows(int B, size_t ld_src, const float* src, std::vector<float>& out);
   // tensor parallelism: publish a command to the followers (rank 0); no-op on one rank
   bool leader() const { return opt_.tp_size > 1 && opt_.tp_rank == 0; }
+  std::string group_fault() const;  // leader: the followers' failures as the channel holds them ("" = none)
+  int fault_after_ = 0;             // follower test hook (LFK_TP_FAULT): fail the n-th command
+  bool fault_dev_ = false;          // ... as a device-side fault word instead of a host failure
   void mirror(const TPMsg& m);
   void prefill_chunk(int slot, const int* toks, int T, int pos, bool head);
   int slot_begin_impl(int slot, const std::vector<int>& prompt, int n_keep, const SamplingOpts& sp);

@@ -99,7 +99,7 @@ void P2PComm::open(const std::vector<std::string>& handles) {
     }
     if (!base) throw std::runtime_error("p2p: no mapping for rank " + std::to_string(p));
     peers_.data[p] = reinterpret_cast<float*>(base);
-    peers_.flags[p] = reinterpret_cast<int*>(base + data_bytes_);
+    peers_.fault[p] = reinterpret_cast<int*>(base + data_bytes_);
   }
   ready_ = true;
 }
@@ -140,6 +140,37 @@ int P2PComm::error() const {
   return e;
 }
 
-void P2PComm::reset_error() { p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "reset err"); }
+std::vector<int> P2PComm::faults() const {
+  std::vector<int> f((size_t)world_, 0);
+  if (!ready_) return f;
+  p2pchk(hipMemcpy(f.data(), peers_.fault[rank_], sizeof(int) * world_, hipMemcpyDeviceToHost), "read faults");
+  return f;
+}
+
+std::string P2PComm::fault_report() const {
+  std::string out;
+  const std::vector<int> f = faults();
+  for (int r = 0; r < world_; ++r)
+    if (f[r]) {
+      const int c = f[r];
+      const std::string what = c >= 1000 ? "its host failed a command" :
+                               c >= 300 ? "its epilogue all-reduce wait for rank " + std::to_string(c % 100) + " timed out" :
+                               "its collective wait for rank " + std::to_string(c % 100) + " timed out";
+      out += (out.empty() ? "" : "; ") + std::string("rank ") + std::to_string(r) + ": " + what +
+             " (code " + std::to_string(c) + ")";
+    }
+  return out;
+}
+
+void P2PComm::raise_fault(int code) {
+  if (!ready_ || code == 0) return;
+  for (int p = 0; p < world_; ++p)
+    p2pchk(hipMemcpy(peers_.fault[p] + rank_, &code, sizeof(int), hipMemcpyHostToDevice), "raise fault");
+}
+
+void P2PComm::reset_error() {
+  p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "reset err");
+  if (ready_) p2pchk(hipMemset(peers_.fault[rank_], 0, sizeof(int) * kP2PMaxRanks), "reset faults");
+}
 
 }  // namespace lfk

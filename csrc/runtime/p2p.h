@@ -29,6 +29,11 @@ class P2PComm {
   void allreduce(const float* src, float* dst, int n, hipStream_t s);
   void allgather(const float* src, float* dst, int n, hipStream_t s);  // dst [world][n]
   int error() const;                                   // device error word (0 = ok)
+  // the group's fault words as stored in this rank's region (fault[r]: rank r's code, 0 = none):
+  // any rank's timed-out wait, or a host failure raise_fault() published
+  std::vector<int> faults() const;
+  std::string fault_report() const;                    // "" = no rank faulted
+  void raise_fault(int code);                          // this rank's code into every rank's region
   bool uncached() const { return uncached_; }          // region allocated hipDeviceMallocUncached
   // diagnostics: per rank (mapped pointer, allocation base, allocation size) as seen here
   std::vector<std::vector<unsigned long long>> mappings() const;

@@ -9,6 +9,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <chrono>
@@ -18,6 +19,7 @@ namespace lfk {
 
 static constexpr uint32_t kMagic = 0x4c464b54;  // "LFKT"
 static constexpr int kMaxFollowers = 8;
+static constexpr int kFaultMsg = 240;
 
 struct alignas(64) TPChannel::Hdr {
   uint32_t magic;
@@ -27,6 +29,9 @@ struct alignas(64) TPChannel::Hdr {
   alignas(64) std::atomic<uint32_t> seq;          // commands published (futex word)
   alignas(64) std::atomic<uint32_t> ack[kMaxFollowers];  // last command each rank copied
   std::atomic<int32_t> follower_pid[kMaxFollowers];      // set by attach(): the leader's liveness probe
+  // a follower's failure (report_fault): the message first, then the word (release)
+  alignas(64) std::atomic<int32_t> fault[kMaxFollowers];
+  char fault_msg[kMaxFollowers][kFaultMsg];
   alignas(64) uint32_t len;                        // bytes of the current command
 };
 
@@ -72,6 +77,7 @@ std::unique_ptr<TPChannel> TPChannel::create(const std::string& name, int world,
   c->h_->seq.store(0);
   for (auto& a : c->h_->ack) a.store(0);
   for (auto& p : c->h_->follower_pid) p.store(0);
+  for (auto& f : c->h_->fault) f.store(0);
   c->payload_ = static_cast<uint8_t*>(p) + sizeof(Hdr);
   std::atomic_thread_fence(std::memory_order_release);
   c->h_->magic = kMagic;
@@ -111,6 +117,26 @@ TPChannel::~TPChannel() {
 int TPChannel::world() const { return h_->world; }
 
 bool TPChannel::leader_alive() const { return pid_alive(h_->leader_pid); }
+
+void TPChannel::report_fault(const std::string& msg) {
+  if (rank_ == 0) return;
+  if (h_->fault[rank_].load(std::memory_order_acquire)) return;  // the first failure is the one kept
+  const size_t n = std::min(msg.size(), (size_t)kFaultMsg - 1);
+  std::memcpy(h_->fault_msg[rank_], msg.data(), n);
+  h_->fault_msg[rank_][n] = 0;
+  h_->fault[rank_].store(1, std::memory_order_release);
+}
+
+std::string TPChannel::fault_report() const {
+  std::string out;
+  for (int r = 1; r < h_->world; ++r) {
+    std::string what;
+    if (h_->fault[r].load(std::memory_order_acquire)) what = h_->fault_msg[r];
+    else if (!pid_alive(h_->follower_pid[r].load(std::memory_order_relaxed))) what = "exited";
+    if (!what.empty()) out += (out.empty() ? "" : "; ") + std::string("rank ") + std::to_string(r) + ": " + what;
+  }
+  return out;
+}
 
 void TPChannel::publish(const TPMsg& m) {
   if (rank_ != 0) throw std::runtime_error("tp channel: only rank 0 publishes");

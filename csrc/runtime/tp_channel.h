@@ -75,6 +75,10 @@ class TPChannel {
   // follower: the next command (true), or false after timeout_ms without one
   bool receive(TPMsg& m, int timeout_ms);
   bool leader_alive() const;
+  // follower: publish this rank's failure (message kept, first failure wins); leader: every
+  // follower's published failure or exit, "" while the group is sound (a shared-memory read)
+  void report_fault(const std::string& msg);
+  std::string fault_report() const;
   int rank() const { return rank_; }
   int world() const;
 

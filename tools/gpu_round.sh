@@ -44,6 +44,8 @@ for s in "$@"; do
     tp8) step tp8 170 $PYT tests/test_tp8_gpu.py --timeout 160 -s ;;
     rccl) step rccl 400 $PYT tests/test_rccl_gpu.py tests/test_serve_tp_gpu.py --timeout 300 ;;
     p2pu) step p2pu 200 $PYT tests/test_p2p_allreduce.py --timeout 150 ;;
+    tpepi) step tpepi 300 $PYT tests/test_tp_epilogue_gpu.py --timeout 120 ;;
+    tpfault) step tpfault 700 $PYT tests/test_tp_fault_gpu.py --timeout 320 ;;
     qkvsk) step qkvsk 300 $PYT tests/test_kernels_gpu.py -k "qkv_splitk or attn_decode or bmm_rows" --timeout 120 ;;
     bmmt) step bmmt 400 $PYT tests/test_kernels_gpu.py -k "bmm or bprep" --timeout 120 ;;
     t16t) step t16t 400 $PYT tests/test_kernels_gpu.py -k "t16 or rmsnorm_f16 or attn_prefill" --timeout 120 ;;
