@@ -124,6 +124,14 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   nq_ = sp.nq;
   nkvd_ = sp.nkvd;
   F_l_ = sp.F_l;
+  // negative-test hook (tests/test_tp_gpu.py): LFK_TP_FAULT=<rank>:0:shard makes that rank load the
+  // FFN features of the NEXT shard - a deliberately wrong expert / FFN shard the TP acceptance must catch
+  if (const char* e = std::getenv("LFK_TP_FAULT")) {
+    int rk = -1, n = -1;
+    char kind[8] = {0};
+    if (tp > 1 && std::sscanf(e, "%d:%d:%7s", &rk, &n, kind) == 3 && rk == r && std::strcmp(kind, "shard") == 0)
+      f0_ = (f0_ + (size_t)F_l_) % (size_t)hp_.n_ff;
+  }
   V_l_ = sp.V_l;
   V_pad_ = sp.V_pad;
   V_real_l_ = std::max(0, std::min(V_l_, hp_.n_vocab - r * V_l_));

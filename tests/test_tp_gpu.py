@@ -15,10 +15,13 @@ model:
     K/V the prefill wrote, whose f16 / bf16 roundings (0.1-0.4 % ulps) the sharded summation
     flips (measured 0.3-0.55 % vs TP=1, r4) - a wrong shard moves the logits by tens of %;
     MoE: the same, except where the exact model's router puts two experts within rounding
-    noise of the top-k boundary somewhere in the sequence (an expert flip moves the logits
-    far more than any rounding);
+    noise of the top-k boundary AT THE COMPARED TOKEN (an expert flip moves the logits far
+    more than any rounding);
   * greedy generations identical, or diverging only at a near-tie of the exact model's
-    logits (MoE: or of its router, anywhere in the prefix up to the divergence);
+    logits (MoE: or of its router at the divergence token). "Rounding noise" is measured in
+    the same run: twice the larger of TP's and TP=1's logit error against the exact model;
+  * a negative case: rank 1 loads the NEXT shard's FFN / expert features (LFK_TP_FAULT
+    "1:0:shard") - the logits check must fail it;
   * continuous batching under TP: every row's text identical to TP=1, or its divergence
     justified the same way;
   * seeded sampling (identical draws until rounding noise moves a probability boundary),
@@ -92,6 +95,14 @@ def _exercise(llm, with_app):
     return out
 
 
+def _logits_only(llm):
+    """The negative case's engine outputs: prefill and graph-decode logits (as _exercise draws them)."""
+    eng = llm._backend.engine
+    toks = [int(t) for t in np.random.default_rng(11).integers(3, 400, 44)]
+    return {"prefill": eng.eval_logits(toks[:39], 0),
+            "decode": [eng.decode_logits(toks[39 + i], 39 + i) for i in range(4)]}
+
+
 def _worker(rank, world, port, paths, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -113,6 +124,18 @@ def _worker(rank, world, port, paths, q):
             llm.close()               # publishes STOP: the follower's follow() returns
             ref = _exercise(Llama(path, split_mode="none", **kw), with_app=False)
             results.append((spec, got, ref))
+        # negative case: rank 1 holds the wrong FFN / expert shard (the MoE model)
+        spec, path, ts = next(p for p in paths if "mixtral" in p[0])
+        os.environ["LFK_TP_FAULT"] = "1:0:shard"
+        llm = Llama(path, split_mode="row", tensor_split=ts, tp_comm="ipc", device=0, **kw)
+        os.environ.pop("LFK_TP_FAULT")
+        if rank > 0:
+            llm.follow()
+            llm.close()
+        else:
+            bad = _logits_only(llm)
+            llm.close()
+            results.append(("wrong-shard:" + spec, bad, None))
         dist.barrier()
         q.put((rank, results, None))
         dist.destroy_process_group()
@@ -152,33 +175,49 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
     from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
     toks = [int(t) for t in np.random.default_rng(11).integers(3, 400, 44)]   # as _exercise draws them
     report, bad = [], []
-    for (spec, got, ref), (_, path, _) in zip(res[0][0], paths):
+    res0 = res[0][0]
+    refs = {spec: ref for spec, _, ref in res0 if ref is not None}
+    for spec, got, ref in res0:
+        negative = spec.startswith("wrong-shard:")
+        base = spec.split(":", 1)[1] if negative else spec
+        path = next(p for s_, p, _ in paths if s_ == base)
+        ref = refs[base] if negative else ref
         exact = ReferenceLlama(GGUFReader(path), n_ctx=256)
         x_pre = exact.forward(toks[:39], 0).numpy()
         x_dec = [exact.forward([toks[39 + i]], 39 + i).numpy() for i in range(4)]
-
-        moe = "mixtral" in spec
+        moe = "mixtral" in base
+        e_tp = [_rel(got["prefill"], x_pre)] + [_rel(g, x) for g, x in zip(got["decode"], x_dec)]
+        e_1 = [_rel(ref["prefill"], x_pre)] + [_rel(r, x) for r, x in zip(ref["decode"], x_dec)]
+        d_tp1 = [_rel(got["prefill"], ref["prefill"])] + [_rel(a_, b_) for a_, b_ in zip(got["decode"], ref["decode"])]
+        # rounding noise as measured: the engines' logits sit within e of the exact model's, so two
+        # candidates within 2e of each other may swap - never more (a wrong shard moves them by tens of %)
+        noise = 2.0 * max(e_1 + ([] if negative else e_tp))
+        ties = []   # every tie that excused a mismatch: (what, token, layer)
 
         def near_tie(prompt, a, b, k):
             """Tokens a (TP) and b (TP=1) at step k of a greedy run from `prompt`: both are
-            argmax candidates of the exact model within the engines' activation-rounding noise."""
+            argmax candidates of the exact model within the engines' measured rounding noise."""
             m = ReferenceLlama(GGUFReader(path), n_ctx=256)
             lg = m.forward(list(prompt) + list(b[:k]), 0).numpy()
-            return abs(lg[a[k]] - lg[b[k]]) <= 2e-2 * np.abs(lg).max()
+            hit = abs(lg[a[k]] - lg[b[k]]) <= noise * np.abs(lg).max()
+            if hit:
+                ties.append(("logit", len(prompt) + k, None))
+            return hit
 
         def router_tie(seq):
-            """MoE: somewhere in `seq` (every token, every layer) the exact router's k-th and
-            (k+1)-th expert logits lie within rounding noise of each other - an expert flip."""
+            """MoE: at the LAST token of `seq` (the token whose logits are compared / diverged),
+            in some layer, the exact router's k-th and (k+1)-th expert logits lie within the
+            measured rounding noise of each other - an expert flip of that token."""
             if not moe:
                 return False
             m = ReferenceLlama(GGUFReader(path), n_ctx=256)
             tr = []
             m.forward(list(seq), 0, router_trace=tr)
             k = m.hp.n_expert_used
-            for lg in tr:
-                srt = np.sort(lg.numpy(), -1)[:, ::-1]
-                gap = srt[:, k - 1] - srt[:, k]
-                if np.any(gap <= 2e-2 * np.abs(srt).max(-1)):
+            for layer, lg in enumerate(tr):
+                row = np.sort(lg.numpy()[-1])[::-1]
+                if row[k - 1] - row[k] <= noise * np.abs(row).max():
+                    ties.append(("router", len(seq) - 1, layer))
                     return True
             return False
 
@@ -186,15 +225,17 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
             k = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), None)
             if k is None:
                 return len(a) == len(b)
-            return near_tie(prompt, a, b, k) or router_tie(list(prompt) + list(b[:k + 1]))
-        e_tp = [_rel(got["prefill"], x_pre)] + [_rel(g, x) for g, x in zip(got["decode"], x_dec)]
-        e_1 = [_rel(ref["prefill"], x_pre)] + [_rel(r, x) for r, x in zip(ref["decode"], x_dec)]
-        d_tp1 = [_rel(got["prefill"], ref["prefill"])] + [_rel(a_, b_) for a_, b_ in zip(got["decode"], ref["decode"])]
+            # the divergence token: the last one both runs fed before their picks differed
+            return near_tie(prompt, a, b, k) or router_tie(list(prompt) + list(b[:k]))
         seqs = [toks[:39]] + [toks[:40 + i] for i in range(4)]
-        # an expert flip (MoE router near-tie in the sequence) excuses a logits difference
         tol = [5e-3] + [1e-2] * 4   # prefill, decode steps
         logits_ok = all(d <= tl and t <= o + 2e-3 or router_tie(q)
                         for d, tl, t, o, q in zip(d_tp1, tol, e_tp, e_1, seqs))
+        if negative:
+            report.append((spec, {"vs_tp1": [round(v, 5) for v in d_tp1], "ties": ties}, []))
+            if logits_ok:
+                bad.append((spec, "wrong shard passed the logits check"))
+            continue
         sd = next((i for i, (x, y) in enumerate(zip(got["sampled"], ref["sampled"])) if x != y), None)
         prompts = [[1, 5 + i, 9, 12 + i, 30 + 2 * i] for i in range(3)]
         batched_ok = got["batched_n"] == ref["batched_n"] and all(
@@ -215,6 +256,7 @@ def test_tensor_parallel_two_ranks_one_gpu(tmp_path):
             checks["http"] = got["http"] == (200, True) and got["health"] == 2
         report.append((spec, {"vs_tp1": [round(v, 5) for v in d_tp1],
                               "err_tp": [round(v, 5) for v in e_tp], "err_tp1": [round(v, 5) for v in e_1],
+                              "noise": round(noise, 5), "ties": ties,
                               "batched_same": [a == b for a, b in zip(got["batched"], ref["batched"])],
                               "sampled_diff_at": sd, "cancel": got["cancel"]},
                        [k for k, ok in checks.items() if not ok]))
