@@ -27,6 +27,7 @@
 // keeps >= 2 waves per SIMD busy on every projection shape, including the 256-tile Wo /
 // down); one-part launches own their outputs (epilogues: RoPE + KV append, SwiGLU).
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "gemv_dev.h"
@@ -380,6 +381,33 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
   }
 }
 
+// f16 rows xh[b][k0, k0 + kn) into LDS: every thread's loads go out before any LDS store - one
+// memory round trip for the slice (a load-store loop waited for each load in turn: 3-6 round trips,
+// 1.5-3.6 us per launch)
+template <int NW>
+__device__ __forceinline__ void bmm_stage_x_plain(const BmmArgs& a, __half* xs, int ldx, int k0, int kn, int tid,
+                                                  int i_begin = 0) {
+  constexpr int kBlock = NW * 64, U = 8;
+  const int nv = kn >> 3, n = a.B * nv;
+  for (int i0 = i_begin; i0 < n; i0 += U * kBlock) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * kBlock + tid, n - 1);
+      const int b = i / nv, c = i - b * nv;
+      v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kBlock + tid;
+      if (i < n) {
+        const int b = i / nv, c = i - b * nv;
+        *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = v[u];
+      }
+    }
+  }
+}
+
 // Stage x[b][k0, k0 + kn) of the B rows in LDS (f16, row stride ldx halves): from xh, or -
 // with the RMSNorm folded in (a.xf, K = 4096, B <= 8, kBlock >= 512: each thread holds 2
 // float4 of every row) - from the fp32 residual rows: every load is issued first (one memory
@@ -388,7 +416,7 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
 // row B - 1 and are dropped: straight-line code, no predicated loads)
 template <int NW>
 __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                            int tid, int lane, int wave) {
+                                            int tid, int lane, int wave, int i_begin = 0) {
   constexpr int kBlock = NW * 64;
   if (NW >= 8 && a.xf) {
     constexpr int J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
@@ -416,27 +444,7 @@ __device__ __forceinline__ void bmm_stage_x(const BmmArgs& a, __half* xs, float*
       if (lane == 0) rowss[b * NW + wave] = ss;
     }
   } else {
-    // every thread's loads go out before any LDS store: one memory round trip for the slice
-    // (a load-store loop waited for each load in turn: 3-6 round trips, 1.5-3.6 us per launch)
-    constexpr int U = 8;
-    const int nv = kn >> 3, n = a.B * nv;
-    for (int i0 = 0; i0 < n; i0 += U * kBlock) {
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = min(i0 + u * kBlock + tid, n - 1);
-        const int b = i / nv, c = i - b * nv;
-        v[u] = *reinterpret_cast<const uint4*>(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * kBlock + tid;
-        if (i < n) {
-          const int b = i / nv, c = i - b * nv;
-          *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = v[u];
-        }
-      }
-    }
+    bmm_stage_x_plain<NW>(a, xs, ldx, k0, kn, tid, i_begin);
   }
 }
 
@@ -776,10 +784,10 @@ void bmm_kernel(BmmArgs a, BmmArgs a2) {
 // round trip); kn % 256 == 0, so the 64 float4 of a wave lie in one row.
 template <int NW>
 __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
-                                                  int tid, int lane) {
+                                                  int tid, int lane, int i_begin = 0) {
   constexpr int kBlock = NW * 64, U = 4;
   const int nv = kn >> 2, n = a.B * nv;
-  for (int i0 = 0; i0 < n; i0 += U * kBlock) {
+  for (int i0 = i_begin; i0 < n; i0 += U * kBlock) {
     float4 v[U], w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -804,12 +812,140 @@ __device__ __forceinline__ void stage_x_part_norm(const BmmArgs& a, __half* xs, 
   }
 }
 
+// x-first staging (XF): the x loads of a block's first staging pass go out BEFORE its first weight
+// steps, and are written to LDS after those are issued. A CU returns its loads in order: x issued
+// behind the weights waited for those weight bytes (~40 KB per CU at the CU's ~24 GB/s share of
+// HBM - the 2.2-4.2 us x-staged stamps of profiles/r5a_batch_step_b6_block_timeline_layer5.json),
+// while issued first it returns from L2 and the weights stream behind it. (Round 2's x-first form
+// waited for x before it issued any weight: the whole stream started a round trip late.)
+// mode 1: fp32 rows with the RMSNorm folded (K = 4096, B <= 8); 2: one split-K Q|K|V part with
+// its norm; 0: f16 rows (xh)
+// Each form keeps its x registers in ONE ext_vector value local to its function, and runs `issue`
+// - the first weight steps - between its loads and its LDS stores. (Arrays of float4 / uint4 held
+// across the inlined `issue` went to scratch - 144-560 B per lane, stored right behind the loads
+// with a vmcnt wait each - where a single vector value stays in VGPRs.)
+template <int N>
+using f32v = float __attribute__((ext_vector_type(N)));
+template <int N>
+using u32v = unsigned __attribute__((ext_vector_type(N)));
+// global-address-space loads: pointer arithmetic on the staging rows made the compiler emit flat
+// loads, which its waitcnt accounting only ever retires with a full vmcnt(0) + lgkmcnt(0)
+// (through native vector types: HIP's float4 / uint4 copy through a generic reference, which turned
+// the load back into a flat one)
+__device__ __forceinline__ float4 ldg4(const float* p) {
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const v4 t = *(const __attribute__((address_space(1))) v4*)(p);
+  return make_float4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ uint4 ldg4(const __half* p) {
+  typedef unsigned v4 __attribute__((ext_vector_type(4)));
+  const v4 t = *(const __attribute__((address_space(1))) v4*)(p);
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+template <int N>
+__device__ __forceinline__ void vput(f32v<N>& v, int i, float4 t) {
+  v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+}
+template <int N>
+__device__ __forceinline__ float4 vget(const f32v<N>& v, int i) {
+  return make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+template <int NW, class Issue>
+__device__ __forceinline__ void xfirst_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int tid, int lane,
+                                            int wave, Issue&& issue) {
+  constexpr int kBlock = NW * 64, J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
+  f32v<32 * J> xv;
+  f32v<4 * J> w;
+#pragma unroll
+  for (int j = 0; j < J; ++j) vput(w, j, ldg4(a.norm_w + 4 * (tid + j * kBlock)));
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
+#pragma unroll
+    for (int j = 0; j < J; ++j) vput(xv, J * b + j, ldg4(xr + 4 * (tid + j * kBlock)));
+  }
+  issue();
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const float4 x = vget(xv, J * b + j), ww = vget(w, j);
+      ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+      const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
+      const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
+      if (b < a.B) *reinterpret_cast<uint2*>(xs + b * ldx + 4 * (tid + j * kBlock)) = make_uint2(as_u(p0), as_u(p1));
+    }
+    ss = wave_sum_fast(ss);
+    if (lane == 0) rowss[b * NW + wave] = ss;
+  }
+}
+
+// split-K Q|K|V part with its norm (rowss zeroed by the caller before `issue` returns: the first
+// pass's LDS side waits for the caller's barrier inside `issue`)
+template <int NW, class Issue>
+__device__ __forceinline__ void xfirst_part_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
+                                                 int tid, int lane, Issue&& issue) {
+  constexpr int kBlock = NW * 64, U = 4;
+  const int nv = kn >> 2, n = a.B * nv;
+  f32v<4 * U> v, w;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min(u * kBlock + tid, n - 1);
+    const int b = i / nv, c = i - b * nv;
+    vput(v, u, ldg4(a.xf + (size_t)b * a.ldxf + k0 + 4 * c));
+    vput(w, u, ldg4(a.norm_w + k0 + 4 * c));
+  }
+  issue();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int iw = u * kBlock + (tid & ~63);  // the wave's first index (wave-uniform)
+    if (iw < n) {
+      const int i = iw + lane;
+      const int b = i / nv, c = i - b * nv;
+      const float4 x = vget(v, u), ww = vget(w, u);
+      const h2_t p0 = {(_Float16)(x.x * ww.x), (_Float16)(x.z * ww.z)};
+      const h2_t p1 = {(_Float16)(x.y * ww.y), (_Float16)(x.w * ww.w)};
+      *reinterpret_cast<uint2*>(xs + b * ldx + 4 * c) = make_uint2(as_u(p0), as_u(p1));
+      const float ss = wave_sum_fast(x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w);
+      if (lane == 0) atomicAdd(rowss + b, ss);
+    }
+  }
+  if (n > U * kBlock) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, U * kBlock);
+}
+
+// f16 rows (xh)
+template <int NW, class Issue>
+__device__ __forceinline__ void xfirst_plain(const BmmArgs& a, __half* xs, float* rowss, int ldx, int k0, int kn,
+                                             int tid, int lane, int wave, Issue&& issue) {
+  constexpr int kBlock = NW * 64, U = 8;
+  const int nv = kn >> 3, n = a.B * nv;
+  u32v<4 * U> v;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = min(u * kBlock + tid, n - 1);
+    const int b = i / nv, c = i - b * nv;
+    const uint4 t = ldg4(a.xh + (size_t)b * a.ldh + k0 + 8 * c);
+    v[4 * u] = t.x; v[4 * u + 1] = t.y; v[4 * u + 2] = t.z; v[4 * u + 3] = t.w;
+  }
+  issue();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int i = u * kBlock + tid;
+    if (i < n) {
+      const int b = i / nv, c = i - b * nv;
+      *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = make_uint4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
+    }
+  }
+  if (n > U * kBlock) bmm_stage_x_plain<NW>(a, xs, ldx, k0, kn, tid, U * kBlock);
+}
+
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
 // per launch (registers and branches) when they were runtime ones
 // (bid, nblk): the block's index and count in the launch's wave-owned grid (the fused attention +
 // Wo launch runs this body in planes of its grid past the attention's)
-template <int QT, int PD, bool SK, int NW = 8, bool MOE = false>
+template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
   constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -895,12 +1031,29 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
       if (++li < nt) lp = tbase(li);
     }
   };
+  // the first steps: issued whether or not the wave has them (past its last step: the matrix's
+  // first block, never used), so the loads are branch-free - a conditional load makes the
+  // compiler's vmcnt accounting assume the path without it and wait for every later load at the
+  // x staging (XF)
+  auto load_first = [&](BRawT<QT>* dst, bool real) {
+    const uint8_t* p = real ? lp + (size_t)ls * SB : a.w.base;
+    tload<QT>(dst[0], p, 0, lane, r16, kq);
+    tload<QT>(dst[1], p, 1, lane, r16, kq);
+    if (real && ++ls == ns) {
+      ls = 0;
+      if (++li < nt) lp = tbase(li);
+    }
+  };
   // microbenchmark timeline (wave 0, as bmm_kernel's): [0] entry [1] weights issued [2] x staged
   // [3] first tile computed [4] exit [5] tiles of wave 0
   long long* clk = a.dbg_clk ? a.dbg_clk + (size_t)bid * 8 : nullptr;
   if (clk && tid == 0) {
     clk[0] = wall_clock64();
     clk[6] = xcc_id();
+  }
+  if (a.debug == 2) {  // microbenchmark: the launch alone (kernel boundary of this launch shape)
+    if (clk && tid == 0) clk[4] = wall_clock64();
+    return;
   }
   const bool col_ok = r16 < a.B;
   // split-K Q|K|V: the row's position and the RoPE factors of the wave's first tile, loaded
@@ -914,26 +1067,39 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     for (int j = 0; j < 2; ++j) rc[j] = a.qkv.rope[(size_t)pos * (hd >> 1) + ((row + 2 * j) % hd >> 1)];
   };
   if (SK && tid < 8) rowss[tid] = 0.f;  // the part's row sums of squares (stage_x_part_norm)
-  // the first PD steps of weights go out ahead of the x staging round trip (the x loads first
-  // instead, so that their round trip would not queue behind the weights: B = 6 step 2.25 -> 2.61 ms)
+  // staging form: 2 = split-K Q|K|V part with its norm, 1 = whole rows with the norm folded, 0 = f16 rows
+  const int xmode = (SK && a.ss_out) ? 2 : (NW >= 8 && a.xf) ? 1 : 0;
+  // the first PD steps of weights go out ahead of the x staging round trip - or, XF, right behind
+  // the x loads, which then no longer queue behind them; the row's position (split-K Q|K|V: its RoPE
+  // factors load after the staging, beside the first tile's weights) and the zero side job follow
+  // (the side job's stores and the stamp go before the weights: ops of uncertain count behind the x
+  // loads would make the compiler's vmcnt accounting wait for the weights at the x staging)
+  auto issue = [&]() __attribute__((always_inline)) {
+    if (clk && tid == 0) clk[1] = wall_clock64();
+    if (a.zero) {  // side job: zero the next consumer's accumulation rows
+      float4* z = reinterpret_cast<float4*>(a.zero);
+      for (int i = bid * (NW * 64) + tid; i < (a.zero_n >> 2); i += nblk * (NW * 64)) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 #pragma unroll
-  for (int p = 0; p < PD; ++p)
-    if (p < N) load_next(buf[p]);
-  if (clk && tid == 0) clk[1] = wall_clock64();
-  // split-K Q|K|V: the row's position (its RoPE factors load after the staging, beside the
-  // first tile's weights - a load issued ahead of the weights held their issue for a round trip)
-  if constexpr (SK) pos = a.qkv.pos[col_ok ? r16 : 0];
-  if (a.zero) {  // side job: zero the next consumer's accumulation rows
-    float4* z = reinterpret_cast<float4*>(a.zero);
-    for (int i = bid * (NW * 64) + tid; i < (a.zero_n >> 2); i += nblk * (NW * 64)) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  if (SK && a.ss_out) {
-    lds_barrier();  // rowss zeroed
-    stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
+    for (int p = 0; p < PD; ++p) load_first(buf[p], p < N);
+    if constexpr (SK) pos = a.qkv.pos[col_ok ? r16 : 0];
+    if (!XF && xmode == 2) lds_barrier();  // rowss zeroed
+  };
+  // (XF: that barrier goes first - an asm memory clobber between the x loads and their LDS stores
+  // made the compiler keep the x registers in scratch)
+  if (XF && xmode == 2) lds_barrier();
+  if constexpr (XF) {
+    if (xmode == 2) xfirst_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue);
+    else if (xmode == 1) xfirst_norm<NW>(a, xs, rowss, ldx, tid, lane, wave, issue);
+    else xfirst_plain<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave, issue);
   } else {
-    bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
+    issue();
+    if (xmode == 2) stage_x_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane);
+    else bmm_stage_x<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave);
   }
-  __syncthreads();
+  // XF: an LDS-only barrier - __syncthreads() would drain the weight steps just issued (vmcnt(0))
+  if constexpr (XF) lds_barrier();
+  else __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
   if (SK && a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
@@ -953,6 +1119,12 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   int ci = 0, cstep = 0;  // compute cursor (step s0 + cstep of tile ci)
   auto finish = [&]() {   // tile ci is complete in acc + acc2: C[row 4kq + i][col r16]
     acc += acc2;
+    if (a.debug == 3) {  // microbenchmark: no epilogue writes (an empty asm keeps the tile live)
+      asm volatile("" ::"v"(acc[0]), "v"(acc[1]), "v"(acc[2]), "v"(acc[3]));
+      acc = f4_t{0.f, 0.f, 0.f, 0.f};
+      acc2 = acc;
+      return;
+    }
     if (a.xf && !SK) acc *= cs;
     const int gt = tile_of(ci);
     if constexpr (SK) {
@@ -1006,6 +1178,16 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (j0 + r >= N) break;  // wave-uniform
+      if (a.fair) {
+        // issue priority by the steps this wave has left: a CU's waves issue oldest-first, so the
+        // youngest ones got their weights last and the block's last wave ended up to ~4 us after
+        // its first (gate/up: last-wave exit stamps, r5a) with ever fewer bytes in flight meanwhile
+        const int rem = N - (j0 + r);
+        if (rem * 4 > 3 * N) __builtin_amdgcn_s_setprio(3);
+        else if (rem * 2 > N) __builtin_amdgcn_s_setprio(2);
+        else if (rem * 4 > N) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
       if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
       __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
       bmm_step<QT>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
@@ -1017,37 +1199,37 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
       }
     }
   }
-  if (clk && tid == 0) {
-    clk[4] = wall_clock64();
-    clk[5] = nt;
+  if (clk) {  // exit: the block's LAST wave (waves of one block can end microseconds apart)
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(clk + 4), (unsigned long long)wall_clock64());
+    if (tid == 0) clk[5] = nt;
   }
 }
 
 // (the body reads its arguments through the kernarg segment pointer: a reference to the by-value
 // parameter made the compiler copy the whole block to scratch, as in bmm_kernel)
-template <int QT, int PD, bool MOE = false>
+template <int QT, int PD, bool MOE = false, bool XF = false>
 __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, false, 8, MOE>(*ka, 0, blockIdx.x, gridDim.x);
+  wt_body<QT, PD, false, 8, MOE, XF>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
 // split-K Q|K|V of one weight type
-template <int QT, int PD>
+template <int QT, int PD, bool XF = false>
 __global__ __launch_bounds__(512, 2) void bmm_sk_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, true>(*ka, 0, blockIdx.x, gridDim.x);
+  wt_body<QT, PD, true, 8, false, XF>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
 // split-K Q|K|V over two weight types (Q|K Q4_K + V Q6_K / Q5_K on the bumped layers of the
 // K-quant mixes, Q Q4_K + K|V Q8_0 in Mixtral's): groups from a.nb1 on are run B, type QT2 (a
 // uniform branch per block; each run's body keeps its own registers)
-template <int QT, int QT2, int PD>
+template <int QT, int QT2, int PD, bool XF = false>
 __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true>(*ka, 1, blockIdx.x, gridDim.x);
-  else wt_body<QT, PD, true>(*ka, 0, blockIdx.x, gridDim.x);
+  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true, 8, false, XF>(*ka, 1, blockIdx.x, gridDim.x);
+  else wt_body<QT, PD, true, 8, false, XF>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1138,6 +1320,25 @@ bool bmm_supported(int type, int K) {
   return K % 256 == 0;  // 256 k per step
 }
 
+// x-first staging in the wave-owned kernels (XFirst above); LFK_BMM_XFIRST=0 restores the
+// weights-first order for the A/B (read once per process)
+static bool bmm_xfirst() {
+  static const bool on = [] {
+    const char* e = std::getenv("LFK_BMM_XFIRST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// fair issue priority in the wave-owned kernels (BmmArgs::fair); LFK_BMM_FAIR=0 for the A/B
+static bool bmm_fair() {
+  static const bool on = [] {
+    const char* e = std::getenv("LFK_BMM_FAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int bmm_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1181,13 +1382,19 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     }
     a.spp = (steps + kparts - 1) / kparts;
     a.kparts = kparts = (steps + a.spp - 1) / a.spp;
+    a.fair = bmm_fair() ? 1 : 0;
     // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K
     // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
     const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
     // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
     const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
-    if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(G * kparts), dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
+    if (bmm_xfirst()) {
+      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(G * kparts), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(G * kparts), dim3(512), lds, s, a);
+    } else {
+      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(G * kparts), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
+    }
     return;
   }
   if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");
@@ -1245,6 +1452,7 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
     else tb += t;
   }
   const int steps = a.w.K / 256;
+  a.fair = bmm_fair() ? 1 : 0;
   // 4 parts x 8-tile groups measured best at B = 6 (8 x 8: +3 %, 4 x 6 / 2 x 3: +1-4 %, 16 x 6: +15 %)
   const int kparts = std::max(1, std::min(steps, 4));
   a.spp = (steps + kparts - 1) / kparts;
@@ -1254,10 +1462,13 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   a.nb1 = ga;
   const dim3 grid((ga + gb) * a.kparts);
   const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
+  const bool xf = bmm_xfirst();
   if constexpr (QT2 == 0) {
-    hipLaunchKernelGGL((bmm_sk_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+    if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2>), grid, dim3(512), lds, s, a);
   } else {
-    hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
+    if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true>), grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
   }
 }
 

@@ -92,6 +92,9 @@ for s in "$@"; do
     attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
     bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
     gemmt) step gemmt 400 bash -c 'for T in 384 512 1024 2304; do python tools/gemm_bench.py --T $T --t16 || exit 1; done' ;;
+    bound) step bound 200 python tools/boundary_bench.py --json gpurun_out/bound_default.json
+           step bound_devka 200 env HIP_FORCE_DEV_KERNARG=1 python tools/boundary_bench.py --json gpurun_out/bound_devka1.json
+           step bound_hostka 200 env HIP_FORCE_DEV_KERNARG=0 python tools/boundary_bench.py --json gpurun_out/bound_devka0.json ;;
     p2plat) step p2plat 300 python tools/p2p_latency.py --ranks 2,4,8 --json gpurun_out/p2p_latency.json ;;
     # ---- same-box A/B against the older build staged in ab_old/ (drop ./ab_old from .gpurunignore)
     abold) for r in 1 2; do
