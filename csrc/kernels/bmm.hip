@@ -1178,16 +1178,6 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (j0 + r >= N) break;  // wave-uniform
-      if (a.fair) {
-        // issue priority by the steps this wave has left: a CU's waves issue oldest-first, so the
-        // youngest ones got their weights last and the block's last wave ended up to ~4 us after
-        // its first (gate/up: last-wave exit stamps, r5a) with ever fewer bytes in flight meanwhile
-        const int rem = N - (j0 + r);
-        if (rem * 4 > 3 * N) __builtin_amdgcn_s_setprio(3);
-        else if (rem * 2 > N) __builtin_amdgcn_s_setprio(2);
-        else if (rem * 4 > N) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
       if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
       __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
       bmm_step<QT>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
@@ -1330,15 +1320,6 @@ static bool bmm_xfirst() {
   return on;
 }
 
-// fair issue priority in the wave-owned kernels (BmmArgs::fair); LFK_BMM_FAIR=0 for the A/B
-static bool bmm_fair() {
-  static const bool on = [] {
-    const char* e = std::getenv("LFK_BMM_FAIR");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static int bmm_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1382,7 +1363,6 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     }
     a.spp = (steps + kparts - 1) / kparts;
     a.kparts = kparts = (steps + a.spp - 1) / a.spp;
-    a.fair = bmm_fair() ? 1 : 0;
     // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K
     // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
     const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
@@ -1452,7 +1432,6 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
     else tb += t;
   }
   const int steps = a.w.K / 256;
-  a.fair = bmm_fair() ? 1 : 0;
   // 4 parts x 8-tile groups measured best at B = 6 (8 x 8: +3 %, 4 x 6 / 2 x 3: +1-4 %, 16 x 6: +15 %)
   const int kparts = std::max(1, std::min(steps, 4));
   a.spp = (steps + kparts - 1) / kparts;

@@ -133,7 +133,6 @@ struct BmmArgs {
   const uint8_t* seg_base[3] = {};
   int seg_rows[3] = {};
   float* seg_out[3] = {};
-  int fair = 0;                    // wave-owned kernels: issue priority by steps left (set by the launcher)
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only (bmm_kernel); wave-owned
                                    // kernels: 2 = exit at entry, 3 = no epilogue writes (tools/boundary_bench.py)
   // Q|K|V epilogue (one K part only, see bmm_qkv_fits): instead of accumulating into `out`,
