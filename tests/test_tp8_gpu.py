@@ -144,12 +144,16 @@ def test_tensor_parallel_eight_ranks_70b_width(tmp_path):
               "err_tp1": [round(v, 5) for v in e_1], "greedy_diverge_at": k, "tie": tie,
               "batched_same": [a == b for a, b in zip(got["batched"], ref["batched"])],
               "batched_ties": got["batched_ties"]}
-    print("TP8 report:", report)
     assert d[0] <= 5e-3 and max(d[1:]) <= 2e-2, report
     assert all(t <= o + 5e-3 for t, o in zip(e_tp, e_1)), report
-    assert k is None or tie <= 2e-2, report
+    # a near-tie is one within the rounding noise this run measured: twice the larger logit error
+    # of TP = 8 or TP = 1 against the exact model (capped at the old fixed 2e-2)
+    noise = min(2e-2, 2.0 * max(e_tp + e_1))
+    report["noise"] = round(noise, 5)
+    assert k is None or tie <= noise, report
     # continuous batching under TP = 8: every row's text equal, or diverging at a near-tie of the
     # exact model (eight-way sharded sums move the batched rows' logits ~1 %, measured r4)
-    assert all(a == b or (t is not None and t <= 2e-2)
+    assert all(a == b or (t is not None and t <= noise)
                for a, b, t in zip(got["batched"], ref["batched"], got["batched_ties"])), report
     assert got["healthy"], report
+    print("TP8 report:", report)
