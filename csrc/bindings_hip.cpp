@@ -371,6 +371,28 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("ldo"), py::arg("B"), py::arg("stream"), py::arg("debug") = 0, py::arg("h_out") = 0,
      py::arg("ldh_out") = 0, py::arg("xf") = 0, py::arg("ldxf") = 0, py::arg("norm") = 0, py::arg("eps") = 1e-5f,
      py::arg("store_out") = false, py::arg("dbg_clk") = 0);
+  // the gate/up + down chain in one launch (tests/test_kernels_gpu.py::test_bmm_ffn_chain_*): gate/up
+  // rows in the SwiGLU tile16 copy (wg, 2F x K), down (wd, K x F) over the f16 SwiGLU output hout
+  // [B][F]; out [B][K] accumulates; cnt >= 64 ints, zeroed by the caller
+  m.def("chain_layout", []() { return std::make_tuple(kChainStride, kChainXcds, kChainInts); });
+  m.def("bmm_ffn_chain", [](uintptr_t wg, int tg, int F, int K, uintptr_t xh, uintptr_t xf, uintptr_t norm, float eps,
+                            uintptr_t wd, int td, uintptr_t hout, uintptr_t out, int B, uintptr_t cnt,
+                            uintptr_t stream) {
+    BmmArgs gu, dn;
+    gu.w = make_qmat(P<void>(wg), tg, 2 * F, K);
+    gu.xh = P<__half>(xh); gu.ldh = K; gu.n_out = 2 * F; gu.B = B;
+    gu.swiglu_epi = true; gu.h_out = P<__half>(hout); gu.ldh_out = F;
+    if (xf) {
+      gu.xf = P<float>(xf); gu.ldxf = K; gu.norm_w = P<float>(norm); gu.eps = eps;
+    }
+    dn.w = make_qmat(P<void>(wd), td, K, F);
+    dn.xh = P<__half>(hout); dn.ldh = F; dn.out = P<float>(out); dn.ldo = K; dn.n_out = K; dn.B = B;
+    if (!bmm_ffn_chain_supported(gu, dn)) throw std::runtime_error("bmm_ffn_chain: unsupported shapes");
+    bmm_ffn_chain(gu, dn, P<int>(cnt), nullptr, S(stream));
+    hip_ok("bmm_ffn_chain");
+  }, py::arg("wg"), py::arg("tg"), py::arg("F"), py::arg("K"), py::arg("xh"), py::arg("xf"), py::arg("norm"),
+     py::arg("eps"), py::arg("wd"), py::arg("td"), py::arg("hout"), py::arg("out"), py::arg("B"), py::arg("cnt"),
+     py::arg("stream"));
   m.def("bmm_norm_fits", &bmm_norm_fits);
   m.def("bmm_supported", &bmm_supported);
   m.def("t16_bytes", &t16_bytes);

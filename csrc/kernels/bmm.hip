@@ -940,6 +940,57 @@ __device__ __forceinline__ void xfirst_plain(const BmmArgs& a, __half* xs, float
   if (n > U * kBlock) bmm_stage_x_plain<NW>(a, xs, ldx, k0, kn, tid, U * kBlock);
 }
 
+// In-launch chain (BmmArgs::chain_*), consumer side: thread 0 waits (bounded, sc1 polls) until the
+// block's K part has all of its producer tiles, then the block stages its x with sc1 loads (the
+// producer wrote it write-through from other CUs; a plain load could hit a stale L2 line of the
+// previous layer's use of the same buffer).
+__device__ __forceinline__ void chain_wait(const BmmArgs& a, int kp, int tid) {
+  if (tid < 64) {  // wave 0: lanes 0-7 poll the part's 8 XCD shards, the sum is broadcast from lane 0
+    const int need = min(a.chain_tpp, a.chain_tiles - kp * a.chain_tpp);
+    const int* c = a.chain_cnt + (kp * kChainXcds + (tid & (kChainXcds - 1))) * kChainStride;
+    const long long t0 = wall_clock64();
+    for (;;) {
+      int v = tid < kChainXcds ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      if (__shfl(v, 0) >= need) break;
+      if (wall_clock64() - t0 > 200000000LL) {  // 2 s (100 MHz): report, never hang the stream
+        if (a.chain_err && tid == 0) __hip_atomic_store(a.chain_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      for (int i = 0; i < a.chain_poll; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  lds_barrier();
+}
+
+template <int NW>
+__device__ __forceinline__ void xstage_sc1(const BmmArgs& a, __half* xs, int ldx, int k0, int kn, int tid) {
+  constexpr int kBlock = NW * 64, U = 8;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.xh), 0, 0x7FFFFFFF, 0x00020000);
+  const int nv = kn >> 3, n = a.B * nv;
+  for (int i0 = 0; i0 < n; i0 += U * kBlock) {
+    u32v<4 * U> v;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u * kBlock + tid, n - 1);
+      const int b = i / nv, c = i - b * nv;
+      const u32v<4> t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(((size_t)b * a.ldh + k0 + 8 * c) * sizeof(__half)), 0,
+                                                          16);  // aux 16: sc1
+      v[4 * u] = t.x; v[4 * u + 1] = t.y; v[4 * u + 2] = t.z; v[4 * u + 3] = t.w;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * kBlock + tid;
+      if (i < n) {
+        const int b = i / nv, c = i - b * nv;
+        *reinterpret_cast<uint4*>(xs + b * ldx + 8 * c) = make_uint4(v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
+      }
+    }
+  }
+}
+
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
 // per launch (registers and branches) when they were runtime ones
@@ -1089,7 +1140,11 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // made the compiler keep the x registers in scratch)
   if (XF && xmode == 2) lds_barrier();
   if constexpr (XF) {
-    if (xmode == 2) xfirst_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue);
+    if (!SK && a.chain_role == 2) {  // chain consumer: the weights do not depend on the producer
+      issue();
+      chain_wait(a, kp, tid);
+      xstage_sc1<NW>(a, xs, ldx, k0, kn, tid);
+    } else if (xmode == 2) xfirst_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue);
     else if (xmode == 1) xfirst_norm<NW>(a, xs, rowss, ldx, tid, lane, wave, issue);
     else xfirst_plain<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave, issue);
   } else {
@@ -1157,7 +1212,16 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
         const float rw = moe_sw ? a.ew[(size_t)r16 * a.ew_ld + gt / tpe] : 1.f;
         const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
         const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
-        *reinterpret_cast<uint2*>(a.h_out + (size_t)r16 * a.ldh_out + f0) = make_uint2(as_u(p0), as_u(p1));
+        __half* h = a.h_out + (size_t)r16 * a.ldh_out + f0;
+        if (!MOE && a.chain_role == 1)  // chain producer: write-through (a consumer CU reads it next)
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(h),
+                             ((unsigned long long)as_u(p1) << 32) | as_u(p0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          *reinterpret_cast<uint2*>(h) = make_uint2(as_u(p0), as_u(p1));
+      }
+      if (!MOE && a.chain_role == 1) {  // the tile's rows have landed: count it for its consumer part
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_fetch_add(a.chain_cnt + (gt / a.chain_tpp * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else if (col_ok) {
       float* o = a.out + (size_t)r16 * a.ldo;
@@ -1221,6 +1285,18 @@ __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true, 8, false, XF>(*ka, 1, blockIdx.x, gridDim.x);
   else wt_body<QT, PD, true, 8, false, XF>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
+}
+
+// The SwiGLU gate/up (QT1, producer) and the down projection (QT2, consumer) in ONE launch:
+// blocks [0, a.nb1) run the gate/up, the rest the down (their own BmmArgs: the second kernarg).
+template <int QT1, int QT2>
+__global__ __launch_bounds__(512, 2) void bmm_chain_kernel(BmmArgs a, BmmArgs b) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int n1 = ka[0].nb1;
+  if ((int)blockIdx.x < n1) wt_body<QT1, 2, false, 8, false, true>(ka[0], 0, blockIdx.x, n1);
+  else wt_body<QT2, 2, false, 8, false, true>(ka[1], 0, blockIdx.x - n1, gridDim.x - n1);
+  (void)a;
+  (void)b;
 }
 
 // ---------------------------------------------------------------- activation prep
@@ -1331,6 +1407,39 @@ static int bmm_cus() {
   return cus;
 }
 
+// The wave-owned launch shape (K parts, steps per part, one block per CU): sets a.spp / a.kparts,
+// returns the block count and the dynamic LDS (wt_k: split-K shapes; else the one-part SwiGLU)
+static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
+  int tiles = (a.n_out + 15) / 16;
+  for (int i = 1; i < a.nseg; ++i) tiles += (a.seg_rows[i] + 15) / 16;
+  const int steps = a.w.K / 256;
+  const int cus = bmm_cus();
+  int kparts = 1;
+  if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
+    // (8 parts for the 256-tile shapes; 4 / 16 measured 7 / 13 % slower steps, r3 sweep)
+    kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
+    if (a.ew) {
+      // MoE down (K = the experts' F concatenated): every part inside one expert, the parts of
+      // an unrouted expert skipped whole; parts per expert: the count nearest the dense rule
+      // whose staged slice fits the LDS and divides the expert's steps
+      const int spe = a.steps_per_expert, E = steps / spe;
+      int ppe = std::max(1, (kparts + E / 2) / E);
+      while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + 8) * 2 > 150 * 1024)) ++ppe;
+      kparts = E * ppe;
+    }
+    // the staged slice (B rows x part) stays within the LDS
+    while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
+  }
+  a.spp = (steps + kparts - 1) / kparts;
+  a.kparts = kparts = (steps + a.spp - 1) / a.spp;
+  // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K
+  // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
+  const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
+  // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
+  lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
+  return G * kparts;
+}
+
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
@@ -1344,36 +1453,14 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   const bool wt_k = !a.swiglu_epi && (!a.ew || a.steps_per_expert > 0) && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
                     a.nseg == 1 && a.B <= 8;
   if (wt_sw || wt_k) {
-    const int cus = bmm_cus();
-    int kparts = 1;
-    if (wt_k) {  // one 8-wave block per CU: parts = CUs x 8 waves / tiles, >= 2 steps per part
-      // (8 parts for the 256-tile shapes; 4 / 16 measured 7 / 13 % slower steps, r3 sweep)
-      kparts = std::max(1, std::min(steps / 2, (cus * 8 + tiles / 2) / std::max(1, tiles)));
-      if (a.ew) {
-        // MoE down (K = the experts' F concatenated): every part inside one expert, the parts of
-        // an unrouted expert skipped whole; parts per expert: the count nearest the dense rule
-        // whose staged slice fits the LDS and divides the expert's steps
-        const int spe = a.steps_per_expert, E = steps / spe;
-        int ppe = std::max(1, (kparts + E / 2) / E);
-        while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + 8) * 2 > 150 * 1024)) ++ppe;
-        kparts = E * ppe;
-      }
-      // the staged slice (B rows x part) stays within the LDS
-      while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
-    }
-    a.spp = (steps + kparts - 1) / kparts;
-    a.kparts = kparts = (steps + a.spp - 1) / a.spp;
-    // tile groups: one block per CU over all parts, at most 8 tiles (one per wave) per split-K
-    // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
-    const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
-    // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
-    const size_t lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
+    size_t lds = 0;
+    const int nblk = wt_config(a, wt_k, lds);
     if (bmm_xfirst()) {
-      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(G * kparts), dim3(512), lds, s, a);
-      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(G * kparts), dim3(512), lds, s, a);
+      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
     } else {
-      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(G * kparts), dim3(512), lds, s, a);
-      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(G * kparts), dim3(512), lds, s, a);
+      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(nblk), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(nblk), dim3(512), lds, s, a);
     }
     return;
   }
@@ -1513,6 +1600,37 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
     case T_Q8_0: launch_bmm<T_Q8_0>(a, s); break;
     default: throw std::runtime_error("bmm: unsupported weight type");
   }
+}
+
+bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn) {
+  return gu.swiglu_epi && !gu.ew && !gu.qkv_epi && gu.nseg == 1 && gu.B <= 8 && (!gu.xf || gu.w.K == 4096) &&
+         !dn.swiglu_epi && !dn.ew && !dn.qkv_epi && !dn.xf && !dn.one_part && !dn.store_out && dn.nseg == 1 &&
+         dn.B == gu.B && gu.w.type == T_Q4_K && (dn.w.type == T_Q4_K || dn.w.type == T_Q6_K) && bmm_xfirst() &&
+         dn.xh == gu.h_out && dn.ldh == gu.ldh_out && dn.w.K == gu.n_out / 2;
+}
+
+void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, hipStream_t s) {
+  if (!bmm_ffn_chain_supported(gu0, dn0) || !cnt) throw std::runtime_error("bmm_ffn_chain: unsupported shapes");
+  BmmArgs gu = gu0, dn = dn0;
+  bmm_check(gu);
+  bmm_check(dn);
+  size_t lds1 = 0, lds2 = 0;
+  const int n1 = wt_config(gu, false, lds1), n2 = wt_config(dn, true, lds2);
+  // a consumer block takes K part kp = bid % kparts: its 256 * spp features are 32 * spp gate/up tiles
+  gu.chain_role = 1; gu.chain_cnt = cnt; gu.chain_tpp = 32 * dn.spp;
+  dn.chain_role = 2; dn.chain_cnt = cnt; dn.chain_tpp = 32 * dn.spp; dn.chain_tiles = (gu.n_out + 15) / 16;
+  dn.chain_err = err;
+  if (dn.kparts > kChainMaxParts) throw std::runtime_error("bmm_ffn_chain: too many K parts for the counters");
+  static const int poll = [] {
+    const char* e = std::getenv("LFK_CHAIN_POLL");
+    return e ? std::max(1, std::atoi(e)) : 8;
+  }();
+  dn.chain_poll = poll;
+  gu.nb1 = n1;
+  const dim3 grid(n1 + n2);
+  const size_t lds = std::max(lds1, lds2);
+  if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, gu, dn);
+  else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, gu, dn);
 }
 
 bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {

@@ -133,6 +133,18 @@ struct BmmArgs {
   const uint8_t* seg_base[3] = {};
   int seg_rows[3] = {};
   float* seg_out[3] = {};
+  // in-launch chain (bmm_ffn_chain: the SwiGLU gate/up and the down projection in ONE launch): the
+  // producer run (chain_role 1) stores each finished tile's f16 outputs write-through and counts the
+  // tile in chain_cnt[tile / chain_tpp]; the consumer run (2) issues its first weight steps, waits
+  // until chain_cnt[its K part] holds all of that part's producer tiles, then stages its x with
+  // L2-bypassing loads. Consumer blocks come after every producer block in the grid and a CU holds
+  // one block of either (LDS), so a consumer only ever waits for blocks already running or done.
+  int chain_role = 0;
+  int* chain_cnt = nullptr;        // zeroed before the launch (per layer: the step's first kernel)
+  int chain_tpp = 0;               // producer tiles per counter (= the consumer's K part / 8 features)
+  int chain_tiles = 0;             // producer tiles in all
+  int* chain_err = nullptr;        // host-mapped: a consumer's bounded wait timed out
+  int chain_poll = 0;              // consumer poll interval: s_sleep units (64 clocks) between polls
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only (bmm_kernel); wave-owned
                                    // kernels: 2 = exit at entry, 3 = no epilogue writes (tools/boundary_bench.py)
   // Q|K|V epilogue (one K part only, see bmm_qkv_fits): instead of accumulating into `out`,
@@ -207,6 +219,16 @@ void bmm(const BmmArgs& a, hipStream_t s);
 // two one-part Q|K|V runs of different weight types (Q|K Q4_K + V Q6_K / Q5_K: the bumped
 // layers of the K-quant mixes) in one launch; false = unsupported pair or shape (caller
 // launches them one by one)
+// The dense SwiGLU gate/up (gu, swiglu_epi) and the down projection over its output (dn) in ONE
+// launch with a per-K-part in-launch hand-off (BmmArgs::chain_*). cnt: kChainInts ints, zero
+// before the launch (kChainXcds counters per K part, each on a 128-B line of its own); err: host-mapped
+// word set if a consumer's bounded wait timed out.
+// Each K part's count is sharded over the XCDs (the producer's XCC id picks the shard; the
+// consumer sums the 8): same-address atomics serialise at ~12 ns each under load.
+constexpr int kChainStride = 32, kChainXcds = 8, kChainMaxParts = 16;
+constexpr int kChainInts = kChainStride * kChainXcds * kChainMaxParts;
+bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn);
+void bmm_ffn_chain(const BmmArgs& gu, const BmmArgs& dn, int* cnt, int* err, hipStream_t s);
 bool bmm_qkv2(const BmmArgs& a, const BmmArgs& b, hipStream_t s);
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);
@@ -433,7 +455,9 @@ void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int h
                      const float2* rope, float* q_out, __half* k_cache, __half* v_cache, hipStream_t s,
                      const int* pos_arr = nullptr, const int* slot_arr = nullptr, size_t slot_stride = 0);
 // batched decode: tok[b] / pos[b] = the current token / position of KV slot slots[b]
-void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s);
+// (+ zero zero[i * zero_stride], i < zero_n: the step's in-launch chain counters)
+void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s, int* zero = nullptr,
+                  int zero_n = 0, int zero_stride = 1);
 // out[i] = x[i] (+) ... small helpers
 void add_inplace(float* x, const float* y, int n, hipStream_t s);
 void set_i32(int* p, int v, hipStream_t s);

@@ -1,6 +1,7 @@
 // Small kernels: embedding gather (on the GPU, not the CPU),
 // RMSNorm->bf16 for the prefill GEMMs (K2), prefill RoPE + KV append (K5/K6),
 // helpers, and the on-device synthetic weight generator.
+#include <algorithm>
 #include <hip/hip_bf16.h>
 
 #include "kernels.h"
@@ -133,17 +134,23 @@ void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int h
                      q_out, k_cache, v_cache, pos_arr, slot_arr, slot_stride);
 }
 
-__global__ void batch_gather_kernel(const int* slots, int B, const int* state, int* tok, int* pos) {
+__global__ void batch_gather_kernel(const int* slots, int B, const int* state, int* tok, int* pos, int* zero,
+                                    int zero_n, int zero_stride) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) {
     const int* st = state + (size_t)slots[b] * S_NSTATE;
     tok[b] = st[S_TOKEN];
     pos[b] = st[S_POS];
   }
+  if (b < zero_n) zero[(size_t)b * zero_stride] = 0;
 }
-void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s) {
+// (+ zero zero[i * zero_stride], i < zero_n: the step's in-launch chain counters)
+void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s, int* zero,
+                  int zero_n, int zero_stride) {
   if (B <= 0) return;
-  hipLaunchKernelGGL(batch_gather_kernel, dim3((B + 63) / 64), dim3(64), 0, s, slots, B, state, tok, pos);
+  const int n = std::max(B, zero ? zero_n : 0);
+  hipLaunchKernelGGL(batch_gather_kernel, dim3((n + 63) / 64), dim3(64), 0, s, slots, B, state, tok, pos, zero,
+                     zero ? zero_n : 0, zero_stride);
 }
 
 __global__ void add_inplace_kernel(float* x, const float* y, int n) {

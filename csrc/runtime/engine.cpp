@@ -197,6 +197,7 @@ Engine::~Engine() {
   }
   if (h_rmeta_) hipHostFree(h_rmeta_);
   if (wo_err_h_) hipHostFree(wo_err_h_);
+  if (chain_err_h_) hipHostFree(chain_err_h_);
   for (auto& e : step_ev_) if (e) hipEventDestroy(e);
   if (stream_) hipStreamDestroy(stream_);
 }
@@ -425,6 +426,14 @@ void Engine::setup_batch_mfma() {
     HIPCHK(hipMemsetAsync(step_clk_, 0, sizeof(long long) * 5 * kStepClkBlocks * 16, stream_));
   }
   if (!bg_) return;
+  if (const char* e = std::getenv("LFK_FFN_CHAIN")) ffn_chain_ = e[0] != '0';  // A/B
+  if (ffn_chain_) {
+    chain_cnt_ = (int*)dalloc(sizeof(int) * kChainInts * hp_.n_layer);
+    HIPCHK(hipMemsetAsync(chain_cnt_, 0, sizeof(int) * kChainInts * hp_.n_layer, stream_));
+    HIPCHK(hipHostMalloc((void**)&chain_err_h_, sizeof(int), hipHostMallocMapped));
+    *chain_err_h_ = 0;
+    HIPCHK(hipHostGetDevicePointer((void**)&chain_err_, chain_err_h_, 0));
+  }
   const int E = std::max(1, hp_.n_expert);
   xh_b_ = (__half*)dalloc(2ull * bmax_ * std::max({hp_.n_embd, nq_, F_l_}));
   {
@@ -530,6 +539,7 @@ void Engine::check_device_err() {
     throw std::runtime_error(last_error_);
   }
   if (wo_err_h_ && __atomic_load_n(wo_err_h_, __ATOMIC_ACQUIRE)) e = 200;  // the batched Wo's wait
+  if (!e && chain_err_h_ && __atomic_load_n(chain_err_h_, __ATOMIC_ACQUIRE)) e = 201;  // the FFN chain's
   if (e != 0) {
     healthy_ = false;
     last_error_ = "in-kernel hand-off wait timed out (code " + std::to_string(e) + ")";
@@ -1264,9 +1274,22 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
     a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
     a.dbg_clk = clk_of(l, 3);
+    BmmArgs dn;
+    dn.w = L.t_down; dn.xh = hh_b_; dn.ldh = F_l_; dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
+    dn.dbg_clk = clk_of(l, 4);
+    if (sk) {  // (the down projection re-zeroes the split-K Q|K|V rows for the next layer)
+      dn.zero = qkv_b_; dn.zero_n = (int)qkv_b_zero_n();
+    }
+    // gate/up and down in ONE launch, the down blocks waiting per K part on the gate/up tiles
+    // they read (bmm_ffn_chain): the down weight stream starts under the gate/up's last tiles
+    // instead of after a kernel boundary
+    if (ffn_chain_ && !tp && bmm_ffn_chain_supported(a, dn)) {
+      bmm_ffn_chain(a, dn, chain_cnt_ + kChainInts * l, chain_err_, s);
+      return;
+    }
     bmm(a, s);
     tp_begin();
-    down_rows(L.t_down, hh_b_, F_l_, acc, B, s, sk, clk_of(l, 4));
+    bmm(dn, s);
     tp_end();
     return;
   }
@@ -1288,7 +1311,9 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
 // device memory, so one captured graph per B serves every step).
 void Engine::enqueue_batch_step(int B, hipStream_t s) {
   const int d = hp_.n_embd;
-  batch_gather(bslots_, B, state_, btok_, bpos_, s);
+  // (its launch also zeroes the FFN chain counters of every layer)
+  batch_gather(bslots_, B, state_, btok_, bpos_, s, chain_cnt_, chain_cnt_ ? kChainInts / kChainStride * hp_.n_layer : 0,
+               kChainStride);
   embed_rows(tok_embd_, btok_, B, x_, s);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);

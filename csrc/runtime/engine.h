@@ -397,6 +397,12 @@ class Engine : public SlotBackend {
   bool moe_route_fuse_ = true;  // single-row MoE: the router inside the gate/up GEMV (LFK_MOE_ROUTE_FUSE A/B)
   int* wo_err_h_ = nullptr;   // host view
   int* wo_err_ = nullptr;     // device view
+  // batched dense FFN as one launch (bmm_ffn_chain): per-layer K-part counters (64 per layer),
+  // zeroed by each step's first kernel; a timed-out consumer wait sets *chain_err_ (host-mapped)
+  bool ffn_chain_ = true;     // LFK_FFN_CHAIN=0: two launches (A/B)
+  int* chain_cnt_ = nullptr;
+  int* chain_err_h_ = nullptr;
+  int* chain_err_ = nullptr;
   int* dec_done_ = nullptr;   // single-row decode: [n_layer][64] done counters (attn_wo1)
   size_t qkv_b_zero_n() const { return (size_t)bmax_ * (nq_ + 2 * nkvd_) + 16; }
 

@@ -195,7 +195,8 @@ def test_attn_decode(torch, hd, H, Hkv, L):
     pos = torch.tensor([L - 1], dtype=torch.int32, device="cuda")
     ws = torch.zeros(hip().attn_decode_workspace_floats(n_ctx, H, hd), device="cuda")
     out = torch.zeros(H, hd, device="cuda")
-    cnt = torch.zeros(64, dtype=torch.int32, device="cuda")
+    stride, xcds, n_ints = hip().chain_layout()
+    cnt = torch.zeros(n_ints, dtype=torch.int32, device="cuda")
     scale = 1 / np.sqrt(hd)
     for _ in range(3):  # repeated launches: counters must return to zero
         out.zero_()
@@ -553,6 +554,55 @@ def test_bmm_swiglu_epilogue_vs_fp32(torch, t, B, F, K):
         row = _swizzle4(got[b, :F][None])[0]   # the swizzle is its own inverse
         assert rel_err(row, ref[b]) < 3e-3, (b, rel_err(row, ref[b]))
         assert np.all(got[b, F:] == 7.0)
+
+
+@pytest.mark.parametrize("td", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B", [1, 6])
+@pytest.mark.parametrize("norm", [False, True])
+def test_bmm_ffn_chain_matches_two_launches(torch, td, B, norm):
+    """The gate/up + down chain in ONE launch (bmm_ffn_chain: down blocks wait per K part on the
+    gate/up tiles they read, then stage them with sc1 loads) against the same two projections as
+    separate launches, on the 8B FFN shape: the SwiGLU rows bit-identical, the down sums equal up
+    to the split-K atomics' order. Run three times over the same counters' fresh zeros."""
+    rng = np.random.default_rng(B * 10 + int(td) + norm)
+    F, K = 14336, 4096
+    raw_g, _ = make_matrix(GGMLType.Q4_K, 2 * F, K, rng)
+    raw_d, _ = make_matrix(td, K, F, rng)
+    dwg = dev_bytes(to_planar(GGMLType.Q4_K, raw_g, 2 * F, K))
+    dwd = dev_bytes(to_planar(td, raw_d, K, F))
+    tg = torch.empty(hip().t16_bytes(int(GGMLType.Q4_K), 2 * F, K), dtype=torch.uint8, device="cuda")
+    tdw = torch.empty(hip().t16_bytes(int(td), K, F), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dwg.data_ptr(), int(GGMLType.Q4_K), 2 * F, K, tg.data_ptr(), stream(), swiglu=True)
+    hip().t16_repack(dwd.data_ptr(), int(td), K, F, tdw.data_ptr(), stream(), swiglu=False)
+    X = rng.standard_normal((B, K)).astype(np.float32)
+    dxh = torch.from_numpy(_swizzle4(X.astype(np.float16))).cuda()
+    dxf = torch.from_numpy(X * 3).cuda()
+    nw = torch.from_numpy((0.5 + rng.random(K)).astype(np.float32)).cuda()
+    resid = torch.from_numpy(rng.standard_normal((B, K)).astype(np.float32)).cuda()
+    xf_ptr, norm_ptr = (dxf.data_ptr(), nw.data_ptr()) if norm else (0, 0)
+    # reference: the two launches
+    h_ref = torch.zeros(B, F, dtype=torch.float16, device="cuda")
+    out_ref = resid.clone()
+    hip().bmm(tg.data_ptr(), int(GGMLType.Q4_K), 2 * F, K, dxh.data_ptr(), K, 0, 0, B, stream(),
+              h_out=h_ref.data_ptr(), ldh_out=F, xf=xf_ptr, ldxf=K if norm else 0, norm=norm_ptr, eps=1e-5)
+    hip().bmm(tdw.data_ptr(), int(td), K, F, h_ref.data_ptr(), F, out_ref.data_ptr(), K, B, stream())
+    torch.cuda.synchronize()
+    stride, xcds, n_ints = hip().chain_layout()
+    cnt = torch.zeros(n_ints, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        cnt.zero_()
+        h = torch.full((B, F), 3.0, dtype=torch.float16, device="cuda")
+        out = resid.clone()
+        hip().bmm_ffn_chain(tg.data_ptr(), int(GGMLType.Q4_K), F, K, dxh.data_ptr(), xf_ptr, norm_ptr, 1e-5,
+                            tdw.data_ptr(), int(td), h.data_ptr(), out.data_ptr(), B, cnt.data_ptr(), stream())
+        torch.cuda.synchronize()
+        assert torch.equal(h, h_ref)
+        assert rel_err(out.cpu().numpy() - resid.cpu().numpy(), out_ref.cpu().numpy() - resid.cpu().numpy()) < 1e-5
+        # every K part counted all of its 224 gate/up tiles
+        c = cnt.cpu().numpy()
+        per_part = c.reshape(-1, xcds, stride)[:, :, 0].sum(1)
+        assert per_part[:8].tolist() == [224] * 8 and not per_part[8:].any(), per_part
+        assert c.sum() == 8 * 224
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
