@@ -354,7 +354,7 @@ __device__ __forceinline__ int raw_word(const BRawT<T>& w) {
 // MFMA A fragments, B = the staged x row of column r16 (xrow indexed by global k), one
 // accumulator per chunk h (two dependent chains of 4 MFMAs instead of one of 8: the MFMA
 // read-after-write stalls were 24 % of the gate/up kernel's wave cycles)
-template <int QT>
+template <int QT, bool RAW = false>
 __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, const __half* xrow, f4_t& acc, f4_t& acc2) {
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -365,7 +365,13 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
     const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
     const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
     HFrag F;
-    dequant_frags<QT>(wc[h], c, F);
+    if constexpr (RAW) {  // microbenchmark (wt_body DBG 7): the MFMAs on the raw quant words
+      const int rw = raw_word<QT>(wc[h]);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) F.w[i] = (unsigned)rw + i;
+    } else {
+      dequant_frags<QT>(wc[h], c, F);
+    }
     const uint4 xr[4] = {x0, x1, x2, x3};
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -991,12 +997,20 @@ __device__ __forceinline__ void xstage_sc1(const BmmArgs& a, __half* xs, int ldx
   }
 }
 
+// The staged x rows' stride past the part (f16 elements): rows 24 halves = 12 banks apart make the
+// ds_read_b128 B-operand reads of the K-quant chunk order conflict-free at B <= 6 (1.5-way at 7-8;
+// 8 halves: 2-way from B = 4). Lane groups of ds_read_b128 per MI355X_MICROARCH's LDS table.
+constexpr int kWtXPad = 24;
+
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
 // per launch (registers and branches) when they were runtime ones
 // (bid, nblk): the block's index and count in the launch's wave-owned grid (the fused attention +
 // Wo launch runs this body in planes of its grid past the attention's)
-template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false>
+// DBG (microbenchmarks, tools/boundary_bench.py; BmmArgs::debug 4-7): 4 = the weight stream alone
+// (no x staging, no MFMA), 5 = x staging + weight stream (no MFMA), 6 = weight stream + MFMA (no x
+// staging), 7 = as 6 with the MFMAs on the raw quant words (no dequantisation)
+template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false, int DBG = 0>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
   constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1009,7 +1023,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // down: 8 parts x 32 groups of 8 tiles = one block per CU for the 256-tile shapes)
   const int kparts = a.kparts, kp = bid % kparts, grp = bid / kparts, G = nblk / kparts;
   const int s0 = kp * a.spp, ns = min(steps, s0 + a.spp) - s0;  // this part's steps [s0, s0 + ns)
-  const int k0 = s0 * 256, kn = ns * 256, ldx = kn + 8;
+  const int k0 = s0 * 256, kn = ns * 256, ldx = kn + kWtXPad;
   if (MOE && !SK && a.ew && a.steps_per_expert > 0) {
     // MoE down: the part of an unrouted expert adds nothing (and its SwiGLU rows were never
     // written - its gate/up tiles were skipped): the whole block leaves, before any barrier
@@ -1139,7 +1153,8 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // (XF: that barrier goes first - an asm memory clobber between the x loads and their LDS stores
   // made the compiler keep the x registers in scratch)
   if (XF && xmode == 2) lds_barrier();
-  if constexpr (XF) {
+  if constexpr (DBG == 4 || DBG == 6) issue();
+  else if constexpr (XF) {
     if (!SK && a.chain_role == 2) {  // chain consumer: the weights do not depend on the producer
       issue();
       chain_wait(a, kp, tid);
@@ -1244,7 +1259,10 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
       if (j0 + r >= N) break;  // wave-uniform
       if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
       __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
-      bmm_step<QT>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
+      if constexpr (DBG == 4 || DBG == 5)
+        asm volatile("" ::"v"(raw_word<QT>(buf[r][0])), "v"(raw_word<QT>(buf[r][1])));
+      else
+        bmm_step<QT, DBG == 7>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
       if (++cstep == ns) {
         finish();
         cstep = 0;
@@ -1265,6 +1283,13 @@ template <int QT, int PD, bool MOE = false, bool XF = false>
 __global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   wt_body<QT, PD, false, 8, MOE, XF>(*ka, 0, blockIdx.x, gridDim.x);
+  (void)a;
+}
+
+template <int QT, int DBG>
+__global__ __launch_bounds__(512, 2) void bmm_wt_dbg_kernel(BmmArgs a) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  wt_body<QT, 2, false, 8, false, true, DBG>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1424,11 +1449,11 @@ static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
       // whose staged slice fits the LDS and divides the expert's steps
       const int spe = a.steps_per_expert, E = steps / spe;
       int ppe = std::max(1, (kparts + E / 2) / E);
-      while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + 8) * 2 > 150 * 1024)) ++ppe;
+      while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + kWtXPad) * 2 > 150 * 1024)) ++ppe;
       kparts = E * ppe;
     }
     // the staged slice (B rows x part) stays within the LDS
-    while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + 8) * 2 > 150 * 1024) ++kparts;
+    while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + kWtXPad) * 2 > 150 * 1024) ++kparts;
   }
   a.spp = (steps + kparts - 1) / kparts;
   a.kparts = kparts = (steps + a.spp - 1) / a.spp;
@@ -1436,7 +1461,7 @@ static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
   // group (two blocks per CU - twice the weight bytes in flight - measured the same, r3 sweep)
   const int G = std::max(1, std::min(std::max(1, cus / kparts), wt_k ? (tiles + 7) / 8 : tiles));
   // more than half the CU's LDS: one block per CU, so the even tile split is an even CU split
-  lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + 8) * 2, 81 * 1024);
+  lds = std::max<size_t>(256 + (size_t)a.B * (a.spp * 256 + kWtXPad) * 2, 81 * 1024);
   return G * kparts;
 }
 
@@ -1455,6 +1480,13 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   if (wt_sw || wt_k) {
     size_t lds = 0;
     const int nblk = wt_config(a, wt_k, lds);
+    if (a.debug >= 4 && !a.ew) {  // microbenchmarks (wt_body's DBG)
+      if (a.debug == 4) hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 4>), dim3(nblk), dim3(512), lds, s, a);
+      else if (a.debug == 5) hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 5>), dim3(nblk), dim3(512), lds, s, a);
+      else if (a.debug == 6) hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 6>), dim3(nblk), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 7>), dim3(nblk), dim3(512), lds, s, a);
+      return;
+    }
     if (bmm_xfirst()) {
       if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
       else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
@@ -1527,7 +1559,7 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   const int ga = (ta + a.tpg - 1) / a.tpg, gb = (tb + a.tpg - 1) / a.tpg;
   a.nb1 = ga;
   const dim3 grid((ga + gb) * a.kparts);
-  const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + 8) * 2;
+  const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + kWtXPad) * 2;
   const bool xf = bmm_xfirst();
   if constexpr (QT2 == 0) {
     if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);

@@ -146,7 +146,9 @@ struct BmmArgs {
   int* chain_err = nullptr;        // host-mapped: a consumer's bounded wait timed out
   int chain_poll = 0;              // consumer poll interval: s_sleep units (64 clocks) between polls
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only (bmm_kernel); wave-owned
-                                   // kernels: 2 = exit at entry, 3 = no epilogue writes (tools/boundary_bench.py)
+                                   // kernels: 2 = exit at entry, 3 = no epilogue writes, 4 = weight stream only,
+                                   // 5 = x staging + weights, 6 = weights + MFMA, 7 = 6 without the
+                                   // dequantisation (tools/boundary_bench.py)
   // Q|K|V epilogue (one K part only, see bmm_qkv_fits): instead of accumulating into `out`,
   // segment kinds seg_kind[i] (0 = Q, 1 = K, 2 = V) are finished in the epilogue - RoPE on
   // adjacent pairs for Q and K, Q rows to q_out[b][row], K / V rows as f16 into the slot

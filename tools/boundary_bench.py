@@ -39,7 +39,12 @@ def main():
     ap.add_argument("--rows", type=int, default=6)
     ap.add_argument("--n", type=int, default=24, help="launches per chain")
     ap.add_argument("--json", default=None)
-    ap.add_argument("--debug", default="0,3,2", help="BmmArgs::debug forms to run")
+    ap.add_argument("--debug", default="0,3,2", help="BmmArgs::debug forms to run (wave-owned kernels: "
+                    "0 full, 2 exit at entry, 3 no epilogue writes, 4 weight stream only, 5 x staging + "
+                    "weights, 6 weights + MFMA)")
+    ap.add_argument("--norm", action="store_true", help="gate/up stages f32 x rows with the RMSNorm folded "
+                    "(as the engine's batched step does)")
+    ap.add_argument("--chains", default="wo,gu,down,layer")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -54,9 +59,13 @@ def main():
     xh = torch.randn(16, 14336, device="cuda").half()
     out = torch.zeros(16, 28672, device="cuda")
     hout = torch.zeros(16, 14336, dtype=torch.float16, device="cuda")
+    xf = torch.randn(16, 4096, device="cuda")
+    nw = torch.ones(4096, device="cuda")
     chains = {"wo": ["wo"] * args.n, "gu": ["gu"] * args.n, "down": ["down"] * args.n,
               "layer": (["wo", "gu", "down"] * args.n)[:args.n]}
-    res = {"env": {k: os.environ.get(k) for k in ("HIP_FORCE_DEV_KERNARG", "GPU_MAX_HW_QUEUES")}}
+    chains = {k: v for k, v in chains.items() if k in args.chains.split(",")}
+    res = {"env": {k: os.environ.get(k) for k in ("HIP_FORCE_DEV_KERNARG", "GPU_MAX_HW_QUEUES")},
+           "norm": args.norm}
     for dbg, (cname, seq) in [(int(d), c) for d in args.debug.split(",") for c in chains.items()]:
         clk = torch.zeros(len(seq), 8192 * 8, dtype=torch.int64, device="cuda")
         use = {k: 0 for k in SHAPES}
@@ -66,8 +75,11 @@ def main():
                 t, R, K, sw = SHAPES[name]
                 w = bufs[name][use[name] % len(bufs[name])]
                 use[name] += 1
+                nx = sw and args.norm
                 h.bmm(w.data_ptr(), t, R, K, xh.data_ptr(), K, out.data_ptr(), R, B, st, debug=dbg,
-                      h_out=hout.data_ptr() if sw else 0, ldh_out=R // 2, dbg_clk=clk[i].data_ptr())
+                      h_out=hout.data_ptr() if sw else 0, ldh_out=R // 2, dbg_clk=clk[i].data_ptr(),
+                      xf=xf.data_ptr() if nx else 0, ldxf=K if nx else 0, norm=nw.data_ptr() if nx else 0,
+                      eps=1e-5)
         g = torch.cuda.CUDAGraph()
         cs = torch.cuda.Stream()
         with torch.cuda.stream(cs):

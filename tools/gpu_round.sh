@@ -88,6 +88,8 @@ for s in "$@"; do
     prefprof) prof prefprof 300 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
     bmmpmc) pmc bmmpmc tools/batch_bench.py --batches 6 --steps 4 ;;
     t16pmc) pmc t16pmc tools/gemm_bench.py --eager --reps 5 --T 512 --t16 ;;
+    # the wave-owned projections by part (full / weights + MFMA / weights only), counters per kernel
+    wtpmc) pmc wtpmc tools/boundary_bench.py --debug 0,6,4 --chains gu,down --n 12 --norm ;;
     blocks) step blocks 200 python tools/step_blocks.py --json gpurun_out/blocks.json ;;
     attntl) step attntl 200 python tools/attn_timeline.py --rows 6 --L 700 ;;
     bmmtl) step bmmtl 200 python tools/bmm_timeline.py --rows 6 --json gpurun_out/bmm_tl6.json ;;
@@ -118,6 +120,15 @@ for s in "$@"; do
            step abe_off_prof 240 env $AB_ENV rocprofv3 --kernel-trace --stats -d gpurun_out/abe_off_prof -o k \
              --output-format csv -- python3 tools/batch_bench.py --batches 6 --steps 32
            python3 tools/step_slots.py gpurun_out/abe_off_prof/k_kernel_trace.csv > gpurun_out/abe_off_slots.txt ;;
+    # ---- same-box A/B of several env configurations: AB_CONFIGS="A=1,B=2 C=3" (space-separated
+    #      configs, comma-separated vars; "-" = the defaults), alternating, two rounds
+    abmulti) for r in 1 2; do
+               i=0
+               for c in $AB_CONFIGS; do
+                 i=$((i + 1))
+                 step "abm_${i}_$r" 200 env $(echo "$c" | tr ',' ' ' | sed 's/^-$//') python tools/batch_bench.py --batches 6,8 --steps 64
+               done
+             done ;;
     # ---- round-end check of the committed tree
     final) bash "$0" gputests smoke bench20 serial stepprof decprof || exit $? ;;
     *) echo "unknown target $s" >&2; exit 2 ;;
