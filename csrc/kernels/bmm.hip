@@ -343,6 +343,44 @@ __device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, in
   }
 }
 
+// tload through a buffer resource over the matrix (IL kernels): the step's byte offset is a
+// uniform scalar (soffset), the lane's part a constant voffset and the plane offsets immediates -
+// no per-step 64-bit address arithmetic, whose temporaries the register allocator placed in the
+// registers of loads still in flight (a vmcnt wait on them drained the ring at every round)
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+template <int T>
+__device__ __forceinline__ void tload_rs(BRawT<T>& w, __amdgpu_buffer_rsrc_t rs, int so, int h, int l, int r16, int kq) {
+  auto b128 = [&](int vo, int imm) {  // quant planes: non-temporal (aux 2: each weight is read once per step)
+    const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so + imm, 2));
+    return make_int4(t.x, t.y, t.z, t.w);
+  };
+  auto b128c = [&](int vo, int imm) {
+    const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so + imm, 0));
+    return make_int4(t.x, t.y, t.z, t.w);
+  };
+  auto b64 = [&](int vo, int imm) {
+    const v2i_t t = __builtin_bit_cast(v2i_t, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so + imm, 0));
+    return make_uint2((unsigned)t.x, (unsigned)t.y);
+  };
+  if constexpr (T == T_Q4_K) {
+    w.q = b128(l * 16, h * 1024);
+    w.m = b64(r16 * 32 + 8 * (kq >> 1), 2048 + 16 * h);
+  } else if constexpr (T == T_Q5_K) {
+    w.q = b128(l * 16, h * 1024);
+    w.h = b128c(r16 * 32 + 16 * (kq & 1), 2048);
+    w.m = b64(r16 * 32 + 8 * (kq >> 1), 2560 + 16 * h);
+  } else if constexpr (T == T_Q6_K) {
+    w.l = b128(l * 16, h * 1024);
+    w.x = b64(l * 8, 2048 + h * 512);
+    w.s = __builtin_amdgcn_raw_buffer_load_b32(rs, r16 * 32 + kq * 4, so + 3072 + 16 * h, 0);
+  } else {
+    w.a = b128(l * 16, h * 2048);
+    w.b = b128(l * 16, h * 2048 + 1024);
+    w.d = __builtin_amdgcn_raw_buffer_load_b16(rs, l * 2, so + 4096 + h * 128, 0);
+  }
+}
+
 template <int T>
 __device__ __forceinline__ int raw_word(const BRawT<T>& w) {
   if constexpr (T == T_Q4_K || T == T_Q5_K) return w.q.x;
@@ -353,18 +391,20 @@ __device__ __forceinline__ int raw_word(const BRawT<T>& w) {
 // One 256-k step of a 16-row tile: lane l's chunks 8s + 4h + kq (h = 0, 1) dequantised into
 // MFMA A fragments, B = the staged x row of column r16 (xrow indexed by global k), one
 // accumulator per chunk h (two dependent chains of 4 MFMAs instead of one of 8: the MFMA
-// read-after-write stalls were 24 % of the gate/up kernel's wave cycles)
-template <int QT, bool RAW = false>
+// read-after-write stalls were 24 % of the gate/up kernel's wave cycles).
+// IL: all 8 B-operand LDS reads first (the dequantisation then covers their latency; read per
+// chunk, each group of 4 was waited for right behind its issue), both chunks dequantised, and the
+// two accumulators' MFMAs alternating (one chain after the other stalled on every MFMA)
+template <int QT, bool RAW = false, bool IL = false>
 __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, const __half* xrow, f4_t& acc, f4_t& acc2) {
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = 8 * s + 4 * h + kq;
-    int off_lo, off_hi;
-    chunk_runs<QT>(c, off_lo, off_hi);
-    const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
-    const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
-    const uint4 x0 = xl[0], x1 = xl[1], x2 = xh[0], x3 = xh[1];
-    HFrag F;
+  // MFMA m takes 8 weights of ONE run: the low run's 0-7 / 8-15 (m = 0 / 1), then the high run's
+  // (m = 2 / 3) - pairs of quant dwords 2(m % 2), 2(m % 2) + 1 - so its B operand is the 16-byte
+  // LDS read as it stands (taking 4 halves from each run cost 3 v_mov per MFMA)
+  auto frag = [](const HFrag& F, int m) {
+    const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
+    return make_uint4(F.w[4 * dw + sh], F.w[4 * dw + sh + 1], F.w[4 * dw + 4 + sh], F.w[4 * dw + 5 + sh]);
+  };
+  auto deq = [&](int h, int c, HFrag& F) {
     if constexpr (RAW) {  // microbenchmark (wt_body DBG 7): the MFMAs on the raw quant words
       const int rw = raw_word<QT>(wc[h]);
 #pragma unroll
@@ -372,17 +412,44 @@ __device__ __forceinline__ void bmm_step(const BRawT<QT>* wc, int s, int kq, con
     } else {
       dequant_frags<QT>(wc[h], c, F);
     }
-    const uint4 xr[4] = {x0, x1, x2, x3};
+  };
+  if constexpr (IL) {
+    uint4 xr[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int off_lo, off_hi;
+      chunk_runs<QT>(8 * s + 4 * h + kq, off_lo, off_hi);
+      const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+      const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+      xr[h][0] = xl[0]; xr[h][1] = xl[1]; xr[h][2] = xh[0]; xr[h][3] = xh[1];
+    }
+    HFrag F0, F1;
+    deq(0, 8 * s + kq, F0);
+    deq(1, 8 * s + 4 + kq, F1);
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      // MFMA m takes 8 weights of ONE run: the low run's 0-7 / 8-15 (m = 0 / 1), then the high
-      // run's (m = 2 / 3) - pairs of quant dwords 2(m % 2), 2(m % 2) + 1 - so its B operand is
-      // the 16-byte LDS read as it stands (taking 4 halves from each run cost 3 v_mov per MFMA)
-      const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
-      const uint4 av = make_uint4(F.w[4 * dw + sh], F.w[4 * dw + sh + 1], F.w[4 * dw + 4 + sh], F.w[4 * dw + 5 + sh]);
-      f4_t& ac = h == 0 ? acc : acc2;
-      ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, av),
-                                                  __builtin_bit_cast(h8_t, xr[m]), ac, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, frag(F0, m)),
+                                                   __builtin_bit_cast(h8_t, xr[0][m]), acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, frag(F1, m)),
+                                                    __builtin_bit_cast(h8_t, xr[1][m]), acc2, 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = 8 * s + 4 * h + kq;
+      int off_lo, off_hi;
+      chunk_runs<QT>(c, off_lo, off_hi);
+      const uint4* xl = reinterpret_cast<const uint4*>(xrow + off_lo);
+      const uint4* xh = reinterpret_cast<const uint4*>(xrow + off_hi);
+      const uint4 xr[4] = {xl[0], xl[1], xh[0], xh[1]};
+      HFrag F;
+      deq(h, c, F);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        f4_t& ac = h == 0 ? acc : acc2;
+        ac = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8_t, frag(F, m)),
+                                                    __builtin_bit_cast(h8_t, xr[m]), ac, 0, 0, 0);
+      }
     }
   }
 }
@@ -1001,6 +1068,25 @@ __device__ __forceinline__ void xstage_sc1(const BmmArgs& a, __half* xs, int ldx
 // ds_read_b128 B-operand reads of the K-quant chunk order conflict-free at B <= 6 (1.5-way at 7-8;
 // 8 halves: 2-way from B = 4). Lane groups of ds_read_b128 per MI355X_MICROARCH's LDS table.
 constexpr int kWtXPad = 24;
+// weight steps in flight per wave in the IL kernels (LFK_BMM_PD=3 / 4 for the A/B)
+static int bmm_pd() {
+  static const int v = [] {
+    const char* e = std::getenv("LFK_BMM_PD");
+    const int p = e ? std::atoi(e) : 2;
+    return p == 3 || p == 4 ? p : 2;
+  }();
+  return v;
+}
+// interleaved step (bmm_step's IL) in the dense wave-owned kernels; LFK_BMM_IL=0 for the A/B
+static bool bmm_il() {
+  static const bool v = [] {
+    const char* e = std::getenv("LFK_BMM_IL");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+// ... whose weight loads go through a 2 GB buffer resource over the matrix
+static bool bmm_il_fits(const BmmArgs& a) { return t16_bytes(a.w.type, a.w.rows, a.w.K) < 0x7FFFFFFFull; }
 
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
@@ -1010,7 +1096,8 @@ constexpr int kWtXPad = 24;
 // DBG (microbenchmarks, tools/boundary_bench.py; BmmArgs::debug 4-7): 4 = the weight stream alone
 // (no x staging, no MFMA), 5 = x staging + weight stream (no MFMA), 6 = weight stream + MFMA (no x
 // staging), 7 = as 6 with the MFMAs on the raw quant words (no dequantisation)
-template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false, int DBG = 0>
+template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false, int DBG = 0, bool IL = false,
+          int EPI = 0>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
   constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1100,10 +1187,17 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // first block, never used), so the loads are branch-free - a conditional load makes the
   // compiler's vmcnt accounting assume the path without it and wait for every later load at the
   // x staging (XF)
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.w.base), 0, 0x7FFFFFFF, 0x00020000);
   auto load_first = [&](BRawT<QT>* dst, bool real) {
-    const uint8_t* p = real ? lp + (size_t)ls * SB : a.w.base;
-    tload<QT>(dst[0], p, 0, lane, r16, kq);
-    tload<QT>(dst[1], p, 1, lane, r16, kq);
+    if constexpr (IL) {  // (IL is never SK: one matrix, based at a.w.base, < 2 GB - the launcher checks)
+      const int so = real ? (int)(lp - a.w.base) + ls * SB : 0;
+      tload_rs<QT>(dst[0], wrs, so, 0, lane, r16, kq);
+      tload_rs<QT>(dst[1], wrs, so, 1, lane, r16, kq);
+    } else {
+      const uint8_t* p = real ? lp + (size_t)ls * SB : a.w.base;
+      tload<QT>(dst[0], p, 0, lane, r16, kq);
+      tload<QT>(dst[1], p, 1, lane, r16, kq);
+    }
     if (real && ++ls == ns) {
       ls = 0;
       if (++li < nt) lp = tbase(li);
@@ -1216,7 +1310,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
         for (int i = 0; i < 4; ++i)
           if (row0 + i < n_out) atomicAdd(o + row0 + i, y[i]);
       }
-    } else if (a.swiglu_epi) {
+    } else if (EPI == 1 || (EPI == 0 && a.swiglu_epi)) {
       // rows 0-7 (lanes 0-31): gate of features 8 gt + 4 kq + i; rows 8-15 (lanes 32-63): up
       f4_t up;
 #pragma unroll
@@ -1234,9 +1328,18 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
         else
           *reinterpret_cast<uint2*>(h) = make_uint2(as_u(p0), as_u(p1));
       }
-      if (!MOE && a.chain_role == 1) {  // the tile's rows have landed: count it for its consumer part
+      if (EPI == 0 && !MOE && a.chain_role == 1) {  // the tile's rows have landed: count it for its consumer part
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add(a.chain_cnt + (gt / a.chain_tpp * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else if (EPI == 2) {  // split-K only: fp32 atomics, no read-modify-write path
+      if (col_ok) {
+        float* o = a.out + (size_t)r16 * a.ldo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = gt * 16 + 4 * kq + i;
+          if (row < a.n_out) atomicAdd(o + row, acc[i]);
+        }
       }
     } else if (col_ok) {
       float* o = a.out + (size_t)r16 * a.ldo;
@@ -1253,22 +1356,50 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     acc = f4_t{0.f, 0.f, 0.f, 0.f};
     acc2 = acc;
   };
-  for (int j0 = 0; j0 < N; j0 += R) {
+  auto step = [&](int r, int j0) __attribute__((always_inline)) {
+    // branch-free (past the wave's last step: the matrix's first block, never used): under an
+    // `if` the waitcnt pass merged the paths with and without these loads and waited for every
+    // load in flight - vmcnt(0) every 1-2 steps, the PD-deep ring drained
+    if constexpr (IL) load_first(buf[(r + PD) % R], j0 + r + PD < N);
+    else if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
+    __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
+    if constexpr (DBG == 4 || DBG == 5)
+      asm volatile("" ::"v"(raw_word<QT>(buf[r][0])), "v"(raw_word<QT>(buf[r][1])));
+    else
+      bmm_step<QT, DBG == 7, IL>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
+    if (++cstep == ns) {
+      finish();
+      cstep = 0;
+      ++ci;
+      if (clk && tid == 0 && ci == 1) clk[3] = wall_clock64();
+    }
+  };
+  int j0 = 0;
+  if constexpr (IL) {
+    // whole rounds of R steps without an exit inside (the loop back-edge then has ONE predecessor
+    // state: the waitcnt pass's merge of the early-exit paths waited for more loads than needed),
+    // then the remaining N % R steps
+    for (; j0 + R <= N; j0 += R) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) step(r, j0);
+    }
+  }
+  for (; j0 < N; j0 += R) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (j0 + r >= N) break;  // wave-uniform
-      if (j0 + r + PD < N) load_next(buf[(r + PD) % R]);
-      __builtin_amdgcn_sched_barrier(0);  // one step per scheduling region (register count)
-      if constexpr (DBG == 4 || DBG == 5)
-        asm volatile("" ::"v"(raw_word<QT>(buf[r][0])), "v"(raw_word<QT>(buf[r][1])));
-      else
-        bmm_step<QT, DBG == 7>(buf[r], s0 + cstep, kq, xrow, acc, acc2);
-      if (++cstep == ns) {
-        finish();
-        cstep = 0;
-        ++ci;
-        if (clk && tid == 0 && ci == 1) clk[3] = wall_clock64();
-      }
+      step(r, j0);
+    }
+  }
+  // EPI 1 (the SwiGLU epilogue alone): the chain producer counts its tiles once all are stored - a
+  // vmcnt(0) at every tile end made the waitcnt pass drain the weight ring in the step loop
+  if constexpr (EPI == 1 && !MOE) {
+    if (a.chain_role == 1 && nt > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0)
+        for (int i = 0; i < nt; ++i)
+          __hip_atomic_fetch_add(a.chain_cnt + (tile_of(i) / a.chain_tpp * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride,
+                                 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (clk) {  // exit: the block's LAST wave (waves of one block can end microseconds apart)
@@ -1279,10 +1410,12 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
 
 // (the body reads its arguments through the kernarg segment pointer: a reference to the by-value
 // parameter made the compiler copy the whole block to scratch, as in bmm_kernel)
-template <int QT, int PD, bool MOE = false, bool XF = false>
-__global__ __launch_bounds__(512, 2) void bmm_wt_kernel(BmmArgs a) {
+// (PD > 2: one block per CU - the launchers' LDS request - so a register budget of 256, not 128)
+// EPI: the epilogue as a compile-time kind (0 any, 1 SwiGLU, 2 split-K atomics)
+template <int QT, int PD, bool MOE = false, bool XF = false, bool IL = false, int EPI = 0>
+__global__ __launch_bounds__(512, PD > 2 ? 1 : 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, false, 8, MOE, XF>(*ka, 0, blockIdx.x, gridDim.x);
+  wt_body<QT, PD, false, 8, MOE, XF, 0, IL, EPI>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1314,12 +1447,12 @@ __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
 
 // The SwiGLU gate/up (QT1, producer) and the down projection (QT2, consumer) in ONE launch:
 // blocks [0, a.nb1) run the gate/up, the rest the down (their own BmmArgs: the second kernarg).
-template <int QT1, int QT2>
-__global__ __launch_bounds__(512, 2) void bmm_chain_kernel(BmmArgs a, BmmArgs b) {
+template <int QT1, int QT2, bool IL = false, int PD = 2>
+__global__ __launch_bounds__(512, PD > 2 ? 1 : 2) void bmm_chain_kernel(BmmArgs a, BmmArgs b) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int n1 = ka[0].nb1;
-  if ((int)blockIdx.x < n1) wt_body<QT1, 2, false, 8, false, true>(ka[0], 0, blockIdx.x, n1);
-  else wt_body<QT2, 2, false, 8, false, true>(ka[1], 0, blockIdx.x - n1, gridDim.x - n1);
+  if ((int)blockIdx.x < n1) wt_body<QT1, PD, false, 8, false, true, 0, IL, IL ? 1 : 0>(ka[0], 0, blockIdx.x, n1);
+  else wt_body<QT2, PD, false, 8, false, true, 0, IL, IL ? 2 : 0>(ka[1], 0, blockIdx.x - n1, gridDim.x - n1);
   (void)a;
   (void)b;
 }
@@ -1465,6 +1598,13 @@ static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
   return G * kparts;
 }
 
+template <int QT, int EPI>
+static void launch_wt_il(int pd, int nblk, size_t lds, const BmmArgs& a, hipStream_t s) {
+  if (pd == 3) hipLaunchKernelGGL((bmm_wt_kernel<QT, 3, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
+  else if (pd == 4) hipLaunchKernelGGL((bmm_wt_kernel<QT, 4, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
+  else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
+}
+
 template <int QT>
 static void launch_bmm(BmmArgs a, hipStream_t s) {
   int tiles = (a.n_out + 15) / 16;
@@ -1489,6 +1629,12 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     }
     if (bmm_xfirst()) {
       if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
+      else if (bmm_il() && bmm_il_fits(a)) {
+        const int pd = bmm_pd(), epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
+        if (epi == 1) launch_wt_il<QT, 1>(pd, nblk, lds, a, s);
+        else if (epi == 2) launch_wt_il<QT, 2>(pd, nblk, lds, a, s);
+        else launch_wt_il<QT, 0>(pd, nblk, lds, a, s);
+      }
       else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
     } else {
       if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(nblk), dim3(512), lds, s, a);
@@ -1661,8 +1807,21 @@ void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, h
   gu.nb1 = n1;
   const dim3 grid(n1 + n2);
   const size_t lds = std::max(lds1, lds2);
-  if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, gu, dn);
-  else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, gu, dn);
+  if (bmm_il() && bmm_il_fits(gu) && bmm_il_fits(dn)) {
+    const int pd = bmm_pd();
+    if (dn.w.type == T_Q6_K) {
+      if (pd == 3) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true, 3>), grid, dim3(512), lds, s, gu, dn);
+      else if (pd == 4) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true, 4>), grid, dim3(512), lds, s, gu, dn);
+      else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true>), grid, dim3(512), lds, s, gu, dn);
+    } else {
+      if (pd == 3) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true, 3>), grid, dim3(512), lds, s, gu, dn);
+      else if (pd == 4) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true, 4>), grid, dim3(512), lds, s, gu, dn);
+      else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true>), grid, dim3(512), lds, s, gu, dn);
+    }
+  } else {
+    if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, gu, dn);
+    else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, gu, dn);
+  }
 }
 
 bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
