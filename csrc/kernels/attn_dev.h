@@ -170,6 +170,13 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
       const int kv = tid / (HD / 2), pr = tid % (HD / 2);
       nv = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
     }
+    if (a.rope) {  // deferred RoPE: rotate q's pairs and the new key's at the row's position
+      const float2* rr = a.rope + (size_t)min(max(*a.pos, 0), a.n_ctx - 1) * (HD / 2);
+      auto rot = [](float2 v, float2 cs) { return make_float2(v.x * cs.x - v.y * cs.y, v.x * cs.y + v.y * cs.x); };
+#pragma unroll
+      for (int j = 0; j < QPT; ++j) qv[j] = rot(qv[j], rr[min(tid + 256 * j, G * HD / 2 - 1) % (HD / 2)]);
+      if (tid < HD / 2) nv = rot(nv, rr[tid]);
+    }
   }
   const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
   uint4 kr[NLD], vr[NLD];

@@ -1085,8 +1085,7 @@ static bool bmm_il() {
   }();
   return v;
 }
-// ... whose weight loads go through a 2 GB buffer resource over the matrix
-static bool bmm_il_fits(const BmmArgs& a) { return t16_bytes(a.w.type, a.w.rows, a.w.K) < 0x7FFFFFFFull; }
+
 
 // SK: the split-K Q|K|V launch (segments, RoPE'd atomic partials, per-part norm staging) - a
 // compile-time switch: the generic code paths cost the gate/up / Wo / down instantiations ~0.7 us
@@ -1187,12 +1186,17 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // first block, never used), so the loads are branch-free - a conditional load makes the
   // compiler's vmcnt accounting assume the path without it and wait for every later load at the
   // x staging (XF)
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.w.base), 0, 0x7FFFFFFF, 0x00020000);
+  // IL: a buffer resource over the wave's current tile (its steps at soffset ls * SB); the
+  // matrix's first block for the steps past the wave's last
+  auto rsrc = [](const uint8_t* p) { return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p), 0, 0x7FFFFFFF, 0x00020000); };
+  const auto rs0 = rsrc(a.w.base);
+  auto rs_cur = rsrc(lp);
   auto load_first = [&](BRawT<QT>* dst, bool real) {
-    if constexpr (IL) {  // (IL is never SK: one matrix, based at a.w.base, < 2 GB - the launcher checks)
-      const int so = real ? (int)(lp - a.w.base) + ls * SB : 0;
-      tload_rs<QT>(dst[0], wrs, so, 0, lane, r16, kq);
-      tload_rs<QT>(dst[1], wrs, so, 1, lane, r16, kq);
+    if constexpr (IL) {
+      const auto rs = real ? rs_cur : rs0;
+      const int so = real ? ls * SB : 0;
+      tload_rs<QT>(dst[0], rs, so, 0, lane, r16, kq);
+      tload_rs<QT>(dst[1], rs, so, 1, lane, r16, kq);
     } else {
       const uint8_t* p = real ? lp + (size_t)ls * SB : a.w.base;
       tload<QT>(dst[0], p, 0, lane, r16, kq);
@@ -1200,7 +1204,10 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     }
     if (real && ++ls == ns) {
       ls = 0;
-      if (++li < nt) lp = tbase(li);
+      if (++li < nt) {
+        lp = tbase(li);
+        if constexpr (IL) rs_cur = rsrc(lp);
+      }
     }
   };
   // microbenchmark timeline (wave 0, as bmm_kernel's): [0] entry [1] weights issued [2] x staged
@@ -1241,7 +1248,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
     }
 #pragma unroll
     for (int p = 0; p < PD; ++p) load_first(buf[p], p < N);
-    if constexpr (SK) pos = a.qkv.pos[col_ok ? r16 : 0];
+    if constexpr (SK && !IL) pos = a.qkv.pos[col_ok ? r16 : 0];
     if (!XF && xmode == 2) lds_barrier();  // rowss zeroed
   };
   // (XF: that barrier goes first - an asm memory clobber between the x loads and their LDS stores
@@ -1267,7 +1274,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   if (clk && tid == 0) clk[2] = wall_clock64();
   if (SK && a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
-  if constexpr (SK) {
+  if constexpr (SK && !IL) {  // (IL: the RoPE is the attention's - bmm_qkv_sk_defers_rope)
     pos = min(max(pos, 0), a.qkv.n_ctx - 1);
     rope_load(0);
   }
@@ -1297,14 +1304,16 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
       float* o = (sg == 0 ? a.out : sg == 1 ? a.seg_out[1] : a.seg_out[2]) + (size_t)r16 * a.ldo;
       const int row0 = (gt - seg_first(sg)) * 16 + 4 * kq;
       f4_t y = acc;
-      if (kind < 2) {  // RoPE on the adjacent pairs (0, 1), (2, 3) of this lane's rows
+      if (!IL && kind < 2) {  // RoPE on the adjacent pairs (0, 1), (2, 3) of this lane's rows
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           y[2 * j] = acc[2 * j] * rc[j].x - acc[2 * j + 1] * rc[j].y;
           y[2 * j + 1] = acc[2 * j] * rc[j].y + acc[2 * j + 1] * rc[j].x;
         }
       }
-      if (ci + 1 < nt) rope_load(ci + 1);
+      if constexpr (!IL) {
+        if (ci + 1 < nt) rope_load(ci + 1);
+      }
       if (col_ok) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -1427,21 +1436,21 @@ __global__ __launch_bounds__(512, 2) void bmm_wt_dbg_kernel(BmmArgs a) {
 }
 
 // split-K Q|K|V of one weight type
-template <int QT, int PD, bool XF = false>
+template <int QT, int PD, bool XF = false, bool IL = false>
 __global__ __launch_bounds__(512, 2) void bmm_sk_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  wt_body<QT, PD, true, 8, false, XF>(*ka, 0, blockIdx.x, gridDim.x);
+  wt_body<QT, PD, true, 8, false, XF, 0, IL>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
 // split-K Q|K|V over two weight types (Q|K Q4_K + V Q6_K / Q5_K on the bumped layers of the
 // K-quant mixes, Q Q4_K + K|V Q8_0 in Mixtral's): groups from a.nb1 on are run B, type QT2 (a
 // uniform branch per block; each run's body keeps its own registers)
-template <int QT, int QT2, int PD, bool XF = false>
+template <int QT, int QT2, int PD, bool XF = false, bool IL = false>
 __global__ __launch_bounds__(512, 2) void bmm_wt2_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
-  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true, 8, false, XF>(*ka, 1, blockIdx.x, gridDim.x);
-  else wt_body<QT, PD, true, 8, false, XF>(*ka, 0, blockIdx.x, gridDim.x);
+  if ((int)blockIdx.x / ka->kparts >= ka->nb1) wt_body<QT2, PD, true, 8, false, XF, 0, IL>(*ka, 1, blockIdx.x, gridDim.x);
+  else wt_body<QT, PD, true, 8, false, XF, 0, IL>(*ka, 0, blockIdx.x, gridDim.x);
   (void)a;
 }
 
@@ -1629,7 +1638,7 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     }
     if (bmm_xfirst()) {
       if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
-      else if (bmm_il() && bmm_il_fits(a)) {
+      else if (bmm_il()) {
         const int pd = bmm_pd(), epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
         if (epi == 1) launch_wt_il<QT, 1>(pd, nblk, lds, a, s);
         else if (epi == 2) launch_wt_il<QT, 2>(pd, nblk, lds, a, s);
@@ -1708,13 +1717,21 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + kWtXPad) * 2;
   const bool xf = bmm_xfirst();
   if constexpr (QT2 == 0) {
-    if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);
+    if (bmm_il()) {  // (un-RoPE'd sums: bmm_qkv_sk_defers_rope)
+      if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true, true>), grid, dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, false, true>), grid, dim3(512), lds, s, a);
+    } else if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);
     else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2>), grid, dim3(512), lds, s, a);
   } else {
-    if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true>), grid, dim3(512), lds, s, a);
+    if (bmm_il()) {
+      if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true, true>), grid, dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, false, true>), grid, dim3(512), lds, s, a);
+    } else if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true>), grid, dim3(512), lds, s, a);
     else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
   }
 }
+
+bool bmm_qkv_sk_defers_rope() { return bmm_il(); }
 
 bool bmm_qkv_sk_supported(int tq, int tk, int tv, int K, int B) {
   if (B < 1 || B > 8 || K % 256 || !bmm_supported(tq, K) || !bmm_supported(tk, K) || !bmm_supported(tv, K)) return false;
@@ -1807,7 +1824,7 @@ void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, h
   gu.nb1 = n1;
   const dim3 grid(n1 + n2);
   const size_t lds = std::max(lds1, lds2);
-  if (bmm_il() && bmm_il_fits(gu) && bmm_il_fits(dn)) {
+  if (bmm_il()) {
     const int pd = bmm_pd();
     if (dn.w.type == T_Q6_K) {
       if (pd == 3) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true, 3>), grid, dim3(512), lds, s, gu, dn);

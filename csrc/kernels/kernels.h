@@ -232,6 +232,9 @@ constexpr int kChainInts = kChainStride * kChainXcds * kChainMaxParts;
 bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn);
 void bmm_ffn_chain(const BmmArgs& gu, const BmmArgs& dn, int* cnt, int* err, hipStream_t s);
 bool bmm_qkv2(const BmmArgs& a, const BmmArgs& b, hipStream_t s);
+// the split-K Q|K|V leaves its sums un-RoPE'd (the batched attention rotates q and the new key:
+// AttnDecodeArgs::rope) - the interleaved-step kernels, whose loop then loads weights only
+bool bmm_qkv_sk_defers_rope();
 // the batched path's weight copy: per 16-row tile and 256-k step one contiguous block
 size_t t16_bytes(int type, int rows, int K);
 // swiglu: `planar` is a gate/up matrix in 32-row gate / up groups (upload_gate_up); the copy
@@ -355,6 +358,9 @@ struct AttnDecodeArgs {
   size_t qkv_ld = 0, k_off = 0, v_off = 0;
   const float* ss = nullptr;
   float inv_k = 0.f, eps = 1e-5f;
+  // split-K Q|K|V with its RoPE deferred (bmm_qkv_sk_defers_rope): q and the new key are rotated
+  // here, by the factors rope[pos][hd / 2] (null: the sums arrive RoPE'd)
+  const float2* rope = nullptr;
   static constexpr int kTouchRanges = 6;
   const uint8_t* pf[kTouchRanges] = {};
   size_t pf_bytes[kTouchRanges] = {};

@@ -1220,6 +1220,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   if (sk) {
     aa.qkv_raw = qkv_b_; aa.qkv_ld = ncol; aa.k_off = nq_; aa.v_off = nq_ + nkvd_;
     aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
+    if (bmm_qkv_sk_defers_rope()) aa.rope = rope_;
   }
   aa.dbg_clk = clk_of(l, 1);
   // (the batched Wo stays its own launch: in one launch with the attention - Wo planes streaming

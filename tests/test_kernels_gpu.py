@@ -808,11 +808,16 @@ def test_bmm_qkv_splitk_then_attention(torch, types, B, hd, H, Hkv, K):
     ss_ref = (X.astype(np.float64) ** 2).sum(1)
     assert np.allclose(ss.cpu().numpy()[:B], ss_ref, rtol=1e-5)
     raw_ref = []
+    # the interleaved-step kernels leave the sums un-RoPE'd; the attention then rotates q / the new key
+    deferred = hip().bmm_qkv_sk_defers_rope()
     for b in range(B):
         q = _rope_pairs(xw[b] @ mats[0][1].astype(np.float64).T, pos[b], tab)
         k = _rope_pairs(xw[b] @ mats[1][1].astype(np.float64).T, pos[b], tab)
         v = xw[b] @ mats[2][1].astype(np.float64).T
-        for name, g, r in (("q", got[b, :nq], q), ("k", got[b, nq:nq + nkv], k), ("v", got[b, nq + nkv:], v)):
+        qg, kg = got[b, :nq], got[b, nq:nq + nkv]
+        if deferred:
+            qg, kg = _rope_pairs(qg, pos[b], tab), _rope_pairs(kg, pos[b], tab)
+        for name, g, r in (("q", qg, q), ("k", kg, k), ("v", got[b, nq + nkv:], v)):
             assert rel_err(g, r) < 3e-3, (b, name, rel_err(g, r))
         raw_ref.append((q, k, v))
     # stage 2: the batched attention over the raw sums
@@ -828,7 +833,8 @@ def test_bmm_qkv_splitk_then_attention(torch, types, B, hd, H, Hkv, K):
     hip().attn_decode(out.data_ptr(), dK.data_ptr(), dV.data_ptr(), dpos.data_ptr(), n_ctx, H, Hkv, hd, scale,
                       part.data_ptr(), aout.data_ptr(), stream(), cnt.data_ptr(), batch=B, slots=dslots.data_ptr(),
                       slot_stride=slot_stride, out_h=aouth.data_ptr(), qkv_raw=out.data_ptr(), qkv_ld=ldo, k_off=nq,
-                      v_off=nq + nkv, ss=ss.data_ptr(), inv_k=1.0 / K, eps=eps)
+                      v_off=nq + nkv, ss=ss.data_ptr(), inv_k=1.0 / K, eps=eps,
+                      rope=dtab.data_ptr() if deferred else 0)
     torch.cuda.synchronize()
     Kg, Vg, ao = dK.cpu().numpy(), dV.cpu().numpy(), aout.cpu().numpy()
     for b in range(B):
