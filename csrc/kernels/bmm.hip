@@ -1018,16 +1018,20 @@ __device__ __forceinline__ void xfirst_plain(const BmmArgs& a, __half* xs, float
 // producer wrote it write-through from other CUs; a plain load could hit a stale L2 line of the
 // previous layer's use of the same buffer).
 __device__ __forceinline__ void chain_wait(const BmmArgs& a, int kp, int tid) {
-  if (tid < 64) {  // wave 0: lanes 0-7 poll the part's 8 XCD shards, the sum is broadcast from lane 0
+  if (tid < 64) {
+    // wave 0: lanes 0-7 poll the part's 8 XCD shards, lanes 8-15 those of the producers' x-staged
+    // count (every producer must have read its x before this block's epilogue adds into the
+    // residual rows that x is read from); the sums are broadcast from lanes 0 and 8
     const int need = min(a.chain_tpp, a.chain_tiles - kp * a.chain_tpp);
-    const int* c = a.chain_cnt + (kp * kChainXcds + (tid & (kChainXcds - 1))) * kChainStride;
+    const int part = tid < kChainXcds ? kp : kChainStagedPart;
+    const int* c = a.chain_cnt + (part * kChainXcds + (tid & (kChainXcds - 1))) * kChainStride;
     const long long t0 = wall_clock64();
     for (;;) {
-      int v = tid < kChainXcds ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      int v = tid < 2 * kChainXcds ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
       v += __shfl_xor(v, 1);
       v += __shfl_xor(v, 2);
       v += __shfl_xor(v, 4);
-      if (__shfl(v, 0) >= need) break;
+      if (__shfl(v, 0) >= need && __shfl(v, 8) >= a.chain_staged) break;
       if (wall_clock64() - t0 > 200000000LL) {  // 2 s (100 MHz): report, never hang the stream
         if (a.chain_err && tid == 0) __hip_atomic_store(a.chain_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -1068,15 +1072,6 @@ __device__ __forceinline__ void xstage_sc1(const BmmArgs& a, __half* xs, int ldx
 // ds_read_b128 B-operand reads of the K-quant chunk order conflict-free at B <= 6 (1.5-way at 7-8;
 // 8 halves: 2-way from B = 4). Lane groups of ds_read_b128 per MI355X_MICROARCH's LDS table.
 constexpr int kWtXPad = 24;
-// weight steps in flight per wave in the IL kernels (LFK_BMM_PD=3 / 4 for the A/B)
-static int bmm_pd() {
-  static const int v = [] {
-    const char* e = std::getenv("LFK_BMM_PD");
-    const int p = e ? std::atoi(e) : 2;
-    return p == 3 || p == 4 ? p : 2;
-  }();
-  return v;
-}
 // interleaved step (bmm_step's IL) in the dense wave-owned kernels; LFK_BMM_IL=0 for the A/B
 static bool bmm_il() {
   static const bool v = [] {
@@ -1272,6 +1267,10 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   if constexpr (XF) lds_barrier();
   else __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
+  // chain producer: its x is read (the loads landed before their LDS stores, the barrier above)
+  if (!SK && a.chain_role == 1 && tid == 0)
+    __hip_atomic_fetch_add(a.chain_cnt + (kChainStagedPart * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (SK && a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
   if (N == 0) return;
   if constexpr (SK && !IL) {  // (IL: the RoPE is the attention's - bmm_qkv_sk_defers_rope)
@@ -1553,16 +1552,6 @@ bool bmm_supported(int type, int K) {
   return K % 256 == 0;  // 256 k per step
 }
 
-// x-first staging in the wave-owned kernels (XFirst above); LFK_BMM_XFIRST=0 restores the
-// weights-first order for the A/B (read once per process)
-static bool bmm_xfirst() {
-  static const bool on = [] {
-    const char* e = std::getenv("LFK_BMM_XFIRST");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 static int bmm_cus() {
   static const int cus = [] {
     int dev = 0, n = 0;
@@ -1607,11 +1596,11 @@ static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
   return G * kparts;
 }
 
+// (2 weight steps in flight per wave: 3 / 4 measured 1-4 % slower steps with the IL loop too,
+// profiles/README.md round 5)
 template <int QT, int EPI>
-static void launch_wt_il(int pd, int nblk, size_t lds, const BmmArgs& a, hipStream_t s) {
-  if (pd == 3) hipLaunchKernelGGL((bmm_wt_kernel<QT, 3, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
-  else if (pd == 4) hipLaunchKernelGGL((bmm_wt_kernel<QT, 4, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
-  else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
+static void launch_wt_il(int nblk, size_t lds, const BmmArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true, true, EPI>), dim3(nblk), dim3(512), lds, s, a);
 }
 
 template <int QT>
@@ -1636,18 +1625,15 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
       else hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 7>), dim3(nblk), dim3(512), lds, s, a);
       return;
     }
-    if (bmm_xfirst()) {
-      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
-      else if (bmm_il()) {
-        const int pd = bmm_pd(), epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
-        if (epi == 1) launch_wt_il<QT, 1>(pd, nblk, lds, a, s);
-        else if (epi == 2) launch_wt_il<QT, 2>(pd, nblk, lds, a, s);
-        else launch_wt_il<QT, 0>(pd, nblk, lds, a, s);
-      }
-      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
+    // (x-first staging everywhere: weights-first measured 2.295 vs 2.246 ms per B = 6 step, r5b)
+    if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
+    else if (bmm_il()) {
+      const int epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
+      if (epi == 1) launch_wt_il<QT, 1>(nblk, lds, a, s);
+      else if (epi == 2) launch_wt_il<QT, 2>(nblk, lds, a, s);
+      else launch_wt_il<QT, 0>(nblk, lds, a, s);
     } else {
-      if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true>), dim3(nblk), dim3(512), lds, s, a);
-      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2>), dim3(nblk), dim3(512), lds, s, a);
+      hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
     }
     return;
   }
@@ -1715,19 +1701,12 @@ static void launch_qkv_sk(BmmArgs a, hipStream_t s) {
   a.nb1 = ga;
   const dim3 grid((ga + gb) * a.kparts);
   const size_t lds = 256 + (size_t)a.B * (a.spp * 256 + kWtXPad) * 2;
-  const bool xf = bmm_xfirst();
   if constexpr (QT2 == 0) {
-    if (bmm_il()) {  // (un-RoPE'd sums: bmm_qkv_sk_defers_rope)
-      if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true, true>), grid, dim3(512), lds, s, a);
-      else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, false, true>), grid, dim3(512), lds, s, a);
-    } else if (xf) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2>), grid, dim3(512), lds, s, a);
+    if (bmm_il()) hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true, true>), grid, dim3(512), lds, s, a);  // (un-RoPE'd sums)
+    else hipLaunchKernelGGL((bmm_sk_kernel<QT, 2, true>), grid, dim3(512), lds, s, a);
   } else {
-    if (bmm_il()) {
-      if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true, true>), grid, dim3(512), lds, s, a);
-      else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, false, true>), grid, dim3(512), lds, s, a);
-    } else if (xf) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true>), grid, dim3(512), lds, s, a);
-    else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2>), grid, dim3(512), lds, s, a);
+    if (bmm_il()) hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true, true>), grid, dim3(512), lds, s, a);
+    else hipLaunchKernelGGL((bmm_wt2_kernel<QT, QT2, 2, true>), grid, dim3(512), lds, s, a);
   }
 }
 
@@ -1800,7 +1779,7 @@ void bmm(const BmmArgs& a0, hipStream_t s) {
 bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn) {
   return gu.swiglu_epi && !gu.ew && !gu.qkv_epi && gu.nseg == 1 && gu.B <= 8 && (!gu.xf || gu.w.K == 4096) &&
          !dn.swiglu_epi && !dn.ew && !dn.qkv_epi && !dn.xf && !dn.one_part && !dn.store_out && dn.nseg == 1 &&
-         dn.B == gu.B && gu.w.type == T_Q4_K && (dn.w.type == T_Q4_K || dn.w.type == T_Q6_K) && bmm_xfirst() &&
+         dn.B == gu.B && gu.w.type == T_Q4_K && (dn.w.type == T_Q4_K || dn.w.type == T_Q6_K) &&
          dn.xh == gu.h_out && dn.ldh == gu.ldh_out && dn.w.K == gu.n_out / 2;
 }
 
@@ -1815,26 +1794,15 @@ void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, h
   gu.chain_role = 1; gu.chain_cnt = cnt; gu.chain_tpp = 32 * dn.spp;
   dn.chain_role = 2; dn.chain_cnt = cnt; dn.chain_tpp = 32 * dn.spp; dn.chain_tiles = (gu.n_out + 15) / 16;
   dn.chain_err = err;
-  if (dn.kparts > kChainMaxParts) throw std::runtime_error("bmm_ffn_chain: too many K parts for the counters");
-  static const int poll = [] {
-    const char* e = std::getenv("LFK_CHAIN_POLL");
-    return e ? std::max(1, std::atoi(e)) : 8;
-  }();
-  dn.chain_poll = poll;
+  if (dn.kparts > kChainStagedPart) throw std::runtime_error("bmm_ffn_chain: too many K parts for the counters");
+  dn.chain_staged = n1;  // every gate/up block has read its x rows before any down block adds into them
+  dn.chain_poll = 8;  // (1-40 s_sleep units between polls measured the same, r5d)
   gu.nb1 = n1;
   const dim3 grid(n1 + n2);
   const size_t lds = std::max(lds1, lds2);
   if (bmm_il()) {
-    const int pd = bmm_pd();
-    if (dn.w.type == T_Q6_K) {
-      if (pd == 3) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true, 3>), grid, dim3(512), lds, s, gu, dn);
-      else if (pd == 4) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true, 4>), grid, dim3(512), lds, s, gu, dn);
-      else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true>), grid, dim3(512), lds, s, gu, dn);
-    } else {
-      if (pd == 3) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true, 3>), grid, dim3(512), lds, s, gu, dn);
-      else if (pd == 4) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true, 4>), grid, dim3(512), lds, s, gu, dn);
-      else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true>), grid, dim3(512), lds, s, gu, dn);
-    }
+    if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K, true>), grid, dim3(512), lds, s, gu, dn);
+    else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K, true>), grid, dim3(512), lds, s, gu, dn);
   } else {
     if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, gu, dn);
     else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, gu, dn);

@@ -145,6 +145,7 @@ struct BmmArgs {
   int chain_tiles = 0;             // producer tiles in all
   int* chain_err = nullptr;        // host-mapped: a consumer's bounded wait timed out
   int chain_poll = 0;              // consumer poll interval: s_sleep units (64 clocks) between polls
+  int chain_staged = 0;            // consumer: producer blocks that must have staged their x first
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only (bmm_kernel); wave-owned
                                    // kernels: 2 = exit at entry, 3 = no epilogue writes, 4 = weight stream only,
                                    // 5 = x staging + weights, 6 = weights + MFMA, 7 = 6 without the
@@ -229,6 +230,7 @@ void bmm(const BmmArgs& a, hipStream_t s);
 // consumer sums the 8): same-address atomics serialise at ~12 ns each under load.
 constexpr int kChainStride = 32, kChainXcds = 8, kChainMaxParts = 16;
 constexpr int kChainInts = kChainStride * kChainXcds * kChainMaxParts;
+constexpr int kChainStagedPart = kChainMaxParts - 1;  // the last part's counters: producers' x staged
 bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn);
 void bmm_ffn_chain(const BmmArgs& gu, const BmmArgs& dn, int* cnt, int* err, hipStream_t s);
 bool bmm_qkv2(const BmmArgs& a, const BmmArgs& b, hipStream_t s);

@@ -601,8 +601,9 @@ def test_bmm_ffn_chain_matches_two_launches(torch, td, B, norm):
         # every K part counted all of its 224 gate/up tiles
         c = cnt.cpu().numpy()
         per_part = c.reshape(-1, xcds, stride)[:, :, 0].sum(1)
-        assert per_part[:8].tolist() == [224] * 8 and not per_part[8:].any(), per_part
-        assert c.sum() == 8 * 224
+        assert per_part[:8].tolist() == [224] * 8 and not per_part[8:-1].any(), per_part
+        # the last part counts the gate/up blocks that staged their x (one per block)
+        assert per_part[-1] > 0 and c.sum() == 8 * 224 + per_part[-1], per_part
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
