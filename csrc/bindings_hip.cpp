@@ -393,6 +393,26 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("wg"), py::arg("tg"), py::arg("F"), py::arg("K"), py::arg("xh"), py::arg("xf"), py::arg("norm"),
      py::arg("eps"), py::arg("wd"), py::arg("td"), py::arg("hout"), py::arg("out"), py::arg("B"), py::arg("cnt"),
      py::arg("stream"));
+  // Wo -> gate/up -> down in one launch (tests/test_kernels_gpu.py::test_bmm_wo_ffn_chain_*): Wo adds
+  // W_o . xa into the residual rows `resid`, the gate/up stages norm(resid), the down adds into resid
+  m.def("bmm_wo_ffn_chain", [](uintptr_t wo, int to, int Kwo, uintptr_t xa, uintptr_t wg, int tg, int F, int K,
+                               uintptr_t norm, float eps, uintptr_t wd, int td, uintptr_t xh, uintptr_t hout,
+                               uintptr_t resid, int B, uintptr_t cnt, uintptr_t stream) {
+    BmmArgs o, gu, dn;
+    o.w = make_qmat(P<void>(wo), to, K, Kwo);
+    o.xh = P<__half>(xa); o.ldh = Kwo; o.out = P<float>(resid); o.ldo = K; o.n_out = K; o.B = B;
+    gu.w = make_qmat(P<void>(wg), tg, 2 * F, K);
+    gu.xh = P<__half>(xh); gu.ldh = K; gu.n_out = 2 * F; gu.B = B;
+    gu.swiglu_epi = true; gu.h_out = P<__half>(hout); gu.ldh_out = F;
+    gu.xf = P<float>(resid); gu.ldxf = K; gu.norm_w = P<float>(norm); gu.eps = eps;
+    dn.w = make_qmat(P<void>(wd), td, K, F);
+    dn.xh = P<__half>(hout); dn.ldh = F; dn.out = P<float>(resid); dn.ldo = K; dn.n_out = K; dn.B = B;
+    if (!bmm_wo_ffn_chain_supported(o, gu, dn)) throw std::runtime_error("bmm_wo_ffn_chain: unsupported shapes");
+    bmm_wo_ffn_chain(o, gu, dn, P<int>(cnt), nullptr, S(stream));
+    hip_ok("bmm_wo_ffn_chain");
+  }, py::arg("wo"), py::arg("to"), py::arg("Kwo"), py::arg("xa"), py::arg("wg"), py::arg("tg"), py::arg("F"),
+     py::arg("K"), py::arg("norm"), py::arg("eps"), py::arg("wd"), py::arg("td"), py::arg("xh"), py::arg("hout"),
+     py::arg("resid"), py::arg("B"), py::arg("cnt"), py::arg("stream"));
   m.def("bmm_norm_fits", &bmm_norm_fits);
   m.def("bmm_supported", &bmm_supported);
   m.def("t16_bytes", &t16_bytes);

@@ -923,7 +923,9 @@ template <int N>
 __device__ __forceinline__ float4 vget(const f32v<N>& v, int i) {
   return make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
 }
-template <int NW, class Issue>
+// (SC1: the rows with sc1 loads - written in this launch by atomics from other CUs, a plain load
+// could hit a stale L2 line)
+template <int NW, bool SC1 = false, class Issue>
 __device__ __forceinline__ void xfirst_norm(const BmmArgs& a, __half* xs, float* rowss, int ldx, int tid, int lane,
                                             int wave, Issue&& issue) {
   constexpr int kBlock = NW * 64, J = NW >= 8 ? 1024 / kBlock : 1;  // float4 of a 4096-wide row per thread
@@ -931,11 +933,20 @@ __device__ __forceinline__ void xfirst_norm(const BmmArgs& a, __half* xs, float*
   f32v<4 * J> w;
 #pragma unroll
   for (int j = 0; j < J; ++j) vput(w, j, ldg4(a.norm_w + 4 * (tid + j * kBlock)));
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.xf), 0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
     const float* xr = a.xf + (size_t)min(b, a.B - 1) * a.ldxf;
 #pragma unroll
-    for (int j = 0; j < J; ++j) vput(xv, J * b + j, ldg4(xr + 4 * (tid + j * kBlock)));
+    for (int j = 0; j < J; ++j) {
+      if constexpr (SC1) {
+        const int off = (int)(((size_t)min(b, a.B - 1) * a.ldxf + 4 * (tid + j * kBlock)) * sizeof(float));
+        const f32v<4> t = __builtin_bit_cast(f32v<4>, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 16));  // sc1
+        vput(xv, J * b + j, make_float4(t[0], t[1], t[2], t[3]));
+      } else {
+        vput(xv, J * b + j, ldg4(xr + 4 * (tid + j * kBlock)));
+      }
+    }
   }
   issue();
 #pragma unroll
@@ -1017,6 +1028,27 @@ __device__ __forceinline__ void xfirst_plain(const BmmArgs& a, __half* xs, float
 // block's K part has all of its producer tiles, then the block stages its x with sc1 loads (the
 // producer wrote it write-through from other CUs; a plain load could hit a stale L2 line of the
 // previous layer's use of the same buffer).
+// wave 0 waits (bounded, sc1 polls) until the 8 XCD shards of counter `part` sum to `need`
+__device__ __forceinline__ void count_wait(const BmmArgs& a, int part, int need, int tid) {
+  if (tid < 64) {
+    const int* c = a.chain_cnt + (part * kChainXcds + (tid & (kChainXcds - 1))) * kChainStride;
+    const long long t0 = wall_clock64();
+    for (;;) {
+      int v = tid < kChainXcds ? __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      v += __shfl_xor(v, 4);
+      if (__shfl(v, 0) >= need) break;
+      if (wall_clock64() - t0 > 200000000LL) {  // 2 s (100 MHz): report, never hang the stream
+        if (a.chain_err && tid == 0) __hip_atomic_store(a.chain_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      for (int i = 0; i < a.chain_poll; ++i) __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  lds_barrier();
+}
+
 __device__ __forceinline__ void chain_wait(const BmmArgs& a, int kp, int tid) {
   if (tid < 64) {
     // wave 0: lanes 0-7 poll the part's 8 XCD shards, lanes 8-15 those of the producers' x-staged
@@ -1090,8 +1122,12 @@ static bool bmm_il() {
 // DBG (microbenchmarks, tools/boundary_bench.py; BmmArgs::debug 4-7): 4 = the weight stream alone
 // (no x staging, no MFMA), 5 = x staging + weight stream (no MFMA), 6 = weight stream + MFMA (no x
 // staging), 7 = as 6 with the MFMAs on the raw quant words (no dequantisation)
+// CR: the in-launch chain role of the x staging, compile-time (0 x-first, kChainConsume: wait for the
+// K part's gate/up tiles, kChainWaitWo: wait for every Wo block) - as a runtime branch the staging
+// paths with the weights issued before x merged into the step loop, and the waitcnt pass then
+// drained the weight ring at every round of every wave-owned kernel
 template <int QT, int PD, bool SK, int NW = 8, bool MOE = false, bool XF = false, int DBG = 0, bool IL = false,
-          int EPI = 0>
+          int EPI = 0, int CR = 0>
 __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const int bid, const int nblk) {
   constexpr int R = PD + 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1249,12 +1285,27 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // (XF: that barrier goes first - an asm memory clobber between the x loads and their LDS stores
   // made the compiler keep the x registers in scratch)
   if (XF && xmode == 2) lds_barrier();
+  // kChainWoDone: the block's waves count their exits here; the last one publishes the block
+  __shared__ int wo_exits;
+  if (tid == 0) wo_exits = 0;  // (ordered before any exit by the staging barrier below)
+  auto wo_arrive = [&]() {
+    if (!SK && (a.chain_role & kChainWoDone)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's residual atomics are done
+      if (lane == 0 && atomicAdd(&wo_exits, 1) == NW - 1)
+        __hip_atomic_fetch_add(a.chain_cnt + (kChainWoPart * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   if constexpr (DBG == 4 || DBG == 6) issue();
   else if constexpr (XF) {
-    if (!SK && a.chain_role == 2) {  // chain consumer: the weights do not depend on the producer
+    if constexpr (!SK && CR == kChainConsume) {  // chain consumer: the weights do not depend on the producer
       issue();
       chain_wait(a, kp, tid);
       xstage_sc1<NW>(a, xs, ldx, k0, kn, tid);
+    } else if constexpr (!SK && CR == kChainWaitWo) {  // x = the rows Wo adds into (xmode 1)
+      issue();
+      count_wait(a, kChainWoPart, a.chain_wo, tid);
+      xfirst_norm<NW, true>(a, xs, rowss, ldx, tid, lane, wave, [] {});
     } else if (xmode == 2) xfirst_part_norm<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, issue);
     else if (xmode == 1) xfirst_norm<NW>(a, xs, rowss, ldx, tid, lane, wave, issue);
     else xfirst_plain<NW>(a, xs, rowss, ldx, k0, kn, tid, lane, wave, issue);
@@ -1268,11 +1319,14 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   else __syncthreads();
   if (clk && tid == 0) clk[2] = wall_clock64();
   // chain producer: its x is read (the loads landed before their LDS stores, the barrier above)
-  if (!SK && a.chain_role == 1 && tid == 0)
+  if (!SK && (a.chain_role & kChainProduce) && tid == 0)
     __hip_atomic_fetch_add(a.chain_cnt + (kChainStagedPart * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (SK && a.ss_out && run == 0 && grp == 0 && tid < a.B) atomicAdd(a.ss_out + tid, rowss[tid]);
-  if (N == 0) return;
+  if (N == 0) {
+    wo_arrive();
+    return;
+  }
   if constexpr (SK && !IL) {  // (IL: the RoPE is the attention's - bmm_qkv_sk_defers_rope)
     pos = min(max(pos, 0), a.qkv.n_ctx - 1);
     rope_load(0);
@@ -1330,13 +1384,13 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
         const h2_t p0 = {(_Float16)(silu(acc[0]) * up[0] * rw), (_Float16)(silu(acc[2]) * up[2] * rw)};
         const h2_t p1 = {(_Float16)(silu(acc[1]) * up[1] * rw), (_Float16)(silu(acc[3]) * up[3] * rw)};
         __half* h = a.h_out + (size_t)r16 * a.ldh_out + f0;
-        if (!MOE && a.chain_role == 1)  // chain producer: write-through (a consumer CU reads it next)
+        if (!MOE && (a.chain_role & kChainProduce))  // chain producer: write-through (a consumer CU reads it next)
           __hip_atomic_store(reinterpret_cast<unsigned long long*>(h),
                              ((unsigned long long)as_u(p1) << 32) | as_u(p0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
           *reinterpret_cast<uint2*>(h) = make_uint2(as_u(p0), as_u(p1));
       }
-      if (EPI == 0 && !MOE && a.chain_role == 1) {  // the tile's rows have landed: count it for its consumer part
+      if (EPI == 0 && !MOE && (a.chain_role & kChainProduce)) {  // the tile's rows have landed: count it for its consumer part
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add(a.chain_cnt + (gt / a.chain_tpp * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -1402,7 +1456,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   // EPI 1 (the SwiGLU epilogue alone): the chain producer counts its tiles once all are stored - a
   // vmcnt(0) at every tile end made the waitcnt pass drain the weight ring in the step loop
   if constexpr (EPI == 1 && !MOE) {
-    if (a.chain_role == 1 && nt > 0) {
+    if ((a.chain_role & kChainProduce) && nt > 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0)
         for (int i = 0; i < nt; ++i)
@@ -1410,6 +1464,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
                                  1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  wo_arrive();
   if (clk) {  // exit: the block's LAST wave (waves of one block can end microseconds apart)
     if (lane == 0) atomicMax(reinterpret_cast<unsigned long long*>(clk + 4), (unsigned long long)wall_clock64());
     if (tid == 0) clk[5] = nt;
@@ -1460,9 +1515,23 @@ __global__ __launch_bounds__(512, PD > 2 ? 1 : 2) void bmm_chain_kernel(BmmArgs 
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const int n1 = ka[0].nb1;
   if ((int)blockIdx.x < n1) wt_body<QT1, PD, false, 8, false, true, 0, IL, IL ? 1 : 0>(ka[0], 0, blockIdx.x, n1);
-  else wt_body<QT2, PD, false, 8, false, true, 0, IL, IL ? 2 : 0>(ka[1], 0, blockIdx.x - n1, gridDim.x - n1);
+  else wt_body<QT2, PD, false, 8, false, true, 0, IL, IL ? 2 : 0, kChainConsume>(ka[1], 0, blockIdx.x - n1, gridDim.x - n1);
   (void)a;
   (void)b;
+}
+
+// Wo (QT0, split-K into the residual) -> gate/up (QT1) -> down (QT2) in ONE launch (bmm_wo_ffn_chain)
+template <int QT0, int QT1, int QT2>
+__global__ __launch_bounds__(512, 2) void bmm_chain3_kernel(BmmArgs a, BmmArgs b, BmmArgs c) {
+  const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int n0 = ka[0].nb1, n1 = ka[1].nb1;
+  const int bid = blockIdx.x;
+  if (bid < n0) wt_body<QT0, 2, false, 8, false, true, 0, true, 2>(ka[0], 0, bid, n0);
+  else if (bid < n0 + n1) wt_body<QT1, 2, false, 8, false, true, 0, true, 1, kChainWaitWo>(ka[1], 0, bid - n0, n1);
+  else wt_body<QT2, 2, false, 8, false, true, 0, true, 2, kChainConsume>(ka[2], 0, bid - n0 - n1, gridDim.x - n0 - n1);
+  (void)a;
+  (void)b;
+  (void)c;
 }
 
 // ---------------------------------------------------------------- activation prep
@@ -1791,8 +1860,8 @@ void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, h
   size_t lds1 = 0, lds2 = 0;
   const int n1 = wt_config(gu, false, lds1), n2 = wt_config(dn, true, lds2);
   // a consumer block takes K part kp = bid % kparts: its 256 * spp features are 32 * spp gate/up tiles
-  gu.chain_role = 1; gu.chain_cnt = cnt; gu.chain_tpp = 32 * dn.spp;
-  dn.chain_role = 2; dn.chain_cnt = cnt; dn.chain_tpp = 32 * dn.spp; dn.chain_tiles = (gu.n_out + 15) / 16;
+  gu.chain_role = kChainProduce; gu.chain_cnt = cnt; gu.chain_tpp = 32 * dn.spp;
+  dn.chain_role = kChainConsume; dn.chain_cnt = cnt; dn.chain_tpp = 32 * dn.spp; dn.chain_tiles = (gu.n_out + 15) / 16;
   dn.chain_err = err;
   if (dn.kparts > kChainStagedPart) throw std::runtime_error("bmm_ffn_chain: too many K parts for the counters");
   dn.chain_staged = n1;  // every gate/up block has read its x rows before any down block adds into them
@@ -1807,6 +1876,33 @@ void bmm_ffn_chain(const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, h
     if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, gu, dn);
     else hipLaunchKernelGGL((bmm_chain_kernel<T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, gu, dn);
   }
+}
+
+bool bmm_wo_ffn_chain_supported(const BmmArgs& wo, const BmmArgs& gu, const BmmArgs& dn) {
+  return bmm_il() && bmm_ffn_chain_supported(gu, dn) && gu.xf && wo.w.type == T_Q4_K && !wo.ew && !wo.xf &&
+         !wo.swiglu_epi && !wo.qkv_epi && !wo.one_part && !wo.store_out && !wo.zero && wo.nseg == 1 && wo.B == gu.B &&
+         wo.out == gu.xf && wo.ldo == gu.ldxf && wo.n_out == gu.w.K;
+}
+
+void bmm_wo_ffn_chain(const BmmArgs& wo0, const BmmArgs& gu0, const BmmArgs& dn0, int* cnt, int* err, hipStream_t s) {
+  if (!bmm_wo_ffn_chain_supported(wo0, gu0, dn0) || !cnt) throw std::runtime_error("bmm_wo_ffn_chain: unsupported shapes");
+  BmmArgs wo = wo0, gu = gu0, dn = dn0;
+  bmm_check(wo);
+  bmm_check(gu);
+  bmm_check(dn);
+  size_t lds0 = 0, lds1 = 0, lds2 = 0;
+  const int n0 = wt_config(wo, true, lds0), n1 = wt_config(gu, false, lds1), n2 = wt_config(dn, true, lds2);
+  if (wo.kparts < 2 || dn.kparts < 2) throw std::runtime_error("bmm_wo_ffn_chain: one-part Wo / down");
+  if (dn.kparts > kChainWoPart) throw std::runtime_error("bmm_wo_ffn_chain: too many K parts for the counters");
+  wo.chain_role = kChainWoDone; wo.chain_cnt = cnt; wo.nb1 = n0;
+  gu.chain_role = kChainProduce | kChainWaitWo; gu.chain_cnt = cnt; gu.chain_tpp = 32 * dn.spp; gu.chain_wo = n0;
+  gu.chain_err = err; gu.chain_poll = 8; gu.nb1 = n1;
+  dn.chain_role = kChainConsume; dn.chain_cnt = cnt; dn.chain_tpp = 32 * dn.spp; dn.chain_tiles = (gu.n_out + 15) / 16;
+  dn.chain_err = err; dn.chain_staged = n1; dn.chain_poll = 8;
+  const dim3 grid(n0 + n1 + n2);
+  const size_t lds = std::max(lds0, std::max(lds1, lds2));
+  if (dn.w.type == T_Q6_K) hipLaunchKernelGGL((bmm_chain3_kernel<T_Q4_K, T_Q4_K, T_Q6_K>), grid, dim3(512), lds, s, wo, gu, dn);
+  else hipLaunchKernelGGL((bmm_chain3_kernel<T_Q4_K, T_Q4_K, T_Q4_K>), grid, dim3(512), lds, s, wo, gu, dn);
 }
 
 bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {

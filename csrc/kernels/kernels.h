@@ -146,6 +146,7 @@ struct BmmArgs {
   int* chain_err = nullptr;        // host-mapped: a consumer's bounded wait timed out
   int chain_poll = 0;              // consumer poll interval: s_sleep units (64 clocks) between polls
   int chain_staged = 0;            // consumer: producer blocks that must have staged their x first
+  int chain_wo = 0;                // kChainWaitWo: Wo blocks that must be done before the x staging
   int debug = 0;                   // microbenchmarks only: 1 = weight stream only (bmm_kernel); wave-owned
                                    // kernels: 2 = exit at entry, 3 = no epilogue writes, 4 = weight stream only,
                                    // 5 = x staging + weights, 6 = weights + MFMA, 7 = 6 without the
@@ -231,8 +232,15 @@ void bmm(const BmmArgs& a, hipStream_t s);
 constexpr int kChainStride = 32, kChainXcds = 8, kChainMaxParts = 16;
 constexpr int kChainInts = kChainStride * kChainXcds * kChainMaxParts;
 constexpr int kChainStagedPart = kChainMaxParts - 1;  // the last part's counters: producers' x staged
+constexpr int kChainWoPart = kChainMaxParts - 2;      // ... the one before: Wo blocks done (bmm_wo_ffn_chain)
+// BmmArgs::chain_role bits
+constexpr int kChainProduce = 1, kChainConsume = 2, kChainWoDone = 4, kChainWaitWo = 8;
 bool bmm_ffn_chain_supported(const BmmArgs& gu, const BmmArgs& dn);
 void bmm_ffn_chain(const BmmArgs& gu, const BmmArgs& dn, int* cnt, int* err, hipStream_t s);
+// ... with the Wo projection (wo: split-K into the residual rows gu stages) in the same launch: the
+// gate/up blocks issue their first weight steps, wait until every Wo block is done, then stage x
+bool bmm_wo_ffn_chain_supported(const BmmArgs& wo, const BmmArgs& gu, const BmmArgs& dn);
+void bmm_wo_ffn_chain(const BmmArgs& wo, const BmmArgs& gu, const BmmArgs& dn, int* cnt, int* err, hipStream_t s);
 bool bmm_qkv2(const BmmArgs& a, const BmmArgs& b, hipStream_t s);
 // the split-K Q|K|V leaves its sums un-RoPE'd (the batched attention rotates q and the new key:
 // AttnDecodeArgs::rope) - the interleaved-step kernels, whose loop then loads weights only

@@ -426,7 +426,7 @@ void Engine::setup_batch_mfma() {
     HIPCHK(hipMemsetAsync(step_clk_, 0, sizeof(long long) * 5 * kStepClkBlocks * 16, stream_));
   }
   if (!bg_) return;
-  if (const char* e = std::getenv("LFK_FFN_CHAIN")) ffn_chain_ = e[0] != '0';  // A/B
+  if (const char* e = std::getenv("LFK_FFN_CHAIN")) ffn_chain_ = std::max(0, std::min(2, std::atoi(e)));  // A/B
   if (ffn_chain_) {
     chain_cnt_ = (int*)dalloc(sizeof(int) * kChainInts * hp_.n_layer);
     HIPCHK(hipMemsetAsync(chain_cnt_, 0, sizeof(int) * kChainInts * hp_.n_layer, stream_));
@@ -1228,8 +1228,34 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   // ms, r4: the in-launch hand-off costs what the boundary did and the weight stream slowed the
   // attention's K / V loads)
   attn_decode(aa, s);
+  // dense FFN on the SwiGLU epilogue path: its gate/up and down (and, ffn_chain_ 2, Wo before them)
+  BmmArgs wo, gu, dn;
+  wo.w = L.t_wo; wo.xh = xh_b_; wo.ldh = nq_; wo.out = acc; wo.ldo = d; wo.n_out = d; wo.B = B;
+  wo.dbg_clk = clk_of(l, 2);
+  const bool dense_ffn = !(moe_b_ && fused) && bg_ffn_ && fused;
+  if (dense_ffn) {
+    if (fnorm) {
+      gu.xf = x_; gu.ldxf = d; gu.norm_w = L.ffn_norm; gu.eps = hp_.rms_eps;
+    }
+    gu.w = L.t_gu; gu.xh = xh_b_; gu.ldh = d;
+    gu.out = nullptr; gu.ldo = 0; gu.n_out = 2 * F_l_; gu.B = B;
+    gu.swiglu_epi = true; gu.h_out = hh_b_; gu.ldh_out = F_l_;
+    gu.dbg_clk = clk_of(l, 3);
+    dn.w = L.t_down; dn.xh = hh_b_; dn.ldh = F_l_; dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
+    dn.dbg_clk = clk_of(l, 4);
+    if (sk) {  // (the down projection re-zeroes the split-K Q|K|V rows for the next layer)
+      dn.zero = qkv_b_; dn.zero_n = (int)qkv_b_zero_n();
+    }
+    // Wo, gate/up and down in ONE launch: the gate/up blocks start on the CUs the Wo frees and issue
+    // their weights while the last Wo partials land (bmm_wo_ffn_chain)
+    if (ffn_chain_ >= 2 && !tp && fnorm && B <= kBmmMaxRows && bmm_wo_ffn_chain_supported(wo, gu, dn)) {
+      bmm_wo_ffn_chain(wo, gu, dn, chain_cnt_ + kChainInts * l, chain_err_, s);
+      return;
+    }
+  }
   tp_begin();
-  bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
+  if (B <= kBmmMaxRows) bmm(wo, s);
+  else bmm_rows(L.t_wo, xh_b_, nq_, acc, d, d, B, s, clk_of(l, 2));
   tp_end();
   if (moe_b_ && fused) {
     // MoE: dense per-row expert weights (f32 router on the normed rows), then every expert's
@@ -1262,33 +1288,18 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     tp_end();
     return;
   }
-  if (bg_ffn_ && fused) {
+  if (dense_ffn) {
     // SwiGLU in the gate/up epilogue: one K part, silu(gate) * up straight to the down
     // projection's f16 input (hh_b_; xh_b_ is still being read by other blocks)
-    BmmArgs a;
-    if (fnorm) {
-      a.xf = x_; a.ldxf = d; a.norm_w = L.ffn_norm; a.eps = hp_.rms_eps;
-    } else {
-      bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
-    }
-    a.w = L.t_gu; a.xh = xh_b_; a.ldh = d;
-    a.out = nullptr; a.ldo = 0; a.n_out = 2 * F_l_; a.B = B;
-    a.swiglu_epi = true; a.h_out = hh_b_; a.ldh_out = F_l_;
-    a.dbg_clk = clk_of(l, 3);
-    BmmArgs dn;
-    dn.w = L.t_down; dn.xh = hh_b_; dn.ldh = F_l_; dn.out = acc; dn.ldo = d; dn.n_out = d; dn.B = B;
-    dn.dbg_clk = clk_of(l, 4);
-    if (sk) {  // (the down projection re-zeroes the split-K Q|K|V rows for the next layer)
-      dn.zero = qkv_b_; dn.zero_n = (int)qkv_b_zero_n();
-    }
+    if (!fnorm) bprep_rows(x_, d, false, L.ffn_norm, d, B, nullptr, 0, s);
     // gate/up and down in ONE launch, the down blocks waiting per K part on the gate/up tiles
     // they read (bmm_ffn_chain): the down weight stream starts under the gate/up's last tiles
     // instead of after a kernel boundary
-    if (ffn_chain_ && !tp && bmm_ffn_chain_supported(a, dn)) {
-      bmm_ffn_chain(a, dn, chain_cnt_ + kChainInts * l, chain_err_, s);
+    if (ffn_chain_ >= 1 && !tp && bmm_ffn_chain_supported(gu, dn)) {
+      bmm_ffn_chain(gu, dn, chain_cnt_ + kChainInts * l, chain_err_, s);
       return;
     }
-    bmm(a, s);
+    bmm(gu, s);
     tp_begin();
     bmm(dn, s);
     tp_end();

@@ -399,7 +399,10 @@ class Engine : public SlotBackend {
   int* wo_err_ = nullptr;     // device view
   // batched dense FFN as one launch (bmm_ffn_chain): per-layer K-part counters (64 per layer),
   // zeroed by each step's first kernel; a timed-out consumer wait sets *chain_err_ (host-mapped)
-  bool ffn_chain_ = true;     // LFK_FFN_CHAIN=0: two launches (A/B)
+  // in-launch chains of the batched layer: 1 = gate/up + down in one launch (Wo its own launch),
+  // 2 = Wo + gate/up + down in one launch (measured the same as 1: 2.209 vs 2.204 ms per B = 6
+  // step, r5g), 0 = three launches (LFK_FFN_CHAIN, A/B)
+  int ffn_chain_ = 1;
   int* chain_cnt_ = nullptr;
   int* chain_err_h_ = nullptr;
   int* chain_err_ = nullptr;

@@ -606,6 +606,55 @@ def test_bmm_ffn_chain_matches_two_launches(torch, td, B, norm):
         assert per_part[-1] > 0 and c.sum() == 8 * 224 + per_part[-1], per_part
 
 
+@pytest.mark.parametrize("td", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B", [1, 6])
+def test_bmm_wo_ffn_chain_matches_three_launches(torch, td, B):
+    """Wo -> gate/up -> down in ONE launch (bmm_wo_ffn_chain: the gate/up blocks wait until every Wo
+    block has added its split-K partials into the residual rows, stage norm(rows) with sc1 loads; the
+    down blocks wait per K part and until every gate/up block has read its rows, then add into them)
+    against the three projections as separate launches on the 8B shapes. Three runs over fresh zeros."""
+    rng = np.random.default_rng(B * 7 + int(td))
+    F, K = 14336, 4096
+    raw_o, _ = make_matrix(GGMLType.Q4_K, K, K, rng)
+    raw_g, _ = make_matrix(GGMLType.Q4_K, 2 * F, K, rng)
+    raw_d, _ = make_matrix(td, K, F, rng)
+    mats = []
+    for t, R, C, raw, sw in ((GGMLType.Q4_K, K, K, raw_o, False), (GGMLType.Q4_K, 2 * F, K, raw_g, True),
+                             (td, K, F, raw_d, False)):
+        dw = dev_bytes(to_planar(t, raw, R, C))
+        tw = torch.empty(hip().t16_bytes(int(t), R, C), dtype=torch.uint8, device="cuda")
+        hip().t16_repack(dw.data_ptr(), int(t), R, C, tw.data_ptr(), stream(), swiglu=sw)
+        mats.append(tw)
+    to_, tg, tdw = mats
+    XA = rng.standard_normal((B, K)).astype(np.float32)
+    dxa = torch.from_numpy(_swizzle4(XA.astype(np.float16))).cuda()
+    resid0 = torch.from_numpy((rng.standard_normal((B, K)) * 2).astype(np.float32)).cuda()
+    nw = torch.from_numpy((0.5 + rng.random(K)).astype(np.float32)).cuda()
+    xh = torch.zeros(B, K, dtype=torch.float16, device="cuda")  # (unused: the norm path stages resid)
+    # reference: three launches
+    r_ref = resid0.clone()
+    h_ref = torch.zeros(B, F, dtype=torch.float16, device="cuda")
+    hip().bmm(to_.data_ptr(), int(GGMLType.Q4_K), K, K, dxa.data_ptr(), K, r_ref.data_ptr(), K, B, stream())
+    hip().bmm(tg.data_ptr(), int(GGMLType.Q4_K), 2 * F, K, xh.data_ptr(), K, 0, 0, B, stream(),
+              h_out=h_ref.data_ptr(), ldh_out=F, xf=r_ref.data_ptr(), ldxf=K, norm=nw.data_ptr(), eps=1e-5)
+    hip().bmm(tdw.data_ptr(), int(td), K, F, h_ref.data_ptr(), F, r_ref.data_ptr(), K, B, stream())
+    torch.cuda.synchronize()
+    _, _, n_ints = hip().chain_layout()
+    cnt = torch.zeros(n_ints, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        cnt.zero_()
+        r = resid0.clone()
+        h = torch.full((B, F), 3.0, dtype=torch.float16, device="cuda")
+        hip().bmm_wo_ffn_chain(to_.data_ptr(), int(GGMLType.Q4_K), K, dxa.data_ptr(), tg.data_ptr(), int(GGMLType.Q4_K),
+                               F, K, nw.data_ptr(), 1e-5, tdw.data_ptr(), int(td), xh.data_ptr(), h.data_ptr(),
+                               r.data_ptr(), B, cnt.data_ptr(), stream())
+        torch.cuda.synchronize()
+        # the SwiGLU rows: equal up to the f16 rounding of inputs whose split-K sums differ in order
+        hd = (h.float() - h_ref.float()).abs().max().item()
+        assert hd <= 2e-2 * max(1.0, h_ref.float().abs().max().item()), hd
+        assert rel_err(r.cpu().numpy() - resid0.cpu().numpy(), r_ref.cpu().numpy() - resid0.cpu().numpy()) < 1e-3
+
+
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
 @pytest.mark.parametrize("B", [1, 6, 16])
 @pytest.mark.parametrize("mode", ["store", "swiglu"])
