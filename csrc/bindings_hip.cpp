@@ -499,9 +499,9 @@ PYBIND11_MODULE(_hip, m) {
                           int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,
                           int debug_stop, uintptr_t dbg_clk, int batch, uintptr_t slots, size_t slot_stride,
                           uintptr_t out_h, uintptr_t qkv_raw, size_t qkv_ld, size_t k_off, size_t v_off, uintptr_t ss,
-                          float inv_k, float eps, uintptr_t rope) {
+                          float inv_k, float eps, uintptr_t rope_freq) {
     AttnDecodeArgs a;
-    a.rope = P<float2>(rope);
+    a.rope_freq = P<float>(rope_freq);
     a.qkv_raw = P<float>(qkv_raw); a.qkv_ld = qkv_ld; a.k_off = k_off; a.v_off = v_off;
     a.ss = P<float>(ss); a.inv_k = inv_k; a.eps = eps;
     if (batch > 0) {  // rows b: query q + b*n_head*hd, slot slots[b], position pos[b], own workspaces
@@ -523,7 +523,7 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("debug_stop") = 0, py::arg("dbg_clk") = 0, py::arg("batch") = 0, py::arg("slots") = 0,
      py::arg("slot_stride") = 0, py::arg("out_h") = 0, py::arg("qkv_raw") = 0, py::arg("qkv_ld") = 0,
      py::arg("k_off") = 0, py::arg("v_off") = 0, py::arg("ss") = 0, py::arg("inv_k") = 0.f, py::arg("eps") = 1e-5f,
-     py::arg("rope") = 0);
+     py::arg("rope_freq") = 0);
   // split-K Q|K|V (BmmArgs::qkv_sk) over tile16 copies: RoPE'd partial sums added into out [B][ldo]
   // (Q at 0, K at nq, V at nq + nkv), the rows' sums of squares into ss_out [B]
   m.def("bmm_qkv_sk", [](uintptr_t wq, int tq, int nq, uintptr_t wk, int tk, uintptr_t wv, int tv, int nkv, int K,

@@ -159,39 +159,45 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
     const int i = min(tid + 256 * j, G * HD / 2 - 1);
     qv[j] = reinterpret_cast<const float2*>(a.q + (size_t)kvh * G * HD)[i];
   }
-  float2 nv = make_float2(0.f, 0.f);
-  float ssv = 0.f;
-  if (a.qkv_raw) {
-    // the row's sum of squares as a VECTOR load beside q (a scalar one at the top was one more
-    // dependent round trip before any K / V load went out)
-    ssv = __hip_atomic_load(const_cast<float*>(a.ss + (a.batch > 0 ? blockIdx.z : 0)), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-    if (tid < HD) {  // the new key (tid < HD / 2) and value pairs
-      const int kv = tid / (HD / 2), pr = tid % (HD / 2);
-      nv = reinterpret_cast<const float2*>(a.qkv_raw + (kv ? a.v_off : a.k_off) + (size_t)kvh * HD)[pr];
-    }
-    if (a.rope) {  // deferred RoPE: rotate q's pairs and the new key's at the row's position
-      const float2* rr = a.rope + (size_t)min(max(*a.pos, 0), a.n_ctx - 1) * (HD / 2);
-      auto rot = [](float2 v, float2 cs) { return make_float2(v.x * cs.x - v.y * cs.y, v.x * cs.y + v.y * cs.x); };
+  // split-K Q|K|V: the row's sum of squares (a VECTOR load beside q - a scalar one at the top was one
+  // more dependent round trip before any K / V load went out), the new key / value pairs and, RoPE
+  // deferred, the pairs' frequencies - all issued unconditionally (from q when unused) and before
+  // K / V, so that waiting for them never waits for the K / V rows
+  const bool raw = a.qkv_raw != nullptr, drope = raw && a.rope_freq != nullptr;
+  const float ssv = __hip_atomic_load(const_cast<float*>(raw ? a.ss + (a.batch > 0 ? blockIdx.z : 0) : a.q),
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int kvsel = tid / (HD / 2), pr = tid % (HD / 2);
+  const float2 nv = reinterpret_cast<const float2*>(
+      raw && tid < HD ? a.qkv_raw + (kvsel ? a.v_off : a.k_off) + (size_t)kvh * HD : a.q)[raw && tid < HD ? pr : 0];
+  float fq[QPT];
 #pragma unroll
-      for (int j = 0; j < QPT; ++j) qv[j] = rot(qv[j], rr[min(tid + 256 * j, G * HD / 2 - 1) % (HD / 2)]);
-      if (tid < HD / 2) nv = rot(nv, rr[tid]);
-    }
-  }
+  for (int j = 0; j < QPT; ++j) fq[j] = (drope ? a.rope_freq : a.q)[drope ? min(tid + 256 * j, G * HD / 2 - 1) % (HD / 2) : 0];
   const size_t row = ((size_t)kvh * a.n_ctx + min(key, a.n_ctx - 1)) * HD + sub * DPL;
   uint4 kr[NLD], vr[NLD];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) kr[i] = *reinterpret_cast<const uint4*>(a.k_cache + row + 8 * i);
 #pragma unroll
   for (int i = 0; i < NLD; ++i) vr[i] = *reinterpret_cast<const uint4*>(a.v_cache + row + 8 * i);
-  const float rs = a.qkv_raw ? rsqrtf(ssv * a.inv_k + a.eps) : 1.f;
+  const float rs = raw ? rsqrtf(ssv * a.inv_k + a.eps) : 1.f;
   const float qscale = a.scale * rs;
+  // deferred RoPE (adjacent pairs): angle = pos * freq in fp32, as llama.cpp computes it
+  const float pf = (float)min(max(*a.pos, 0), a.n_ctx - 1);
+  auto rot = [&](float2 v, float f) {
+    if (!drope) return v;
+    float sn, cs;
+    sincosf(pf * f, &sn, &cs);
+    return make_float2(v.x * cs - v.y * sn, v.x * sn + v.y * cs);
+  };
 #pragma unroll
   for (int j = 0; j < QPT; ++j) {
     const int i = tid + 256 * j;
-    if (i < G * HD / 2) qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(qv[j].x * qscale), (_Float16)(qv[j].y * qscale)};
+    const float2 q2 = rot(qv[j], fq[j]);
+    if (i < G * HD / 2) qs[i / (HD / 2)][i % (HD / 2)] = h2v{(_Float16)(q2.x * qscale), (_Float16)(q2.y * qscale)};
   }
-  if (a.qkv_raw && tid < HD) kvn[tid / (HD / 2)][tid % (HD / 2)] = h2v{(_Float16)(nv.x * rs), (_Float16)(nv.y * rs)};
+  if (raw && tid < HD) {
+    const float2 n2 = tid < HD / 2 ? rot(nv, fq[0]) : nv;  // (fq[0]: pair tid % (HD / 2) = tid here)
+    kvn[tid / (HD / 2)][tid % (HD / 2)] = h2v{(_Float16)(n2.x * rs), (_Float16)(n2.y * rs)};
+  }
   const int L = min(*a.pos + 1, a.n_ctx);
   LFK_STAMP(0);
   if (start >= L || a.debug_stop == 1) return;

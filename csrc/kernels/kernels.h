@@ -369,8 +369,8 @@ struct AttnDecodeArgs {
   const float* ss = nullptr;
   float inv_k = 0.f, eps = 1e-5f;
   // split-K Q|K|V with its RoPE deferred (bmm_qkv_sk_defers_rope): q and the new key are rotated
-  // here, by the factors rope[pos][hd / 2] (null: the sums arrive RoPE'd)
-  const float2* rope = nullptr;
+  // here by pos * rope_freq[pair] (fp32; null: the sums arrive RoPE'd)
+  const float* rope_freq = nullptr;
   static constexpr int kTouchRanges = 6;
   const uint8_t* pf[kTouchRanges] = {};
   size_t pf_bytes[kTouchRanges] = {};

@@ -317,6 +317,7 @@ void Engine::alloc_buffers() {
   HIPCHK(hipMemset(kc_, 0, kv * 2 * NS));
   HIPCHK(hipMemset(vc_, 0, kv * 2 * NS));
   rope_ = (float2*)dalloc(sizeof(float2) * opt_.n_ctx * (hd / 2));
+  rope_freq_ = (float*)dalloc(sizeof(float) * (hd / 2));
   attn_part_ = (float*)dalloc(sizeof(float) * attn_decode_workspace_floats(opt_.n_ctx, nh_l_, hd));
   attn_cnt_ = (int*)dalloc(sizeof(int) * 64);
   HIPCHK(hipMemset(attn_cnt_, 0, sizeof(int) * 64));
@@ -557,6 +558,9 @@ void Engine::build_rope() {
       t[(size_t)p * (hd / 2) + i] = make_float2((float)std::cos(a), (float)std::sin(a));
     }
   HIPCHK(hipMemcpy(rope_, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
+  std::vector<float> f(hd / 2);
+  for (int i = 0; i < hd / 2; ++i) f[i] = (float)std::pow((double)hp_.rope_base, -2.0 * i / hd);
+  HIPCHK(hipMemcpy(rope_freq_, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice));
 }
 
 // ------------------------------------------------------------------------ schedule
@@ -1220,7 +1224,7 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   if (sk) {
     aa.qkv_raw = qkv_b_; aa.qkv_ld = ncol; aa.k_off = nq_; aa.v_off = nq_ + nkvd_;
     aa.ss = ss_b_; aa.inv_k = 1.f / (float)d; aa.eps = hp_.rms_eps;
-    if (bmm_qkv_sk_defers_rope()) aa.rope = rope_;
+    if (bmm_qkv_sk_defers_rope()) aa.rope_freq = rope_freq_;
   }
   aa.dbg_clk = clk_of(l, 1);
   // (the batched Wo stays its own launch: in one launch with the attention - Wo planes streaming

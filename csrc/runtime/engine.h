@@ -306,6 +306,7 @@ class Engine : public SlotBackend {
   __half* kc_ = nullptr;      // [n_layer][nkv_l][n_ctx][hd]
   __half* vc_ = nullptr;
   float2* rope_ = nullptr;
+  float* rope_freq_ = nullptr;  // [hd / 2]: the pairs' angular frequencies (deferred batched RoPE)
   float* attn_part_ = nullptr;
   // [64] per-kv-head split counters (last-arriver combine); word 63 is reserved as the
   // weight touch's pf_sink, which is why the touch needs nkv_l_ < 63

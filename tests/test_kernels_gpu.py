@@ -847,6 +847,7 @@ def test_bmm_qkv_splitk_then_attention(torch, types, B, hd, H, Hkv, K):
     ldo = nq + 2 * nkv
     dx, dn = torch.from_numpy(X).cuda(), torch.from_numpy(nw).cuda()
     dtab, dpos, dslots = torch.from_numpy(tab).cuda(), torch.from_numpy(pos).cuda(), torch.from_numpy(slots).cuda()
+    dfreq = torch.from_numpy((5e5 ** (-np.arange(0, hd, 2, dtype=np.float64) / hd)).astype(np.float32)).cuda()
     out = torch.zeros(B, ldo, device="cuda")
     ss = torch.zeros(16, device="cuda")
     hip().bmm_qkv_sk(mats[0][0].data_ptr(), int(tq), nq, mats[1][0].data_ptr(), int(tk), mats[2][0].data_ptr(), int(tv),
@@ -884,7 +885,7 @@ def test_bmm_qkv_splitk_then_attention(torch, types, B, hd, H, Hkv, K):
                       part.data_ptr(), aout.data_ptr(), stream(), cnt.data_ptr(), batch=B, slots=dslots.data_ptr(),
                       slot_stride=slot_stride, out_h=aouth.data_ptr(), qkv_raw=out.data_ptr(), qkv_ld=ldo, k_off=nq,
                       v_off=nq + nkv, ss=ss.data_ptr(), inv_k=1.0 / K, eps=eps,
-                      rope=dtab.data_ptr() if deferred else 0)
+                      rope_freq=dfreq.data_ptr() if deferred else 0)
     torch.cuda.synchronize()
     Kg, Vg, ao = dK.cpu().numpy(), dV.cpu().numpy(), aout.cpu().numpy()
     for b in range(B):
