@@ -1133,6 +1133,17 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* rowss = reinterpret_cast<float*>(smem);            // [8 rows][NW waves] folded norm
   __half* xs = reinterpret_cast<__half*>(smem + 256);
+  // the prologue's kernarg fields in ONE batch of scalar loads: read where first used, each behind
+  // its own s_waitcnt, they were ~10 dependent round trips (~1.2 us) before the first weight load
+  {
+    const int f0 = a.w.K, f1 = a.kparts, f2 = a.spp, f3 = a.n_out, f4 = a.B, f5 = a.nseg, f6 = a.debug, f7 = a.chain_role;
+    const int f8 = a.ldh, f9 = a.ldxf, f10 = a.zero_n, f11 = a.ldo, f12 = a.nb1, f13 = a.tpg, f14 = a.seg_split;
+    const void *p0 = a.w.base, *p1 = a.xh, *p2 = a.xf, *p3 = a.norm_w, *p4 = a.zero, *p5 = a.dbg_clk, *p6 = a.out,
+               *p7 = a.chain_cnt, *p8 = a.ss_out;
+    asm volatile("" ::"s"(f0), "s"(f1), "s"(f2), "s"(f3), "s"(f4), "s"(f5), "s"(f6), "s"(f7), "s"(f8), "s"(f9), "s"(f10),
+                 "s"(f11), "s"(f12), "s"(f13), "s"(f14), "s"(p0), "s"(p1), "s"(p2), "s"(p3), "s"(p4), "s"(p5), "s"(p6),
+                 "s"(p7), "s"(p8), "s"(nblk));
+  }
   const int lane = threadIdx.x & 63, wave = wave_id(), tid = threadIdx.x;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
