@@ -99,6 +99,18 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bid, cons
   static_assert(!WAIT || (SPLITK && !EARLY && !TL), "the in-flight wait is a split-K, non-EARLY form");
   static_assert(!ROUTE || (EARLY && !SPLITK && NORM && BLOCK == 1024 && EPI == EPI_SWIGLU), "routed form");
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // the prologue's kernarg fields in ONE batch of scalar loads (read where first used, each behind
+  // its own s_waitcnt, they were 4-5 dependent round trips before the first weight load)
+  {
+    const void *p0 = a.w.base, *p1 = a.x, *p2 = a.norm_w, *p3 = a.out, *p4 = a.expert_ids, *p5 = a.dbg_clk,
+               *p6 = a.resid, *p7 = a.wait;
+    const int f0 = a.w.K, f1 = a.n_out, f2 = a.n_slots, f3 = a.debug, f4 = a.wait_n, f5 = a.grid_div, f6 = a.w.rows;
+    const size_t z0 = a.w.P.p0, z1 = a.w.P.p1, z2 = a.w.P.p2, z3 = a.w.P.p3, z4 = a.w.P.s0, z5 = a.w.P.s1,
+                 z6 = a.w.P.s2, z7 = a.w.P.s3;
+    asm volatile("" ::"s"(p0), "s"(p1), "s"(p2), "s"(p3), "s"(p4), "s"(p5), "s"(p6), "s"(p7), "s"(f0), "s"(f1), "s"(f2),
+                 "s"(f3), "s"(f4), "s"(f5), "s"(f6), "s"(z0), "s"(z1), "s"(z2), "s"(z3), "s"(z4), "s"(z5), "s"(z6),
+                 "s"(z7), "s"(nblk));
+  }
   // TL: per-block timeline (wall_clock64 ticks, microbenchmarks only):
   // [entry, prologue done, first item done, exit, items done by wave 0]
   long long* tl = nullptr;
@@ -693,6 +705,10 @@ __global__ __launch_bounds__(BLOCK) void gemv_qkv_kernel(QkvLaunch a) {
   int8_t* xq = reinterpret_cast<int8_t*>(smem);
   float* xd = reinterpret_cast<float*>(smem + a.K);
   float* red = xd + (a.K >> 5);
+  // the prologue's kernarg fields in one scalar batch (as gemv_body's)
+  asm volatile("" ::"s"(a.x), "s"(a.norm_w), "s"(a.K), "s"(a.pos), "s"(a.nseg), "s"(a.g1), "s"(a.blocks0),
+               "s"(a.seg[0].base), "s"(a.seg[1].base), "s"(a.seg[2].base), "s"(a.seg[0].rows), "s"(a.seg[1].rows),
+               "s"(a.seg[2].rows), "s"(a.seg[0].P.s0), "s"(a.seg[1].P.s0), "s"(a.seg[2].P.s0));
   const int pos = *a.pos;
   XPrologue<true, BLOCK> xp;   // QKV always follows the attention RMSNorm
   xp.load(a.x, a.norm_w, a.K);
