@@ -1706,7 +1706,11 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
       return;
     }
     // (x-first staging everywhere: weights-first measured 2.295 vs 2.246 ms per B = 6 step, r5b)
-    if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
+    if (a.ew && bmm_il()) {  // MoE: the experts' SwiGLU gate/up (EPI 1) and grouped down (split-K, EPI 2)
+      if (wt_sw) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true, true, 1>), dim3(nblk), dim3(512), lds, s, a);
+      else if (a.kparts > 1) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true, true, 2>), dim3(nblk), dim3(512), lds, s, a);
+      else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true, true, 0>), dim3(nblk), dim3(512), lds, s, a);
+    } else if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
     else if (bmm_il()) {
       const int epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
       if (epi == 1) launch_wt_il<QT, 1>(nblk, lds, a, s);
