@@ -1405,6 +1405,15 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) __hip_atomic_fetch_add(a.chain_cnt + (gt / a.chain_tpp * kChainXcds + (xcc_id() & (kChainXcds - 1))) * kChainStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+    } else if (EPI == 3) {  // one part, plain stores (the batched head's logits): no loads in the loop
+      if (col_ok) {
+        float* o = a.out + (size_t)r16 * a.ldo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = gt * 16 + 4 * kq + i;
+          if (row < a.n_out) o[row] = acc[i];
+        }
+      }
     } else if (EPI == 2) {  // split-K only: fp32 atomics, no read-modify-write path
       if (col_ok) {
         float* o = a.out + (size_t)r16 * a.ldo;
@@ -1485,7 +1494,7 @@ __device__ __forceinline__ void wt_body(const BmmArgs& a, const int run, const i
 // (the body reads its arguments through the kernarg segment pointer: a reference to the by-value
 // parameter made the compiler copy the whole block to scratch, as in bmm_kernel)
 // (PD > 2: one block per CU - the launchers' LDS request - so a register budget of 256, not 128)
-// EPI: the epilogue as a compile-time kind (0 any, 1 SwiGLU, 2 split-K atomics)
+// EPI: the epilogue as a compile-time kind (0 any, 1 SwiGLU, 2 split-K atomics, 3 one-part plain stores)
 template <int QT, int PD, bool MOE = false, bool XF = false, bool IL = false, int EPI = 0>
 __global__ __launch_bounds__(512, PD > 2 ? 1 : 2) void bmm_wt_kernel(BmmArgs a) {
   const BmmArgs* ka = (const BmmArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1663,6 +1672,7 @@ static int wt_config(BmmArgs& a, bool wt_k, size_t& lds) {
       while (ppe < spe && (spe % ppe || (size_t)a.B * (spe / ppe * 256 + kWtXPad) * 2 > 150 * 1024)) ++ppe;
       kparts = E * ppe;
     }
+    if (a.store_out) kparts = 1;  // plain stores: one owner per output
     // the staged slice (B rows x part) stays within the LDS
     while (!a.ew && kparts < steps && (size_t)a.B * ((steps + kparts - 1) / kparts * 256 + kWtXPad) * 2 > 150 * 1024) ++kparts;
   }
@@ -1693,11 +1703,12 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
   // 8-tile group) blocks
   const bool wt_sw = a.swiglu_epi && !a.qkv_epi && a.nseg == 1 && (!a.xf || a.w.K == 4096) &&
                      a.B <= 8;
-  const bool wt_k = !a.swiglu_epi && (!a.ew || a.steps_per_expert > 0) && !a.qkv_epi && !a.xf && !a.one_part && !a.store_out &&
+  const bool wt_k = !a.swiglu_epi && (!a.ew || a.steps_per_expert > 0) && !a.qkv_epi && !a.xf && !a.one_part &&
                     a.nseg == 1 && a.B <= 8;
   if (wt_sw || wt_k) {
     size_t lds = 0;
     const int nblk = wt_config(a, wt_k, lds);
+    if (a.store_out && a.kparts > 1) throw std::runtime_error("bmm: store_out needs one K part");
     if (a.debug >= 4 && !a.ew) {  // microbenchmarks (wt_body's DBG)
       if (a.debug == 4) hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 4>), dim3(nblk), dim3(512), lds, s, a);
       else if (a.debug == 5) hipLaunchKernelGGL((bmm_wt_dbg_kernel<QT, 5>), dim3(nblk), dim3(512), lds, s, a);
@@ -1712,9 +1723,10 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
       else hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true, true, 0>), dim3(nblk), dim3(512), lds, s, a);
     } else if (a.ew) hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, true, true>), dim3(nblk), dim3(512), lds, s, a);
     else if (bmm_il()) {
-      const int epi = wt_sw ? 1 : a.kparts > 1 ? 2 : 0;
+      const int epi = wt_sw ? 1 : a.kparts > 1 ? 2 : a.store_out ? 3 : 0;
       if (epi == 1) launch_wt_il<QT, 1>(nblk, lds, a, s);
       else if (epi == 2) launch_wt_il<QT, 2>(nblk, lds, a, s);
+      else if (epi == 3) launch_wt_il<QT, 3>(nblk, lds, a, s);
       else launch_wt_il<QT, 0>(nblk, lds, a, s);
     } else {
       hipLaunchKernelGGL((bmm_wt_kernel<QT, 2, false, true>), dim3(nblk), dim3(512), lds, s, a);
@@ -1722,6 +1734,8 @@ static void launch_bmm(BmmArgs a, hipStream_t s) {
     return;
   }
   if (a.zero) throw std::runtime_error("bmm: the zero side job runs on the wave-owned kernels only");
+  if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi && !a.one_part)
+    throw std::runtime_error("bmm: store_out needs one K part");
   if (a.qkv_epi || a.swiglu_epi || a.xf || a.one_part) {
     // one K part (the epilogue needs whole rows); 8-wave blocks (the folded norm needs 8), 2 per
     // CU by LDS (16-wave blocks staging x once per CU: 5 % slower steps, r2)
@@ -1814,8 +1828,6 @@ static void bmm_check(const BmmArgs& a) {
     throw std::runtime_error("bmm: swiglu epilogue");
   if (a.xf && !a.qkv_sk && (!a.norm_w || !bmm_norm_fits(a.w.K, a.B) || a.ldxf < a.w.K || a.ldxf % 4))
     throw std::runtime_error("bmm: folded norm");
-  if (a.store_out && !a.xf && !a.qkv_epi && !a.swiglu_epi && !a.one_part)
-    throw std::runtime_error("bmm: store_out needs one K part");
   if (a.one_part && !bmm_qkv_fits(a.w.K, a.B)) throw std::runtime_error("bmm: one_part x slice exceeds LDS");
   if (a.ew && (a.ew_ld < 1 || (a.swiglu_epi ? a.tiles_per_expert < 1 || ((a.n_out + 15) / 16) % a.tiles_per_expert
                                             : a.steps_per_expert < 1 || (a.w.K / 256) % a.steps_per_expert)))

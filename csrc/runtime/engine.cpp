@@ -1333,8 +1333,16 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
   embed_rows(tok_embd_, btok_, B, x_, s);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
-    bprep_rows(x_, d, false, out_norm_, d, B, logits_b_, B * V_pad_, s);
-    bmm_rows(t_output_, xh_b_, d, logits_b_, V_pad_, V_l_, B, s);
+    // the head stores its logits (one K part, plain stores: no zeroed rows to add into)
+    bprep_rows(x_, d, false, out_norm_, d, B, nullptr, 0, s);
+    for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
+      BmmArgs h;
+      h.w = t_output_; h.xh = xh_b_ + (size_t)b0 * d; h.ldh = d;
+      h.out = logits_b_ + (size_t)b0 * V_pad_; h.ldo = V_pad_; h.n_out = V_l_;
+      h.B = std::min(kBmmMaxRows, B - b0);
+      h.store_out = true;
+      bmm(h, s);
+    }
   } else {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_rows_layer(l, B, 0, true, s);
     rmsnorm_bf16(x_, out_norm_, hp_.rms_eps, B, d, xb_, s);

@@ -656,6 +656,32 @@ def test_bmm_wo_ffn_chain_matches_three_launches(torch, td, B):
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("B", [1, 6, 8])
+@pytest.mark.parametrize("R", [130, 4100])
+def test_bmm_store_head_vs_fp32(torch, t, B, R):
+    """The batched head's form: f16 rows, one K part, plain stores over whatever the output held
+    (the wave-owned kernel's compile-time store epilogue: no zeroed rows to add into), rows past
+    n_out untouched."""
+    K = 4096
+    rng = np.random.default_rng(B * 13 + int(t) + R)
+    raw, W = make_matrix(t, R, K, rng)
+    dw = dev_bytes(to_planar(t, raw, R, K))
+    X = rng.standard_normal((B, K)).astype(np.float32)
+    dxh = torch.from_numpy(_swizzle4(X.astype(np.float16))).cuda()
+    tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+    hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream(), swiglu=False)
+    ldo = R + 6
+    out = torch.full((B, ldo), 5.0, device="cuda")
+    hip().bmm(tw.data_ptr(), int(t), R, K, dxh.data_ptr(), K, out.data_ptr(), ldo, B, stream(), store_out=True)
+    torch.cuda.synchronize()
+    pre = X.astype(np.float16).astype(np.float64) @ W.astype(np.float64).T
+    got = out.cpu().numpy()
+    for b in range(B):
+        assert rel_err(got[b, :R], pre[b]) < 3e-3, (b, rel_err(got[b, :R], pre[b]))
+        assert np.all(got[b, R:] == 5.0)
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
 @pytest.mark.parametrize("B", [1, 6, 16])
 @pytest.mark.parametrize("mode", ["store", "swiglu"])
 def test_bmm_folded_norm_vs_fp32(torch, t, B, mode):
