@@ -435,6 +435,10 @@ PYBIND11_MODULE(_hip, m) {
         c.allreduce(P<float>(src), P<float>(dst), n, S(stream));
         hip_ok("p2p_allreduce");
       })
+      .def("allreduce_add", [](P2PComm& c, uintptr_t src, uintptr_t dst, int n, uintptr_t stream) {
+        c.allreduce_add(P<float>(src), P<float>(dst), n, S(stream));
+        hip_ok("p2p_allreduce_add");
+      })
       .def("allgather", [](P2PComm& c, uintptr_t src, uintptr_t dst, int n, uintptr_t stream) {
         c.allgather(P<float>(src), P<float>(dst), n, S(stream));
         hip_ok("p2p_allgather");

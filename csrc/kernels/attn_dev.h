@@ -101,6 +101,13 @@ __device__ __forceinline__ void attn_decode_body(AttnDecodeArgs a) {
   long long* const tl = TL ? a.dbg_clk + 16 * ((size_t)(blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) : nullptr;
 #define LFK_STAMP(i) do { if constexpr (TL) { if (stamp) tl[(i) + 1] = wall_clock64(); } } while (0)
   if constexpr (TL) { if (stamp) { tl[0] = wall_clock64(); tl[15] = xcc_id(); } }
+  // the prologue's kernarg fields in one scalar batch (as bmm's and gemv's prologues): read where
+  // first used they were three dependent round trips before the first K / V load, not two
+  asm volatile("" ::"s"(a.q), "s"(a.k_cache), "s"(a.v_cache), "s"(a.pos), "s"(a.n_ctx), "s"(a.n_head), "s"(a.scale),
+               "s"(a.part), "s"(a.counters), "s"(a.out), "s"(a.debug_stop), "s"(a.batch), "s"(a.slots),
+               "s"(a.slot_stride), "s"(a.q_stride), "s"(a.out_stride), "s"(a.part_stride), "s"(a.out_h),
+               "s"(a.out_h_stride), "s"(a.done), "s"(a.qkv_raw), "s"(a.qkv_ld), "s"(a.k_off), "s"(a.v_off), "s"(a.ss),
+               "s"(a.inv_k), "s"(a.eps), "s"(a.rope_freq));
   if ((int)blockIdx.z == (a.batch > 0 ? a.batch : 1)) {  // weight-touch plane (see AttnDecodeArgs::pf)
     const int nb = gridDim.x * gridDim.y, b = blockIdx.y * gridDim.x + blockIdx.x;
     uint32_t acc = 0;

@@ -322,6 +322,10 @@ struct P2PArgs {
   int n = 0, max_n = 0, rank = 0, world = 1;
   int stride = 0;                  // granules per (slot, rank): max_n + kP2PMaxBlocks (+ the fused area)
   int gather = 0;                  // 0: all-reduce (sum), 1: all-gather
+  // all-reduce only: dst[i] += sum (instead of =), and src[i] is zeroed once pushed - the batched
+  // row-parallel projections accumulate into a buffer that stays zero between launches, so no
+  // copy / fill node seeds it per collective (and rank 0 needs no residual copy)
+  int accumulate = 0;
   int* epochs = nullptr;           // [kP2PMaxBlocks] local, zero-initialised, advanced per launch
   int* err = nullptr;              // set on a timed-out wait
 };

@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
   //    heartbeat (last, so that a peer seeing it mostly finds the data there too)
   for (int i = i0 + tid; i < i1; i += blockDim.x) {
     const u64_t g = ((u64_t)ep << 32) | __float_as_uint(a.src[i]);
+    if (a.accumulate) const_cast<float*>(a.src)[i] = 0.f;  // (this lane's own element, read above)
 #pragma unroll
     for (int p = 0; p < kP2PMaxRanks; ++p)
       if (p < W)
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
 #pragma unroll
       for (int p = 0; p < kP2PMaxRanks; ++p)
         if (p < W) sum += v[p];
-      a.dst[i] = sum;
+      a.dst[i] = a.accumulate ? a.dst[i] + sum : sum;  // (dst identical on every rank: so is the result)
     }
   }
 }
@@ -156,6 +157,8 @@ void p2p_collective(const P2PArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   if (a.n > a.max_n) throw std::runtime_error("p2p: message larger than the slot");
   if (a.stride < a.max_n + kP2PMaxBlocks) throw std::runtime_error("p2p: slot stride");
+  if (a.accumulate && a.gather) throw std::runtime_error("p2p: accumulate is an all-reduce mode");
+  if (a.accumulate && a.src == a.dst) throw std::runtime_error("p2p: accumulate needs distinct src / dst");
   hipLaunchKernelGGL(p2p_collective_kernel, dim3(kP2PMaxBlocks), dim3(256), 0, s, a);
 }
 

@@ -374,6 +374,10 @@ void Engine::alloc_buffers() {
     attn_cnt_b_ = (int*)dalloc(sizeof(int) * 64 * bmax_);
     HIPCHK(hipMemset(attn_cnt_b_, 0, sizeof(int) * 64 * bmax_));
     gu_b_ = (float*)dalloc(sizeof(float) * bmax_ * 2 * F_l_);
+    if (tp_on_) {  // the batched row-parallel partials (zero between launches: P2PArgs::accumulate)
+      tmp_b_ = (float*)dalloc(sizeof(float) * bmax_ * d);
+      HIPCHK(hipMemset(tmp_b_, 0, sizeof(float) * bmax_ * d));
+    }
     HIPCHK(hipHostMalloc((void**)&h_bslots_, sizeof(int) * bmax_, hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&h_btok_, sizeof(int) * bmax_, hipHostMallocDefault));
     for (int i = 0; i < 2; ++i) {
@@ -621,7 +625,9 @@ std::vector<std::pair<std::string, std::string>> Engine::comm_info() const {
   put("decode_row_parallel_allreduce", !tp_on_ ? "none (tp=1)" : epi ? "gemv epilogue granules (no collective launch)" : coll);
   const size_t brow = (size_t)std::max(bmax_, 1) * hp_.n_embd;
   put("batched_row_parallel_allreduce",
-      !tp_on_ ? "none (tp=1)" : p2p && brow <= (size_t)p2p_->max_n() ? "p2p one-shot collective kernel" : comm_ ? "rccl all-reduce" : "none");
+      !tp_on_ ? "none (tp=1)"
+      : p2p && brow <= (size_t)p2p_->max_n() ? "p2p one-shot collective kernel (accumulating: no copy / fill nodes)"
+      : comm_ ? "rccl all-reduce" : "none");
   const size_t pre = (size_t)opt_.n_batch * hp_.n_embd;
   put("prefill_allreduce",
       !tp_on_ ? "none (tp=1)" : p2p && pre <= (size_t)p2p_->max_n() ? "p2p one-shot collective kernel" : comm_ ? "rccl all-reduce" : "none");
@@ -1132,15 +1138,20 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
   const int d = hp_.n_embd, hd = hp_.head_dim, ncol = nq_ + 2 * nkvd_;
   // row-parallel Wo / down under TP: accumulate this rank's partial into tmp_ (holding the
   // residual on rank 0, zeros elsewhere), then all-reduce into x_
+  // P2P path: the partials go to tmp_b_, which the accumulating all-reduce (x_ += sum) leaves zeroed
+  // for the next projection - no copy / fill node per collective. RCCL fallback: the residual seeds
+  // rank 0's tmp_, zeros the others', and the all-reduce stores the sum into x_.
   const bool tp = tp_on_;
-  float* acc = tp ? tmp_ : x_;
+  const bool tp_acc = tp && tmp_b_ && p2p_ && p2p_->ready() && (size_t)B * d <= (size_t)p2p_->max_n();
+  float* acc = tp_acc ? tmp_b_ : tp ? tmp_ : x_;
   auto tp_begin = [&]() {
-    if (!tp) return;
+    if (!tp || tp_acc) return;
     if (opt_.tp_rank == 0) HIPCHK(hipMemcpyAsync(tmp_, x_, sizeof(float) * B * d, hipMemcpyDeviceToDevice, s));
     else HIPCHK(hipMemsetAsync(tmp_, 0, sizeof(float) * B * d, s));
   };
   auto tp_end = [&]() {
-    if (tp) allreduce_into(tmp_, x_, (size_t)B * d, s);
+    if (tp_acc) p2p_->allreduce_add(tmp_b_, x_, B * d, s);
+    else if (tp) allreduce_into(tmp_, x_, (size_t)B * d, s);
   };
   const size_t kv_layer = (size_t)nkv_l_ * opt_.n_ctx * hd;
   __half* kcl = kc_ + kv_layer * (l - opt_.layer_begin);  // slot 0's layer l; the kernels add slot * slot_stride_
@@ -1299,8 +1310,13 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
     // gate/up and down in ONE launch, the down blocks waiting per K part on the gate/up tiles
     // they read (bmm_ffn_chain): the down weight stream starts under the gate/up's last tiles
     // instead of after a kernel boundary
-    if (ffn_chain_ >= 1 && !tp && bmm_ffn_chain_supported(gu, dn)) {
+    // (under TP with more than two ranks on ONE GPU - the eight-rank rehearsal - the chain's down
+    // blocks, waiting on their gate/up, and the peers' spinning collectives can hold each other's
+    // CUs: a 2 s chain timeout in r5; the same rule as tp_epilogue's)
+    const bool tp_chain = tp_acc && !(p2p_->shared_device() && p2p_->world() > 2);
+    if (ffn_chain_ >= 1 && (!tp || tp_chain) && bmm_ffn_chain_supported(gu, dn)) {
       bmm_ffn_chain(gu, dn, chain_cnt_ + kChainInts * l, chain_err_, s);
+      tp_end();
       return;
     }
     bmm(gu, s);

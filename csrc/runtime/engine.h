@@ -294,6 +294,7 @@ class Engine : public SlotBackend {
   // buffers
   float* x_ = nullptr;        // [n_batch][d]
   float* tmp_ = nullptr;      // [n_batch][d]  (TP partial / MoE expert output)
+  float* tmp_b_ = nullptr;    // [bmax][d] TP: batched row-parallel partials, kept zero by the accumulating all-reduce
   __hip_bfloat16* xb_ = nullptr;    // [n_batch][d]
   float* qkv_ = nullptr;      // [n_batch][nq + 2 nkvd]
   float* q_ = nullptr;        // [n_batch][nq]

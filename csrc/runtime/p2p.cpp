@@ -104,17 +104,20 @@ void P2PComm::open(const std::vector<std::string>& handles) {
   ready_ = true;
 }
 
-void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_t s) {
+void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_t s, int accumulate) {
   if (!ready_) throw std::runtime_error("p2p: open() the peer handles first");
   P2PArgs a;
   a.peers = peers_;
   a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_; a.gather = gather;
+  a.accumulate = accumulate;
   a.stride = stride();
   a.epochs = epochs_; a.err = err_;
   p2p_collective(a, s);
 }
 
 void P2PComm::allreduce(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 0, s); }
+
+void P2PComm::allreduce_add(float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 0, s, 1); }
 
 void P2PComm::allgather(const float* src, float* dst, int n, hipStream_t s) { launch(src, dst, n, 1, s); }
 

@@ -27,6 +27,8 @@ class P2PComm {
   bool ready() const { return ready_; }
   int max_n() const { return max_n_; }
   void allreduce(const float* src, float* dst, int n, hipStream_t s);
+  // dst += the all-reduced src, and src is left zeroed (P2PArgs::accumulate)
+  void allreduce_add(float* src, float* dst, int n, hipStream_t s);
   void allgather(const float* src, float* dst, int n, hipStream_t s);  // dst [world][n]
   int error() const;                                   // device error word (0 = ok)
   // the group's fault words as stored in this rank's region (fault[r]: rank r's code, 0 = none):
@@ -61,7 +63,7 @@ class P2PComm {
   bool ready_ = false;
   bool shared_device_ = false;
   bool uncached_ = false;
-  void launch(const float* src, float* dst, int n, int gather, hipStream_t s);
+  void launch(const float* src, float* dst, int n, int gather, hipStream_t s, int accumulate = 0);
 };
 
 }  // namespace lfk

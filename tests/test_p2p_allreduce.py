@@ -72,6 +72,20 @@ def _worker(rank, world, port, q, uncached):
             parts = [_inputs(r, 200 + it, n) for r in range(world)]
             ref = sum(parts) if it % 2 else np.concatenate(parts)
             worst = max(worst, float(np.abs(y.cpu().numpy() - ref).max()))
+        # accumulating mode (the batched row-parallel projections): dst += sum, src left zeroed
+        base = torch.from_numpy(_inputs(7, 500)).cuda()   # the same "residual" on both ranks
+        acc = base.clone()
+        ref = _inputs(7, 500).astype(np.float32)
+        for it in range(4):
+            n = [N, 1000, 37, N][it]
+            src.zero_()
+            src[:n].copy_(torch.from_numpy(_inputs(rank, 600 + it, n)))
+            dist.barrier()
+            c.allreduce_add(src.data_ptr(), acc.data_ptr(), n, s.cuda_stream)
+            torch.cuda.synchronize()
+            ref[:n] += sum(_inputs(r, 600 + it, n) for r in range(world))
+            assert float(src.abs().max()) == 0.0, "accumulate: src not zeroed"
+            worst = max(worst, float(np.abs(acc.cpu().numpy() - ref).max()))
         # graph replay: the captured launch advances its epochs on the device
         g = torch.cuda.CUDAGraph()
         cs = torch.cuda.Stream()
@@ -138,6 +152,11 @@ def test_p2p_uncached_region_one_rank():
         c.allgather(x.data_ptr(), z.data_ptr(), n, s.cuda_stream)
         torch.cuda.synchronize()
         assert torch.equal(y, x) and torch.equal(z, x)
+        xs = x.clone()
+        y0 = y.clone()
+        c.allreduce_add(xs.data_ptr(), y.data_ptr(), n, s.cuda_stream)   # one rank: y += x, x zeroed
+        torch.cuda.synchronize()
+        assert torch.equal(y, y0 + x) and float(xs.abs().max()) == 0.0
     x = torch.from_numpy(_inputs(0, 400, N)).cuda()
     y = torch.zeros(N, device="cuda")
     g = torch.cuda.CUDAGraph()
