@@ -299,6 +299,22 @@ struct CandRow {
   }
 };
 
+// one wave: the <= KMAX top-K superset of the n survivors in LDS, compacted into tval / tidx
+template <int NW>
+__device__ __forceinline__ int top_superset(int n, int K, const float* cval, const int* cidx, float* tval, int* tidx) {
+  const int lane = threadIdx.x & 63;
+  float w[NW];
+  int wi[NW];
+#pragma unroll
+  for (int e = 0; e < NW; ++e) {
+    const int i = 64 * e + lane;
+    w[e] = i < n ? cval[i] : -FLT_MAX;
+    wi[e] = i < n ? cidx[i] : 0x7fffffff;
+  }
+  const float T = n > KMAX ? wave_superset_threshold<NW>(w, K) : -FLT_MAX;
+  return wave_collect<NW>(w, wi, T, KMAX, tval, tidx);
+}
+
 template <int NE2, bool TL = false>
 __global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int nb_l) {
   const int brow = blockIdx.x;
@@ -322,6 +338,14 @@ __global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int n
   const SamplerParamsDev& P = *a.p;
   const int K = P.top_k;
   if (tid == 0) ncol = 0;
+  // Two lower bounds of the global K-th largest value: (a) each slice bound
+  // (that slice alone holds >= K values above it); (b) a superset threshold of
+  // the slice MAXIMA (>= K distinct slices have their maximum above it).
+  // (b) keeps the survivor count small even for flat (high-entropy) logits.
+  // Their loads go out first and unconditionally (clamped: a repeated bound or maximum changes
+  // neither), so wave 0's threshold search runs while the candidate loads are in flight
+  const float sm0 = cr.smax(min(tid & 63, nb - 1)), sm1 = cr.smax(min((tid & 63) + 64, nb - 1));
+  float lb = cr.bound(min(tid, nb - 1));
   float v[NE2];
   int idx[NE2];
 #pragma unroll
@@ -329,17 +353,12 @@ __global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int n
     const int i = min(256 * e + tid, nb * KMAX - 1);
     cr.cand(i, v[e], idx[e]);
   }
-  // Two lower bounds of the global K-th largest value: (a) each slice bound
-  // (that slice alone holds >= K values above it); (b) a superset threshold of
-  // the slice MAXIMA (>= K distinct slices have their maximum above it).
-  // (b) keeps the survivor count small even for flat (high-entropy) logits.
-  float lb = -FLT_MAX;
-  for (int b = tid; b < nb; b += 256) lb = fmaxf(lb, cr.bound(b));
+  for (int b = tid + 256; b < nb; b += 256) lb = fmaxf(lb, cr.bound(b));
   lb = wave_max_fast(lb);
   if (tid < 64) {
     float mx[2];
-    mx[0] = tid < nb ? cr.smax(tid) : -FLT_MAX;
-    mx[1] = tid + 64 < nb ? cr.smax(tid + 64) : -FLT_MAX;
+    mx[0] = tid < nb ? sm0 : -FLT_MAX;
+    mx[1] = tid + 64 < nb ? sm1 : -FLT_MAX;
     int valid = (mx[0] > -FLT_MAX) + (mx[1] > -FLT_MAX);
     valid = (int)wave_sum_fast((float)valid);
     if (valid >= K) lb = fmaxf(lb, wave_superset_threshold<2>(mx, K));
@@ -348,31 +367,39 @@ __global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int n
   __syncthreads();
   lb = fmaxf(fmaxf(redf[0], redf[1]), fmaxf(redf[2], redf[3]));
   LFK_ST(0);
+  // compaction: ONE LDS atomic per wave for all of its survivors (ballot counts), then each
+  // survivor's slot from the wave's base and its lane's rank (per-element atomics serialised)
+  const int lane0 = tid & 63;
+  int cnt = 0;
 #pragma unroll
   for (int e = 0; e < NE2; ++e) {
     const bool ok = 256 * e + tid < nb * KMAX && idx[e] >= 0 && v[e] >= lb && v[e] > -FLT_MAX;
+    cnt += __popcll(__ballot(ok));
+  }
+  int base = 0;
+  if (lane0 == 0 && cnt) base = atomicAdd(&ncol, cnt);
+  base = __shfl(base, 0);
+#pragma unroll
+  for (int e = 0; e < NE2; ++e) {
+    const bool ok = 256 * e + tid < nb * KMAX && idx[e] >= 0 && v[e] >= lb && v[e] > -FLT_MAX;
+    const unsigned long long m = __ballot(ok);
     if (ok) {
-      const int p = atomicAdd(&ncol, 1);
+      const int p = base + lanes_below(m);
       if (p < CAP2) { cval[p] = v[e]; cidx[p] = idx[e]; }
     }
+    base += __popcll(m);
   }
   __syncthreads();
   LFK_ST(1);
   if (tid >= 64) return;
   const int lane = tid;
   const int n = min(ncol, CAP2);
-  constexpr int NW = CAP2 / 64;
-  float w[NW];
-  int wi[NW];
-#pragma unroll
-  for (int e = 0; e < NW; ++e) {
-    const int i = 64 * e + lane;
-    w[e] = i < n ? cval[i] : -FLT_MAX;
-    wi[e] = i < n ? cidx[i] : 0x7fffffff;
-  }
-  const float T = n > KMAX ? wave_superset_threshold<NW>(w, K) : -FLT_MAX;
   if (lane == 0 && ncol > CAP2) a.state[S_NSTATE - 1] = ncol;  // overflow marker (diagnostics)
-  const int mcol = wave_collect<NW>(w, wi, T, KMAX, tval, tidx);
+  // the usual survivor count (< 256) on 4 registers per lane: the threshold search's every
+  // round walks all NW registers of the one working wave, so the CAP2 / 64 = 32-register form
+  // cost ~8x the instructions for the same answer (entries past n are -FLT_MAX in both)
+  const int mcol = n <= 256 ? top_superset<4>(n, K, cval, cidx, tval, tidx)
+                            : top_superset<CAP2 / 64>(n, K, cval, cidx, tval, tidx);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
