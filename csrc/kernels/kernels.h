@@ -480,6 +480,9 @@ void rope_kv_prefill(const float* qkv, int T, int pos0, int n_q, int n_kv, int h
 // (+ zero zero[i * zero_stride], i < zero_n: the step's in-launch chain counters)
 void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos, hipStream_t s, int* zero = nullptr,
                   int zero_n = 0, int zero_stride = 1);
+// the same, and x[b] = the embedding of row b's token (one launch: the batched step's first)
+void batch_gather_embed(const int* slots, int B, const int* state, int* tok, int* pos, const QMat& emb, float* x,
+                        hipStream_t s, int* zero = nullptr, int zero_n = 0, int zero_stride = 1);
 // out[i] = x[i] (+) ... small helpers
 void add_inplace(float* x, const float* y, int n, hipStream_t s);
 void set_i32(int* p, int v, hipStream_t s);

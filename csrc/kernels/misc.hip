@@ -10,11 +10,10 @@
 namespace lfk {
 
 template <int QT>
-__device__ void embed_body(const QMat& e, const int* tokens, int T, float* x) {
-  const int t = blockIdx.x;
+__device__ void embed_row(const QMat& e, int token, int t, float* x) {
   // clamped: a token id can only come from the host (validated) or the sampler, but a
   // corrupted id must not turn into an out-of-bounds read that faults the GPU
-  const size_t row = (size_t)min(max(tokens[t], 0), e.rows - 1);
+  const size_t row = (size_t)min(max(token, 0), e.rows - 1);
   const int nq = e.K >> 5;
   for (int q = threadIdx.x; q < nq; q += blockDim.x) {
     float v[32];
@@ -23,6 +22,10 @@ __device__ void embed_body(const QMat& e, const int* tokens, int T, float* x) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
   }
+}
+template <int QT>
+__device__ void embed_body(const QMat& e, const int* tokens, int T, float* x) {
+  embed_row<QT>(e, tokens[blockIdx.x], blockIdx.x, x);
 }
 
 // side job: zero [zero, zero + zero_n) ints (the decode step's done counters, attn_wo1)
@@ -150,6 +153,27 @@ void batch_gather(const int* slots, int B, const int* state, int* tok, int* pos,
   if (B <= 0) return;
   const int n = std::max(B, zero ? zero_n : 0);
   hipLaunchKernelGGL(batch_gather_kernel, dim3((n + 63) / 64), dim3(64), 0, s, slots, B, state, tok, pos, zero,
+                     zero ? zero_n : 0, zero_stride);
+}
+
+// batched decode step head: block b gathers row b's token / position from its slot's state and
+// embeds that token (one launch instead of batch_gather + embed_rows)
+__global__ __launch_bounds__(128) void batch_embed_kernel(QMat e, const int* slots, const int* state, int* tok, int* pos,
+                                                          float* x, int* zero, int zero_n, int zero_stride) {
+  const int b = blockIdx.x;
+  for (int i = b * 128 + threadIdx.x; i < zero_n; i += gridDim.x * 128) zero[(size_t)i * zero_stride] = 0;
+  const int* st = state + (size_t)slots[b] * S_NSTATE;
+  const int token = st[S_TOKEN];
+  if (threadIdx.x == 0) {
+    tok[b] = token;
+    pos[b] = st[S_POS];
+  }
+  LFK_DISPATCH_TYPE(e.type, embed_row<QT>(e, token, b, x));
+}
+void batch_gather_embed(const int* slots, int B, const int* state, int* tok, int* pos, const QMat& emb, float* x,
+                        hipStream_t s, int* zero, int zero_n, int zero_stride) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(batch_embed_kernel, dim3(B), dim3(128), 0, s, emb, slots, state, tok, pos, x, zero,
                      zero ? zero_n : 0, zero_stride);
 }
 

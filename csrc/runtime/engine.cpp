@@ -1344,9 +1344,8 @@ void Engine::enqueue_batch_layer(int l, int B, hipStream_t s) {
 void Engine::enqueue_batch_step(int B, hipStream_t s) {
   const int d = hp_.n_embd;
   // (its launch also zeroes the FFN chain counters of every layer)
-  batch_gather(bslots_, B, state_, btok_, bpos_, s, chain_cnt_, chain_cnt_ ? kChainInts / kChainStride * hp_.n_layer : 0,
-               kChainStride);
-  embed_rows(tok_embd_, btok_, B, x_, s);
+  batch_gather_embed(bslots_, B, state_, btok_, bpos_, tok_embd_, x_, s, chain_cnt_,
+                     chain_cnt_ ? kChainInts / kChainStride * hp_.n_layer : 0, kChainStride);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
     // the head stores its logits (one K part, plain stores: no zeroed rows to add into)
