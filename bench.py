@@ -34,9 +34,20 @@ measured, every rank frees its engine and rank 0 runs ONE tensor-parallel pass o
 GPUs in a fresh ``torch.distributed.run`` child (its own process group; the DP ranks wait at a
 gloo barrier and touch no GPU meanwhile), bounded by ``--tp-timeout`` seconds. Its result -
 tokens/s at C clients, p50, the serial rate, and which comm path each TP message takes with the
-rank count RCCL reports (``Engine.comm_info``) - goes into ``config.tp`` (BASELINE's "8B across 2
-MI355X, RCCL all-reduce" at N = 2; ``--tp-model llama3-70b-q4_k_m`` for "70B across 8"). A failed
-or timed-out pass is recorded there with its error and never touches the DP headline.
+rank count RCCL reports (``Engine.comm_info``) - goes into ``config.tp``. The pass's model follows
+BASELINE.json's multi-GPU configs (``--tp-model`` default ``auto``): N >= 8 shards Llama-3-70B
+Q4_K_M ("70B across 8"), smaller N the headline 8B ("8B tensor_split across 2 MI355X").
+
+Correctness gate of the TP pass (``config.tp.check``): before the child starts, rank 0 records a
+TP = 1 reference on its own GPU - the prefill logits of a fixed 48-token prompt and 16 greedy
+decode steps with every step's logits (the DP engine when the TP model is the headline model, a
+TP = 1 engine of the TP model otherwise: one MI355X holds the 70B). The TP child replays the same
+prompt on the sharded engine and compares: every step's logits within ``TP_CHECK_TOL`` of TP = 1
+(relative to the largest logit; a wrong shard or a stale peer granule moves them by tens of %),
+greedy tokens identical, or diverging only where TP = 1's own logits put the two picks within twice
+the deviation measured at that step (a rounding near-tie). A failed check marks the pass failed
+(``ok: false``) with the numbers kept. A failed or timed-out pass is recorded in ``config.tp`` with
+its error and never touches the DP headline.
 
 Load: ``--clients C`` concurrent clients (default 6 = the reference pod's admission
 capacity, 1 in flight + MAX_QUEUE_SIZE 5, reference api.py:19,113) post the K timed
@@ -45,9 +56,11 @@ continuous batch. After the timed run, ``--serial-steps`` requests from ONE clie
 reference's one-generation-at-a-time serving) are timed as well and reported in
 ``config.serial`` (rank 0's GPU group, same engine).
 
-The bench raises the server timeout to 600 s and the queue to >= C so no request of the
-measurement is rejected (production: 25 s / 5, reference api.py:17-19); both overrides
-are recorded in the JSON. Weights are random-init of the exact Llama-3-8B Q4_K_M shapes
+Admission runs the production settings (the chart's): at most MAX_QUEUE_SIZE + 1 = 6 requests
+admitted at once (the reference pod's capacity, reference api.py:19,113), all six decoding as rows
+of one batch. Only the server timeout is raised (600 s instead of 25 s, so a slow first request of
+a cold box is measured rather than 408'd), and the admission cap only when ``--clients`` exceeds
+6; both are recorded in ``bench_overrides``. Weights are random-init of the exact Llama-3-8B Q4_K_M shapes
 and type mix (a synthetic GGUF written once per node), prompts are synthetic chat requests.
 """
 from __future__ import annotations
@@ -123,14 +136,95 @@ _LAUNCHER_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP
                   "ROLE_RANK", "ROLE_NAME", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
 
 
-def tp_pass_cmd(args, world: int, json_out: str) -> list:
+def resolve_tp_model(args, world: int) -> str:
+    """The TP pass's model: BASELINE.json's multi-GPU configs - "70B across 8" at N >= 8, the
+    headline 8B ("8B tensor_split across 2") below; an explicit --tp-model wins."""
+    if args.tp_model and args.tp_model != "auto":
+        return args.tp_model
+    return "llama3-70b-q4_k_m" if world >= 8 else args.model
+
+
+def tp_pass_cmd(args, world: int, json_out: str, check_ref: str = "") -> list:
     """The TP child: this script under its own torch.distributed.run, --parallel tp over `world` GPUs."""
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
-            "--gpus", str(world), "--parallel", "tp", "--model", args.tp_model or args.model,
-            "--steps", str(args.tp_steps), "--warmup", "1", "--serial-steps", "1", "--tp-pass", "off",
-            "--clients", str(args.clients), "--max-batch", str(args.max_batch), "--n-ctx", str(args.n_ctx),
-            "--model-dir", args.model_dir, "--json-out", json_out]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           "--gpus", str(world), "--parallel", "tp", "--model", resolve_tp_model(args, world),
+           "--steps", str(args.tp_steps), "--warmup", "1", "--serial-steps", "1", "--tp-pass", "off",
+           "--clients", str(args.clients), "--max-batch", str(args.max_batch), "--n-ctx", str(args.n_ctx),
+           "--model-dir", args.model_dir, "--json-out", json_out]
+    if check_ref:
+        cmd += ["--tp-check-ref", check_ref]
+    return cmd
+
+
+# ------------------------------------------------------------------ TP correctness gate
+TP_CHECK_PROMPT = 48      # prompt tokens (one prefill chunk)
+TP_CHECK_STEPS = 16       # greedy decode steps
+TP_CHECK_TOL = 5e-2       # per-step logits vs TP = 1, relative to the largest |logit|
+
+
+def _rel(a, b) -> float:
+    import numpy as np
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-12))
+
+
+def tp_check_prompt(n_vocab: int) -> list:
+    import numpy as np
+    return [int(t) for t in np.random.default_rng(2024).integers(3, min(n_vocab, 30000), TP_CHECK_PROMPT)]
+
+
+def tp_check_record(eng, n_vocab: int, steps: int = TP_CHECK_STEPS):
+    """Greedy run of the fixed prompt on an engine (eval_logits / decode_logits on slot 0):
+    (tokens, logits per step [steps + 1, V]) - row 0 is the prefill's."""
+    import numpy as np
+    prompt = tp_check_prompt(n_vocab)
+    rows = [np.asarray(eng.eval_logits(prompt, 0), np.float32)[:n_vocab]]
+    toks = []
+    for k in range(steps):
+        t = int(np.argmax(rows[-1]))
+        toks.append(t)
+        rows.append(np.asarray(eng.decode_logits(t, len(prompt) + k), np.float32)[:n_vocab])
+    return np.asarray(toks, np.int64), np.stack(rows)
+
+
+def tp_check_compare(ref_toks, ref_logits, toks, logits, tol: float = TP_CHECK_TOL) -> dict:
+    """The gate: logits of every step both runs fed identically within `tol` of TP = 1; greedy
+    tokens equal, or diverging where TP = 1's logits of the two picks lie within twice the
+    deviation measured at that step."""
+    import numpy as np
+    n = min(len(ref_toks), len(toks))
+    dev, div, gap = [], None, None
+    for k in range(n + 1):
+        if k < len(ref_logits) and k < len(logits):
+            dev.append(_rel(logits[k], ref_logits[k]))
+        if k == n:
+            break
+        if int(toks[k]) != int(ref_toks[k]):
+            div = k
+            r = np.asarray(ref_logits[k], np.float64)
+            gap = float(abs(r[int(toks[k])] - r[int(ref_toks[k])]) / max(np.abs(r).max(), 1e-12))
+            break
+    ok_logits = bool(dev) and max(dev) <= tol
+    ok_greedy = len(toks) == len(ref_toks) and (div is None or gap <= 2.0 * dev[div])
+    return {"status": "passed" if ok_logits and ok_greedy else "failed",
+            "prompt_tokens": TP_CHECK_PROMPT, "greedy_steps": int(len(ref_toks)),
+            "max_rel_dev_vs_tp1": round(max(dev), 6) if dev else None,
+            "prefill_rel_dev_vs_tp1": round(dev[0], 6) if dev else None, "tol": tol,
+            "greedy_identical_steps": int(div if div is not None else n),
+            "divergence": None if div is None else {"step": div, "tp1_gap": round(gap, 6),
+                                                     "allowed": round(2.0 * dev[div], 6)}}
+
+
+def tp_check_save(path: str, toks, logits):
+    import numpy as np
+    np.savez(path, toks=np.asarray(toks, np.int64), logits=np.asarray(logits, np.float32))
+
+
+def tp_check_load(path: str):
+    import numpy as np
+    with np.load(path) as z:   # (allow_pickle stays False: plain arrays written by tp_check_save)
+        return z["toks"], z["logits"]
 
 
 def run_tp_pass(cmd: list, json_out: str, timeout_s: float, heartbeat_s: float = 60.0) -> dict:
@@ -170,11 +264,42 @@ def run_tp_pass(cmd: list, json_out: str, timeout_s: float, heartbeat_s: float =
         return {"ok": False, "error": f"{type(e).__name__}: {e}", "wall_s": round(time.time() - t0, 1),
                 "log": log_path, "log_tail": tail}
     cfg = res.get("config", {})
-    return {"ok": True, "model": cfg.get("model"), "parallelism": cfg.get("parallelism"), "scaling": "strong",
-            "value": res.get("value"), "unit": res.get("unit"), "ms_per_step": res.get("ms_per_step"),
-            "p50_response_ms": cfg.get("p50_response_ms"), "requests": cfg.get("requests"),
-            "avg_output_tokens": cfg.get("avg_output_tokens"), "serial": cfg.get("serial"),
-            "comm": cfg.get("comm"), "wall_s": round(time.time() - t0, 1)}
+    check = cfg.get("check")
+    out = {"ok": True, "model": cfg.get("model"), "parallelism": cfg.get("parallelism"), "scaling": "strong",
+           "value": res.get("value"), "unit": res.get("unit"), "ms_per_step": res.get("ms_per_step"),
+           "p50_response_ms": cfg.get("p50_response_ms"), "requests": cfg.get("requests"),
+           "avg_output_tokens": cfg.get("avg_output_tokens"), "serial": cfg.get("serial"),
+           "comm": cfg.get("comm"), "check": check, "wall_s": round(time.time() - t0, 1)}
+    if check is not None and check.get("status") != "passed":
+        # a fast number from a wrong model is no result: the pass fails, its numbers are kept
+        out["ok"] = False
+        out["error"] = "TP correctness check failed against the TP = 1 reference"
+    return out
+
+
+def tp_reference_engine(args, tp_model: str, device: int, ref_path: str):
+    """The TP = 1 reference of a TP model other than the headline one (the 70B at N >= 8): its
+    synthetic GGUF (written once; the TP child reuses it) on ONE GPU, the fixed greedy run recorded,
+    the engine freed before the child starts. -> (ref_path, None) or ("", error)."""
+    try:
+        from llama_fastapi_k8s_gpu_amd.engine.llama import Llama
+        from llama_fastapi_k8s_gpu_amd.gguf.synthetic import write_synthetic_gguf
+        path = os.path.join(args.model_dir, f"{tp_model}-s0.gguf")
+        if not os.path.exists(path):
+            t0 = time.time()
+            write_synthetic_gguf(tp_model, path, seed=0)
+            print(f"[bench] wrote synthetic {tp_model} in {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+        ref = Llama(path, n_gpu_layers=-1, n_ctx=args.n_ctx, split_mode="none", verbose=False, device=device)
+        try:
+            tp_check_save(ref_path, *tp_check_record(ref._backend.engine, ref.n_vocab()))
+        finally:
+            ref.close()
+            del ref
+            import gc
+            gc.collect()
+        return ref_path, None
+    except Exception as e:
+        return "", f"{type(e).__name__}: {e}"
 
 
 def _launch_ranks(n: int) -> int:
@@ -200,7 +325,10 @@ def main() -> int:
         os.environ.get("TMPDIR", "/tmp"), "llama_amd_models")))
     ap.add_argument("--tp-pass", choices=["auto", "on", "off"], default="auto",
                     help="N > 1: a tensor-parallel pass over the same GPUs after the DP headline (config.tp)")
-    ap.add_argument("--tp-model", default="", help="model of the TP pass (default: --model)")
+    ap.add_argument("--tp-model", default="auto",
+                    help="model of the TP pass (auto: llama3-70b-q4_k_m at N >= 8, else --model)")
+    ap.add_argument("--tp-check-ref", default="",
+                    help="(TP child) TP = 1 reference (.npz) to check the sharded engine against")
     ap.add_argument("--tp-steps", type=int, default=2, help="timed rounds of the TP pass")
     ap.add_argument("--tp-timeout", type=float, default=480.0, help="wall bound of the TP pass (s)")
     ap.add_argument("--json-out", default="", help="also write rank 0's JSON result to this file")
@@ -268,11 +396,23 @@ def main() -> int:
         return 0
 
     comm = llm._backend.engine.comm_info() if tp and hasattr(getattr(llm, "_backend", None), "engine") else None
+    check = None
+    if tp and args.tp_check_ref:
+        # the correctness gate: the fixed prompt's greedy run on the sharded engine against TP = 1
+        try:
+            ref_toks, ref_logits = tp_check_load(args.tp_check_ref)
+            got_toks, got_logits = tp_check_record(llm._backend.engine, llm.n_vocab(), len(ref_toks))
+            check = tp_check_compare(ref_toks, ref_logits, got_toks, got_logits)
+        except Exception as e:
+            check = {"status": "failed", "error": f"{type(e).__name__}: {e}"}
+        print(f"[bench] tp check: {check}", file=sys.stderr, flush=True)
     eng = CountingEngine(llm)
     settings = Settings()
     settings.timeout_seconds = BENCH_TIMEOUT_S  # measure latency, do not 408 long generations in the bench
     settings.max_batch = max_batch
-    settings.max_queue_size = max(settings.max_queue_size, args.clients)
+    # production admission (MAX_QUEUE_SIZE + 1 = 6 admitted at once); raised only for more clients
+    if args.clients > settings.admission_cap:
+        settings.max_admitted = args.clients
     app = create_app(settings, engine=eng)
     serial_steps = args.serial_steps if args.serial_steps >= 0 else max(2, args.steps // 4)
 
@@ -366,12 +506,29 @@ def main() -> int:
                                   "p50_response_ms": round(statistics.median(serial_lat) * 1e3, 1)
                                   if serial_lat else None,
                                   "scope": "rank 0's GPU group" if world > 1 else "whole job"},
+                       "admission": {"max_queue_size": settings.max_queue_size,
+                                     "admission_cap": settings.admission_cap, "max_batch": max_batch},
                        "bench_overrides": {"timeout_seconds": BENCH_TIMEOUT_S,
-                                           "max_queue_size": settings.max_queue_size,
-                                           "production": {"timeout_seconds": 25.0, "max_queue_size": 5}}},
+                                           **({"admission_cap": settings.admission_cap}
+                                              if settings.max_admitted is not None else {}),
+                                           "production": {"timeout_seconds": 25.0, "max_queue_size": 5,
+                                                          "admission_cap": 6}}},
         }
         if comm is not None:
             res["config"]["comm"] = comm
+        if check is not None:
+            res["config"]["check"] = check
+    # the TP pass's TP = 1 reference (rank 0, its own GPU): the DP engine when the TP model is the
+    # headline model, recorded before that engine goes
+    tp_model = resolve_tp_model(args, world) if tp_pass else ""
+    ref_path, ref_err = "", None
+    if tp_pass and rank == 0:
+        ref_path = os.path.join(tempfile.gettempdir(), f"lfk_bench_tpref_{os.getpid()}.npz")
+        if tp_model == args.model:
+            try:
+                tp_check_save(ref_path, *tp_check_record(llm._backend.engine, llm.n_vocab()))
+            except Exception as e:
+                ref_path, ref_err = "", f"{type(e).__name__}: {e}"
     # the TP pass: every rank's engine is gone (its memory with it); rank 0 runs the child while
     # the others wait at the barrier below
     del llm
@@ -380,9 +537,16 @@ def main() -> int:
     if tp_pass:
         dist.barrier()
         if rank == 0:
-            print(f"[bench] tp pass: tp{world} over {args.tp_model or args.model}", file=sys.stderr, flush=True)
+            if tp_model != args.model and ref_path:
+                ref_path, ref_err = tp_reference_engine(args, tp_model, device, ref_path)
+            print(f"[bench] tp pass: tp{world} over {tp_model}", file=sys.stderr, flush=True)
             out = os.path.join(tempfile.gettempdir(), f"lfk_bench_tp{world}_{os.getpid()}.json")
-            res["config"]["tp"] = run_tp_pass(tp_pass_cmd(args, world, out), out, args.tp_timeout)
+            tpres = run_tp_pass(tp_pass_cmd(args, world, out, ref_path), out, args.tp_timeout)
+            if not ref_path and tpres.get("ok"):
+                # no TP = 1 reference: the pass's number is unverified, so it does not count
+                tpres.update(ok=False, check={"status": "failed", "error": f"no TP = 1 reference: {ref_err}"},
+                             error="TP correctness check unavailable")
+            res["config"]["tp"] = tpres
     if rank == 0:
         if args.json_out:
             with open(args.json_out, "w") as f:

@@ -38,8 +38,9 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<Engine>(m, "Engine")
       .def(py::init([](const std::string& path, int n_ctx, int n_batch, int device, bool use_graph, int tp_rank,
                        int tp_size, py::bytes nccl_id, int layer_begin, const std::vector<float>& tensor_split,
-                       int n_slots, const std::string& comm, int layer_end) {
+                       int n_slots, const std::string& comm, int layer_end, const std::string& test_fault) {
              EngineOptions o;
+             o.test_fault = test_fault;
              o.layer_begin = layer_begin;
              o.layer_end = layer_end;
              o.n_slots = n_slots;
@@ -59,7 +60,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("use_graph") = true, py::arg("tp_rank") = 0, py::arg("tp_size") = 1,
            py::arg("nccl_id") = py::bytes(""), py::arg("layer_begin") = 0,
            py::arg("tensor_split") = std::vector<float>{}, py::arg("n_slots") = 1, py::arg("comm") = "auto",
-           py::arg("layer_end") = -1)
+           py::arg("layer_end") = -1, py::arg("test_fault") = "")
       .def(
           "generate",
           [](Engine& e, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,

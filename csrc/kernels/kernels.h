@@ -328,6 +328,9 @@ struct P2PArgs {
   int accumulate = 0;
   int* epochs = nullptr;           // [kP2PMaxBlocks] local, zero-initialised, advanced per launch
   int* err = nullptr;              // set on a timed-out wait
+  // host-mapped mirror [kP2PMaxRanks] of this rank's fault words, refreshed by every launch: the
+  // engine's per-step health check reads it with no copy (the sampler's all-gather runs every step)
+  int* fault_h = nullptr;
 };
 void p2p_collective(const P2PArgs& a, hipStream_t s);
 

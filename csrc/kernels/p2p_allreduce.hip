@@ -48,7 +48,7 @@ static constexpr long long kP2PWaitTicks = 2000000000LL;
 
 typedef unsigned long long u64_t;
 
-__global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
+__device__ __forceinline__ void p2p_collective_body(const P2PArgs& a) {
   __shared__ unsigned s_ep;
   const int b = blockIdx.x, tid = threadIdx.x;
   const int W = a.world, R = a.rank;
@@ -149,6 +149,20 @@ __global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
         if (p < W) sum += v[p];
       a.dst[i] = a.accumulate ? a.dst[i] + sum : sum;  // (dst identical on every rank: so is the result)
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void p2p_collective_kernel(P2PArgs a) {
+  p2p_collective_body(a);
+  // the fault words as this launch leaves them, mirrored to host-mapped memory (a fault a later
+  // block raises is mirrored by the next launch)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.fault_h) {
+#pragma unroll
+    for (int p = 0; p < kP2PMaxRanks; ++p)
+      if (p < a.world)
+        __hip_atomic_store(a.fault_h + p, __hip_atomic_load(a.peers.fault[a.rank] + p, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

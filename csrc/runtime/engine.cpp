@@ -124,13 +124,22 @@ Engine::Engine(const std::string& path, const EngineOptions& opts) : opt_(opts) 
   nq_ = sp.nq;
   nkvd_ = sp.nkvd;
   F_l_ = sp.F_l;
-  // negative-test hook (tests/test_tp_gpu.py): LFK_TP_FAULT=<rank>:0:shard makes that rank load the
-  // FFN features of the NEXT shard - a deliberately wrong expert / FFN shard the TP acceptance must catch
-  if (const char* e = std::getenv("LFK_TP_FAULT")) {
+  // fault-injection test hook (EngineOptions::test_fault; never set in production), parsed once
+  if (!opt_.test_fault.empty()) {
     int rk = -1, n = -1;
     char kind[8] = {0};
-    if (tp > 1 && std::sscanf(e, "%d:%d:%7s", &rk, &n, kind) == 3 && rk == r && std::strcmp(kind, "shard") == 0)
-      f0_ = (f0_ + (size_t)F_l_) % (size_t)hp_.n_ff;
+    const int got = std::sscanf(opt_.test_fault.c_str(), "%d:%d:%7s", &rk, &n, kind);
+    if (got < 2) throw std::runtime_error("test_fault: expected <rank>:<n>[:dev|:shard]");
+    std::fprintf(stderr, "[lfk] WARNING: fault-injection test hook active on rank %d: %s\n", r,
+                 opt_.test_fault.c_str());
+    if (rk == r && tp > 1) {
+      if (got == 3 && std::strcmp(kind, "shard") == 0) {
+        f0_ = (f0_ + (size_t)F_l_) % (size_t)hp_.n_ff;
+      } else if (n > 0) {
+        fault_after_ = n;
+        fault_dev_ = got == 3 && std::strcmp(kind, "dev") == 0;
+      }
+    }
   }
   V_l_ = sp.V_l;
   V_pad_ = sp.V_pad;
@@ -536,7 +545,8 @@ void Engine::check_device_err() {
   // follower's host failure lands in the control channel: either poisons the group here
   int e = 0;
   std::string group;
-  if (p2p_ && p2p_->ready()) group = p2p_->fault_report();
+  // (the P2P fault words through their host-mapped mirror: no blocking copy per step)
+  if (p2p_ && p2p_->ready()) group = p2p_->fault_report(/*fresh=*/false);
   if (group.empty()) group = group_fault();
   if (!group.empty()) {
     healthy_ = false;
@@ -554,16 +564,19 @@ void Engine::check_device_err() {
 
 void Engine::build_rope() {
   const int hd = hp_.head_dim, n = opt_.n_ctx;
+  // one angle for every path: the fp32 product pos * freq (as the batched attention's deferred
+  // RoPE forms it on the device, and as llama.cpp does), its cos / sin taken exactly - so a key
+  // is rotated the same whether a prefill, a single-row decode or a batched step wrote it (a
+  // double-precision angle drifted from the fp32 one by up to pos * 2^-24 rad)
+  std::vector<float> f(hd / 2);
+  for (int i = 0; i < hd / 2; ++i) f[i] = (float)std::pow((double)hp_.rope_base, -2.0 * i / hd);
   std::vector<float2> t((size_t)n * (hd / 2));
   for (int p = 0; p < n; ++p)
     for (int i = 0; i < hd / 2; ++i) {
-      const double inv = std::pow((double)hp_.rope_base, -2.0 * i / hd);
-      const double a = p * inv;
-      t[(size_t)p * (hd / 2) + i] = make_float2((float)std::cos(a), (float)std::sin(a));
+      const float a = (float)p * f[i];
+      t[(size_t)p * (hd / 2) + i] = make_float2((float)std::cos((double)a), (float)std::sin((double)a));
     }
   HIPCHK(hipMemcpy(rope_, t.data(), t.size() * sizeof(float2), hipMemcpyHostToDevice));
-  std::vector<float> f(hd / 2);
-  for (int i = 0; i < hd / 2; ++i) f[i] = (float)std::pow((double)hp_.rope_base, -2.0 * i / hd);
   HIPCHK(hipMemcpy(rope_freq_, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice));
 }
 
@@ -1348,13 +1361,15 @@ void Engine::enqueue_batch_step(int B, hipStream_t s) {
                      chain_cnt_ ? kChainInts / kChainStride * hp_.n_layer : 0, kChainStride);
   if (bg_) {
     for (int l = 0; l < hp_.n_layer; ++l) enqueue_batch_layer(l, B, s);
-    // the head stores its logits (one K part, plain stores: no zeroed rows to add into)
+    // the head stores its logits (one K part, plain stores: no zeroed rows to add into); the
+    // store-only epilogue runs on the wave-owned kernel, which takes at most 8 rows per launch
     bprep_rows(x_, d, false, out_norm_, d, B, nullptr, 0, s);
-    for (int b0 = 0; b0 < B; b0 += kBmmMaxRows) {
+    constexpr int kHeadRows = 8;
+    for (int b0 = 0; b0 < B; b0 += kHeadRows) {
       BmmArgs h;
       h.w = t_output_; h.xh = xh_b_ + (size_t)b0 * d; h.ldh = d;
       h.out = logits_b_ + (size_t)b0 * V_pad_; h.ldo = V_pad_; h.n_out = V_l_;
-      h.B = std::min(kBmmMaxRows, B - b0);
+      h.B = std::min(kHeadRows, B - b0);
       h.store_out = true;
       bmm(h, s);
     }
@@ -1435,17 +1450,7 @@ void Engine::tp_ctl_create(const std::string& name) {
 void Engine::tp_ctl_attach(const std::string& name) {
   if (opt_.tp_size < 2 || opt_.tp_rank == 0) throw std::runtime_error("tp_ctl_attach: follower ranks only");
   tp_ctl_ = TPChannel::attach(name, opt_.tp_rank);
-  // test hook: LFK_TP_FAULT=<rank>:<n>[:dev] - follower <rank> fails its n-th command, as a host
-  // failure (reported over the channel), or with ":dev" as a device-side fault word (what a
-  // timed-out collective wait stores) while it goes on replaying (tests/test_tp_fault_gpu.py)
-  if (const char* e = std::getenv("LFK_TP_FAULT")) {
-    int rk = -1, n = 0;
-    char kind[8] = {0};
-    if (std::sscanf(e, "%d:%d:%7s", &rk, &n, kind) >= 2 && rk == opt_.tp_rank && n > 0) {
-      fault_after_ = n;
-      fault_dev_ = std::strcmp(kind, "dev") == 0;
-    }
-  }
+  // (the fault-injection hook, EngineOptions::test_fault, was parsed by the constructor)
 }
 
 void Engine::tp_stop() {
@@ -1477,7 +1482,7 @@ void Engine::follow() {
     }
     try {
       if (fault_after_ > 0 && --fault_after_ == 0) {
-        if (!fault_dev_) throw std::runtime_error("injected follower fault (LFK_TP_FAULT)");
+        if (!fault_dev_) throw std::runtime_error("injected follower fault (test hook)");
         if (p2p_ && p2p_->ready()) p2p_->raise_fault(300 + opt_.tp_rank);  // as a timed-out epilogue wait
       }
       switch (op) {

@@ -53,6 +53,11 @@ struct EngineOptions {
   // [0, n_slots) can decode together through batch_step() (also under tensor parallelism)
   int n_slots = 1;
   bool verbose = false;
+  // fault-injection test hook, "<rank>:<n>[:dev|:shard]" (empty in production; set only by the tests
+  // through the Python backend's explicit opt-in, runtime/hip_backend.py): follower <rank> fails its
+  // n-th command (host failure, or ":dev" a device-side fault word), or ":shard" (n = 0) loads the
+  // NEXT shard's FFN features - a deliberately wrong shard the TP acceptance must catch
+  std::string test_fault;
 };
 
 
@@ -220,7 +225,7 @@ class Engine : public SlotBackend {
   // tensor parallelism: publish a command to the followers (rank 0); no-op on one rank
   bool leader() const { return opt_.tp_size > 1 && opt_.tp_rank == 0; }
   std::string group_fault() const;  // leader: the followers' failures as the channel holds them ("" = none)
-  int fault_after_ = 0;             // follower test hook (LFK_TP_FAULT): fail the n-th command
+  int fault_after_ = 0;             // follower test hook (EngineOptions::test_fault): fail the n-th command
   bool fault_dev_ = false;          // ... as a device-side fault word instead of a host failure
   void mirror(const TPMsg& m);
   void prefill_chunk(int slot, const int* toks, int T, int pos, bool head);

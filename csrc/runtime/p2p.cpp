@@ -52,6 +52,10 @@ P2PComm::P2PComm(int rank, int world, int max_n, int device, bool uncached, int 
   }
   p2pchk(hipMalloc((void**)&err_, sizeof(int) * 4), "hipMalloc err");
   p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "hipMemset err");
+  p2pchk(hipHostMalloc((void**)&fault_h_, sizeof(int) * kP2PMaxRanks, hipHostMallocMapped | hipHostMallocCoherent),
+         "hipHostMalloc fault mirror");
+  std::memset(fault_h_, 0, sizeof(int) * kP2PMaxRanks);
+  p2pchk(hipHostGetDevicePointer((void**)&fault_hd_, fault_h_, 0), "hipHostGetDevicePointer fault mirror");
   p2pchk(hipDeviceSynchronize(), "sync");
 }
 
@@ -62,6 +66,7 @@ P2PComm::~P2PComm() {
   if (epochs_) (void)hipFree(epochs_);
   if (fused_epochs_) (void)hipFree(fused_epochs_);
   if (err_) (void)hipFree(err_);
+  if (fault_h_) (void)hipHostFree(fault_h_);
 }
 
 std::string P2PComm::handle() const {
@@ -111,7 +116,7 @@ void P2PComm::launch(const float* src, float* dst, int n, int gather, hipStream_
   a.src = src; a.dst = dst; a.n = n; a.max_n = max_n_; a.rank = rank_; a.world = world_; a.gather = gather;
   a.accumulate = accumulate;
   a.stride = stride();
-  a.epochs = epochs_; a.err = err_;
+  a.epochs = epochs_; a.err = err_; a.fault_h = fault_hd_;
   p2p_collective(a, s);
 }
 
@@ -143,16 +148,20 @@ int P2PComm::error() const {
   return e;
 }
 
-std::vector<int> P2PComm::faults() const {
+std::vector<int> P2PComm::faults(bool fresh) const {
   std::vector<int> f((size_t)world_, 0);
   if (!ready_) return f;
+  if (!fresh) {
+    for (int r = 0; r < world_; ++r) f[r] = __atomic_load_n(fault_h_ + r, __ATOMIC_ACQUIRE);
+    return f;
+  }
   p2pchk(hipMemcpy(f.data(), peers_.fault[rank_], sizeof(int) * world_, hipMemcpyDeviceToHost), "read faults");
   return f;
 }
 
-std::string P2PComm::fault_report() const {
+std::string P2PComm::fault_report(bool fresh) const {
   std::string out;
-  const std::vector<int> f = faults();
+  const std::vector<int> f = faults(fresh);
   for (int r = 0; r < world_; ++r)
     if (f[r]) {
       const int c = f[r];
@@ -174,6 +183,7 @@ void P2PComm::raise_fault(int code) {
 void P2PComm::reset_error() {
   p2pchk(hipMemset(err_, 0, sizeof(int) * 4), "reset err");
   if (ready_) p2pchk(hipMemset(peers_.fault[rank_], 0, sizeof(int) * kP2PMaxRanks), "reset faults");
+  std::memset(fault_h_, 0, sizeof(int) * kP2PMaxRanks);
 }
 
 }  // namespace lfk

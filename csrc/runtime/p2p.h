@@ -33,8 +33,10 @@ class P2PComm {
   int error() const;                                   // device error word (0 = ok)
   // the group's fault words as stored in this rank's region (fault[r]: rank r's code, 0 = none):
   // any rank's timed-out wait, or a host failure raise_fault() published
-  std::vector<int> faults() const;
-  std::string fault_report() const;                    // "" = no rank faulted
+  // fresh = false: the host-mapped mirror the last collective launch left (no copy; the engine's
+  // per-step check), true: a blocking read of the region itself
+  std::vector<int> faults(bool fresh = true) const;
+  std::string fault_report(bool fresh = true) const;   // "" = no rank faulted
   void raise_fault(int code);                          // this rank's code into every rank's region
   bool uncached() const { return uncached_; }          // region allocated hipDeviceMallocUncached
   // diagnostics: per rank (mapped pointer, allocation base, allocation size) as seen here
@@ -59,6 +61,8 @@ class P2PComm {
   std::vector<void*> imported_;
   int* epochs_ = nullptr;
   int* err_ = nullptr;
+  int* fault_h_ = nullptr;   // host-mapped mirror of this rank's fault words (P2PArgs::fault_h)
+  int* fault_hd_ = nullptr;  // ... its device-side address
   P2PPeers peers_;
   bool ready_ = false;
   bool shared_device_ = false;

@@ -129,10 +129,16 @@ void TPChannel::report_fault(const std::string& msg) {
 
 std::string TPChannel::fault_report() const {
   std::string out;
+  const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  const bool probe = now - probe_ns_ >= 100000000LL;
+  if (probe) probe_ns_ = now;
+  if ((int)exited_.size() != h_->world) exited_.assign(h_->world, 0);
   for (int r = 1; r < h_->world; ++r) {
     std::string what;
+    if (probe && !exited_[r]) exited_[r] = !pid_alive(h_->follower_pid[r].load(std::memory_order_relaxed));
     if (h_->fault[r].load(std::memory_order_acquire)) what = h_->fault_msg[r];
-    else if (!pid_alive(h_->follower_pid[r].load(std::memory_order_relaxed))) what = "exited";
+    else if (exited_[r]) what = "exited";
     if (!what.empty()) out += (out.empty() ? "" : "; ") + std::string("rank ") + std::to_string(r) + ": " + what;
   }
   return out;

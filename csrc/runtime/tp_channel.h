@@ -91,6 +91,10 @@ class TPChannel {
   size_t bytes_ = 0;
   Hdr* h_ = nullptr;
   uint8_t* payload_ = nullptr;
+  // fault_report()'s follower liveness probes (kill + /proc reads) run at most every 100 ms: the
+  // engine asks after every step, and a fault flag in the shared header needs no probe
+  mutable int64_t probe_ns_ = 0;
+  mutable std::vector<int> exited_;
   uint32_t last_ = 0;  // follower: the last sequence number it consumed
 };
 

@@ -82,6 +82,11 @@ class Settings:
     max_context_tokens: int = 1024
     timeout_seconds: float = 25.0
     max_queue_size: int = 5
+    # requests admitted at once (in flight + waiting); the next one gets 503. None = the reference's
+    # capacity, max_queue_size + 1 (1 in flight + 5 queued, reference api.py:19,113,156-160), whatever
+    # max_batch is: with max_batch = 6 all six admitted requests decode together. 0 = the uncapped
+    # form (max_batch in flight + max_queue_size waiting)
+    max_admitted: Optional[int] = None
     message_char_cap: int = 400        # reference api.py:36-39
     # True: the reference's prompt heuristics exactly (the 400-char cap applies to the system
     # message too, C6). False: system messages keep their full text.
@@ -93,6 +98,13 @@ class Settings:
     cooperative_cancel: bool = True     # stop timed-out generations
     openai_api: bool = True             # /v1/models, /v1/completions, /v1/chat/completions
     sampling: SamplingDefaults = field(default_factory=SamplingDefaults)
+
+    @property
+    def admission_cap(self) -> int:
+        """Requests admitted at once (in flight + queued), 0 = no cap beyond the queue's."""
+        if self.max_admitted is None:
+            return self.max_queue_size + 1
+        return max(0, int(self.max_admitted))
 
     @property
     def model_path(self) -> str:
@@ -125,6 +137,8 @@ class Settings:
         s.max_context_tokens = _env("MAX_CONTEXT_TOKENS", s.max_context_tokens, int)
         s.timeout_seconds = _env("TIMEOUT_SECONDS", s.timeout_seconds, float)
         s.max_queue_size = _env("MAX_QUEUE_SIZE", s.max_queue_size, int)
+        adm = _env("MAX_ADMITTED", None)
+        s.max_admitted = int(adm) if adm is not None else None
         s.message_char_cap = _env("MESSAGE_CHAR_CAP", s.message_char_cap, int)
         s.parity_mode = _env("PARITY_MODE", s.parity_mode, bool)
         s.exact_token_guard = _env("EXACT_TOKEN_GUARD", s.exact_token_guard, bool)

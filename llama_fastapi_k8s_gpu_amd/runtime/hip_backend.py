@@ -53,6 +53,20 @@ def _tp_setup(split_mode: str, tensor_split, comm: str):
     return rank, ws, local, nccl_id, check_tensor_split(tensor_split, ws)
 
 
+def _test_fault() -> str:
+    """The fault-injection test hook (EngineOptions::test_fault): ``LFK_TP_FAULT`` is honoured only
+    with the explicit opt-in ``LFK_TEST_HOOKS=1`` (the fault tests set both); a stray
+    ``LFK_TP_FAULT`` in a pod is ignored, loudly."""
+    spec = os.environ.get("LFK_TP_FAULT", "")
+    if not spec:
+        return ""
+    if os.environ.get("LFK_TEST_HOOKS") != "1":
+        logger.warning("LFK_TP_FAULT=%s ignored: fault injection needs LFK_TEST_HOOKS=1", spec)
+        return ""
+    logger.warning("fault-injection test hook active: LFK_TP_FAULT=%s", spec)
+    return spec
+
+
 class HipBackend:
     name = "hip"
 
@@ -78,7 +92,8 @@ class HipBackend:
         self.max_batch = max_batch
         self.engine = hip.Engine(model_path, n_ctx=n_ctx, n_batch=min(n_batch, n_ctx), device=device,
                                  use_graph=use_graphs, tp_rank=rank, tp_size=size, nccl_id=nccl_id,
-                                 tensor_split=ts, n_slots=max_batch + 1 if max_batch > 1 else 1, comm=comm)
+                                 tensor_split=ts, n_slots=max_batch + 1 if max_batch > 1 else 1, comm=comm,
+                                 test_fault=_test_fault() if size > 1 else "")
         self.n_ctx = n_ctx
         self.n_vocab = int(hparams.n_vocab)
         self.n_batch = min(n_batch, n_ctx)  # the engine's prefill chunk bound (eval_logits rejects T > n_batch)

@@ -22,11 +22,16 @@ Documented deviations:
     are dropped by the real (chat-templated) token count, so a token-dense prompt
     no longer fails at the context limit; ``PARITY_MODE=0`` exempts
     the system message from the 400-char cap (Appendix C6).
-  * ``MAX_BATCH=M`` (default 1 = the reference): M consumer tasks and a
-    Semaphore(M) feed the engine's continuous batch, so M generations run at once
-    (M in flight + ``MAX_QUEUE_SIZE`` waiting; the next request gets 503). FIFO
-    admission, timeouts and error strings are unchanged. M is capped by the
-    engine's ``batch_width`` (1 for engines without a batch scheduler).
+  * ``MAX_BATCH=M`` (1 = the reference; the chart ships 6): M consumer tasks and a
+    Semaphore(M) feed the engine's continuous batch, so M generations run at once.
+    Admission keeps the reference's capacity: at most ``MAX_QUEUE_SIZE + 1`` requests
+    (6) are admitted at once, in flight or waiting, and the next one gets 503 - with
+    M = 6 every admitted request decodes as a row of one batch instead of waiting its
+    turn (``MAX_ADMITTED`` overrides the cap; 0 = M in flight + the queue). An admitted
+    request counts until its consumer finishes with it (a timed-out generation still
+    running holds its place, as the reference's in-flight thread does). FIFO admission,
+    timeouts and error strings are unchanged. M is capped by the engine's
+    ``batch_width`` (1 for engines without a batch scheduler).
 """
 from __future__ import annotations
 
@@ -163,6 +168,7 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             if future.cancelled():
                 logger.info("Future was cancelled before processing; skipping.")
                 queue.task_done()
+                _release(app_)
                 continue
             metrics.queue_wait.observe(time.monotonic() - request_data['t_enqueue'])
             try:
@@ -188,6 +194,18 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
                     logger.info("Future was cancelled during processing; exception not set.")
             finally:
                 queue.task_done()
+                _release(app_)
+
+    def _release(app_: FastAPI):
+        app_.state.admitted = max(0, app_.state.admitted - 1)
+
+    def _admit(app_: FastAPI, request_data: dict):
+        """Enqueue under the admission cap (503 past it, or when the queue is full)."""
+        cap = settings.admission_cap
+        if cap and app_.state.admitted >= cap:
+            raise asyncio.QueueFull
+        app_.state.queue.put_nowait(request_data)
+        app_.state.admitted += 1
 
     @asynccontextmanager
     async def lifespan(app_: FastAPI):
@@ -195,7 +213,10 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
             # The reference loads the model at import (api.py:24-28); we load it
             # before the server accepts traffic, off the event loop.
             app_.state.engine = await asyncio.to_thread(factory, settings)
-        app_.state.queue = asyncio.Queue(maxsize=settings.max_queue_size)
+        # (under the admission cap the queue may hold every admitted request: the cap is the bound)
+        cap = settings.admission_cap
+        app_.state.queue = asyncio.Queue(maxsize=max(settings.max_queue_size, cap) if cap else settings.max_queue_size)
+        app_.state.admitted = 0
         # generations in flight: MAX_BATCH, capped by what the engine actually runs at once
         # (its continuous batch); an engine without a scheduler (CPU, hybrid, a backend that
         # fell back to one row) keeps the reference's one-at-a-time consumer, so requests
@@ -241,7 +262,7 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
         request_data = {'messages': messages, 'future': future, 'cancel': cancel,
                         't_enqueue': time.monotonic()}
         try:
-            queue.put_nowait(request_data)
+            _admit(request.app, request_data)
         except asyncio.QueueFull:
             metrics.requests.labels("rejected_503").inc()
             raise HTTPException(status_code=503, detail="Server too busy. Please try again later.")
@@ -266,8 +287,7 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
         """Enqueue an engine job (OpenAI routes) behind the same FIFO as /response."""
         fut = asyncio.get_running_loop().create_future()
         try:
-            app.state.queue.put_nowait({'job': job, 'future': fut, 'cancel': cancel,
-                                        't_enqueue': time.monotonic()})
+            _admit(app, {'job': job, 'future': fut, 'cancel': cancel, 't_enqueue': time.monotonic()})
         except asyncio.QueueFull:
             metrics.requests.labels("rejected_503").inc()
             raise HTTPException(status_code=503, detail="Server too busy. Please try again later.")
@@ -290,6 +310,8 @@ def create_app(settings: Optional[Settings] = None, engine: Any = None,
         info = {"status": "ok", "ready": bool(getattr(st, "ready", False)) and eng is not None}
         q = getattr(st, "queue", None)
         info["queue_depth"] = q.qsize() if q is not None else 0
+        info["admitted"] = int(getattr(st, "admitted", 0))
+        info["admission_cap"] = settings.admission_cap
         healthy = True
         if eng is not None and hasattr(eng, "health"):
             try:

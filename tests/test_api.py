@@ -246,3 +246,46 @@ def test_exact_token_trim_shortens_last_message():
     assert out[1]["content"] == "p" * 30 and out[0]["content"] == "d" * 29 and count(out) == 59
     with pytest.raises(ValueError):   # only the system prompt left: a clear error, not a cut persona
         exact_token_trim([{"role": "system", "content": "p" * 80}], count, 60)
+
+
+def test_batched_admission_keeps_reference_capacity():
+    """MAX_BATCH=6 (the chart default): the reference's capacity (1 in flight + 5 queued = 6
+    admitted, reference api.py:19,113,156-160) is kept as a TOTAL cap - the 7th and 8th concurrent
+    requests get 503 - while the 6 admitted ones run at once instead of one after another."""
+    import time
+    app, eng = make("sleep:0.4", timeout_seconds=20, max_batch=6)
+    t0 = time.perf_counter()
+    rs = asyncio.run(_concurrent(app, 8))
+    wall = time.perf_counter() - t0
+    codes = [r.status_code for r in rs]
+    assert codes[:6] == [200] * 6 and codes[6:] == [503, 503], codes
+    assert rs[6].json() == {"detail": "Server too busy. Please try again later."}
+    assert len(eng.calls) == 6
+    assert wall < 6 * 0.4 * 0.6, wall   # concurrent (a serial run of 6 would take >= 2.4 s)
+
+
+def test_admission_slot_freed_when_consumer_finishes():
+    """An admitted request holds its place until its consumer is done with it: after the
+    first wave completes, a new wave of 6 is admitted in full."""
+    app, eng = make("sleep:0.2", timeout_seconds=20, max_batch=6)
+
+    async def two_waves():
+        async with app.router.lifespan_context(app):
+            transport = httpx.ASGITransport(app=app)
+            async with httpx.AsyncClient(transport=transport, base_url="http://t", timeout=60) as c:
+                first = await asyncio.gather(*[c.post("/response", json=body()) for _ in range(6)])
+                second = await asyncio.gather(*[c.post("/response", json=body()) for _ in range(7)])
+                h = (await c.get("/health")).json()
+                return first, second, h
+    first, second, h = asyncio.run(two_waves())
+    assert [r.status_code for r in first] == [200] * 6
+    assert sorted(r.status_code for r in second) == [200] * 6 + [503]
+    assert h["admitted"] == 0 and h["admission_cap"] == 6
+
+
+def test_uncapped_admission_mode():
+    """MAX_ADMITTED=0: the uncapped form - M generations in flight plus MAX_QUEUE_SIZE waiting."""
+    app, eng = make("sleep:0.3", timeout_seconds=20, max_batch=2, max_admitted=0)
+    rs = asyncio.run(_concurrent(app, 9))
+    codes = [r.status_code for r in rs]
+    assert codes.count(200) == 7 and codes.count(503) == 2, codes

@@ -299,3 +299,33 @@ def test_batch_step_six_rows_d8192(tmp_path):
             assert rel_err(logits[b], want) < 5e-2, (step, s, rel_err(logits[b], want))
             seqs[s].append(toks[b])
     assert eng.healthy, eng.last_error
+
+
+@pytest.mark.parametrize("n_rows", [9, 12, 16])
+def test_batch_step_more_than_eight_rows(models, n_rows):
+    """Batches past 8 rows (MAX_BATCH / n_slots > 8): the layers run their 16-row forms and the
+    lm_head, whose store-only epilogue takes at most 8 rows per launch, runs in 8-row chunks -
+    every row against the fp32 reference, greedy pick = argmax of its logits."""
+    from llama_fastapi_k8s_gpu_amd.gguf.reader import GGUFReader
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-llama3-q4_k_m"]
+    eng = load_hip().Engine(path, n_ctx=128, n_batch=64, device=0, use_graph=True, n_slots=16)
+    assert eng.max_batch == 16
+    ref = ReferenceLlama(GGUFReader(path), n_ctx=128)
+    rng = np.random.default_rng(30 + n_rows)
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    slots = [int(s) for s in rng.permutation(16)[:n_rows]]
+    seqs = {}
+    for s in slots:
+        prompt = [int(t) for t in rng.integers(3, 300, 3 + s)]
+        seqs[s] = prompt + [eng.slot_begin(s, prompt, 0, greedy)]
+    for step in range(2):
+        toks = eng.batch_step(slots)
+        logits = eng.batch_logits(len(slots))
+        for b, s in enumerate(slots):
+            want = ref.forward(seqs[s], 0).numpy()
+            assert rel_err(logits[b], want) < 5e-2, (n_rows, step, s, rel_err(logits[b], want))
+            assert toks[b] == int(np.argmax(logits[b]))
+            seqs[s].append(toks[b])
+    assert eng.healthy, eng.last_error

@@ -84,7 +84,9 @@ def test_env_rendered_into_settings(monkeypatch):
     assert s.model_path == "/app/models/Llama-3-8B-Instruct-Q4_K_M.gguf"
     assert s.n_gpu_layers == -1 and s.n_ctx == 1024 and s.max_queue_size == 5 and s.timeout_seconds == 25
     assert s.tensor_split is None and s.seed is None and s.chat_format is None
-    assert s.max_batch == 1   # reference serving (one generation at a time) unless engine.maxBatch is set
+    # the chart serves continuous batching under the reference's admission capacity: every one of
+    # the 6 admitted requests (1 in flight + 5 queued in the reference) decodes as a row of one batch
+    assert s.max_batch == 6 and s.admission_cap == 6
 
 
 def test_docker_files():

@@ -58,7 +58,7 @@ def test_follower_fault_fails_requests_and_health(tmp_path, kind):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MODEL_PATH=path, SPLIT_MODE="row", TP_COMM="ipc", TP_DEVICE="0", HOST="127.0.0.1",
                PORT=str(port), N_CTX="256", N_BATCH="64", MAX_BATCH="3", SEED="5", PYTHONPATH=root,
-               LFK_TP_FAULT="1:4" + (":dev" if kind == "dev" else ""))
+               LFK_TP_FAULT="1:4" + (":dev" if kind == "dev" else ""), LFK_TEST_HOOKS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(mport), "-m", "llama_fastapi_k8s_gpu_amd.serve"]
     log = open(tmp_path / "serve.log", "w")

@@ -126,9 +126,10 @@ def _worker(rank, world, port, paths, q):
             results.append((spec, got, ref))
         # negative case: rank 1 holds the wrong FFN / expert shard (the MoE model)
         spec, path, ts = next(p for p in paths if "mixtral" in p[0])
-        os.environ["LFK_TP_FAULT"] = "1:0:shard"
+        os.environ.update(LFK_TP_FAULT="1:0:shard", LFK_TEST_HOOKS="1")
         llm = Llama(path, split_mode="row", tensor_split=ts, tp_comm="ipc", device=0, **kw)
         os.environ.pop("LFK_TP_FAULT")
+        os.environ.pop("LFK_TEST_HOOKS")
         if rank > 0:
             llm.follow()
             llm.close()
