@@ -160,7 +160,12 @@ def tp_pass_cmd(args, world: int, json_out: str, check_ref: str = "") -> list:
 # ------------------------------------------------------------------ TP correctness gate
 TP_CHECK_PROMPT = 48      # prompt tokens (one prefill chunk)
 TP_CHECK_STEPS = 16       # greedy decode steps
-TP_CHECK_TOL = 5e-2       # per-step logits vs TP = 1, relative to the largest |logit|
+TP_CHECK_TOL = 0.15       # per-step logits vs TP = 1: max |difference| relative to the largest |logit|
+TP_CHECK_COS = 0.99       # ... and cosine similarity of the logit vectors
+# (rounding noise measured on the one-GPU TP = 2 rehearsal, 8B, 32 layers: max relative deviation
+# 0.35 % at the prefill and up to 2.7 % on the decode steps, which read the K / V the prefill's
+# f16 roundings wrote; deeper models accumulate more. A wrong shard or a stale granule gives
+# unrelated logits: cosine far below 0.99)
 
 
 def _rel(a, b) -> float:
@@ -188,16 +193,24 @@ def tp_check_record(eng, n_vocab: int, steps: int = TP_CHECK_STEPS):
     return np.asarray(toks, np.int64), np.stack(rows)
 
 
-def tp_check_compare(ref_toks, ref_logits, toks, logits, tol: float = TP_CHECK_TOL) -> dict:
-    """The gate: logits of every step both runs fed identically within `tol` of TP = 1; greedy
-    tokens equal, or diverging where TP = 1's logits of the two picks lie within twice the
-    deviation measured at that step."""
+def _cos(a, b) -> float:
+    import numpy as np
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.dot(a, b) / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-30))
+
+
+def tp_check_compare(ref_toks, ref_logits, toks, logits, tol: float = TP_CHECK_TOL,
+                     cos_min: float = TP_CHECK_COS) -> dict:
+    """The gate: logits of every step both runs fed identically within `tol` of TP = 1 and at
+    cosine >= `cos_min`; greedy tokens equal, or diverging where TP = 1's logits of the two picks
+    lie within twice the deviation measured at that step."""
     import numpy as np
     n = min(len(ref_toks), len(toks))
-    dev, div, gap = [], None, None
+    dev, cos, div, gap = [], [], None, None
     for k in range(n + 1):
         if k < len(ref_logits) and k < len(logits):
             dev.append(_rel(logits[k], ref_logits[k]))
+            cos.append(_cos(logits[k], ref_logits[k]))
         if k == n:
             break
         if int(toks[k]) != int(ref_toks[k]):
@@ -205,12 +218,13 @@ def tp_check_compare(ref_toks, ref_logits, toks, logits, tol: float = TP_CHECK_T
             r = np.asarray(ref_logits[k], np.float64)
             gap = float(abs(r[int(toks[k])] - r[int(ref_toks[k])]) / max(np.abs(r).max(), 1e-12))
             break
-    ok_logits = bool(dev) and max(dev) <= tol
+    ok_logits = bool(dev) and max(dev) <= tol and min(cos) >= cos_min
     ok_greedy = len(toks) == len(ref_toks) and (div is None or gap <= 2.0 * dev[div])
     return {"status": "passed" if ok_logits and ok_greedy else "failed",
             "prompt_tokens": TP_CHECK_PROMPT, "greedy_steps": int(len(ref_toks)),
             "max_rel_dev_vs_tp1": round(max(dev), 6) if dev else None,
             "prefill_rel_dev_vs_tp1": round(dev[0], 6) if dev else None, "tol": tol,
+            "min_cosine_vs_tp1": round(min(cos), 6) if cos else None, "cos_min": cos_min,
             "greedy_identical_steps": int(div if div is not None else n),
             "divergence": None if div is None else {"step": div, "tp1_gap": round(gap, 6),
                                                      "allowed": round(2.0 * dev[div], 6)}}

@@ -119,7 +119,7 @@ def test_tp_check_gate(tmp_path):
     # a wrong shard (logits off by tens of %): failed
     bad = _FakeEngine(bias=lambda t, p: 0.8 * np.cos(np.arange(97) * 0.37 * (t + 2)))
     c = bench.tp_check_compare(rt, rl, *bench.tp_check_record(bad, ref.V))
-    assert c["status"] == "failed" and c["max_rel_dev_vs_tp1"] > bench.TP_CHECK_TOL
+    assert c["status"] == "failed" and c["min_cosine_vs_tp1"] < bench.TP_CHECK_COS
 
 
 def test_tp_check_greedy_divergence_rule():
