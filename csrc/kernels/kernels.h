@@ -542,6 +542,8 @@ struct SamplerArgs {
   const int* slots = nullptr;
   size_t logits_ld = 0;
   int* batch_out = nullptr;
+  // ... and to host-mapped pinned memory (the batch-step graph's token read-back: no copy node)
+  int* batch_out_host = nullptr;
 };
 int sampler_blocks(int V);
 size_t sampler_cand_words(int V);

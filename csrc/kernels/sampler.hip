@@ -472,6 +472,7 @@ __global__ __launch_bounds__(256) void sample_stage2_kernel(SamplerArgs a, int n
     st[S_RING_LEN] = min(st[S_RING_LEN] + 1, 64);
     if (a.out_tokens) a.out_tokens[st[S_NOUT] % a.out_cap] = tok;
     if (a.batch_out) a.batch_out[brow] = tok;
+    if (a.batch_out_host) __hip_atomic_store(a.batch_out_host + brow, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     LFK_ST(3);
     st[S_NOUT] += 1;
     st[S_STEP] += 1;

@@ -357,6 +357,11 @@ class Engine : public SlotBackend {
   // steps in flight (batch_launch / batch_collect): a ring of two, each with its own pinned
   // token buffer and completion event
   int* h_btok2_[2] = {nullptr, nullptr};
+  // h_btok2_[i] are host-mapped (fine-grained): the batch-step graph of flight parity i has its
+  // sampler store the tokens there directly (btok_dev_[i]: their device addresses; sample_host_ is
+  // the one the step being captured writes)
+  int* btok_dev_[2] = {nullptr, nullptr};
+  int* sample_host_ = nullptr;
   hipEvent_t bev_[2] = {nullptr, nullptr};
   int fl_B_[2] = {0, 0};
   bool fl_b1_[2] = {false, false};

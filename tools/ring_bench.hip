@@ -139,6 +139,65 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+
+// the loader's counted wait: n = DMA instructions allowed to stay outstanding (a multiple of 21)
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  if (n >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+  else if (n >= 42) asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+  else if (n >= 21) asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// MODE 8: one loader wave (wave 7) streams every tile's step s of the block into phase slot s % (D + 1)
+// by LDS-DMA (3 pieces per step block: 2 x 1 KB quant, 512 B scale pairs on 32 lanes), D phases ahead;
+// 7 consumer waves compute; one raw barrier per phase (the loader's counted vmcnt makes the phase's
+// data visible; the consumers' lgkmcnt(0) frees the slot the loader refills next)
+template <int D>
+__device__ __forceinline__ void engine_body(const unsigned char* base, char* smem, const __half* xrow, int blk, int wave,
+                                            int lane, int r16, int kq, f4_t& acc, f4_t& acc2) {
+  constexpr int NS = D + 1, PH = kWavesBusy * kSB;  // slots, bytes per phase
+  static_assert(3 * kWavesBusy * (D - 1) <= 63, "vmcnt range");
+  char* ring = smem + kXBytes;
+  const unsigned ring_lds = (unsigned)(size_t)ring;
+  const unsigned char* tb = base + (size_t)blk * kWavesBusy * kSteps * kSB;
+  auto issue = [&](int ph) {  // loader: phase ph of every tile
+    const unsigned slot = __builtin_amdgcn_readfirstlane(ring_lds + (ph % NS) * PH);
+#pragma unroll
+    for (int c = 0; c < kWavesBusy; ++c) {
+      const unsigned char* p = tb + ((size_t)c * kSteps + ph) * kSB;
+      dma16(p + lane * 16, slot + c * kSB);
+      dma16(p + 1024 + lane * 16, slot + c * kSB + 1024);
+      if (lane < 32) dma16(p + 2048 + lane * 16, slot + c * kSB + 2048);
+    }
+  };
+  const bool loader = wave == kWavesBusy;
+  if (loader) {
+#pragma unroll
+    for (int p = 0; p < D; ++p) issue(p);
+    vm_wait_rt(21 * (D - 1));  // phase 0 landed
+  }
+  lds_barrier();
+#pragma unroll
+  for (int p = 0; p < kSteps; ++p) {
+    if (loader) {
+      if (p + D < kSteps) issue(p + D);
+      const int after = (p + D < kSteps ? p + D : kSteps - 1) - (p + 1);  // phases issued after p + 1
+      if (p + 1 < kSteps) vm_wait_rt(21 * (after > 0 ? after : 0));
+    } else {
+      const char* slot = ring + (p % NS) * PH + wave * kSB;
+      Raw w[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        w[h].q = *reinterpret_cast<const int4*>(slot + h * 1024 + lane * 16);
+        w[h].m = *reinterpret_cast<const uint2*>(slot + 2048 + r16 * 32 + 8 * (2 * h + (kq >> 1)));
+      }
+      step_compute(w, p, kq, xrow, acc, acc2);
+    }
+    lds_barrier();
+  }
+}
+
 // MODE 0 stream only, 1 compute only, 2 register ring (PD), 3 LDS-DMA ring (PD = slots in flight)
 template <int MODE, int PD>
 __global__ __launch_bounds__(512, 1) void ring_kernel(const unsigned char* base, const __half* xsrc, float* out, int dump) {
@@ -148,6 +207,15 @@ __global__ __launch_bounds__(512, 1) void ring_kernel(const unsigned char* base,
   for (int i = tid; i < kXBytes / 16; i += 512)
     reinterpret_cast<uint4*>(xs)[i] = reinterpret_cast<const uint4*>(xsrc)[i];
   __syncthreads();
+  if constexpr (MODE == 8) {
+    const int r16 = lane & 15, kq = lane >> 4;
+    f4_t acc = {0.f, 0.f, 0.f, 0.f}, acc2 = acc;
+    engine_body<PD>(base, smem, xs + r16 * 512, blk, wave, lane, r16, kq, acc, acc2);
+    acc += acc2;
+    if (dump == 1 && wave < kWavesBusy) reinterpret_cast<f4_t*>(out)[blk * 512 + tid] = acc;
+    else if (acc[0] == 1.2345f) out[blk * 512 + tid] = acc[1] + acc[2] + acc[3];
+    return;
+  }
   if (wave >= kWavesBusy) return;
   const int tile = blk * kWavesBusy + wave, r16 = lane & 15, kq = lane >> 4;
   const unsigned char* tp = base + (size_t)tile * kSteps * kSB;
@@ -168,6 +236,71 @@ __global__ __launch_bounds__(512, 1) void ring_kernel(const unsigned char* base,
       for (int h = 0; h < 2; ++h) fold ^= b[h].q.x ^ b[h].q.y ^ b[h].q.z ^ b[h].q.w ^ b[h].m.x ^ b[h].m.y;
     }
     acc[0] = (float)fold;
+  } else if constexpr (MODE == 7) {  // stream, plain global loads (stream_bench.hip's form)
+    constexpr int R = PD + 1;
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    u4 bq[R][2];
+    unsigned fold = 0;
+    auto gl = [&](int s2, int r) {
+      const unsigned char* p = tp + (size_t)s2 * kSB;
+      bq[r][0] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p + lane * 16));
+      bq[r][1] = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p + 1024 + lane * 16));
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) gl(p, p);
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      if (s + PD < kSteps) gl(s + PD, (s + PD) % R);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) fold ^= bq[s % R][h].x ^ bq[s % R][h].y ^ bq[s % R][h].z ^ bq[s % R][h].w;
+    }
+    acc[0] = (float)fold;
+  } else if constexpr (MODE == 9) {  // register ring PD over a step-major layout [step][tile]
+    constexpr int R = PD + 1;
+    Raw buf[R][2];
+    const auto rb = rsrc(base);  // (kernel argument: uniform, no waterfall)
+    const int vt = tile * kSB;   // the wave's tile inside a step band
+    auto ld = [&](Raw* w, int s2) {
+      const int so = s2 * kTiles * kSB;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rb, vt + lane * 16, so + h * 1024, 2));
+        w[h].q = make_int4(t.x, t.y, t.z, t.w);
+        const v2i_t u = __builtin_bit_cast(v2i_t, __builtin_amdgcn_raw_buffer_load_b64(rb, vt + r16 * 32 + 8 * (kq >> 1), so + 2048 + 16 * h, 0));
+        w[h].m = make_uint2((unsigned)u.x, (unsigned)u.y);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) ld(buf[p], p);
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      ld(buf[(s + PD) % R], s + PD < kSteps ? s + PD : 0);
+      __builtin_amdgcn_sched_barrier(0);
+      step_compute(buf[s % R], s, kq, xrow, acc, acc2);
+    }
+  } else if constexpr (MODE == 10) {  // MODE 2 without the waterfall: buffer resource over the kernel argument
+    constexpr int R = PD + 1;
+    Raw buf[R][2];
+    const auto rb = rsrc(base);
+    const int vt = tile * kSteps * kSB;
+    auto ld = [&](Raw* w, int s2) {
+      const int so = s2 * kSB;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rb, vt + lane * 16, so + h * 1024, 2));
+        w[h].q = make_int4(t.x, t.y, t.z, t.w);
+        const v2i_t u = __builtin_bit_cast(v2i_t, __builtin_amdgcn_raw_buffer_load_b64(rb, vt + r16 * 32 + 8 * (kq >> 1), so + 2048 + 16 * h, 0));
+        w[h].m = make_uint2((unsigned)u.x, (unsigned)u.y);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < PD; ++p) ld(buf[p], p);
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      ld(buf[(s + PD) % R], s + PD < kSteps ? s + PD : 0);
+      __builtin_amdgcn_sched_barrier(0);
+      step_compute(buf[s % R], s, kq, xrow, acc, acc2);
+    }
   } else if constexpr (MODE == 4) {  // register ring PD, half the dequantisation (chunk 0's fragments for both)
     constexpr int R = PD + 1;
     Raw buf[R][2];
@@ -193,6 +326,25 @@ __global__ __launch_bounds__(512, 1) void ring_kernel(const unsigned char* base,
       }
       step_compute(w, s, kq, xrow, acc, acc2);
     }
+  } else if constexpr (MODE == 6) {  // MODE 2 with per-step s_memtime stamps (out: [wave][34] u64)
+    constexpr int R = PD + 1;
+    Raw buf[R][2];
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(out) + (size_t)(blk * kWavesBusy + wave) * 34;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+    for (int p = 0; p < PD; ++p) rload(buf[p], rs, p * kSB, lane, r16, kq);
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+      rload(buf[(s + PD) % R], rs, (s + PD < kSteps ? s + PD : 0) * kSB, lane, r16, kq);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * PD) : "memory");
+      const unsigned long long tw = __builtin_amdgcn_s_memtime();
+      step_compute(buf[s % R], s, kq, xrow, acc, acc2);
+      asm volatile("s_nop 0" ::"v"(acc[0]), "v"(acc2[0]));
+      const unsigned long long tc = __builtin_amdgcn_s_memtime();
+      if (lane == 0 && dump == 2) { st[2 + 2 * s] = tw - t0; st[3 + 2 * s] = tc - t0; }
+    }
+    if (lane == 0 && dump == 2) { st[0] = t0; st[1] = __builtin_amdgcn_s_memtime() - t0; }
   } else if constexpr (MODE == 2) {
     constexpr int R = PD + 1;
     Raw buf[R][2];
@@ -226,8 +378,15 @@ __global__ __launch_bounds__(512, 1) void ring_kernel(const unsigned char* base,
     vm_wait<0>();
   }
   acc += acc2;
-  if (dump) reinterpret_cast<f4_t*>(out)[blk * 512 + tid] = acc;
+  if (dump == 1) reinterpret_cast<f4_t*>(out)[blk * 512 + tid] = acc;  // (dump 2: out holds the stamps only)
   else if (acc[0] == 1.2345f) out[blk * 512 + tid] = acc[1] + acc[2] + acc[3];
+}
+
+// (at least 81 KB, as the production launchers request: one block per CU, so every CU runs one
+// block of 7 busy waves - with 16 KB the dispatcher may pack several blocks onto one CU)
+static constexpr size_t lds_of(int mode, int pd) {
+  const size_t need = kXBytes + (mode == 3 || mode == 8 ? (size_t)kWavesBusy * (pd + 1) * kSB : 0);
+  return need > 83 * 1024 ? need : 83 * 1024;
 }
 
 // MODE 5: 16 waves per CU (1024 threads), two waves per tile (8 steps each), register ring PD
@@ -264,11 +423,13 @@ static double run16(const unsigned char* buf, size_t region, int nreg, const __h
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < nreg; ++i) hipLaunchKernelGGL((ring16_kernel<PD>), dim3(kBlocks), dim3(1024), kXBytes, st, buf + i * region, x, out, 0);
+  const size_t lds = lds_of(2, PD);
+  CK(hipFuncSetAttribute((const void*)ring16_kernel<PD>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  for (int i = 0; i < nreg; ++i) hipLaunchKernelGGL((ring16_kernel<PD>), dim3(kBlocks), dim3(1024), lds, st, buf + i * region, x, out, 0);
   CK(hipStreamSynchronize(st));
   CK(hipEventRecord(e0, st));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL((ring16_kernel<PD>), dim3(kBlocks), dim3(1024), kXBytes, st, buf + (i % nreg) * region, x, out, 0);
+    hipLaunchKernelGGL((ring16_kernel<PD>), dim3(kBlocks), dim3(1024), lds, st, buf + (i % nreg) * region, x, out, 0);
   CK(hipEventRecord(e1, st));
   CK(hipEventSynchronize(e1));
   CK(hipGetLastError());
@@ -277,7 +438,6 @@ static double run16(const unsigned char* buf, size_t region, int nreg, const __h
   return ms * 1e3 / iters;
 }
 
-static constexpr size_t lds_of(int mode, int pd) { return kXBytes + (mode == 3 ? (size_t)kWavesBusy * (pd + 1) * kSB : 0); }
 
 template <int MODE, int PD>
 static double run(const unsigned char* buf, size_t region, int nreg, const __half* x, float* out, hipStream_t st, int iters) {
@@ -340,10 +500,11 @@ static double run_concurrent(const unsigned char* buf, size_t region, int nreg, 
   return ms * 1e3 / iters;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const bool memset_init = argc > 1 && argv[1][0] == 'm';
   const size_t bytes = (size_t)kTiles * kSteps * kSB;
   const size_t region = (bytes + 4095) / 4096 * 4096;
-  const int nreg = 20;
+  const int nreg = argc > 2 ? atoi(argv[2]) : 20;
   unsigned char* buf;
   __half* x;
   float* out;
@@ -363,6 +524,10 @@ int main() {
       if (off >= 2048) h[i] &= 0x3BFF3BFFu;
     }
     CK(hipMemcpy(buf, h.data(), region * nreg, hipMemcpyHostToDevice));
+    if (memset_init) {  // A/B: a constant fill (as tools/stream_bench.hip)
+      CK(hipMemset(buf, 0x5a, region * nreg));
+      printf("buffer: memset 0x5a\n");
+    }
     std::vector<unsigned short> hx(kXBytes / 2);
     for (auto& v : hx) {
       s = s * 1664525u + 1013904223u;
@@ -376,9 +541,10 @@ int main() {
     float* out4;
     CK(hipMalloc(&out4, (size_t)kBlocks * 512 * 16));
     const std::vector<float> a = dump<2, 2>(buf, x, out4, st);
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < 5; ++v) {
       const std::vector<float> b = v == 0 ? dump<3, 2>(buf, x, out4, st) : v == 1 ? dump<3, 4>(buf, x, out4, st)
-                                                                                   : dump<2, 4>(buf, x, out4, st);
+                                   : v == 2 ? dump<2, 4>(buf, x, out4, st) : v == 3 ? dump<8, 2>(buf, x, out4, st)
+                                                                                    : dump<8, 4>(buf, x, out4, st);
       double md = 0, mx = 0;
       size_t nan = 0;
       for (size_t i = 0; i < a.size(); ++i) {
@@ -387,13 +553,74 @@ int main() {
         mx = std::max(mx, (double)std::abs(a[i]));
       }
       printf("check %s vs reg PD2: max |diff| %.3g of max |acc| %.3g, nan %zu\n",
-             v == 0 ? "dma D2" : v == 1 ? "dma D4" : "reg PD4", md, mx, nan);
+             v == 0 ? "dma D2" : v == 1 ? "dma D4" : v == 2 ? "reg PD4" : v == 3 ? "engine D2" : "engine D4", md, mx, nan);
+    }
+    {  // the stream variants really read every word: their folds against the host's
+      const std::vector<float> s0 = dump<0, 2>(buf, x, out4, st);
+      std::vector<unsigned> hb(kSteps * kSB / 4);
+      CK(hipMemcpy(hb.data(), buf, hb.size() * 4, hipMemcpyDeviceToHost));  // tile 0 (block 0, wave 0)
+      // lane 0: q words at [s][h*1024 + 0..15], m words at [s][2048 + 8*(2h)] (r16 = 0, kq = 0)
+      unsigned f = 0;
+      for (int st2 = 0; st2 < kSteps; ++st2)
+        for (int h = 0; h < 2; ++h) {
+          const unsigned* q = &hb[(st2 * kSB + h * 1024) / 4];
+          const unsigned* m = &hb[(st2 * kSB + 2048 + 16 * h) / 4];
+          f ^= q[0] ^ q[1] ^ q[2] ^ q[3] ^ m[0] ^ m[1];
+        }
+      printf("check stream fold: device %.6g host %.6g\n", s0[0], (double)(float)f);
     }
     CK(hipFree(out4));
   }
   float* out16;
   CK(hipMalloc(&out16, kBlocks * 1024 * 4));
-  const int iters = 60;
+  {  // per-step stamps of the register ring (MODE 6): where a wave's time goes
+    unsigned long long* stamps;
+    const size_t n = (size_t)kBlocks * kWavesBusy * 34;
+    CK(hipMalloc(&stamps, n * 8));
+    CK(hipFuncSetAttribute((const void*)ring_kernel<6, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(6, 2)));
+    for (int rep = 0; rep < 4; ++rep) {
+      hipLaunchKernelGGL((ring_kernel<6, 2>), dim3(kBlocks), dim3(512), lds_of(6, 2), st, buf + (size_t)(rep % nreg) * region, x,
+                         (float*)stamps, 2);
+      CK(hipStreamSynchronize(st));
+    }
+    std::vector<unsigned long long> h(n);
+    CK(hipMemcpy(h.data(), stamps, n * 8, hipMemcpyDeviceToHost));
+    unsigned long long tmin = ~0ull, tmax = 0;
+    double wait[kSteps] = {0}, comp[kSteps] = {0}, life = 0;
+    const int nw = kBlocks * kWavesBusy;
+    for (int w = 0; w < nw; ++w) {
+      const unsigned long long* r = &h[(size_t)w * 34];
+      tmin = std::min(tmin, r[0]);
+      tmax = std::max(tmax, r[0] + r[1]);
+      life += r[1];
+      unsigned long long prev = 0;
+      for (int s2 = 0; s2 < kSteps; ++s2) {
+        wait[s2] += (double)(r[2 + 2 * s2] - prev);
+        comp[s2] += (double)(r[3 + 2 * s2] - r[2 + 2 * s2]);
+        prev = r[3 + 2 * s2];
+      }
+    }
+    printf("stamps (s_memtime ticks = 100 MHz? see below): wave life avg %.0f, first-start..last-end %llu\n", life / nw, tmax - tmin);
+    for (int s2 = 0; s2 < kSteps; ++s2) printf("  step %2d: wait %7.1f  compute %7.1f\n", s2, wait[s2] / nw, comp[s2] / nw);
+    CK(hipFree(stamps));
+  }
+  const int iters = argc > 3 ? atoi(argv[3]) : 60;
+  {  // one stream launch alone, timed by its own events, on a region no launch touched yet
+    hipEvent_t a0, a1;
+    CK(hipEventCreate(&a0));
+    CK(hipEventCreate(&a1));
+    CK(hipFuncSetAttribute((const void*)ring_kernel<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_of(0, 2)));
+    for (int r = nreg - 3; r < nreg; ++r) {
+      CK(hipStreamSynchronize(st));
+      CK(hipEventRecord(a0, st));
+      hipLaunchKernelGGL((ring_kernel<0, 2>), dim3(kBlocks), dim3(512), lds_of(0, 2), st, buf + (size_t)r * region, x, out, 0);
+      CK(hipEventRecord(a1, st));
+      CK(hipEventSynchronize(a1));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, a0, a1));
+      printf("single cold stream launch (region %d): %.2f us\n", r, ms * 1e3);
+    }
+  }
   auto rep = [&](const char* name, double us) {
     printf("%-22s %8.2f us  %6.2f TB/s\n", name, us, bytes / us * 1e-6);
     fflush(stdout);
@@ -401,8 +628,13 @@ int main() {
   for (int rnd = 0; rnd < 2; ++rnd) {
     printf("-- round %d (%.1f MB per launch)\n", rnd, bytes * 1e-6);
     rep("stream PD2", run<0, 2>(buf, region, nreg, x, out, st, iters));
+    rep("stream global PD2", run<7, 2>(buf, region, nreg, x, out, st, iters));
     rep("compute only", run<1, 2>(buf, region, nreg, x, out, st, iters));
     rep("reg PD2", run<2, 2>(buf, region, nreg, x, out, st, iters));
+    rep("reg PD2 no waterfall", run<10, 2>(buf, region, nreg, x, out, st, iters));
+    rep("reg PD3 no waterfall", run<10, 3>(buf, region, nreg, x, out, st, iters));
+    rep("step-major reg PD2", run<9, 2>(buf, region, nreg, x, out, st, iters));
+    rep("step-major reg PD3", run<9, 3>(buf, region, nreg, x, out, st, iters));
     {
       hipStream_t st2;
       CK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
@@ -415,13 +647,13 @@ int main() {
     }
     rep("reg PD2 half dequant", run<4, 2>(buf, region, nreg, x, out, st, iters));
     rep("16 waves reg PD2", run16<2>(buf, region, nreg, x, (float*)nullptr == nullptr ? out16 : out16, st, iters));
-    rep("16 waves reg PD3", run16<3>(buf, region, nreg, x, out16, st, iters));
     rep("reg PD3", run<2, 3>(buf, region, nreg, x, out, st, iters));
     rep("reg PD4", run<2, 4>(buf, region, nreg, x, out, st, iters));
+    rep("engine D2", run<8, 2>(buf, region, nreg, x, out, st, iters));
+    rep("engine D3", run<8, 3>(buf, region, nreg, x, out, st, iters));
     rep("dma D2", run<3, 2>(buf, region, nreg, x, out, st, iters));
     rep("dma D3", run<3, 3>(buf, region, nreg, x, out, st, iters));
     rep("dma D4", run<3, 4>(buf, region, nreg, x, out, st, iters));
-    rep("dma D6", run<3, 6>(buf, region, nreg, x, out, st, iters));
   }
   CK(hipFree(buf));
   CK(hipFree(x));
