@@ -272,7 +272,11 @@ def run_tp_pass(cmd: list, json_out: str, timeout_s: float, heartbeat_s: float =
         tail = ""
         try:
             with open(log_path, errors="replace") as f:
-                tail = f.read()[-2000:]
+                text = f.read()
+            # the ranks' own errors first (torchrun's summary traceback fills the tail)
+            errs = [l for l in text.splitlines() if ("Error" in l or "error" in l or "Exception" in l)
+                    and "torch/distributed" not in l and "elastic" not in l][:12]
+            tail = "\n".join(errs) + "\n...\n" + text[-1500:]
         except OSError:
             pass
         return {"ok": False, "error": f"{type(e).__name__}: {e}", "wall_s": round(time.time() - t0, 1),
