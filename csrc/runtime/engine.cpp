@@ -335,6 +335,7 @@ void Engine::alloc_buffers() {
   // by every decode step's embedding launch
   if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
   if (const char* e = std::getenv("LFK_MOE_ROUTE_FUSE")) moe_route_fuse_ = e[0] != '0';  // A/B (test_engine_gpu)
+  if (const char* e = std::getenv("LFK_TP_EPILOGUE")) tp_epi_ = e[0] != '0';  // A/B: the separate collective kernel
   if (wo_fuse_ && nkv_l_ <= 64) {
     HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
     *wo_err_h_ = 0;
@@ -603,11 +604,16 @@ void Engine::p2p_open(const std::vector<std::string>& handles) {
 // Decode GEMVs under TP: the row-parallel all-reduce in the epilogue (GemvArgs::tp_*) when the
 // P2P regions carry the fused area (one launch per projection instead of two, no tmp_ copy)
 bool Engine::tp_epilogue(GemvArgs& g) const {
-  if (!p2p_ || !p2p_->ready() || p2p_->fused_n() < hp_.n_embd || g.n_out > p2p_->fused_n()) return false;
+  if (!tp_epi_ || !p2p_ || !p2p_->ready() || p2p_->fused_n() < hp_.n_embd || g.n_out > p2p_->fused_n()) return false;
   // more than two ranks on ONE GPU (the eight-rank rehearsal): a waiting epilogue needs every
   // peer's GEMV resident at once, and eight single-queue processes are not reliably co-scheduled
   // (runs of 15 s to > 170 s, r4) - the separate collective kernel's short waits are
   if (p2p_->shared_device() && p2p_->world() > 2) return false;
+  // ... and two ranks on ONE GPU at the 70B width: the 2-rank 70B rehearsal's epilogue waits timed
+  // out (a rank's spinning waves and its peer's grids did not co-schedule; profiles/README.md,
+  // round 6), while the collective kernel's path ran it to the end. One process per GPU - every
+  // real deployment - has no co-scheduling requirement and keeps the epilogue.
+  if (p2p_->shared_device() && hp_.n_embd > 4096) return false;
   g.tp_peers = p2p_->peers();
   g.tp_world = p2p_->world(); g.tp_rank = p2p_->rank();
   g.tp_stride = p2p_->stride(); g.tp_off = p2p_->fused_offset();
