@@ -489,16 +489,25 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
   m.def("gemm_t16", [](uintptr_t w, int type, int rows, int K, uintptr_t x, int T, uintptr_t out, int ldo,
-                       uintptr_t out_h, int ldh, int epi, uintptr_t stream, uintptr_t resid, int cfg) {
+                       uintptr_t out_h, int ldh, int epi, uintptr_t stream, uintptr_t resid, int cfg,
+                       std::vector<std::pair<uintptr_t, int>> wseg) {
     GemmT16Args a;
     a.w = make_qmat(P<void>(w), type, rows, K);
     a.x = P<__half>(x); a.T = T; a.out = P<float>(out); a.ldo = ldo; a.resid = P<float>(resid);
     a.out_h = P<__half>(out_h); a.ldh = ldh; a.cfg = cfg;
+    if (!wseg.empty()) {  // stacked matrices: (tile16 base, rows) per segment, the first = w
+      if (wseg.size() > 3) throw std::runtime_error("gemm_t16: at most 3 segments");
+      a.nwseg = (int)wseg.size();
+      for (int i = 0; i < a.nwseg; ++i) {
+        a.wseg_base[i] = P<uint8_t>(wseg[i].first);
+        a.wseg_tiles[i] = wseg[i].second / 16;
+      }
+    }
     gemm_t16(a, epi, S(stream));
     hip_ok("gemm_t16");
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
      py::arg("ldo"), py::arg("out_h"), py::arg("ldh"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0,
-     py::arg("cfg") = 0);
+     py::arg("cfg") = 0, py::arg("wseg") = std::vector<std::pair<uintptr_t, int>>{});
 
   m.def("attn_decode", [](uintptr_t q, uintptr_t kc, uintptr_t vc, uintptr_t pos, int n_ctx, int n_head, int n_kv,
                           int hd, float scale, uintptr_t part, uintptr_t out, uintptr_t stream, uintptr_t counters,

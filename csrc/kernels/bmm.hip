@@ -1980,7 +1980,13 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
 // Epilogues: STORE (+ resid), ADD (residual in place), SWIGLU (the tile16 SwiGLU copy's tile =
 // 8 gate + 8 up rows of the same features: lane kq < 2 takes up from lane + 32 and writes
 // silu(g) * u as f16 in the 4-group k order - the next gemm_t16's X).
-static constexpr int kT16Pitch = 128 + 8;  // halves per staged token row (16-B pad: conflict-free b128 reads)
+// Staged X rows are 128 halves (no pad) with their 16-B units XOR-swizzled by the token's row in
+// its 16-row group (unit u of row r at u ^ (r & 15)): ds_read_b128 serves a wave in lane groups
+// {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, ... - two kq values x 8 token rows per group - and
+// no uniform pitch keeps those 16 lanes apart (136 halves: 2-way, measured 2.1 conflict cycles
+// per LDS instruction); the swizzle makes them conflict-free for the Q4_K / Q5_K / Q6_K runs
+// (Q8_0's stay 2-way).
+static constexpr int kT16Pitch = 128;
 
 template <int QT, int EPI, int TM, int NWV>
 __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
@@ -2007,8 +2013,21 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   if (sb >= se) return;  // whole block, before any barrier
   const int nh = 2 * (se - sb);
   const size_t tstride = a.tile_stride ? a.tile_stride : (size_t)steps * SB;
-  const uint8_t* wt0 = a.w.base + (size_t)min(tile0, ntiles - 1) * tstride + (size_t)a.step0 * SB;
-  const uint8_t* wt1 = a.w.base + (size_t)min(tile0 + 1, ntiles - 1) * tstride + (size_t)a.step0 * SB;
+  auto tile_base = [&](int t) __attribute__((always_inline)) {  // (stacked segments: Q|K|V)
+    t = min(t, ntiles - 1);
+    const uint8_t* b = a.w.base;
+    if (a.nwseg > 1 && t >= a.wseg_tiles[0]) {
+      t -= a.wseg_tiles[0];
+      b = a.wseg_base[1];
+      if (a.nwseg > 2 && t >= a.wseg_tiles[1]) {
+        t -= a.wseg_tiles[1];
+        b = a.wseg_base[2];
+      }
+    }
+    return b + (size_t)t * tstride + (size_t)a.step0 * SB;
+  };
+  const uint8_t* wt0 = tile_base(tile0);
+  const uint8_t* wt1 = tile_base(tile0 + 1);
   f4_t acc[2][NG];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -2032,8 +2051,8 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     if constexpr (XL > 5) x5 = *reinterpret_cast<const uint4*>(xrow[XL > 5 ? 5 : 0] + k0);
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
-    __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * (tid & 15)];
-    constexpr int J = (NT / 16) * kT16Pitch;  // piece j + 1 is NT / 16 tokens further
+    __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * ((tid & 15) ^ ((tid >> 4) & 15))];
+    constexpr int J = (NT / 16) * kT16Pitch;  // piece j + 1 is NT / 16 tokens further (same swizzle)
     *reinterpret_cast<uint4*>(d) = x0;
     *reinterpret_cast<uint4*>(d + J) = x1;
     if constexpr (XL > 2) *reinterpret_cast<uint4*>(d + 2 * J) = x2;
@@ -2061,7 +2080,8 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const uint4 bv = *reinterpret_cast<const uint4*>(xb + g * 16 * kT16Pitch + (m < 2 ? off_lo : off_hi) + 8 * (m & 1));
+        const int u = (((m < 2 ? off_lo : off_hi) >> 3) + (m & 1)) ^ r16;  // swizzled 16-B unit
+        const uint4 bv = *reinterpret_cast<const uint4*>(xb + g * 16 * kT16Pitch + 8 * u);
         const int dw = 2 * (m & 1), sh = (m >> 1) * 2;
         const uint4 a0 = make_uint4(F0.w[4 * dw + sh], F0.w[4 * dw + sh + 1], F0.w[4 * dw + 4 + sh], F0.w[4 * dw + 5 + sh]);
         const uint4 a1 = make_uint4(F1.w[4 * dw + sh], F1.w[4 * dw + sh + 1], F1.w[4 * dw + 4 + sh], F1.w[4 * dw + 5 + sh]);
@@ -2159,9 +2179,15 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
     tm = rows >= 2048 ? 128 : 64;
   }
   const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm, gy_busy = (rows + tm - 1) / tm;
+  // split-K (partials by atomic add) only for long K, up to two resident rounds: at K = 4096 the
+  // atomics cost more than the idle CUs (Q / Wo at T = 387: 57 us split in 2 vs 37 us whole at
+  // T = 512), at K = 14336 the second wave per SIMD pays (down: 115 us split in 2 at T = 387 vs
+  // 152 us whole at T = 512; profiles/README.md, round 6); tiny grids (a lone K / V) still split
   int split = 1;
   if (EPI != GEMM_SWIGLU)
-    while (gx * gy_busy * split < cus && steps / (split * 2) >= 2) split *= 2;
+    while (steps / (split * 2) >= 2 &&
+           ((steps / (split * 2) >= 12 && gx * gy_busy * split * 2 <= 2 * cus) || gx * gy_busy * split * 4 <= cus))
+      split *= 2;
   const int spz = (steps + split - 1) / split;
   split = (steps + spz - 1) / spz;  // no empty parts
   if (a.seg_dev && split > 1 && EPI != GEMM_STORE) throw std::runtime_error("gemm_t16: grouped split-K needs STORE");
@@ -2190,6 +2216,16 @@ void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s) {
   if (a.T <= 0) return;
   if (!bmm_supported(a.w.type, a.w.K) || !a.w.base || !a.x) throw std::runtime_error("gemm_t16: unsupported type / K");
   if (a.w.rows % 16) throw std::runtime_error("gemm_t16: rows must be a multiple of 16");
+  if (a.nwseg < 1 || a.nwseg > 3) throw std::runtime_error("gemm_t16: 1-3 stacked segments");
+  if (a.nwseg > 1) {
+    int t = a.wseg_tiles[0];
+    for (int i = 1; i < a.nwseg; ++i) {
+      if (!a.wseg_base[i] || a.wseg_tiles[i] < 1) throw std::runtime_error("gemm_t16: stacked segment");
+      t += a.wseg_tiles[i];
+    }
+    if (a.wseg_tiles[0] < 1 || t * 16 != a.w.rows || a.tile_stride || a.step0 || a.seg_dev)
+      throw std::runtime_error("gemm_t16: stacked segments must cover the rows (plain matrices)");
+  }
   if (epi == GEMM_SWIGLU) {
     if (!a.out_h || a.ldh % 4 || a.ldh < a.w.rows / 2) throw std::runtime_error("gemm_t16: SwiGLU output");
   } else if (!a.out || a.ldo % 4 || a.ldo < a.w.rows || (a.resid && epi != GEMM_STORE)) {

@@ -450,6 +450,12 @@ struct GemmT16Args {
   size_t tile_stride = 0;
   int step0 = 0;
   int cfg = 0;                     // block shape pin (waves * 1000 + tokens; tuning tools), 0: the measured rule
+  // stacked matrices (Q|K|V in one launch): w.rows = every segment's rows, tiles [0, wseg_tiles[0])
+  // from w.base, the next wseg_tiles[1] from wseg_base[1], the rest from wseg_base[2]; one type and
+  // K; output column = stacked row (the segments' outputs adjacent in `out`)
+  int nwseg = 1;
+  const uint8_t* wseg_base[3] = {nullptr, nullptr, nullptr};
+  int wseg_tiles[3] = {0, 0, 0};
 };
 void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s);
 

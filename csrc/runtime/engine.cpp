@@ -868,9 +868,24 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
     if (t16) {
       GemmT16Args g;
       g.x = xh16; g.T = T; g.ldo = ncol; g.out_zeroed = true;
-      g.w = L.t_wq; g.out = qkv_; gemm_t16(g, GEMM_STORE, s);
-      g.w = L.t_wk; g.out = qkv_ + nq_; gemm_t16(g, GEMM_STORE, s);
-      g.w = L.t_wv; g.out = qkv_ + nq_ + nkvd_; gemm_t16(g, GEMM_STORE, s);
+      // Q|K|V stacked into one launch per run of equal weight type (their outputs are adjacent
+      // columns of qkv_): one grid of 384 blocks at d = 4096 instead of three narrow ones
+      const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
+      float* o[3] = {qkv_, qkv_ + nq_, qkv_ + nq_ + nkvd_};
+      for (int i = 0; i < 3;) {
+        int j = i + 1;
+        while (j < 3 && m[j]->type == m[i]->type && m[j]->K == m[i]->K) ++j;
+        g.w = *m[i]; g.out = o[i];
+        g.nwseg = j - i;
+        g.wseg_tiles[0] = m[i]->rows / 16;
+        for (int k = 1; k < g.nwseg; ++k) {
+          g.wseg_base[k] = m[i + k]->base;
+          g.wseg_tiles[k] = m[i + k]->rows / 16;
+          g.w.rows += m[i + k]->rows;
+        }
+        gemm_t16(g, GEMM_STORE, s);
+        i = j;
+      }
     } else {
       GemmArgs g;
       g.x = xb_; g.T = T; g.ldo = ncol; g.out_zeroed = true;

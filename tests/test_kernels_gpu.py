@@ -792,6 +792,38 @@ def test_gemm_t16_vs_fp32(torch, t, T, R, K):
     assert torch.equal(acc[:, R:], base[:, R:])
 
 
+@pytest.mark.parametrize("t,T", [(GGMLType.Q4_K, 387), (GGMLType.Q4_K, 17), (GGMLType.Q6_K, 130)])
+def test_gemm_t16_stacked_qkv(torch, t, T):
+    """Q|K|V in ONE prefill launch (GemmT16Args::wseg_*): three separately repacked tile16 copies
+    (4096 / 1024 / 1024 rows) stacked by tile range, their outputs adjacent columns of one [T][ncol]
+    buffer, against the fp64 products of each matrix."""
+    rng = np.random.default_rng(T + int(t))
+    K, rows = 4096, [4096, 1024, 1024]
+    Ws, tws = [], []
+    for R in rows:
+        raw, W = make_matrix(t, R, K, rng)
+        dw = dev_bytes(to_planar(t, raw, R, K))
+        tw = torch.empty(hip().t16_bytes(int(t), R, K), dtype=torch.uint8, device="cuda")
+        hip().t16_repack(dw.data_ptr(), int(t), R, K, tw.data_ptr(), stream())
+        Ws.append(W)
+        tws.append(tw)
+    Xh = rng.standard_normal((T, K)).astype(np.float16)
+    dx = torch.from_numpy(_swizzle4(Xh)).cuda()
+    ncol = sum(rows)
+    ldo = ncol + 4
+    out = torch.full((T, ldo), 3.0, device="cuda")
+    hip().gemm_t16(tws[0].data_ptr(), int(t), ncol, K, dx.data_ptr(), T, out.data_ptr(), ldo, 0, 0, 0, stream(),
+                   wseg=[(tw.data_ptr(), R) for tw, R in zip(tws, rows)])
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    c = 0
+    for W, R in zip(Ws, rows):
+        ref = Xh.astype(np.float64) @ W.astype(np.float64).T
+        assert rel_err(got[:, c:c + R], ref) < 2e-3, (c, rel_err(got[:, c:c + R], ref))
+        c += R
+    assert np.all(got[:, ncol:] == 3.0)
+
+
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
 @pytest.mark.parametrize("T,F,K", [(40, 96, 2048), (200, 256, 4096), (129, 1792, 1024)])
 def test_gemm_t16_swiglu_vs_fp32(torch, t, T, F, K):

@@ -70,6 +70,7 @@ for s in "$@"; do
     mixprof) export TMPDIR=/tmp; step genmx 900 python tools/gen_model.py mixtral-8x7b-q4_k_m
              prof mixprof 300 tools/decode_bench.py --model mixtral-8x7b-q4_k_m --steps 32 --no-graph
              python3 tools/prof_summary.py gpurun_out/mixprof/k_kernel_stats.csv > gpurun_out/mixprof_summary.md
+             python3 tools/kernel_by_pred.py gpurun_out/mixprof/k_kernel_trace.csv > gpurun_out/mixprof_by_pred.md
              prof mixbprof 300 tools/batch_bench.py --model mixtral-8x7b-q4_k_m --batches 6 --steps 16
              python3 tools/step_kernels.py gpurun_out/mixbprof/k_kernel_trace.csv > gpurun_out/mixbprof_kernels.txt ;;
     tp8bench70) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
@@ -82,10 +83,14 @@ for s in "$@"; do
               python3 tools/step_slots.py gpurun_out/stepprof/k_kernel_trace.csv >> gpurun_out/stepprof_kernels.txt ;;
     dec70prof) step gen70 900 python tools/gen_model.py llama3-70b-q4_k_m
                prof dec70prof 400 tools/decode_bench.py --model llama3-70b-q4_k_m --steps 16 --no-graph
-               python3 tools/prof_summary.py gpurun_out/dec70prof/k_kernel_stats.csv > gpurun_out/dec70prof_summary.md ;;
+               python3 tools/prof_summary.py gpurun_out/dec70prof/k_kernel_stats.csv > gpurun_out/dec70prof_summary.md
+               python3 tools/kernel_by_pred.py gpurun_out/dec70prof/k_kernel_trace.csv > gpurun_out/dec70prof_by_pred.md ;;
     decprof) prof decprof 300 tools/decode_bench.py --steps 64 --no-graph
              python3 tools/prof_summary.py gpurun_out/decprof/k_kernel_stats.csv > gpurun_out/decprof_summary.md ;;
     prefprof) prof prefprof 300 tools/decode_bench.py --prompt 512 --steps 8 --slots 2 ;;
+    # the bench's admission prefill (7-slot engine): 387-token prompts alone, then 6 jointly
+    admprof) prof admprof 300 tools/prefill_bench.py --T 387 --reps 4 --joint 6
+             python3 tools/kernel_by_pred.py gpurun_out/admprof/k_kernel_trace.csv --min-calls 4 --grid > gpurun_out/admprof_by_pred.md ;;
     bmmpmc) pmc bmmpmc tools/batch_bench.py --batches 6 --steps 4 ;;
     t16pmc) pmc t16pmc tools/gemm_bench.py --eager --reps 5 --T 512 --t16 ;;
     # the wave-owned projections by part (full / weights + MFMA / weights only), counters per kernel
