@@ -488,6 +488,32 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
+  // layer split (split_mode=layer): the whole generation over a chain of stage engines, natively
+  m.def("chain_generate",
+        [](std::vector<Engine*> stages, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,
+           const std::vector<int>& stop_ids, py::object poll, py::object on_token) {
+          const SamplingOpts o = sampling_opts(sp);
+          std::function<bool()> pf;
+          std::function<void(int)> tf;
+          if (!poll.is_none()) pf = [poll]() { py::gil_scoped_acquire g; return poll().cast<bool>(); };
+          if (!on_token.is_none()) tf = [on_token](int t) { py::gil_scoped_acquire g; on_token(t); };
+          GenOut r;
+          {
+            py::gil_scoped_release nogil;
+            r = Engine::chain_generate(stages, prompt, n_keep, max_new, o, stop_ids, pf, tf);
+          }
+          py::dict d;
+          d["tokens"] = r.tokens;
+          d["finish"] = r.finish;
+          d["n_evaluated"] = r.n_evaluated;
+          d["n_prefilled"] = r.n_prefilled;
+          d["prefill_s"] = r.prefill_s;
+          d["decode_s"] = r.decode_s;
+          return d;
+        },
+        py::arg("stages"), py::arg("prompt"), py::arg("n_keep"), py::arg("max_new"), py::arg("sampling"),
+        py::arg("stop_ids"), py::arg("poll") = py::none(), py::arg("on_token") = py::none());
+
   m.def("gemm_t16", [](uintptr_t w, int type, int rows, int K, uintptr_t x, int T, uintptr_t out, int ldo,
                        uintptr_t out_h, int ldh, int epi, uintptr_t stream, uintptr_t resid, int cfg,
                        std::vector<std::pair<uintptr_t, int>> wseg) {

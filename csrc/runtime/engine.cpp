@@ -181,6 +181,9 @@ Engine::~Engine() {
   }
   if (graph_exec_) hipGraphExecDestroy(graph_exec_);
   if (graph_exec2_) hipGraphExecDestroy(graph_exec2_);
+  for (hipGraphExec_t g : chain_graph_)
+    if (g) hipGraphExecDestroy(g);
+  if (chain_ev_) hipEventDestroy(chain_ev_);
   for (size_t i = 1; i < sgraph_.size(); ++i)
     if (sgraph_[i]) hipGraphExecDestroy(sgraph_[i]);
   for (size_t i = 1; i < sgraph2_.size(); ++i)
@@ -2028,6 +2031,152 @@ GenOut Engine::generate(const std::vector<int>& prompt, int n_keep, int max_new,
   out.n_evaluated = n_prompt + (int)out.tokens.size() - 1;
   return out;
 }
+
+// ------------------------------------------------------------------ layer-split chain
+void Engine::enqueue_stage_decode(hipStream_t s) {
+  int* st = state_ + (size_t)S_NSTATE * dslot_;
+  // the attention -> Wo done counters: zeroed by the embedding's side job on the first stage, by
+  // a memset node elsewhere
+  if (tok_embd_.base) embed_rows(tok_embd_, st + S_TOKEN, 1, x_, s, dec_done_, 64 * hp_.n_layer);
+  else if (dec_done_) HIPCHK(hipMemsetAsync(dec_done_, 0, sizeof(int) * 64 * hp_.n_layer, s));
+  for (int l = opt_.layer_begin; l < layer_end_; ++l) enqueue_layer_decode(l, s);
+  if (has_head()) enqueue_head(x_, 1, s, dslot_);
+}
+
+// one decode step of this stage: after `prev`'s step (or, on the first stage, after the last
+// stage's state copy-back of the previous step), take prev's hidden row, run the stage graph;
+// the last stage then copies its token / position state to every other stage
+void Engine::chain_step(const Engine* prev, const Engine* last, const std::vector<Engine*>& others) {
+  HIPCHK(hipSetDevice(opt_.device));
+  const Engine* after = prev ? prev : last;
+  HIPCHK(hipStreamWaitEvent(stream_, after->chain_ev_, 0));
+  if (prev)
+    HIPCHK(hipMemcpyPeerAsync(x_, opt_.device, prev->x_, prev->opt_.device, sizeof(float) * hp_.n_embd, stream_));
+  if (!chain_graph_[0]) {
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    enqueue_stage_decode(stream_);
+    HIPCHK(hipStreamEndCapture(stream_, &g));
+    hipError_t e = hipGraphInstantiate(&chain_graph_[0], g, nullptr, nullptr, 0);
+    if (e == hipSuccess) e = hipGraphInstantiate(&chain_graph_[1], g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    HIPCHK(e);
+  }
+  HIPCHK(hipGraphLaunch(chain_graph_[chain_par_], stream_));
+  chain_par_ ^= 1;
+  if (this == last)
+    for (const Engine* o : others)
+      HIPCHK(hipMemcpyPeerAsync(o->state_, o->opt_.device, state_, opt_.device, sizeof(int) * S_NSTATE, stream_));
+  HIPCHK(hipEventRecord(chain_ev_, stream_));
+}
+
+GenOut Engine::chain_generate(const std::vector<Engine*>& st, const std::vector<int>& prompt, int n_keep,
+                              int max_new, const SamplingOpts& sp, const std::vector<int>& stop_ids,
+                              const std::function<bool()>& poll, const std::function<void(int)>& on_token) {
+  const size_t n = st.size();
+  if (n == 0) throw std::runtime_error("chain_generate: no stages");
+  for (size_t i = 0; i < n; ++i) {
+    const Engine* e = st[i];
+    if (!e || e->tp_on_ || e->opt_.tp_size > 1) throw std::runtime_error("chain_generate: stages are single-rank engines");
+    if (e->hp_.n_embd != st[0]->hp_.n_embd || e->opt_.n_ctx != st[0]->opt_.n_ctx)
+      throw std::runtime_error("chain_generate: stages of one model and context");
+    if ((i == 0 && e->opt_.layer_begin != 0) || (i > 0 && e->opt_.layer_begin != st[i - 1]->layer_end_))
+      throw std::runtime_error("chain_generate: stages must cover the layers in order");
+    for (size_t j = 0; j < i; ++j)
+      if (st[j] == e) throw std::runtime_error("chain_generate: a stage listed twice");
+  }
+  Engine* last = st[n - 1];
+#define CHAIN_CHK(x) last->check((x), #x)
+  if (!last->has_head()) throw std::runtime_error("chain_generate: the last stage must hold the head");
+  std::vector<std::unique_lock<std::mutex>> locks;  // every stage's guard, in chain order
+  for (Engine* e : st) locks.emplace_back(e->exec_mu_);
+  std::vector<Engine*> others(st.begin(), st.end() - 1);
+  GenOut out;
+  const int n_prompt = (int)prompt.size();
+  if (n_prompt == 0) throw std::runtime_error("empty prompt");
+  if (n_prompt >= last->opt_.n_ctx) throw std::runtime_error("prompt exceeds context window");
+  (void)last->make_sparams(sp);
+  if (n_keep < 0 || n_keep >= n_prompt) n_keep = 0;
+  const double t0 = now_s();
+  for (Engine* e : st) {
+    CHAIN_CHK(hipSetDevice(e->opt_.device));
+    if (!e->chain_ev_) CHAIN_CHK(hipEventCreateWithFlags(&e->chain_ev_, hipEventDisableTiming));
+    e->begin_slot_state(0, prompt, sp);  // position / token on every stage, sampler state on the last
+  }
+  // prompt chunks: stage 0 embeds, every later stage takes the chunk's hidden rows peer to peer
+  const int NB = std::min(st[0]->opt_.n_batch, last->opt_.n_batch);
+  for (int pos = n_keep; pos < n_prompt;) {
+    const int T = std::min(NB, n_prompt - pos);
+    for (size_t i = 0; i < n; ++i) {
+      Engine* e = st[i];
+      if (T > e->opt_.n_batch) throw std::runtime_error("chain_generate: chunk exceeds a stage's n_batch");
+      CHAIN_CHK(hipSetDevice(e->opt_.device));
+      if (i == 0) {
+        std::memcpy(e->h_tokens_, prompt.data() + pos, sizeof(int) * T);
+        CHAIN_CHK(hipMemcpyAsync(e->tokens_, e->h_tokens_, sizeof(int) * T, hipMemcpyHostToDevice, e->stream_));
+      } else {
+        CHAIN_CHK(hipStreamWaitEvent(e->stream_, st[i - 1]->chain_ev_, 0));
+        CHAIN_CHK(hipMemcpyPeerAsync(e->x_, e->opt_.device, st[i - 1]->x_, st[i - 1]->opt_.device,
+                                  sizeof(float) * T * e->hp_.n_embd, e->stream_));
+      }
+      e->enqueue_prefill(T, pos, e->stream_, /*embed=*/i == 0);
+      if (e == last && pos + T == n_prompt) e->enqueue_head(e->x_ + (size_t)(T - 1) * e->hp_.n_embd, 0, e->stream_, 0);
+      CHAIN_CHK(hipEventRecord(e->chain_ev_, e->stream_));
+    }
+    CHAIN_CHK(hipSetDevice(st[0]->opt_.device));
+    CHAIN_CHK(hipStreamSynchronize(st[0]->stream_));  // h_tokens_ is reused by the next chunk
+    pos += T;
+  }
+  // the first token's state to every stage
+  CHAIN_CHK(hipSetDevice(last->opt_.device));
+  for (const Engine* o : others)
+    CHAIN_CHK(hipMemcpyPeerAsync(o->state_, o->opt_.device, last->state_, last->opt_.device, sizeof(int) * S_NSTATE,
+                              last->stream_));
+  CHAIN_CHK(hipEventRecord(last->chain_ev_, last->stream_));
+  CHAIN_CHK(hipStreamSynchronize(last->stream_));
+  const double t1 = now_s();
+  out.prefill_s = t1 - t0;
+  out.n_prefilled = n_prompt - n_keep;
+  auto is_stop = [&](int t) {
+    for (int s : stop_ids) if (s == t) return true;
+    return false;
+  };
+  auto step = [&](int k) {
+    for (size_t i = 0; i < n; ++i) st[i]->chain_step(i ? st[i - 1] : nullptr, last, others);
+    CHAIN_CHK(hipSetDevice(last->opt_.device));
+    CHAIN_CHK(hipEventRecord(last->step_ev_[k % kDepth], last->stream_));
+  };
+  int tok = last->h_ring_[0];
+  out.tokens.push_back(tok);
+  if (on_token) on_token(tok);
+  out.finish = "length";
+  const int max_steps = std::min(max_new - 1, last->opt_.n_ctx - n_prompt);
+  if (is_stop(tok)) {
+    out.finish = "stop";
+  } else if (max_steps > 0) {
+    int launched = 0;
+    while (launched < std::min(kDepth, max_steps)) step(launched++);
+    for (int i = 1; i <= max_steps; ++i) {
+      CHAIN_CHK(hipEventSynchronize(last->step_ev_[(i - 1) % kDepth]));
+      tok = last->h_ring_[i & 63];
+      out.tokens.push_back(tok);
+      if (on_token) on_token(tok);
+      if (is_stop(tok)) { out.finish = "stop"; break; }
+      if (poll && (i & 3) == 0 && poll()) { out.finish = "cancelled"; break; }
+      if (launched < max_steps) step(launched++);
+    }
+  }
+  for (Engine* e : st) {
+    CHAIN_CHK(hipSetDevice(e->opt_.device));
+    CHAIN_CHK(hipStreamSynchronize(e->stream_));
+    CHAIN_CHK(hipGetLastError());
+  }
+  out.decode_s = now_s() - t1;
+  for (Engine* e : st) e->check_device_err();
+  out.n_evaluated = n_prompt + (int)out.tokens.size() - 1;
+  return out;
+}
+#undef CHAIN_CHK
 
 std::vector<float> Engine::eval_logits(const std::vector<int>& tokens, int pos0) {
   if (!has_head()) throw std::runtime_error("eval_logits: this layer-split stage holds no head (eval_stage)");

@@ -113,6 +113,16 @@ class Engine : public SlotBackend {
   // host round trip between stages. Returns the last row's logits at the head stage, else nothing
   std::vector<float> eval_stage_peer(const Engine& prev, int T, int pos0);
   void bench_decode(int n_steps, int pos0, double* ms_per_step);             // raw decode timing
+  // layer split, whole generation natively (runtime/layer_split_backend.py): `stages` hold
+  // contiguous layer ranges (stage 0 the embedding, the last the head), each on its own device.
+  // Prompt chunks and decode steps hand the hidden states stage to stage device to device; each
+  // stage's decode step is ONE captured hipGraph; the last stage samples on the device (the
+  // engine's sampler: same chain, same uniforms as generate) and its token / position state is
+  // copied back to every stage, so the host only reads tokens - kDepth steps in flight, as in
+  // generate. Cross-stage order by events, never a host wait.
+  static GenOut chain_generate(const std::vector<Engine*>& stages, const std::vector<int>& prompt, int n_keep,
+                               int max_new, const SamplingOpts& sp, const std::vector<int>& stop_ids,
+                               const std::function<bool()>& poll, const std::function<void(int)>& on_token);
 
   const HParams& hparams() const { return hp_; }
   size_t device_bytes() const { return dev_bytes_; }
@@ -436,6 +446,13 @@ class Engine : public SlotBackend {
   bool last_b1_ = false;      // the last batch_step ran its one row on the single-row path
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t graph_exec_ = nullptr, graph_exec2_ = nullptr;
+  // layer-split chain (chain_generate): this stage's decode step (layers, + embedding on the first
+  // stage, + head and sampler on the last), two graph instances alternating by step parity
+  void enqueue_stage_decode(hipStream_t s);
+  void chain_step(const Engine* prev, const Engine* last, const std::vector<Engine*>& others);
+  hipGraphExec_t chain_graph_[2] = {nullptr, nullptr};
+  int chain_par_ = 0;
+  hipEvent_t chain_ev_ = nullptr;
   static constexpr int kDepth = 2;
   hipEvent_t step_ev_[kDepth] = {};
 };

@@ -67,6 +67,16 @@ def _test_fault() -> str:
     return spec
 
 
+
+def gpu_sampling_dict(params: SamplingParams, n_vocab: int) -> dict:
+    """The device sampler's options (the engines' ``sampling`` dict)."""
+    return {"top_k": params.top_k, "top_p": params.top_p, "min_p": params.min_p,
+            "temperature": params.temperature, "repeat_penalty": params.repeat_penalty,
+            "frequency_penalty": params.frequency_penalty, "presence_penalty": params.presence_penalty,
+            "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF, "tfs_z": params.tfs_z,
+            "typical_p": params.typical_p,
+            "logit_bias": {int(t): float(b) for t, b in params.logit_bias.items() if 0 <= int(t) < n_vocab}}
+
 class HipBackend:
     name = "hip"
 
@@ -157,12 +167,7 @@ class HipBackend:
         return {f"hip:{self.device}": int(self.engine.device_bytes)}
 
     def _sp(self, params: SamplingParams) -> dict:
-        return {"top_k": params.top_k, "top_p": params.top_p, "min_p": params.min_p,
-                "temperature": params.temperature, "repeat_penalty": params.repeat_penalty,
-                "frequency_penalty": params.frequency_penalty, "presence_penalty": params.presence_penalty,
-                "last_n": params.last_n, "seed": params.seed & 0xFFFFFFFFFFFFFFFF, "tfs_z": params.tfs_z,
-                "typical_p": params.typical_p,
-                "logit_bias": {int(t): float(b) for t, b in params.logit_bias.items() if 0 <= int(t) < self.n_vocab}}
+        return gpu_sampling_dict(params, self.n_vocab)
 
     def _generate_batched(self, prompt: Sequence[int], max_new: int, params: SamplingParams,
                           stop_ids: Sequence[int], poll: Optional[Callable[[], bool]],

@@ -7,10 +7,16 @@ in those proportions. The same placement here: one MI355X engine per stage, stag
 on device ``i`` holding layers ``[begin_i, end_i)`` and its part of the KV cache; the
 first stage gathers the embedding, the last holds the output norm and head. A token's
 hidden states (``n_embd`` floats per row) pass from stage to stage once per prompt chunk
-or decoded token (device to device, ``hipMemcpyPeerAsync``); sampling is the host C++
-chain (bit-identical uniforms, as the hybrid backend). One MI355X holds every BASELINE model (288 GB), so this is a capacity and
-compatibility placement, not a speed-up: a single decode still walks every layer in
-order. Tensor parallelism (``split_mode="row"``) is the multi-GPU speed path.
+or decoded token (device to device, ``hipMemcpyPeerAsync``). Generation over HIP stages is one
+native call (``Engine::chain_generate``, engine.cpp): each stage's decode step is a captured
+hipGraph, the last stage samples on the device with the single-GPU engine's sampler and its
+token / position state is copied back to every stage, and steps are ordered across devices by
+events - the host only reads tokens, two steps in flight, exactly as the one-GPU ``generate``.
+Sampling options the device sampler lacks (grammar, mirostat, ...) and non-HIP stage objects
+take the host loop (host C++ sampling chain, bit-identical uniforms, as the hybrid backend).
+One MI355X holds every BASELINE model (288 GB), so this is a capacity and compatibility
+placement, not a speed-up: a single decode still walks every layer in order. Tensor
+parallelism (``split_mode="row"``) is the multi-GPU speed path.
 
 Layer assignment follows llama.cpp's full-offload rule: with ``tensor_split`` normalised to
 cumulative fractions ``c_0 < c_1 < ... = 1``, layer ``l`` goes to the first device ``i`` with
@@ -29,6 +35,7 @@ from ..engine.backends import GenerationResult, host_generate
 from ..engine.sampling import SamplingParams
 from . import load_cpu, load_hip
 from .cpu_backend import native_sampling, sampling_dict
+from .hip_backend import gpu_sampling_dict
 
 
 def layer_ranges(n_layer: int, tensor_split: Sequence[float]) -> List[Tuple[int, int, int]]:
@@ -71,8 +78,10 @@ class LayerSplitBackend:
         self.n_ctx = n_ctx
         self.n_batch = min(n_batch, n_ctx)
         self.n_vocab = int(hparams.n_vocab)
+        self._hip = None
         if stage_factory is None:
             hip = load_hip()
+            self._hip = hip
 
             def stage_factory(begin, end, device):
                 return hip.Engine(model_path, n_ctx=n_ctx, n_batch=self.n_batch, device=device, use_graph=False,
@@ -123,9 +132,22 @@ class LayerSplitBackend:
     def eval_logits(self, tokens: Sequence[int], pos0: int = 0) -> np.ndarray:
         return self._forward(tokens, pos0)
 
+    def native_chain(self, params: Optional[SamplingParams] = None) -> bool:
+        """Generation runs natively (``chain_generate``): HIP stages and device-sampler options."""
+        hip = self._hip
+        if hip is None or not hasattr(hip, "chain_generate") or not all(isinstance(s, hip.Engine) for s in self.stages):
+            return False
+        return params is None or params.gpu_compatible(self.n_vocab)
+
     def generate(self, prompt: Sequence[int], n_keep: int, max_new: int, params: SamplingParams,
                  stop_ids: Sequence[int], poll: Optional[Callable[[], bool]] = None,
                  on_token: Optional[Callable[[int], None]] = None) -> GenerationResult:
+        if self.native_chain(params):
+            r = self._hip.chain_generate(self.stages, [int(t) for t in prompt], int(n_keep), int(max_new),
+                                         gpu_sampling_dict(params, self.n_vocab), [int(t) for t in stop_ids],
+                                         poll, on_token)
+            return GenerationResult(list(r["tokens"]), r["finish"], int(r["n_evaluated"]), r["prefill_s"],
+                                    r["decode_s"], int(r["n_prefilled"]))
         fn = None
         if native_sampling(params):
             if self._cpu_mod is None:
