@@ -49,7 +49,9 @@ def main():
         dt = time.perf_counter() - t0
         return r, dt
 
+    r0 = be.generate(prompt, 0, args.new, greedy, [])
     r, dt = run(lambda p, n: be.generate(p, 0, n, greedy, []), args.new)
+    res["chain_runs_first_diff"] = next((i for i, (a, b) in enumerate(zip(r0.tokens, r.tokens)) if a != b), None)
     res["chain"] = {"tokens": len(r.tokens), "decode_ms_per_token": round(r.decode_s * 1e3 / max(1, len(r.tokens) - 1), 3),
                     "prefill_ms": round(r.prefill_s * 1e3, 2), "wall_s": round(dt, 3)}
     be._hip = None  # the host loop the chain replaced
@@ -59,12 +61,15 @@ def main():
     del be, hp
     whole = hip.Engine(path, n_ctx=1024, n_batch=512, device=devs[0], use_graph=True)
     sp = {"temperature": 0.0}
-    whole.generate(prompt, 0, args.new, sp, [])
+    w0 = whole.generate(prompt, 0, args.new, sp, [])
     t0 = time.perf_counter()
     w = whole.generate(prompt, 0, args.new, sp, [])
+    res["one_engine_repeatable"] = list(w0["tokens"]) == list(w["tokens"])
     res["one_engine"] = {"decode_ms_per_token": round(w["decode_s"] * 1e3 / max(1, len(w["tokens"]) - 1), 3),
                          "wall_s": round(time.perf_counter() - t0, 3)}
     res["chain_tokens_equal_one_engine"] = list(w["tokens"]) == list(r.tokens)
+    res["chain_vs_one_engine_first_diff"] = next((i for i, (a, b) in enumerate(zip(w["tokens"], r.tokens)) if a != b), None)
+    res["one_engine_runs_first_diff"] = next((i for i, (a, b) in enumerate(zip(w0["tokens"], w["tokens"])) if a != b), None)
     print(json.dumps(res))
 
 
