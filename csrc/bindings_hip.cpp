@@ -488,6 +488,13 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("w"), py::arg("type"), py::arg("rows"), py::arg("K"), py::arg("x"), py::arg("T"), py::arg("out"),
      py::arg("out_bf16"), py::arg("ldo"), py::arg("epi"), py::arg("stream"), py::arg("resid") = 0);
 
+  m.def("moe_router_rows", [](uintptr_t x, int ldx, int B, uintptr_t nw, float eps, uintptr_t W, int d, int E, int k,
+                              uintptr_t wd, int ld, uintptr_t stream) {
+    moe_router_rows(P<float>(x), ldx, B, P<float>(nw), eps, P<float>(W), d, E, k, P<float>(wd), ld, S(stream));
+    hip_ok("moe_router_rows");
+  }, py::arg("x"), py::arg("ldx"), py::arg("B"), py::arg("nw"), py::arg("eps"), py::arg("W"), py::arg("d"),
+     py::arg("E"), py::arg("k"), py::arg("wd"), py::arg("ld"), py::arg("stream"));
+
   // layer split (split_mode=layer): the whole generation over a chain of stage engines, natively
   m.def("chain_generate",
         [](std::vector<Engine*> stages, const std::vector<int>& prompt, int n_keep, int max_new, py::dict sp,

@@ -128,6 +128,35 @@ def test_moe_route(torch):
     np.testing.assert_allclose(w.cpu().numpy(), (p[[1, 7]] / p[[1, 7]].sum()).numpy(), rtol=1e-5)
 
 
+@pytest.mark.parametrize("E,k,d,B", [(8, 2, 4096, 6), (8, 2, 4096, 1), (16, 4, 2048, 3), (8, 2, 8192, 8)])
+def test_moe_router_rows_vs_fp64(torch, E, k, d, B):
+    """The batched decode router (one block per row: f32 RMSNorm(x) * w . W^T, softmax, top-k,
+    renormalised, as a dense [B][E] weight row, zeros for the unrouted experts) against an fp64
+    reference; the columns past E are untouched."""
+    rng = np.random.default_rng(E * 100 + d + B)
+    ldx = d + 8
+    x = torch.from_numpy(rng.standard_normal((B, ldx)).astype(np.float32)).cuda()
+    nw = torch.from_numpy((1 + 0.1 * rng.standard_normal(d)).astype(np.float32)).cuda()
+    W = torch.from_numpy((0.05 * rng.standard_normal((E, d))).astype(np.float32)).cuda()
+    ld = E + 3
+    one = torch.full((B, ld), 7.0, device="cuda")
+    hip().moe_router_rows(x.data_ptr(), ldx, B, nw.data_ptr(), 1e-5, W.data_ptr(), d, E, k, one.data_ptr(), ld,
+                          stream())
+    torch.cuda.synchronize()
+    xs = x.cpu().numpy()[:, :d].astype(np.float64)
+    n = xs / np.sqrt((xs ** 2).mean(1, keepdims=True) + 1e-5) * nw.cpu().numpy()
+    lg = n @ W.cpu().numpy().astype(np.float64).T
+    p = np.exp(lg - lg.max(1, keepdims=True))
+    p /= p.sum(1, keepdims=True)
+    got = one.cpu().numpy()
+    for b in range(B):
+        top = np.argsort(-p[b], kind="stable")[:k]
+        ref = np.zeros(E)
+        ref[top] = p[b][top] / p[b][top].sum()
+        np.testing.assert_allclose(got[b, :E], ref, rtol=1e-4, atol=1e-6)
+        assert np.all(got[b, E:] == 7.0)
+
+
 @pytest.mark.parametrize("tq,tk,tv", [(GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q6_K),   # two runs, one launch
                                       (GGMLType.Q4_K, GGMLType.Q8_0, GGMLType.Q8_0),
                                       (GGMLType.Q4_K, GGMLType.Q4_K, GGMLType.Q4_K),   # one run
