@@ -2033,11 +2033,11 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int g = 0; g < NG; ++g) acc[j][g] = f4_t{0.f, 0.f, 0.f, 0.f};
-  static_assert(XL >= 2 && XL <= 6 && XL * NT == TM * 16, "X pieces per thread");
+  static_assert(XL >= 2 && XL <= 8 && XL * NT == TM * 16, "X pieces per thread");
   // X piece p = tid + NT j: token p / 16, 16-B column p % 16 of the 128-k slice (rows past T
   // load row T - 1: finite values whose outputs are never stored). Named registers, not an
   // array: the array was put in scratch.
-  uint4 x0, x1, x2, x3, x4, x5;
+  uint4 x0, x1, x2, x3, x4, x5, x6, x7;
   const __half* xrow[XL];
 #pragma unroll
   for (int j = 0; j < XL; ++j) xrow[j] = a.x + (size_t)min(t0 + ((tid + NT * j) >> 4), a.T - 1) * K + 8 * (tid & 15);
@@ -2049,6 +2049,8 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     if constexpr (XL > 3) x3 = *reinterpret_cast<const uint4*>(xrow[XL > 3 ? 3 : 0] + k0);
     if constexpr (XL > 4) x4 = *reinterpret_cast<const uint4*>(xrow[XL > 4 ? 4 : 0] + k0);
     if constexpr (XL > 5) x5 = *reinterpret_cast<const uint4*>(xrow[XL > 5 ? 5 : 0] + k0);
+    if constexpr (XL > 6) x6 = *reinterpret_cast<const uint4*>(xrow[XL > 6 ? 6 : 0] + k0);
+    if constexpr (XL > 7) x7 = *reinterpret_cast<const uint4*>(xrow[XL > 7 ? 7 : 0] + k0);
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
     __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * ((tid & 15) ^ ((tid >> 4) & 15))];
@@ -2059,6 +2061,8 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     if constexpr (XL > 3) *reinterpret_cast<uint4*>(d + 3 * J) = x3;
     if constexpr (XL > 4) *reinterpret_cast<uint4*>(d + 4 * J) = x4;
     if constexpr (XL > 5) *reinterpret_cast<uint4*>(d + 5 * J) = x5;
+    if constexpr (XL > 6) *reinterpret_cast<uint4*>(d + 6 * J) = x6;
+    if constexpr (XL > 7) *reinterpret_cast<uint4*>(d + 7 * J) = x7;
   };
   auto load_w = [&](int i, BRawT<QT>& w0, BRawT<QT>& w1) __attribute__((always_inline)) {
     const int s = sb + (i >> 1), h = i & 1;
@@ -2171,12 +2175,15 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   const int rows = a.seg_dev ? std::max(1, std::min(a.T, a.rows_hint > 0 ? a.rows_hint : a.T)) : a.T;
   int nw = 4, tm = 64;
   const int pin_nw = a.cfg / 1000, pin_tm = a.cfg % 1000;
-  if (((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && pin_tm == 64))) {
+  if (((pin_nw == 8 && (pin_tm == 128 || pin_tm == 64)) || (pin_nw == 4 && (pin_tm == 64 || pin_tm == 128)))) {
     nw = pin_nw;
     tm = pin_tm;
   } else if (EPI == GEMM_SWIGLU) {
-    nw = 8;
-    tm = rows >= 2048 ? 128 : 64;
+    // (round 6, tools/gemm_bench.py --only gateup, alternating twice: T = 300 4 x 64 121 / 120 us vs
+    // 8 x 64 134 / 135; T = 512 4 x 128 168 / 167 vs 181 / 177; T = 1024 4 x 128 303 / 304 vs 317 /
+    // 322; T = 387 all within 2 %; T = 2304 8 x 128 best)
+    nw = rows >= 2048 ? 8 : rows >= 448 || rows <= 320 ? 4 : 8;
+    tm = rows >= 448 ? 128 : 64;
   }
   const int gx = (ntiles + 2 * nw - 1) / (2 * nw), gy = (a.T + tm - 1) / tm, gy_busy = (rows + tm - 1) / tm;
   // split-K (partials by atomic add) only for long K, up to two resident rounds: at K = 4096 the
@@ -2198,6 +2205,7 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   }
   const dim3 grid(gx, gy, split);
   if (nw == 8 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 8>), grid, dim3(512), 0, s, a);
+  else if (nw == 4 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 4>), grid, dim3(256), 0, s, a);
   else if (nw == 8) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 8>), grid, dim3(512), 0, s, a);
   else hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 4>), grid, dim3(256), 0, s, a);
 }

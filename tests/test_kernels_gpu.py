@@ -854,7 +854,8 @@ def test_gemm_t16_stacked_qkv(torch, t, T):
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
-@pytest.mark.parametrize("T,F,K", [(40, 96, 2048), (200, 256, 4096), (129, 1792, 1024)])
+@pytest.mark.parametrize("T,F,K", [(40, 96, 2048), (200, 256, 4096), (129, 1792, 1024),
+                                   (330, 512, 1024), (500, 384, 2048), (2050, 256, 512)])  # each block shape
 def test_gemm_t16_swiglu_vs_fp32(torch, t, T, F, K):
     """Prefill gate/up on the SwiGLU tile16 copy: silu(gate) * up as f16 in the 4-group k order."""
     rng = np.random.default_rng(T * 3 + F + int(t))
