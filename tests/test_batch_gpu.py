@@ -329,3 +329,40 @@ def test_batch_step_more_than_eight_rows(models, n_rows):
             assert toks[b] == int(np.argmax(logits[b]))
             seqs[s].append(toks[b])
     assert eng.healthy, eng.last_error
+
+
+def test_batched_and_serial_decode_agree_near_n_ctx(models):
+    """RoPE from one source on every path: rows decoded batched (deferred RoPE in the batched
+    attention, fp32 pos * freq) and the same sequences decoded one at a time (the rope table, built
+    from the same fp32 angles) agree at positions near n_ctx = 1024, where a rotation computed two
+    ways would drift the most - both against the fp32 reference, and against each other."""
+    from llama_fastapi_k8s_gpu_amd.gguf.reader import GGUFReader
+    from llama_fastapi_k8s_gpu_amd.models.llama import ReferenceLlama
+    from llama_fastapi_k8s_gpu_amd.runtime import load_hip
+    path = models["tiny-llama3-q4_k_m"]
+    hip = load_hip()
+    bat = hip.Engine(path, n_ctx=1024, n_batch=512, device=0, use_graph=True, n_slots=3)
+    one = hip.Engine(path, n_ctx=1024, n_batch=512, device=0, use_graph=False)
+    ref = ReferenceLlama(GGUFReader(path), n_ctx=1024)
+    rng = np.random.default_rng(77)
+    greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
+    prompts = [[int(t) for t in rng.integers(3, 300, n)] for n in (1010, 990)]
+    seqs = []
+    for s, p in enumerate(prompts):
+        seqs.append(p + [bat.slot_begin(s, p, 0, greedy)])
+    for step in range(2):
+        toks = bat.batch_step([0, 1])
+        lb = bat.batch_logits(2)
+        for b in range(2):
+            seq = seqs[b]
+            # the one-row engine: the same history on its prefill path, then this step's token decoded
+            one.eval_logits(seq[:512], 0)
+            one.eval_logits(seq[512:-1], 512)
+            ls = one.decode_logits(seq[-1], len(seq) - 1)
+            want = ref.forward(seq, 0).numpy()
+            assert rel_err(lb[b], want) < 5e-2, (step, b, rel_err(lb[b], want))
+            assert rel_err(ls, want) < 5e-2, (step, b, rel_err(ls, want))
+            assert rel_err(lb[b], ls) < 5e-2, (step, b, rel_err(lb[b], ls))
+            assert toks[b] == int(np.argmax(lb[b]))
+            seqs[b].append(toks[b])
+    assert bat.healthy, bat.last_error
