@@ -235,7 +235,10 @@ class Engine : public SlotBackend {
   // tensor parallelism: publish a command to the followers (rank 0); no-op on one rank
   bool leader() const { return opt_.tp_size > 1 && opt_.tp_rank == 0; }
   std::string group_fault() const;  // leader: the followers' failures as the channel holds them ("" = none)
-  bool tp_epi_ = true;              // GEMV-epilogue all-reduce allowed (LFK_TP_EPILOGUE=0: the collective kernel)
+  bool tp_epi_ = true;
+  // rows of the activation buffers: n_batch, or kJointRows for a joint admission (alloc_buffers)
+  static constexpr int kJointRows = 4096;
+  int nb_cap_ = 0;              // GEMV-epilogue all-reduce allowed (LFK_TP_EPILOGUE=0: the collective kernel)
   int fault_after_ = 0;             // follower test hook (EngineOptions::test_fault): fail the n-th command
   bool fault_dev_ = false;          // ... as a device-side fault word instead of a host failure
   void mirror(const TPMsg& m);
