@@ -114,6 +114,16 @@ class CountingEngine:
         return self.llm.health()
 
 
+def _sched_stats(eng) -> dict:
+    """The batch scheduler's counters (admitted, joint / chunked admissions), if the backend has one."""
+    try:
+        h = eng.health()
+    except Exception:
+        return {}
+    b = h.get("batching") if isinstance(h, dict) else None
+    return dict(b) if isinstance(b, dict) else {}
+
+
 def make_request(i: int) -> dict:
     names = ["Mia.f", "Leo", "Ava.f", "Max"]
     ctx = []
@@ -461,6 +471,7 @@ def main() -> int:
                 else:
                     torch.cuda.synchronize(device)
                 n0 = len(eng.completion_tokens)
+                st0 = _sched_stats(eng)
                 t_start = time.perf_counter()
                 await drive(range(args.steps * nc), latencies, args.clients)
                 # TP: rank 0's last step completed its all-reduces, so every rank is done with it
@@ -470,12 +481,17 @@ def main() -> int:
                     torch.cuda.synchronize(device)
                 elapsed = time.perf_counter() - t_start
                 n1 = len(eng.completion_tokens)
+                st1 = _sched_stats(eng)
                 ts = time.perf_counter()
                 if serial_steps > 0:
                     await drive(range(2000, 2000 + serial_steps), serial_lat, 1)
-                return elapsed, n0, n1, time.perf_counter() - ts
+                # the continuous batch's admissions over the timed rounds (how the C requests of a
+                # round entered: one joint prefill, or several)
+                sched = ({k: st1[k] - st0.get(k, 0) for k in ("admitted", "joint_admissions", "chunked_admissions")
+                          if isinstance(st1.get(k), (int, float))} if st1 else None)
+                return elapsed, n0, n1, time.perf_counter() - ts, sched
 
-    elapsed, n0, n1, serial_s = asyncio.run(run())
+    elapsed, n0, n1, serial_s, sched = asyncio.run(run())
     llm.close()   # TP: publishes STOP, the followers' follow() returns
     del app, eng.llm
     toks = sum(eng.completion_tokens[n0:n1])
@@ -532,6 +548,8 @@ def main() -> int:
                                            "production": {"timeout_seconds": 25.0, "max_queue_size": 5,
                                                           "admission_cap": 6}}},
         }
+        if sched:
+            res["config"]["scheduler"] = sched
         if comm is not None:
             res["config"]["comm"] = comm
         if check is not None:
