@@ -194,16 +194,28 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs 
   const int G = a.n_head / a.n_kv_head, QTB = 4 / HB;
   const int kvh = blockIdx.x;
   const int qblk = gridDim.y - 1 - blockIdx.y;  // latest (longest) query tiles dispatch first
-  const int head = kvh * G + blockIdx.z * HB + wave % HB;
+  // packed pieces: z = piece x head group; the piece's rows, positions and KV slot
+  int T = a.T, pos0 = a.pos0, hz = blockIdx.z;
+  size_t row0 = 0, cache0 = 0;
+  if (a.n_pieces > 0) {
+    const int HZ = G / HB, pc = blockIdx.z / HZ;
+    hz = blockIdx.z - pc * HZ;
+    T = a.pc_n[pc];
+    pos0 = a.pc_pos[pc];
+    row0 = (size_t)a.pc_row[pc];
+    cache0 = (size_t)a.pc_slot[pc] * a.slot_stride;
+    if (qblk * QTB * 32 >= T) return;  // a shorter piece's missing tiles: whole block, no barrier yet
+  }
+  const int head = kvh * G + hz * HB + wave % HB;
   const int tq = (qblk * QTB + wave / HB) * 32;
-  const int nkeys = a.pos0 + min(a.T, (qblk + 1) * QTB * 32);  // keys the block needs
-  const int wkeys = a.pos0 + min(a.T, tq + 32);                 // keys this wave needs
+  const int nkeys = pos0 + min(T, (qblk + 1) * QTB * 32);  // keys the block needs
+  const int wkeys = pos0 + min(T, tq + 32);                 // keys this wave needs
   const int t = tq + lr;
-  const int qpos = a.pos0 + min(t, a.T - 1);  // padded query columns attend like the last real one
+  const int qpos = pos0 + min(t, T - 1);  // padded query columns attend like the last real one
 
   f16x8_t qf[NKK];
   {
-    const float* qr = a.q + ((size_t)min(t, a.T - 1) * a.n_head + head) * HD + 8 * hh;
+    const float* qr = a.q + ((row0 + min(t, T - 1)) * a.n_head + head) * HD + 8 * hh;
     const float qs = a.scale * 1.44269504088896341f;
     f32x4_t qv[2 * NKK];  // all loads issued before the first use (one round trip)
 #pragma unroll
@@ -215,8 +227,8 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs 
       qf[kk] = __builtin_convertvector(v, f16x8_t);
     }
   }
-  const _Float16* kb = reinterpret_cast<const _Float16*>(a.k_cache) + (size_t)kvh * a.n_ctx * HD;
-  const _Float16* vb = reinterpret_cast<const _Float16*>(a.v_cache) + (size_t)kvh * a.n_ctx * HD;
+  const _Float16* kb = reinterpret_cast<const _Float16*>(a.k_cache) + cache0 + (size_t)kvh * a.n_ctx * HD;
+  const _Float16* vb = reinterpret_cast<const _Float16*>(a.v_cache) + cache0 + (size_t)kvh * a.n_ctx * HD;
   // rows clamped to the last needed key: the rows past it hold real (finite) data that the
   // mask gives weight 0, so no NaN can leak into P.V; every load is unconditional
   int goff[NCH], soff[NCH], skey[NCH];
@@ -315,13 +327,13 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs 
   }
   l += __shfl_xor(l, 32);
   const float inv = 1.f / l;
-  if (t < a.T) {
+  if (t < T) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int d = 32 * dt + 8 * rg + 4 * hh;  // o[dt][4rg + 0..3] = dims d .. d+3
-        const size_t off = (size_t)t * a.out_stride + (size_t)head * HD + d;
+        const size_t off = (row0 + t) * a.out_stride + (size_t)head * HD + d;
         const float v0 = o[dt][4 * rg] * inv, v1 = o[dt][4 * rg + 1] * inv;
         const float v2 = o[dt][4 * rg + 2] * inv, v3 = o[dt][4 * rg + 3] * inv;
         if constexpr (OUT == 1) {
@@ -341,18 +353,31 @@ __global__ __launch_bounds__(256) void attn_prefill_mfma_kernel(AttnPrefillArgs 
 template <int HD>
 static void launch_attn_prefill_mfma(const AttnPrefillArgs& a, int G, hipStream_t s) {
   const int HB = std::min(G, 4), QTB = 4 / HB;
-  dim3 grid(a.n_kv_head, (a.T + 32 * QTB - 1) / (32 * QTB), G / HB);
+  int tmax = a.T;
+  if (a.n_pieces > 0) {
+    tmax = 0;
+    for (int i = 0; i < a.n_pieces; ++i) tmax = std::max(tmax, a.pc_n[i]);
+  }
+  dim3 grid(a.n_kv_head, (tmax + 32 * QTB - 1) / (32 * QTB), (G / HB) * std::max(1, a.n_pieces));
   if (a.out_h) hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 2>), grid, dim3(256), 0, s, a, HB);
   else if (a.out_bf16) hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 1>), grid, dim3(256), 0, s, a, HB);
   else hipLaunchKernelGGL((attn_prefill_mfma_kernel<HD, 0>), grid, dim3(256), 0, s, a, HB);
 }
 
 void attn_prefill(const AttnPrefillArgs& a, hipStream_t s) {
-  if (a.T <= 0) return;
+  if (a.n_pieces < 0 || a.n_pieces > AttnPrefillArgs::kMaxPieces) throw std::runtime_error("attn_prefill: 0-16 pieces");
+  if (a.n_pieces > 0) {
+    for (int i = 0; i < a.n_pieces; ++i)
+      if (a.pc_n[i] <= 0 || a.pc_pos[i] < 0 || a.pc_pos[i] + a.pc_n[i] > a.n_ctx || a.pc_row[i] < 0 || a.pc_slot[i] < 0)
+        throw std::runtime_error("attn_prefill: bad piece");
+  } else if (a.T <= 0) {
+    return;
+  }
   if (a.n_head % a.n_kv_head) throw std::runtime_error("attn_prefill: n_head % n_kv_head");
   if (a.head_dim != 128 && a.head_dim != 64) throw std::runtime_error("attn_prefill: head_dim must be 64 or 128");
-  if (a.pos0 + a.T > a.n_ctx) throw std::runtime_error("attn_prefill: pos0 + T > n_ctx");
+  if (a.n_pieces == 0 && a.pos0 + a.T > a.n_ctx) throw std::runtime_error("attn_prefill: pos0 + T > n_ctx");
   const int G = a.n_head / a.n_kv_head;
+  if (a.n_pieces > 0 && !((G & (G - 1)) == 0 && G <= 16)) throw std::runtime_error("attn_prefill: pieces need the MFMA path");
   if ((G & (G - 1)) == 0 && G <= 16) {  // GQA group a power of two (every Llama/Mixtral)
     if (a.head_dim == 128) launch_attn_prefill_mfma<128>(a, G, s);
     else launch_attn_prefill_mfma<64>(a, G, s);

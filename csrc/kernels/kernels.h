@@ -403,6 +403,13 @@ struct AttnPrefillArgs {
   __hip_bfloat16* out_bf16 = nullptr;  // bf16 (the Wo GEMM's input; MFMA path only)
   __half* out_h = nullptr;        // or f16 in bmm's 4-group k order (gemm_t16's input; MFMA path)
   int out_stride = 0;
+  // packed prompts in ONE launch (MFMA path; a joint admission's pieces): piece i = q / out rows
+  // [pc_row, pc_row + pc_n) at positions pc_pos.., against KV slot pc_slot (caches + slot *
+  // slot_stride halves); T / pos0 are then unused (grid z = pieces x head groups)
+  static constexpr int kMaxPieces = 16;
+  int n_pieces = 0;
+  int pc_row[kMaxPieces] = {}, pc_n[kMaxPieces] = {}, pc_pos[kMaxPieces] = {}, pc_slot[kMaxPieces] = {};
+  size_t slot_stride = 0;
 };
 void attn_prefill(const AttnPrefillArgs& a, hipStream_t s);
 

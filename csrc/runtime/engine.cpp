@@ -346,6 +346,7 @@ void Engine::alloc_buffers() {
   if (const char* e = std::getenv("LFK_WO_FUSE")) wo_fuse_ = e[0] != '0';  // A/B
   if (const char* e = std::getenv("LFK_MOE_ROUTE_FUSE")) moe_route_fuse_ = e[0] != '0';  // A/B (test_engine_gpu)
   if (const char* e = std::getenv("LFK_TP_EPILOGUE")) tp_epi_ = e[0] != '0';  // A/B: the separate collective kernel
+  if (const char* e = std::getenv("LFK_PIECES_ATTN")) pieces_attn_ = e[0] != '0';  // A/B: one launch per piece
   if (wo_fuse_ && nkv_l_ <= 64) {
     HIPCHK(hipHostMalloc((void**)&wo_err_h_, sizeof(int), hipHostMallocMapped));
     *wo_err_h_ = 0;
@@ -907,15 +908,36 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
       __half* kcl = kc_ + kv_layer * (l - opt_.layer_begin);  // slot 0's layer l; + slot * slot_stride_
       __half* vcl = vc_ + kv_layer * (l - opt_.layer_begin);
       rope_kv_prefill(qkv_, T, 0, nq_, nkvd_, hd, opt_.n_ctx, rope_, q_, kcl, vcl, s, rpos_, rslots_, slot_stride_);
-      for (const PrefillSeg& g : *segs_) {
+      // every piece in one launch (up to 16 per launch; grid z = pieces): the pieces of a joint
+      // admission ran one launch each, ~100 blocks apiece on a 256-CU chip
+      const std::vector<PrefillSeg>& sg = *segs_;
+      const int G = nh_l_ / std::max(1, nkv_l_);
+      const bool mfma = (G & (G - 1)) == 0 && G <= 16;
+      for (size_t i0 = 0; i0 < sg.size();) {
         AttnPrefillArgs pa;
+        pa.q = q_; pa.k_cache = kcl; pa.v_cache = vcl; pa.n_ctx = opt_.n_ctx;
+        pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
+        if (t16) pa.out_h = attnh16;
+        else pa.out_bf16 = attnb_;
+        pa.out_stride = nq_;
+        if (mfma && pieces_attn_) {
+          pa.slot_stride = slot_stride_;
+          const size_t i1 = std::min(sg.size(), i0 + AttnPrefillArgs::kMaxPieces);
+          for (size_t i = i0; i < i1; ++i) {
+            const int k = (int)(i - i0);
+            pa.pc_row[k] = sg[i].row; pa.pc_n[k] = sg[i].n; pa.pc_pos[k] = sg[i].pos; pa.pc_slot[k] = sg[i].slot;
+          }
+          pa.n_pieces = (int)(i1 - i0);
+          attn_prefill(pa, s);
+          i0 = i1;
+          continue;
+        }
+        const PrefillSeg& g = sg[i0++];
         pa.q = q_ + (size_t)g.row * nq_;
         pa.k_cache = kcl + slot_stride_ * g.slot; pa.v_cache = vcl + slot_stride_ * g.slot;
-        pa.T = g.n; pa.pos0 = g.pos; pa.n_ctx = opt_.n_ctx;
-        pa.n_head = nh_l_; pa.n_kv_head = nkv_l_; pa.head_dim = hd; pa.scale = 1.f / std::sqrt((float)hd);
+        pa.T = g.n; pa.pos0 = g.pos;
         if (t16) pa.out_h = attnh16 + (size_t)g.row * nq_;
         else pa.out_bf16 = attnb_ + (size_t)g.row * nq_;
-        pa.out_stride = nq_;
         attn_prefill(pa, s);
       }
     } else if (!batched) {

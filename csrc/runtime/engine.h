@@ -236,6 +236,7 @@ class Engine : public SlotBackend {
   bool leader() const { return opt_.tp_size > 1 && opt_.tp_rank == 0; }
   std::string group_fault() const;  // leader: the followers' failures as the channel holds them ("" = none)
   bool tp_epi_ = true;
+  bool pieces_attn_ = true;  // a joint admission's prompt pieces in one attention launch
   // rows of the activation buffers: n_batch, or kJointRows for a joint admission (alloc_buffers)
   static constexpr int kJointRows = 4096;
   int nb_cap_ = 0;              // GEMV-epilogue all-reduce allowed (LFK_TP_EPILOGUE=0: the collective kernel)
