@@ -1988,13 +1988,17 @@ bool bmm_qkv2(const BmmArgs& a0, const BmmArgs& b0, hipStream_t s) {
 // (Q8_0's stay 2-way).
 static constexpr int kT16Pitch = 128;
 
-template <int QT, int EPI, int TM, int NWV>
-__global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
-  constexpr int NG = TM / 16, NT = NWV * 64;
+// KW = 2: the block's K range in two halves, one group of NWV waves each (two waves per SIMD where
+// the grid holds at most one block per CU), the groups' tiles summed through LDS at the end - the
+// second wave per SIMD without split-K atomics.
+template <int QT, int EPI, int TM, int NWV, int KW>
+__global__ __launch_bounds__(NWV * 64 * KW) void gemm_t16_kernel(GemmT16Args a) {
+  constexpr int NG = TM / 16, NT = NWV * 64;  // NT: the threads of one K group
   constexpr int XL = TM * 16 / NT;  // 16-B X pieces per thread per half step
   constexpr int SB = t16_step_bytes(QT);
-  __shared__ __attribute__((aligned(16))) __half xs[2][TM * kT16Pitch];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __shared__ __attribute__((aligned(16))) __half xs[2][KW][TM * kT16Pitch];
+  const int kg = KW > 1 ? (int)threadIdx.x / NT : 0;  // this thread's K group
+  const int tid = threadIdx.x - kg * NT, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
   const int ntiles = (a.w.rows + 15) >> 4;
@@ -2009,9 +2013,11 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     if (a.out_h) a.out_h += (size_t)r0 * a.ldh;
   }
   const int spz = (steps + (int)gridDim.z - 1) / (int)gridDim.z;
-  const int sb = blockIdx.z * spz, se = min(steps, sb + spz);
-  if (sb >= se) return;  // whole block, before any barrier
-  const int nh = 2 * (se - sb);
+  const int sb0 = blockIdx.z * spz, se = min(steps, sb0 + spz);
+  if (sb0 >= se) return;  // whole block, before any barrier
+  const int spg = (se - sb0) / KW;  // steps per K group (the launcher keeps them whole)
+  const int sb = sb0 + kg * spg;    // this group's first step
+  const int nh = 2 * spg;
   const size_t tstride = a.tile_stride ? a.tile_stride : (size_t)steps * SB;
   auto tile_base = [&](int t) __attribute__((always_inline)) {  // (stacked segments: Q|K|V)
     t = min(t, ntiles - 1);
@@ -2053,7 +2059,7 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     if constexpr (XL > 7) x7 = *reinterpret_cast<const uint4*>(xrow[XL > 7 ? 7 : 0] + k0);
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
-    __half* d = &xs[buf][(tid >> 4) * kT16Pitch + 8 * ((tid & 15) ^ ((tid >> 4) & 15))];
+    __half* d = &xs[buf][kg][(tid >> 4) * kT16Pitch + 8 * ((tid & 15) ^ ((tid >> 4) & 15))];
     constexpr int J = (NT / 16) * kT16Pitch;  // piece j + 1 is NT / 16 tokens further (same swizzle)
     *reinterpret_cast<uint4*>(d) = x0;
     *reinterpret_cast<uint4*>(d + J) = x1;
@@ -2079,7 +2085,7 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     HFrag F0, F1;
     dequant_frags<QT>(w0, c, F0);
     dequant_frags<QT>(w1, c, F1);
-    const __half* xb = &xs[i & 1][r16 * kT16Pitch];
+    const __half* xb = &xs[i & 1][kg][r16 * kT16Pitch];
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
 #pragma unroll
@@ -2115,6 +2121,22 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
     half(i + 1, wb0, wb1);
     store_x(i & 1);
     lds_barrier();
+  }
+  if constexpr (KW > 1) {  // group 1's tiles into LDS (the X buffers are free), group 0 adds them
+    static_assert(2 * NG * NT * 16 <= sizeof(xs), "the K groups' reduction fits the X buffers");
+    f4_t* red = reinterpret_cast<f4_t*>(&xs[0][0][0]);
+    if (kg == 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) red[((j * NG + g) * NWV + wave) * 64 + lane] = acc[j][g];
+    }
+    lds_barrier();
+    if (kg == 1) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acc[j][g] += red[((j * NG + g) * NWV + wave) * 64 + lane];
   }
   // ---- epilogue: acc[j][g][e] = (weight row 16 tile + 4 kq + e, token t0 + 16 g + r16)
 #pragma unroll
@@ -2162,6 +2184,15 @@ __global__ __launch_bounds__(NWV * 64) void gemm_t16_kernel(GemmT16Args a) {
   }
 }
 
+// two K groups per block for the narrow prefill projections (LFK_T16_KW=0/1 A/B; read once)
+static bool t16_kw() {
+  static const bool on = [] {
+    const char* e = std::getenv("LFK_T16_KW");
+    return e ? e[0] != '0' : true;
+  }();
+  return on;
+}
+
 template <int QT, int EPI>
 static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   // block shape (waves x 32 rows, TM tokens), measured over T = 384-2304 on the 8B shapes
@@ -2190,8 +2221,12 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
   // atomics cost more than the idle CUs (Q / Wo at T = 387: 57 us split in 2 vs 37 us whole at
   // T = 512), at K = 14336 the second wave per SIMD pays (down: 115 us split in 2 at T = 387 vs
   // 152 us whole at T = 512; profiles/README.md, round 6); tiny grids (a lone K / V) still split
+  // two K groups per block where the grid leaves CUs with one 4-wave block or none (whole steps
+  // per group; the grouped MoE form keeps its split-K sizing)
+  const int kw = EPI != GEMM_SWIGLU && nw == 4 && tm == 64 && a.cfg == 0 && !a.seg_dev && t16_kw() &&
+                         gx * gy_busy <= cus && steps % 2 == 0 ? 2 : 1;
   int split = 1;
-  if (EPI != GEMM_SWIGLU)
+  if (EPI != GEMM_SWIGLU && kw == 1)
     while (steps / (split * 2) >= 2 &&
            ((steps / (split * 2) >= 12 && gx * gy_busy * split * 2 <= 2 * cus) || gx * gy_busy * split * 4 <= cus))
       split *= 2;
@@ -2204,10 +2239,11 @@ static void launch_gemm_t16(const GemmT16Args& a, hipStream_t s) {
     if (e != hipSuccess) throw std::runtime_error("gemm_t16: memset failed");
   }
   const dim3 grid(gx, gy, split);
-  if (nw == 8 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 8>), grid, dim3(512), 0, s, a);
-  else if (nw == 4 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 4>), grid, dim3(256), 0, s, a);
-  else if (nw == 8) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 8>), grid, dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 4>), grid, dim3(256), 0, s, a);
+  if (nw == 8 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 8, 1>), grid, dim3(512), 0, s, a);
+  else if (nw == 4 && tm == 128) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 128, 4, 1>), grid, dim3(256), 0, s, a);
+  else if (nw == 8) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 8, 1>), grid, dim3(512), 0, s, a);
+  else if (kw == 2) hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 4, 2>), grid, dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((gemm_t16_kernel<QT, EPI, 64, 4, 1>), grid, dim3(256), 0, s, a);
 }
 
 template <int QT>
