@@ -311,8 +311,10 @@ void Engine::alloc_buffers() {
   // weights instead of five n_batch chunks, at the GEMMs' large-T efficiency (the activations of
   // 4096 rows are ~0.55 GB at the 8B, ~1.1 GB at the 70B)
   nb_cap_ = opt_.n_batch;
+  long long joint = kJointRows;
+  if (const char* e = std::getenv("LFK_JOINT_ROWS")) joint = std::atoll(e);  // A/B, tests (0: n_batch chunks)
   if (opt_.n_slots > 1 && opt_.tp_size == 1)
-    nb_cap_ = std::max(nb_cap_, (int)std::min<long long>(kJointRows, (long long)opt_.n_slots * opt_.n_ctx));
+    nb_cap_ = std::max(nb_cap_, (int)std::min<long long>(joint, (long long)opt_.n_slots * opt_.n_ctx));
   const int B = nb_cap_, d = hp_.n_embd, hd = hp_.head_dim;
   const int E = std::max(hp_.n_expert, 1), KU = std::max(hp_.n_expert_used, 1);
   x_ = (float*)dalloc(sizeof(float) * B * d);

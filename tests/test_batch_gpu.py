@@ -108,16 +108,21 @@ def test_batch_step_d4096_fused_paths(tmp_path):
     assert eng.healthy, eng.last_error
 
 
+@pytest.mark.parametrize("joint_rows", ["default", "0"])
 @pytest.mark.parametrize("spec", ["tiny-llama3-q4_k_m", "tiny-mixtral-q4_k_m"])
-def test_joint_admission_matches_sequential(models, spec):
+def test_joint_admission_matches_sequential(models, spec, joint_rows, monkeypatch):
     """slots_begin packs several prompts into shared prefill chunks (per-row KV slot and
-    position, one attention launch per prompt piece; n_batch 32 makes pieces cross chunk
-    boundaries, one prompt reuses its slot's resident prefix): first tokens and the rows of
-    the following batched steps equal slot-by-slot admission."""
+    position, every prompt piece of a chunk in one attention launch; one prompt reuses its slot's
+    resident prefix): first tokens and the rows of the following batched steps equal slot-by-slot
+    admission. Default: the whole admission in one pass (Engine::kJointRows); LFK_JOINT_ROWS=0:
+    chunks of n_batch = 32 rows, so pieces cross chunk boundaries."""
     from llama_fastapi_k8s_gpu_amd.runtime import load_hip
     hip = load_hip()
+    if joint_rows != "default":
+        monkeypatch.setenv("LFK_JOINT_ROWS", joint_rows)
     kw = dict(n_ctx=256, n_batch=32, device=0, use_graph=False, n_slots=4)
     joint, seq = hip.Engine(models[spec], **kw), hip.Engine(models[spec], **kw)
+    monkeypatch.delenv("LFK_JOINT_ROWS", raising=False)
     rng = np.random.default_rng(12)
     greedy = {"temperature": 0.0, "top_k": 1, "repeat_penalty": 1.0}
     base = [int(t) for t in rng.integers(3, 300, 21)]
