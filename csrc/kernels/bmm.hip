@@ -349,10 +349,10 @@ __device__ __forceinline__ void tload(BRawT<T>& w, const uint8_t* blk, int h, in
 // registers of loads still in flight (a vmcnt wait on them drained the ring at every round)
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
-template <int T>
+template <int T, bool NTQ = true>
 __device__ __forceinline__ void tload_rs(BRawT<T>& w, __amdgpu_buffer_rsrc_t rs, int so, int h, int l, int r16, int kq) {
   auto b128 = [&](int vo, int imm) {  // quant planes: non-temporal (aux 2: each weight is read once per step)
-    const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so + imm, 2));
+    const v4i_t t = __builtin_bit_cast(v4i_t, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so + imm, NTQ ? 2 : 0));
     return make_int4(t.x, t.y, t.z, t.w);
   };
   auto b128c = [&](int vo, int imm) {
@@ -1997,8 +1997,10 @@ __global__ __launch_bounds__(NWV * 64 * KW) void gemm_t16_kernel(GemmT16Args a) 
   constexpr int XL = TM * 16 / NT;  // 16-B X pieces per thread per half step
   constexpr int SB = t16_step_bytes(QT);
   __shared__ __attribute__((aligned(16))) __half xs[2][KW][TM * kT16Pitch];
-  const int kg = KW > 1 ? (int)threadIdx.x / NT : 0;  // this thread's K group
-  const int tid = threadIdx.x - kg * NT, lane = tid & 63, wave = tid >> 6;
+  // (wave-uniform by construction; readfirstlane tells the compiler, so the weight tiles' buffer
+  // resources stay scalar instead of waterfall loops)
+  const int kg = KW > 1 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / NT) : 0;  // this thread's K group
+  const int tid = threadIdx.x - kg * NT, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, kq = lane >> 4;
   const int K = a.w.K, steps = K >> 8;
   const int ntiles = (a.w.rows + 15) >> 4;
@@ -2044,19 +2046,27 @@ __global__ __launch_bounds__(NWV * 64 * KW) void gemm_t16_kernel(GemmT16Args a) 
   // load row T - 1: finite values whose outputs are never stored). Named registers, not an
   // array: the array was put in scratch.
   uint4 x0, x1, x2, x3, x4, x5, x6, x7;
-  const __half* xrow[XL];
+  // the X and weight loads go through buffer resources - per-lane 32-bit voffsets fixed for the
+  // kernel, the step's offset a uniform soffset - instead of 64-bit address arithmetic per load:
+  // 257 -> 240 VALU per 64 MFMAs in the main loop of this VALU-bound kernel; 387-token admission
+  // 12.8 -> 11.2 ms (profiles/README.md, round 6)
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<__half*>(a.x), 0, 0x7FFFFFFF, 0x00020000);
+  int xvo[XL];  // bytes: T x K x 2 stays far below 2 GB (T <= 4096 rows, K <= 28672)
 #pragma unroll
-  for (int j = 0; j < XL; ++j) xrow[j] = a.x + (size_t)min(t0 + ((tid + NT * j) >> 4), a.T - 1) * K + 8 * (tid & 15);
+  for (int j = 0; j < XL; ++j) xvo[j] = (min(t0 + ((tid + NT * j) >> 4), a.T - 1) * K + 8 * (tid & 15)) * 2;
+  auto xld = [&](int j, int k0) __attribute__((always_inline)) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsx, xvo[j], k0 * 2, 0));
+  };
   auto load_x = [&](int i) __attribute__((always_inline)) {
     const int k0 = (sb + (i >> 1)) * 256 + 128 * (i & 1);
-    x0 = *reinterpret_cast<const uint4*>(xrow[0] + k0);
-    x1 = *reinterpret_cast<const uint4*>(xrow[1] + k0);
-    if constexpr (XL > 2) x2 = *reinterpret_cast<const uint4*>(xrow[XL > 2 ? 2 : 0] + k0);
-    if constexpr (XL > 3) x3 = *reinterpret_cast<const uint4*>(xrow[XL > 3 ? 3 : 0] + k0);
-    if constexpr (XL > 4) x4 = *reinterpret_cast<const uint4*>(xrow[XL > 4 ? 4 : 0] + k0);
-    if constexpr (XL > 5) x5 = *reinterpret_cast<const uint4*>(xrow[XL > 5 ? 5 : 0] + k0);
-    if constexpr (XL > 6) x6 = *reinterpret_cast<const uint4*>(xrow[XL > 6 ? 6 : 0] + k0);
-    if constexpr (XL > 7) x7 = *reinterpret_cast<const uint4*>(xrow[XL > 7 ? 7 : 0] + k0);
+    x0 = xld(0, k0);
+    x1 = xld(1, k0);
+    if constexpr (XL > 2) x2 = xld(XL > 2 ? 2 : 0, k0);
+    if constexpr (XL > 3) x3 = xld(XL > 3 ? 3 : 0, k0);
+    if constexpr (XL > 4) x4 = xld(XL > 4 ? 4 : 0, k0);
+    if constexpr (XL > 5) x5 = xld(XL > 5 ? 5 : 0, k0);
+    if constexpr (XL > 6) x6 = xld(XL > 6 ? 6 : 0, k0);
+    if constexpr (XL > 7) x7 = xld(XL > 7 ? 7 : 0, k0);
   };
   auto store_x = [&](int buf) __attribute__((always_inline)) {
     __half* d = &xs[buf][kg][(tid >> 4) * kT16Pitch + 8 * ((tid & 15) ^ ((tid >> 4) & 15))];
@@ -2070,10 +2080,12 @@ __global__ __launch_bounds__(NWV * 64 * KW) void gemm_t16_kernel(GemmT16Args a) 
     if constexpr (XL > 6) *reinterpret_cast<uint4*>(d + 6 * J) = x6;
     if constexpr (XL > 7) *reinterpret_cast<uint4*>(d + 7 * J) = x7;
   };
+  const auto rw0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wt0), 0, 0x7FFFFFFF, 0x00020000);
+  const auto rw1 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wt1), 0, 0x7FFFFFFF, 0x00020000);
   auto load_w = [&](int i, BRawT<QT>& w0, BRawT<QT>& w1) __attribute__((always_inline)) {
     const int s = sb + (i >> 1), h = i & 1;
-    tload<QT, false>(w0, wt0 + (size_t)s * SB, h, lane, r16, kq);
-    tload<QT, false>(w1, wt1 + (size_t)s * SB, h, lane, r16, kq);
+    tload_rs<QT, false>(w0, rw0, s * SB, h, lane, r16, kq);  // (cached: each tile serves several token blocks)
+    tload_rs<QT, false>(w1, rw1, s * SB, h, lane, r16, kq);
   };
   auto half = [&](int i, const BRawT<QT>& w0, const BRawT<QT>& w1) __attribute__((always_inline)) {
     const int s = sb + (i >> 1), h = i & 1;
@@ -2261,6 +2273,7 @@ void gemm_t16(const GemmT16Args& a, int epi, hipStream_t s) {
   if (!bmm_supported(a.w.type, a.w.K) || !a.w.base || !a.x) throw std::runtime_error("gemm_t16: unsupported type / K");
   if (a.w.rows % 16) throw std::runtime_error("gemm_t16: rows must be a multiple of 16");
   if (a.nwseg < 1 || a.nwseg > 3) throw std::runtime_error("gemm_t16: 1-3 stacked segments");
+  if ((long long)a.T * a.w.K * 2 >= (1LL << 31)) throw std::runtime_error("gemm_t16: X exceeds the 2 GB buffer offsets");
   if (a.nwseg > 1) {
     int t = a.wseg_tiles[0];
     for (int i = 1; i < a.nwseg; ++i) {
