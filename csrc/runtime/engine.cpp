@@ -877,10 +877,13 @@ void Engine::enqueue_rows_layer(int l, int T, int pos0, bool batched, hipStream_
     const bool t16 = prefill_t16_ && !batched;
     __half* const xh16 = reinterpret_cast<__half*>(xb_);
     __half* const attnh16 = reinterpret_cast<__half*>(attnb_);
-    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, qkv_, ncol, t16);  // + zero the q|k|v rows
+    // (+ zero the q|k|v rows for gemm_dq's split-K partials; the tile16 GEMM splits its stacked
+    // Q|K|V only on tiny grids and then zeroes what it splits itself - a 4096-row admission's
+    // zeroing pass was 57 MB per layer)
+    rmsnorm_bf16(x_, L.attn_norm, hp_.rms_eps, T, d, xb_, s, t16 ? nullptr : qkv_, t16 ? 0 : ncol, t16);
     if (t16) {
       GemmT16Args g;
-      g.x = xh16; g.T = T; g.ldo = ncol; g.out_zeroed = true;
+      g.x = xh16; g.T = T; g.ldo = ncol; g.out_zeroed = false;
       // Q|K|V stacked into one launch per run of equal weight type (their outputs are adjacent
       // columns of qkv_): one grid of 384 blocks at d = 4096 instead of three narrow ones
       const QMat* m[3] = {&L.t_wq, &L.t_wk, &L.t_wv};
